@@ -1,0 +1,260 @@
+#!/usr/bin/env python3
+"""Headline benchmark: batched replica-state merges into a device bucket table.
+
+Workload (BASELINE.json configs[1], SURVEY.md §8d "C2"): a table pre-populated
+with K = 10M buckets (2^24 slots), and per step one batch of n = 100M decoded
+replica messages (name + added/taken/elapsed), Zipf(1.1) over the keys, run
+through the Receive loop semantics (repo.go:54-92: GetBucket by full name,
+then Bucket.Merge) by phip_receive_soa with inputs resident in HBM.  Every
+step uses a fresh batch whose states are later than the previous step's
+(values shifted up by the step index), so every step is a first application
+of its messages to the table; the batches are generated before the timed
+region.
+
+Multi-GPU (torch.distributed, one process per GPU): buckets are sharded by
+owner; each rank holds its own K-bucket shard and merges its own pre-routed
+n-message stream (weak scaling, no data-path collective).  value = all
+merges of all ranks / max-over-ranks time.
+
+Prints ONE JSON line (rank 0).  See DESIGN.md §4 for the roofline accounting.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "bucket-state merges/sec + achieved HBM GB/s at 1/2/4/8 MI355X"
+T0 = 1_700_000_000_000_000_000
+BYTES_PER_MERGE = 88     # msg 32 + slot key 8 + state read 24 + state write 24
+HBM_PEAK_GBS = 8000.0    # MI355X_MICROARCH.md chip-level parameters (spec)
+DOMINANT = "k_receive_fast"
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=5)
+    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--keys", type=int, default=10_000_000)
+    p.add_argument("--messages", type=int, default=100_000_000)
+    p.add_argument("--log2-slots", type=int, default=24)
+    p.add_argument("--zipf", type=float, default=1.1)
+    p.add_argument("--cpu-sample", type=int, default=10_000_000)
+    p.add_argument("--cpu-threads", type=int, default=0)
+    p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--seed", type=int, default=1234)
+    return p.parse_args()
+
+
+# ------------------------------------------------------------ synthetic ----
+def names_for_ids(torch, ids):
+    """ids (int64 tensor) -> (blob uint8, offs int32[n+1]) with name = b"b%d"."""
+    dev = ids.device
+    nd = torch.ones_like(ids)
+    p = torch.full_like(ids, 10)
+    for _ in range(18):
+        nd += (ids >= p).to(torch.int64)
+        p = p * 10
+        if bool((ids < p).all()):
+            break
+    lens = 1 + nd
+    offs = torch.zeros(ids.numel() + 1, dtype=torch.int64, device=dev)
+    offs[1:] = torch.cumsum(lens, 0)
+    total = int(offs[-1])
+    blob = torch.zeros(total + 8, dtype=torch.uint8, device=dev)
+    start = offs[:-1]
+    blob[start] = ord("b")
+    maxd = int(nd.max())
+    for d in range(maxd):
+        m = nd > d
+        pw = torch.pow(torch.tensor(10, dtype=torch.int64, device=dev), (nd[m] - 1 - d))
+        digit = (ids[m] // pw) % 10
+        blob[start[m] + 1 + d] = (48 + digit).to(torch.uint8)
+    assert total < 2**32
+    return blob, offs.to(torch.int32)
+
+
+def zipf_ids(torch, gen, n, K, s, dev):
+    ranks = torch.arange(1, K + 1, dtype=torch.float64, device=dev)
+    cdf = torch.cumsum(ranks.pow(-s), 0)
+    cdf /= cdf[-1].clone()
+    u = torch.rand(n, dtype=torch.float64, device=dev, generator=gen)
+    r = torch.searchsorted(cdf, u).clamp_(max=K - 1)
+    del cdf, ranks, u
+    mult = 2654435761 % K or 1
+    while np.gcd(mult, K) != 1:
+        mult += 1
+    return (r * mult) % K
+
+
+def replica_states(torch, gen, n, step, dev):
+    """SURVEY §8d clean domain, shifted by `step` so each batch is later."""
+    taken = torch.randint(0, 10**6, (n,), device=dev, generator=gen).to(torch.float64) + step * 2e6
+    added = taken + torch.rand(n, dtype=torch.float64, device=dev, generator=gen) * 100.0
+    elapsed = torch.randint(0, 1 << 40, (n,), device=dev, generator=gen, dtype=torch.int64) + step * (1 << 40)
+    return added.view(torch.int64), taken.view(torch.int64), elapsed
+
+
+# ---------------------------------------------------------- CPU baseline ---
+def cpu_baseline(args, K, ids_host, threads):
+    """The Go-structured C++ restatement (global RWMutex + map + per-bucket
+    RWMutex, repo.go:171-235 / bucket.go:240-263) timed on this host on a
+    bounded sample of the same workload."""
+    import torch
+    from oracle import oracle as O
+    L = O.lib()
+    repo = O.Repo()
+    keys = torch.arange(K, dtype=torch.int64)
+    kb, ko = names_for_ids(torch, keys)
+    z = np.zeros(K, np.uint64)
+    L.orc_repo_seed(repo.h, kb.numpy(), ko.numpy().astype(np.uint32), K, z, z,
+                    np.zeros(K, np.int64), np.full(K, T0, np.int64))
+    del kb, ko, keys
+    n = min(args.cpu_sample, ids_host.numel())
+    ids = ids_host[:n]
+    blob, offs = names_for_ids(torch, ids)
+    g = torch.Generator().manual_seed(args.seed + 99)
+    a, t, e = replica_states(torch, g, n, 0, "cpu")
+    blob_np, offs_np = blob.numpy(), offs.numpy().astype(np.uint32)
+    a_np, t_np, e_np = a.numpy().view(np.uint64), t.numpy().view(np.uint64), e.numpy()
+    secs = L.orc_bench_receive(repo.h, blob_np, offs_np, n, a_np, t_np, e_np, T0, threads)
+    n1 = min(n, 2_000_000)
+    # single goroutine, as the reference's Receive loop runs (repo.go:54)
+    repo1 = O.Repo()
+    kb, ko = names_for_ids(torch, torch.arange(K, dtype=torch.int64))
+    L.orc_repo_seed(repo1.h, kb.numpy(), ko.numpy().astype(np.uint32), K, z, z,
+                    np.zeros(K, np.int64), np.full(K, T0, np.int64))
+    secs1 = L.orc_bench_receive(repo1.h, blob_np, offs_np, n1, a_np, t_np, e_np, T0, 1)
+    return dict(value=n / secs, unit="merges/s", cores=threads, kind="port",
+                sample=f"{n} of the step-0 messages (Zipf {args.zipf} over {K} buckets) into a "
+                       f"{K}-bucket Go-structured map, {threads} threads",
+                single_thread=dict(value=n1 / secs1, sample=f"{n1} messages, 1 thread (the "
+                                   "reference's single Receive goroutine)"))
+
+
+def pmc_traffic(workload):
+    """HBM bytes per launch of the dominant kernel from the committed PMC
+    summary (profiles/pmc_summary.json, produced by tools/pmc_summary.py)."""
+    path = os.path.join(ROOT, "profiles", "pmc_summary.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        if d.get("kernel") == DOMINANT and d.get("workload") == workload:
+            return d.get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", init_method="env://")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    import patrol_amd
+
+    K, n = args.keys, args.messages
+    gen = torch.Generator(device=dev).manual_seed(args.seed + 7919 * rank)
+
+    # Shard: rank r owns bucket ids [r*K, (r+1)*K) (owner-routed upstream).
+    base = rank * K
+    repo = patrol_amd.GPURepo(device=local, log2_slots=args.log2_slots, arena_bytes=1 << 20)
+    keys = torch.arange(base, base + K, dtype=torch.int64, device=dev)
+    kb, ko = names_for_ids(torch, keys)
+    st = torch.zeros((K, 4), dtype=torch.int64, device=dev)
+    # added = taken = +0.0 bits, elapsed 0: the zero state GetBucket creates (repo.go:208)
+    st[:, 3] = T0
+    torch.cuda.synchronize()
+    repo.seed_device(kb, ko, st, K)
+    del kb, ko, st, keys
+    assert len(repo) == K
+
+    ids = zipf_ids(torch, gen, n, K, args.zipf, dev)
+    blob, offs = names_for_ids(torch, ids + base)
+    batches = [replica_states(torch, gen, n, j, dev) for j in range(args.warmup + args.steps)]
+    torch.cuda.synchronize()
+
+    def step(j):
+        a, t, e = batches[j]
+        repo.receive_soa(blob, a, t, e, T0 + j, name_offs=offs, n=n, device=True)
+
+    for j in range(args.warmup):
+        step(j)
+    repo.set_timing(True)
+    kern = {}
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for j in range(args.warmup, args.warmup + args.steps):
+        step(j)
+        for name, ms in repo.timings():
+            kern.setdefault(name, []).append(ms)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    repo.set_timing(False)
+    if world > 1:
+        tt = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        el = float(tt.item())
+
+    total = world * n * args.steps
+    dom = kern.get(DOMINANT, [float("nan")])
+    dom_ms = float(np.mean(dom))
+    achieved = BYTES_PER_MERGE * n / (dom_ms / 1e3) / 1e9
+    workload = f"C2 merge: {n} replica messages -> {K}-bucket table (2^{args.log2_slots} slots), Zipf({args.zipf})"
+    traffic = pmc_traffic(workload)
+    out = {
+        "metric": METRIC,
+        "value": total / el,
+        "unit": "merges/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": el / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (seeded Zipf keys, SURVEY §8d replica states; batches resident in HBM)",
+        "config": {"workload": workload, "keys_per_gpu": K, "messages_per_step_per_gpu": n,
+                   "slots_per_gpu": 1 << args.log2_slots, "parallelism": f"shard{world}"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "kernel": DOMINANT, "kernel_ms": dom_ms,
+                     "algorithmic_bytes_per_launch": BYTES_PER_MERGE * n},
+        "kernels_ms": {k: float(np.mean(v)) for k, v in kern.items()},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+        try:
+            out["cpu_baseline"] = cpu_baseline(args, K, ids.cpu(), threads)
+        except Exception as ex:  # the baseline must never hide the GPU result
+            out["cpu_baseline"] = {"error": repr(ex)}
+    elif rank == 0:
+        out["cpu_baseline"] = None
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    repo.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

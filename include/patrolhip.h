@@ -1,0 +1,220 @@
+/*
+ * libpatrolhip — MI355X (gfx950) bucket-state engine for Patrol.
+ *
+ * A C ABI (plain pointers and sizes, no C++ types, no exceptions) that a Go
+ * maintainer binds with cgo to replace Patrol's in-memory bucket map and its
+ * two hot loops (INTEGRATION.md shows the binding):
+ *
+ *   Patrol seam (reference file:line)                 replaced by
+ *   ------------------------------------------------  ------------------------------
+ *   Repo interface              repo.go:15-18          phip_open / phip_get / batched calls
+ *   NewLocalRepo(clock, bs...)  repo.go:179-185        phip_open + phip_seed
+ *   LocalRepo.GetBucket         repo.go:189-211        device table find-or-create (inside every batch)
+ *   LocalRepo.UpsertBucket      repo.go:215-235        phip_upsert_soa
+ *   ReplicatedRepo.Receive loop repo.go:54-92,108-120  phip_receive_datagrams / phip_receive_soa
+ *   Bucket.UnmarshalBinary      bucket.go:71-91        device decode inside phip_receive_datagrams
+ *   Bucket.MarshalBinary        bucket.go:51-68        phip_marshal (host; unicast/broadcast egress)
+ *   Bucket.Merge                bucket.go:240-263      device merge inside receive/upsert/apply
+ *   Bucket.Take                 bucket.go:186-225      phip_take / phip_apply_mixed
+ *   Bucket.IsZero               bucket.go:165-170      receive status (merge vs incast)
+ *   ParseRate                   bucket.go:102-123      phip_parse_rate (host)
+ *   API.takeBucket              api.go:51-86           phip_api_take (host handler logic over phip_take)
+ *
+ * Semantics are the Go reference's, op for op, in batch index order ("seq"):
+ * a batch gives exactly the results of running the Go code on its elements
+ * one after another (DESIGN.md §3 explains how the parallel kernels keep that
+ * guarantee).  Buckets are identified by their full name (the FNV-1a hash is
+ * only the table's probe key; names are always compared).
+ *
+ * Conventions
+ *  - Return 0 (PHIP_OK) or a negative phip_err; never abort.  Details in
+ *    phip_last_error().
+ *  - Input buffers are caller-owned and only read during the call; output
+ *    buffers are caller-owned.  Host pointers are staged into the library's
+ *    own device buffers.  With PHIP_DEVICE_PTRS every pointer of that call
+ *    (inputs and outputs) is device memory of the handle's GPU; the call then
+ *    runs without host copies (the form bench.py times).
+ *  - Times are int64 nanoseconds since the Unix epoch (the `clock()` reading
+ *    Patrol passes around); durations are int64 ns (time.Duration).
+ *  - float64 values cross the ABI as IEEE-754 bit patterns (uint64) so NaN
+ *    payloads and -0.0 survive bit-exactly.
+ *  - One handle per GPU; calls on a handle are serialised by an internal
+ *    mutex and every entry point sets its device (cgo goroutines migrate
+ *    between OS threads).
+ */
+#ifndef PATROLHIP_H
+#define PATROLHIP_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PHIP_ABI_VERSION 1
+
+/* bucket.go:36-44 */
+#define PHIP_BUCKET_FIXED_SIZE 25
+#define PHIP_BUCKET_PACKET_SIZE 256
+#define PHIP_MAX_NAME_LEN 231
+
+typedef struct phip_handle phip_handle;
+
+typedef enum phip_err {
+  PHIP_OK = 0,
+  PHIP_ERR_INVALID = -1,        /* bad argument */
+  PHIP_ERR_HIP = -2,            /* HIP runtime error */
+  PHIP_ERR_FULL = -3,           /* table load factor limit reached */
+  PHIP_ERR_ARENA = -4,          /* long-name arena exhausted */
+  PHIP_ERR_SHORT_BUFFER = -5,   /* io.ErrShortBuffer from a datagram (bucket.go:72,84) */
+  PHIP_ERR_NAME_TOO_LARGE = -6, /* ErrNameTooLarge (bucket.go:48) */
+  PHIP_ERR_NO_DEVICE = -7
+} phip_err;
+
+/* Per-op status codes (one uint8 per op). */
+enum {
+  PHIP_ST_MERGED = 1,          /* non-zero remote merged: repo.go:78-79                 */
+  PHIP_ST_INCAST_REPLY = 2,    /* zero remote, existed && !local.IsZero(): repo.go:86-90 */
+  PHIP_ST_INCAST_NOREPLY = 3,  /* zero remote otherwise                                  */
+  PHIP_ST_SHORT = 4,           /* datagram failed UnmarshalBinary: Receive returns      */
+  PHIP_ST_NOT_PROCESSED = 5,   /* after a PHIP_ST_SHORT (the Go loop has exited)        */
+  PHIP_ST_TAKE_OK = 6,         /* Take returned ok=true                                 */
+  PHIP_ST_TAKE_DENIED = 7,     /* Take returned ok=false (HTTP 429)                     */
+  PHIP_ST_UPSERT_INSERTED = 8, /* UpsertBucket inserted the state as-is (repo.go:225-230) */
+  PHIP_ST_CREATED = 0x80       /* flag: this op's GetBucket created the bucket          */
+};
+
+/* Op kinds for phip_apply_mixed. */
+enum {
+  PHIP_OP_TAKE = 0,     /* GetBucket + Take(now, Rate{freq, per}, count) (api.go:67-74)   */
+  PHIP_OP_RECEIVE = 1,  /* received replica state (repo.go:78-90)                         */
+  PHIP_OP_UPSERT = 2    /* LocalRepo.UpsertBucket of a distinct state (repo.go:215-235)   */
+};
+
+/* Call flags. */
+#define PHIP_DEVICE_PTRS 0x1u   /* all pointers of the call are device memory */
+
+typedef struct phip_config {
+  int32_t device;        /* HIP device ordinal                                          */
+  uint32_t log2_slots;   /* table capacity = 2^log2_slots slots (10..31)                */
+  uint64_t arena_bytes;  /* device arena for names longer than 23 bytes                 */
+  uint32_t max_load_pct; /* refuse inserts beyond this load factor (default 90)         */
+  uint32_t debug_tag_bits; /* 0 in production; 1..63 truncates the name hash so tests can
+                              force tag collisions (names are always compared)          */
+} phip_config;
+
+/* Bucket state as Patrol holds it (bucket.go:20-32, name excluded). */
+typedef struct phip_state {
+  uint64_t added;    /* float64 bits */
+  uint64_t taken;    /* float64 bits */
+  int64_t elapsed;   /* time.Duration ns */
+  int64_t created;   /* local creation time, ns since the Unix epoch */
+} phip_state;
+
+/*
+ * Decoded replica states (the fields UnmarshalBinary fills, bucket.go:78-87).
+ * Name i is names[name_offs[i] .. name_offs[i+1]).  With PHIP_DEVICE_PTRS the
+ * names blob must stay readable 8 bytes past name_offs[n].
+ */
+typedef struct phip_msgs {
+  uint32_t n;
+  uint32_t reserved;
+  const uint8_t* names;
+  const uint32_t* name_offs; /* n+1 entries */
+  const uint64_t* added;     /* float64 bits */
+  const uint64_t* taken;     /* float64 bits */
+  const int64_t* elapsed;
+} phip_msgs;
+
+/* A mixed ordered stream (one entry per op, applied in index order). */
+typedef struct phip_ops {
+  uint32_t n;
+  uint32_t reserved;
+  const uint8_t* kind;       /* PHIP_OP_*                                       */
+  const uint8_t* names;
+  const uint32_t* name_offs; /* n+1 entries                                     */
+  const int64_t* now;        /* clock() reading of each op (also `created`)     */
+  const int64_t* freq;       /* Rate.Freq   (TAKE)                              */
+  const int64_t* per;        /* Rate.Per ns (TAKE)                              */
+  const uint64_t* count;     /* n tokens    (TAKE)                              */
+  const uint64_t* added;     /* float64 bits (RECEIVE/UPSERT)                   */
+  const uint64_t* taken;     /* float64 bits (RECEIVE/UPSERT)                   */
+  const int64_t* elapsed;    /* (RECEIVE/UPSERT)                                */
+} phip_ops;
+
+/* Per-op results (any pointer may be NULL). */
+typedef struct phip_results {
+  uint8_t* status;           /* PHIP_ST_* (| PHIP_ST_CREATED)                   */
+  uint64_t* remaining;       /* TAKE: uint64(remaining) as Go returns it        */
+  uint64_t* have;            /* TAKE: float64 bits of the value truncated       */
+  phip_state* reply;         /* INCAST_REPLY: local state to unicast back       */
+} phip_results;
+
+/* ---- lifecycle ---- */
+int phip_abi_version(void);
+int phip_open(const phip_config* cfg, phip_handle** out);
+void phip_close(phip_handle* h);
+const char* phip_last_error(const phip_handle* h);
+int phip_flush(phip_handle* h);                    /* hipStreamSynchronize */
+uint64_t phip_len(phip_handle* h);                 /* number of buckets */
+uint64_t phip_capacity(phip_handle* h);            /* number of slots */
+
+/* ---- repo ---- */
+/* NewLocalRepo(clock, bs...): insert (or overwrite) buckets as given. */
+int phip_seed(phip_handle* h, const uint8_t* names, const uint32_t* name_offs, uint32_t n,
+              const phip_state* states, uint32_t flags);
+/* Lookup without creating.  Returns 1 found, 0 absent, <0 error. */
+int phip_get(phip_handle* h, const uint8_t* name, uint32_t len, phip_state* out);
+/* Dump every bucket (unordered).  Call with names==NULL to size: *n_out and
+ * *names_bytes_out are filled.  name_offs has n+1 entries. */
+int phip_dump(phip_handle* h, uint8_t* names, uint64_t names_cap, uint64_t* name_offs,
+              phip_state* states, uint64_t max_n, uint64_t* n_out, uint64_t* names_bytes_out);
+
+/* ---- hot path ---- */
+/* ReplicatedRepo.Receive over n raw datagrams (byte-identical wire format,
+ * bucket.go:59-64): bytes[offs[i] .. offs[i+1]).  `now` is the clock reading
+ * used for buckets created by this batch.  Stops at the first malformed
+ * datagram like the Go loop (repo.go:72-73): *stop_index receives its index
+ * (or n) and the call returns PHIP_ERR_SHORT_BUFFER when one was found. */
+int phip_receive_datagrams(phip_handle* h, const uint8_t* bytes, const uint64_t* offs, uint32_t n,
+                           int64_t now, const phip_results* res, uint32_t* stop_index,
+                           uint32_t flags);
+/* The same loop over pre-decoded states. */
+int phip_receive_soa(phip_handle* h, const phip_msgs* m, int64_t now, const phip_results* res,
+                     uint32_t flags);
+/* LocalRepo.UpsertBucket for each state, in order. */
+int phip_upsert_soa(phip_handle* h, const phip_msgs* m, int64_t now, const phip_results* res,
+                    uint32_t flags);
+/* Ordered mixed stream of TAKE / RECEIVE / UPSERT ops. */
+int phip_apply_mixed(phip_handle* h, const phip_ops* ops, const phip_results* res, uint32_t flags);
+/* All-TAKE convenience form of phip_apply_mixed. */
+int phip_take(phip_handle* h, const uint8_t* names, const uint32_t* name_offs, uint32_t n,
+              const int64_t* now, const int64_t* freq, const int64_t* per, const uint64_t* count,
+              uint64_t* remaining_out, uint8_t* ok_out, uint32_t flags);
+
+/* ---- host helpers (no device work) ---- */
+/* ParseRate: returns 0 or <0 on error; freq and per receive the values Go
+ * returns beside the error (api.go:61 uses them). */
+int phip_parse_rate(const char* s, uint32_t len, int64_t* freq, int64_t* per);
+/* MarshalBinary: writes 25+len bytes to out (>= 256 bytes), returns the size
+ * or PHIP_ERR_NAME_TOO_LARGE. */
+int phip_marshal(const uint8_t* name, uint32_t len, const phip_state* s, uint8_t* out);
+/* API.takeBucket (api.go:51-86) over this engine: returns the HTTP status
+ * code (200/429/400) and writes the response body (<= 64 bytes). */
+int phip_api_take(phip_handle* h, const uint8_t* name, uint32_t len, const char* rate,
+                  uint32_t rate_len, const char* count, uint32_t count_len, int64_t now,
+                  char* body, uint32_t* body_len);
+
+/* ---- diagnostics ---- */
+/* Per-kernel timing of the last hot-path call, measured with HIP events on
+ * the handle's stream: writes up to max entries of (name, ms) and returns the
+ * count. */
+int phip_last_timings(phip_handle* h, const char** names, float* ms, int max);
+/* Enable (1) or disable (0) event timing (off by default). */
+void phip_set_timing(phip_handle* h, int on);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PATROLHIP_H */

@@ -1,0 +1,12 @@
+"""patrol_amd — MI355X-native bucket-state engine for Patrol (calavera/patrol).
+
+The product is libpatrolhip (HIP kernels for gfx950 behind the C ABI in
+include/patrolhip.h).  This package holds its sources (csrc/), the in-tree
+build (Makefile -> libpatrolhip.so) and a thin Python binding used by tests
+and bench.py.
+"""
+from ._lib import EXPORTS, LIB_PATH, load  # noqa: F401
+from .engine import BucketState, GPURepo, PatrolHipError, marshal, names_blob, parse_rate  # noqa: F401
+
+__all__ = ["GPURepo", "BucketState", "PatrolHipError", "parse_rate", "marshal", "names_blob",
+           "load", "LIB_PATH", "EXPORTS"]

@@ -1,0 +1,101 @@
+"""ctypes binding of libpatrolhip (include/patrolhip.h).
+
+The library is built in-tree (patrol_amd/libpatrolhip.so, see Makefile /
+__graft_entry__.build()).  There is no fallback: if the shared object is
+missing or fails to load, importing the engine raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libpatrolhip.so")
+
+# Every symbol include/patrolhip.h declares (tests/test_abi.py checks both ways).
+EXPORTS = [
+    "phip_abi_version", "phip_open", "phip_close", "phip_last_error", "phip_flush", "phip_len",
+    "phip_capacity", "phip_seed", "phip_get", "phip_dump", "phip_receive_datagrams",
+    "phip_receive_soa", "phip_upsert_soa", "phip_apply_mixed", "phip_take", "phip_parse_rate",
+    "phip_marshal", "phip_api_take", "phip_last_timings", "phip_set_timing",
+]
+
+PHIP_OK = 0
+PHIP_ERR = {-1: "INVALID", -2: "HIP", -3: "FULL", -4: "ARENA", -5: "SHORT_BUFFER",
+            -6: "NAME_TOO_LARGE", -7: "NO_DEVICE"}
+ST_MERGED, ST_INCAST_REPLY, ST_INCAST_NOREPLY, ST_SHORT, ST_NOT_PROCESSED = 1, 2, 3, 4, 5
+ST_TAKE_OK, ST_TAKE_DENIED, ST_UPSERT_INSERTED, ST_CREATED = 6, 7, 8, 0x80
+OP_TAKE, OP_RECEIVE, OP_UPSERT = 0, 1, 2
+DEVICE_PTRS = 0x1
+
+
+class phip_config(C.Structure):
+    _fields_ = [("device", C.c_int32), ("log2_slots", C.c_uint32), ("arena_bytes", C.c_uint64),
+                ("max_load_pct", C.c_uint32), ("debug_tag_bits", C.c_uint32)]
+
+
+class phip_state(C.Structure):
+    _fields_ = [("added", C.c_uint64), ("taken", C.c_uint64), ("elapsed", C.c_int64),
+                ("created", C.c_int64)]
+
+
+class phip_msgs(C.Structure):
+    _fields_ = [("n", C.c_uint32), ("reserved", C.c_uint32), ("names", C.c_void_p),
+                ("name_offs", C.c_void_p), ("added", C.c_void_p), ("taken", C.c_void_p),
+                ("elapsed", C.c_void_p)]
+
+
+class phip_ops(C.Structure):
+    _fields_ = [("n", C.c_uint32), ("reserved", C.c_uint32), ("kind", C.c_void_p),
+                ("names", C.c_void_p), ("name_offs", C.c_void_p), ("now", C.c_void_p),
+                ("freq", C.c_void_p), ("per", C.c_void_p), ("count", C.c_void_p),
+                ("added", C.c_void_p), ("taken", C.c_void_p), ("elapsed", C.c_void_p)]
+
+
+class phip_results(C.Structure):
+    _fields_ = [("status", C.c_void_p), ("remaining", C.c_void_p), ("have", C.c_void_p),
+                ("reply", C.c_void_p)]
+
+
+_lib = None
+
+
+def load(path: str = LIB_PATH):
+    """Load libpatrolhip.so (raises OSError if it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise OSError(f"libpatrolhip.so not built at {path}: run `make -C patrol_amd` "
+                      "or __graft_entry__.build()")
+    L = C.CDLL(path)
+    vp, u32, u64, i64 = C.c_void_p, C.c_uint32, C.c_uint64, C.c_int64
+    L.phip_abi_version.restype = C.c_int
+    L.phip_open.argtypes = [C.POINTER(phip_config), C.POINTER(vp)]
+    L.phip_close.argtypes = [vp]
+    L.phip_close.restype = None
+    L.phip_last_error.argtypes = [vp]
+    L.phip_last_error.restype = C.c_char_p
+    L.phip_flush.argtypes = [vp]
+    L.phip_len.argtypes = [vp]
+    L.phip_len.restype = u64
+    L.phip_capacity.argtypes = [vp]
+    L.phip_capacity.restype = u64
+    L.phip_seed.argtypes = [vp, vp, vp, u32, vp, u32]
+    L.phip_get.argtypes = [vp, C.c_char_p, u32, C.POINTER(phip_state)]
+    L.phip_dump.argtypes = [vp, vp, u64, vp, vp, u64, C.POINTER(u64), C.POINTER(u64)]
+    L.phip_receive_datagrams.argtypes = [vp, vp, vp, u32, i64, C.POINTER(phip_results),
+                                         C.POINTER(u32), u32]
+    L.phip_receive_soa.argtypes = [vp, C.POINTER(phip_msgs), i64, C.POINTER(phip_results), u32]
+    L.phip_upsert_soa.argtypes = [vp, C.POINTER(phip_msgs), i64, C.POINTER(phip_results), u32]
+    L.phip_apply_mixed.argtypes = [vp, C.POINTER(phip_ops), C.POINTER(phip_results), u32]
+    L.phip_take.argtypes = [vp, vp, vp, u32, vp, vp, vp, vp, vp, vp, u32]
+    L.phip_parse_rate.argtypes = [C.c_char_p, u32, C.POINTER(i64), C.POINTER(i64)]
+    L.phip_marshal.argtypes = [C.c_char_p, u32, C.POINTER(phip_state), C.c_char_p]
+    L.phip_api_take.argtypes = [vp, C.c_char_p, u32, C.c_char_p, u32, C.c_char_p, u32, i64,
+                                C.c_char_p, C.POINTER(u32)]
+    L.phip_last_timings.argtypes = [vp, C.POINTER(C.c_char_p), C.POINTER(C.c_float), C.c_int]
+    L.phip_set_timing.argtypes = [vp, C.c_int]
+    L.phip_set_timing.restype = None
+    _lib = L
+    return L

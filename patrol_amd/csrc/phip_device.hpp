@@ -1,0 +1,190 @@
+// Device-side building blocks of libpatrolhip (gfx950).
+//
+//  * the order-preserving 64-bit key encoding ("E-encoding") that lets one
+//    unsigned atomicMax reproduce Go's asymmetric `if b.x < o.x { b.x = o.x }`
+//    merge (bucket.go:250-256) for every stored value and every replica value
+//    except -0.0 (DESIGN.md §3.2 has the proof sketch);
+//  * the op-for-op restatement of Bucket.Take (bucket.go:186-225) on doubles,
+//    including Go's time.Time saturation and amd64 uint64(float64) rules;
+//  * the slot record of the device hash table and name canonicalisation.
+//
+// Compiled with -ffp-contract=off: every + - / below is one IEEE-754 binary64
+// operation, exactly as the Go compiler emits them on amd64.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "patrolhip.h"
+
+namespace phip {
+
+typedef unsigned long long u64;
+typedef long long i64;
+typedef unsigned int u32;
+typedef unsigned char u8;
+
+constexpr u64 kSign = 0x8000000000000000ull;
+constexpr u64 kInfBits = 0x7FF0000000000000ull;      // +Inf
+constexpr u64 kNanBase = 0xFFE0000000000002ull;      // first E-code of a NaN
+constexpr u64 kNanPerSign = (1ull << 52) - 1;        // NaN payloads per sign
+constexpr u64 kEPosZero = kInfBits;                  // E(+0.0)
+constexpr u64 kENegZero = kInfBits + 1;              // E(-0.0)
+
+__host__ __device__ inline bool is_nan_bits(u64 b) { return (b & ~kSign) > kInfBits; }
+__host__ __device__ inline bool is_zero_bits(u64 b) { return (b & ~kSign) == 0; }
+
+// E: float64 bits -> u64 such that unsigned order is
+//   negatives (by value) < +0 < -0 < positives (by value) < NaNs.
+// It is a bijection on all 2^64 patterns.  Placing -0 just above +0 makes
+// max(E(b), E(o)) equal E(Go's merge result) for every stored b and every
+// replica o != -0.0 (a NaN replica is mapped to 0 = E(-Inf), a no-op).
+__host__ __device__ inline u64 enc_f64(u64 b) {
+  u64 mag = b & ~kSign;
+  if (mag > kInfBits) {                            // NaN
+    u64 idx = mag - kInfBits - 1;
+    if (b & kSign) idx += kNanPerSign;
+    return kNanBase + idx;
+  }
+  if (b & kSign) return mag == 0 ? kENegZero : kInfBits - mag;
+  return mag == 0 ? kEPosZero : kInfBits + 1 + mag;
+}
+
+__host__ __device__ inline u64 dec_f64(u64 e) {
+  if (e < kInfBits) return kSign | (kInfBits - e);
+  if (e == kEPosZero) return 0;
+  if (e == kENegZero) return kSign;
+  if (e < kNanBase) return e - kInfBits - 1;
+  u64 idx = e - kNanBase;
+  if (idx < kNanPerSign) return kInfBits + 1 + idx;
+  return kSign | (kInfBits + 1 + idx - kNanPerSign);
+}
+
+// Replica value as an atomicMax operand (NaN is never adopted by Go's `<`).
+__host__ __device__ inline u64 enc_replica(u64 b) { return is_nan_bits(b) ? 0ull : enc_f64(b); }
+
+__host__ __device__ inline double as_f64(u64 b) { return __builtin_bit_cast(double, b); }
+__host__ __device__ inline u64 as_bits(double x) { return __builtin_bit_cast(u64, x); }
+
+// ------------------------------------------------------------- Take -----
+// x86-64 CVTTSD2SQ (what Go's amd64 backend uses for float->int).
+__device__ inline i64 cvttsd2sq(double x) {
+  if (!(x >= -9223372036854775808.0 && x < 9223372036854775808.0)) return (i64)kSign;
+  return (i64)x;
+}
+// Go uint64(float64) on amd64: cutoff at 2^63 (ssagen floatToUint).
+__device__ inline u64 go_u64(double x) {
+  if (x < 9223372036854775808.0) return (u64)cvttsd2sq(x);
+  return (u64)cvttsd2sq(x - 9223372036854775808.0) | kSign;
+}
+
+// Rate.Tokens (bucket.go:132-143) with Rate.Interval (bucket.go:146-148).
+__device__ inline double rate_tokens(i64 freq, i64 per, i64 d) {
+  if (freq == 0 || per == 0) return 0.0;
+  i64 interval = (freq == -1 && per == (i64)kSign) ? (i64)kSign : per / freq;
+  if (interval == 0) return 0.0;
+  return (double)d / (double)interval;
+}
+
+struct TakeResult {
+  u64 remaining;
+  u64 have_bits;
+  bool ok;
+};
+
+// Bucket.Take (bucket.go:186-225), in the reference's exact operation order.
+// `created` and `now` are int64 ns; created.Add(elapsed) is exact (128-bit,
+// as time.Time cannot overflow here), now.Sub(last) saturates like
+// time.Time.Sub, and elapsed += dt wraps like Go int64.
+__device__ inline TakeResult take_step(double& added, double& taken, i64& elapsed, i64 created,
+                                       i64 now, i64 freq, i64 per, u64 n) {
+  double capacity = (double)freq;                              // :192
+  if (added == 0) added = capacity;                            // :194-196
+  __int128 last = (__int128)created + (__int128)elapsed;       // :198
+  if ((__int128)now < last) last = now;                        // :199-201
+  double tokens = added - taken;                               // :204
+  __int128 dd = (__int128)now - last;                          // :207
+  i64 dt = dd > (__int128)0x7FFFFFFFFFFFFFFFll ? 0x7FFFFFFFFFFFFFFFll
+         : (dd < -(__int128)0x7FFFFFFFFFFFFFFFll - 1 ? (i64)kSign : (i64)dd);
+  double add = rate_tokens(freq, per, dt);                     // :210
+  double missing = capacity - tokens;                          // :211
+  if (add > missing) add = missing;                            // :211-213
+  double t = (double)n;                                        // :215
+  double have = tokens + add;                                  // :216
+  if (t > have) return TakeResult{go_u64(have), as_bits(have), false};   // :216-218
+  elapsed = (i64)((u64)elapsed + (u64)dt);                     // :220
+  added = added + add;                                         // :221
+  taken = taken + t;                                           // :222
+  double rem = added - taken;
+  return TakeResult{go_u64(rem), as_bits(rem), true};          // :224
+}
+
+// Bucket.Merge for one `other` (bucket.go:250-260) on raw values.
+__device__ inline void go_merge(double& a, double& t, i64& e, double oa, double ot, i64 oe) {
+  if (a < oa) a = oa;
+  if (t < ot) t = ot;
+  if (e < oe) e = oe;
+}
+
+// Bucket.IsZero (bucket.go:165-170): -0.0 == 0 is true.
+__host__ __device__ inline bool state_is_zero(u64 a_bits, u64 t_bits, i64 e) {
+  return is_zero_bits(a_bits) && is_zero_bits(t_bits) && e == 0;
+}
+
+// ------------------------------------------------------------ table -----
+// One 64-byte slot record (one HBM burst): state + canonical name.
+//   added/taken  E-encoded float64
+//   name[0] byte0 = len; len <= 23: bytes 1..len of name[] hold the name;
+//           len > 23: name[0] bytes 4..7 = arena offset, name[1..2] = the
+//           first 16 bytes (fast reject), full name in the arena.
+struct alignas(64) Rec {
+  u64 added;
+  u64 taken;
+  i64 elapsed;
+  i64 created;
+  u64 name[3];
+  u32 flags;
+  u32 aux;   // scratch: min seq of the ops of the batch that created it
+};
+static_assert(sizeof(Rec) == 64, "slot record must be one 64-byte burst");
+
+constexpr u32 kRecPublished = 1u;   // name and state written (visible after a kernel boundary)
+constexpr u32 kRecNew = 2u;         // created by the current batch
+
+constexpr u64 kFnvOffset = 0xcbf29ce484222325ull;
+constexpr u64 kFnvPrime = 0x100000001b3ull;
+
+// h * 0x100000001b3 == h * 0x1b3 + (h << 40)
+__host__ __device__ inline u64 fnv_step(u64 h, u8 c) {
+  h ^= c;
+  return h * 0x1b3ull + (h << 40);
+}
+
+__host__ __device__ inline u64 tag_of(u64 h) { return h ? h : 1ull; }
+
+struct Name {
+  u64 w0, w1, w2;   // canonical 24-byte field (see Rec)
+  u64 h;            // FNV-1a 64
+  u64 off;          // byte offset of the name in its source blob
+  u32 len;
+};
+
+__host__ __device__ inline void put_name_byte(Name& nm, u32 pos, u8 c) {
+  u64 v = (u64)c << ((pos & 7) * 8);
+  if (pos < 8) nm.w0 |= v;
+  else if (pos < 16) nm.w1 |= v;
+  else nm.w2 |= v;
+}
+
+// Reads name bytes src[off .. off+len), hashes and canonicalises them.
+__host__ __device__ inline void load_name(const u8* src, u64 off, u32 len, Name& nm) {
+  nm.w0 = len & 0xFFu; nm.w1 = 0; nm.w2 = 0; nm.h = kFnvOffset; nm.off = off; nm.len = len;
+  const bool inl = len <= 23;
+  for (u32 k = 0; k < len; ++k) {
+    u8 c = src[off + k];
+    nm.h = fnv_step(nm.h, c);
+    if (inl) put_name_byte(nm, k + 1, c);
+    else if (k < 16) put_name_byte(nm, k + 8, c);
+  }
+}
+
+}  // namespace phip

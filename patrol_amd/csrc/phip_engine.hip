@@ -1,0 +1,850 @@
+// libpatrolhip host orchestration: the C ABI of include/patrolhip.h.
+//
+// Pipelines:
+//   fast receive  classify -> k_receive_fast -> [insert rounds -> k_receive_fast(miss list)]
+//   ordered       resolve -> [insert rounds -> resolve(miss)] -> sort(slot, seq)
+//                 -> run-length segments -> k_fold_thread / k_fold_wave
+// Everything runs on the handle's own HIP stream; host synchronisation only
+// reads back small counters (miss count, segment count) between stages.
+#include <cstring>
+#include <hip/hip_runtime.h>
+#include <rocprim/rocprim.hpp>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "patrolhip.h"
+#include "phip_kernels.hpp"
+
+using namespace phip;
+
+namespace {
+
+enum BufId {
+  B_NAMES, B_OFFS, B_A, B_T, B_E, B_KIND, B_NOW, B_FREQ, B_PER, B_COUNT,
+  B_STATUS, B_REM, B_HAVE, B_REPLY,
+  B_BYTES, B_DOFFS, B_NOFF, B_NLEN, B_DA, B_DT, B_DE,
+  B_MISS, B_MISS2, B_RETRY, B_CSLOT, B_CMSG,
+  B_SLOT, B_IDX, B_SSLOT, B_SIDX, B_USLOT, B_SCNT, B_SSTART, B_LONG, B_TEMP, B_DUMP,
+  B_STATES, B_NAME1, B_COUNT_
+};
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+};
+
+struct Timing {
+  const char* name;
+  hipEvent_t a, b;
+};
+
+}  // namespace
+
+struct phip_handle {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::mutex mu;
+  std::string err;
+  u32 L = 0;
+  u64 cap = 0;
+  u64 max_load = 0;
+  u64* tags = nullptr;
+  Rec* recs = nullptr;
+  u8* arena = nullptr;
+  u64 arena_cap = 0;
+  u64* arena_cursor = nullptr;
+  u32* ctr = nullptr;        // device counters [16]
+  u32* ctr_host = nullptr;   // pinned mirror
+  u64 n_buckets = 0;
+  u64 tag_mask = ~0ull;
+  DevBuf buf[B_COUNT_];
+  bool timing = false;
+  std::vector<Timing> timings;
+  std::vector<Timing> event_pool;
+  size_t pool_used = 0;
+};
+
+namespace {
+
+int set_err(phip_handle* h, int code, const char* fmt, ...) {
+  char tmp[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(tmp, sizeof tmp, fmt, ap);
+  va_end(ap);
+  if (h) h->err = tmp;
+  return code;
+}
+
+#define HIPCHK(h, x)                                                                      \
+  do {                                                                                    \
+    hipError_t e_ = (x);                                                                  \
+    if (e_ != hipSuccess)                                                                 \
+      return set_err((h), PHIP_ERR_HIP, "%s failed: %s (%s:%d)", #x, hipGetErrorString(e_), \
+                     __FILE__, __LINE__);                                                 \
+  } while (0)
+
+template <class T>
+int ensure(phip_handle* h, BufId id, size_t count, T** out) {
+  size_t bytes = std::max<size_t>(count * sizeof(T), 64) + 64;  // +64: 8-byte over-read slack
+  DevBuf& b = h->buf[id];
+  if (b.cap < bytes) {
+    size_t want = std::max(bytes, b.cap * 3 / 2);
+    if (b.p) HIPCHK(h, hipFree(b.p));
+    b.p = nullptr;
+    b.cap = 0;
+    HIPCHK(h, hipMalloc(&b.p, want));
+    b.cap = want;
+  }
+  *out = (T*)b.p;
+  return PHIP_OK;
+}
+
+inline Table table(phip_handle* h) {
+  Table t;
+  t.tags = h->tags;
+  t.recs = h->recs;
+  t.arena = h->arena;
+  t.L = h->L;
+  t.tag_mask = h->tag_mask;
+  return t;
+}
+
+inline unsigned grid_for(u64 n, unsigned block = kBlock) {
+  return (unsigned)std::max<u64>(1, (n + block - 1) / block);
+}
+
+// Event-timed launch helper.
+struct Launch {
+  phip_handle* h;
+  const char* name;
+  Timing* t = nullptr;
+  Launch(phip_handle* h_, const char* n) : h(h_), name(n) {
+    if (!h->timing) return;
+    if (h->pool_used == h->event_pool.size()) {
+      Timing tm{n, nullptr, nullptr};
+      hipEventCreate(&tm.a);
+      hipEventCreate(&tm.b);
+      h->event_pool.push_back(tm);
+    }
+    t = &h->event_pool[h->pool_used++];
+    t->name = n;
+    hipEventRecord(t->a, h->stream);
+  }
+  ~Launch() {
+    if (t) {
+      hipEventRecord(t->b, h->stream);
+      h->timings.push_back(*t);
+    }
+  }
+};
+
+int read_ctr(phip_handle* h) {
+  HIPCHK(h, hipMemcpyAsync(h->ctr_host, h->ctr, 16 * sizeof(u32), hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  return PHIP_OK;
+}
+
+int reset_ctr(phip_handle* h) {
+  HIPCHK(h, hipMemsetAsync(h->ctr, 0, 16 * sizeof(u32), h->stream));
+  // ctr[5] = first short datagram index: start at "none".
+  HIPCHK(h, hipMemsetAsync(h->ctr + 5, 0xFF, sizeof(u32), h->stream));
+  return PHIP_OK;
+}
+
+int check_flags(phip_handle* h) {
+  if (h->ctr_host[8]) return set_err(h, PHIP_ERR_FULL, "hash table full (probe wrapped)");
+  if (h->ctr_host[7]) return set_err(h, PHIP_ERR_ARENA, "long-name arena exhausted");
+  return PHIP_OK;
+}
+
+void begin_call(phip_handle* h) {
+  h->err.clear();
+  hipSetDevice(h->device);
+  if (h->timing) {
+    h->timings.clear();
+    h->pool_used = 0;
+  }
+}
+
+// Copy a host array into a device staging buffer (or pass device pointers).
+template <class T>
+int stage(phip_handle* h, BufId id, const T* src, size_t count, bool dev, const T** out) {
+  if (!src) { *out = nullptr; return PHIP_OK; }
+  if (dev) { *out = src; return PHIP_OK; }
+  T* d;
+  int rc = ensure(h, id, count, &d);
+  if (rc) return rc;
+  if (count) HIPCHK(h, hipMemcpyAsync(d, src, count * sizeof(T), hipMemcpyHostToDevice, h->stream));
+  *out = d;
+  return PHIP_OK;
+}
+
+template <class T>
+int out_buf(phip_handle* h, BufId id, T* user, size_t count, bool dev, T** out) {
+  if (!user) { *out = nullptr; return PHIP_OK; }
+  if (dev) { *out = user; return PHIP_OK; }
+  return ensure(h, id, count, out);
+}
+
+template <class T>
+int copy_back(phip_handle* h, T* user, const T* dev_buf, size_t count, bool dev) {
+  if (!user || dev || !count) return PHIP_OK;
+  HIPCHK(h, hipMemcpyAsync(user, dev_buf, count * sizeof(T), hipMemcpyDeviceToHost, h->stream));
+  return PHIP_OK;
+}
+
+// ----------------------------------------------------------- inserts -----
+// Insert every name of `list` (all known to be absent) into the table.
+// Claimed slots are accumulated in B_CSLOT/B_CMSG; *n_claimed returns their
+// count (callers clear the NEW flag once done).
+template <class Src>
+int insert_names(phip_handle* h, Src src, u32* list, u32 nlist, const int64_t* now_arr, i64 now0,
+                 u32* n_claimed) {
+  u32 *cslot, *cmsg, *retry, *cur = list;
+  int rc;
+  if ((rc = ensure(h, B_CSLOT, nlist, &cslot)) || (rc = ensure(h, B_CMSG, nlist, &cmsg)) ||
+      (rc = ensure(h, B_RETRY, nlist, &retry)))
+    return rc;
+  u32 total = 0, ncur = nlist;
+  // Swap buffers between rounds: round k reads `cur`, writes retries to `nxt`.
+  u32* nxt = retry;
+  u32* spare = nullptr;
+  if ((rc = ensure(h, B_MISS2, nlist, &spare))) return rc;
+  for (int round = 0; ncur > 0; ++round) {
+    if (round > 64) return set_err(h, PHIP_ERR_INVALID, "insert did not converge");
+    if (h->n_buckets >= h->max_load)
+      return set_err(h, PHIP_ERR_FULL, "table load limit reached: %llu buckets of %llu allowed",
+                     (unsigned long long)h->n_buckets, (unsigned long long)h->max_load);
+    // ctr[3] is the running claimed count (cumulative), ctr[4] the retry count.
+    HIPCHK(h, hipMemsetAsync(h->ctr + 4, 0, sizeof(u32), h->stream));
+    {
+      Launch l(h, "k_claim");
+      k_claim<Src><<<grid_for(ncur), kBlock, 0, h->stream>>>(src, ncur, cur, table(h), cslot, cmsg,
+                                                              nxt, h->ctr);
+    }
+    HIPCHK(h, hipGetLastError());
+    if ((rc = read_ctr(h))) return rc;
+    if ((rc = check_flags(h))) return rc;
+    u32 claimed_total = h->ctr_host[3];
+    u32 fresh = claimed_total - total;
+    if (fresh) {
+      Launch l(h, "k_publish");
+      k_publish<Src><<<grid_for(fresh), kBlock, 0, h->stream>>>(
+          src, total, fresh, cslot, cmsg, h->recs, h->arena, h->arena_cap, h->arena_cursor, now_arr,
+          now0, h->ctr);
+    }
+    HIPCHK(h, hipGetLastError());
+    h->n_buckets += fresh;
+    total = claimed_total;
+    ncur = h->ctr_host[4];
+    // next round reads the retries
+    cur = nxt;
+    nxt = (nxt == retry) ? spare : retry;
+  }
+  *n_claimed = total;
+  return PHIP_OK;
+}
+
+int clear_new(phip_handle* h, u32 n_claimed) {
+  if (!n_claimed) return PHIP_OK;
+  u32* cslot = (u32*)h->buf[B_CSLOT].p;
+  Launch l(h, "k_clear_new");
+  k_clear_new<<<grid_for(n_claimed), kBlock, 0, h->stream>>>(cslot, n_claimed, h->recs);
+  HIPCHK(h, hipGetLastError());
+  return PHIP_OK;
+}
+
+// ------------------------------------------------------- fast receive ----
+template <class Src>
+int fast_receive(phip_handle* h, Src src, const uint64_t* a, const uint64_t* t, const int64_t* e,
+                 u32 n, i64 now,
+                 u8* status) {
+  u32* miss;
+  int rc;
+  if ((rc = ensure(h, B_MISS, n, &miss))) return rc;
+  {
+    Launch l(h, "k_receive_fast");
+    k_receive_fast<Src><<<grid_for(n), kBlock, 0, h->stream>>>(src, a, t, e, n, nullptr, table(h),
+                                                                status, miss, h->ctr, 0);
+  }
+  HIPCHK(h, hipGetLastError());
+  if ((rc = read_ctr(h))) return rc;
+  if ((rc = check_flags(h))) return rc;
+  u32 nmiss = h->ctr_host[2];
+  if (nmiss == 0) return PHIP_OK;
+  u32 n_claimed = 0;
+  if ((rc = insert_names(h, src, miss, nmiss, nullptr, now, &n_claimed))) return rc;
+  // Merge the missed messages into their (now existing) buckets.
+  HIPCHK(h, hipMemsetAsync(h->ctr + 2, 0, sizeof(u32), h->stream));
+  u32* miss2;
+  if ((rc = ensure(h, B_MISS2, nmiss, &miss2))) return rc;
+  {
+    Launch l(h, "k_receive_fast_miss");
+    k_receive_fast<Src><<<grid_for(nmiss), kBlock, 0, h->stream>>>(
+        src, a, t, e, nmiss, miss, table(h), status, miss2, h->ctr, 1);
+  }
+  HIPCHK(h, hipGetLastError());
+  {
+    Launch l(h, "k_mark_created");
+    k_mark_created<Src><<<grid_for(nmiss), kBlock, 0, h->stream>>>(src, nmiss, miss, table(h),
+                                                                    status);
+  }
+  HIPCHK(h, hipGetLastError());
+  if ((rc = read_ctr(h))) return rc;
+  if (h->ctr_host[2]) return set_err(h, PHIP_ERR_INVALID, "internal: %u names missing after insert", h->ctr_host[2]);
+  return clear_new(h, n_claimed);
+}
+
+// ------------------------------------------------------------ ordered ----
+__global__ void k_iota(u32* p, u32 n) {
+  u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) p[i] = i;
+}
+
+template <class Src>
+int resolve_all(phip_handle* h, Src src, u32 n, const int64_t* now_arr, i64 now0, u32** slot_out,
+                u32* n_claimed) {
+  u32 *slot, *miss;
+  int rc;
+  if ((rc = ensure(h, B_SLOT, n, &slot)) || (rc = ensure(h, B_MISS, n, &miss))) return rc;
+  if ((rc = reset_ctr(h))) return rc;
+  {
+    Launch l(h, "k_resolve");
+    k_resolve<Src><<<grid_for(n), kBlock, 0, h->stream>>>(src, n, nullptr, table(h), slot, miss,
+                                                           h->ctr);
+  }
+  HIPCHK(h, hipGetLastError());
+  if ((rc = read_ctr(h))) return rc;
+  if ((rc = check_flags(h))) return rc;
+  u32 nmiss = h->ctr_host[2];
+  *n_claimed = 0;
+  if (nmiss) {
+    if ((rc = insert_names(h, src, miss, nmiss, now_arr, now0, n_claimed))) return rc;
+    HIPCHK(h, hipMemsetAsync(h->ctr + 2, 0, sizeof(u32), h->stream));
+    Launch l(h, "k_resolve_miss");
+    k_resolve<Src><<<grid_for(nmiss), kBlock, 0, h->stream>>>(src, nmiss, miss, table(h), slot,
+                                                               nullptr, h->ctr);
+    HIPCHK(h, hipGetLastError());
+  }
+  *slot_out = slot;
+  return PHIP_OK;
+}
+
+// Apply a mixed op stream in seq order.  The NEW flag of created buckets is
+// consumed (cleared) by the fold itself.
+template <class Src>
+int ordered(phip_handle* h, Src src, u32 n, const OpView& ov, const OutView& ow) {
+  if (n == 0) return PHIP_OK;
+  int rc;
+  u32* slot;
+  u32 n_claimed = 0;
+  if ((rc = resolve_all(h, src, n, ov.now, ov.now0, &slot, &n_claimed))) return rc;
+  u32 *idx, *sslot, *sidx, *uslot, *scnt, *sstart, *lng;
+  if ((rc = ensure(h, B_IDX, n, &idx)) || (rc = ensure(h, B_SSLOT, n, &sslot)) ||
+      (rc = ensure(h, B_SIDX, n, &sidx)) || (rc = ensure(h, B_USLOT, n, &uslot)) ||
+      (rc = ensure(h, B_SCNT, n, &scnt)) || (rc = ensure(h, B_SSTART, n, &sstart)) ||
+      (rc = ensure(h, B_LONG, n, &lng)))
+    return rc;
+  {
+    Launch l(h, "k_iota");
+    k_iota<<<grid_for(n), kBlock, 0, h->stream>>>(idx, n);
+  }
+  // Stable radix sort of (slot, seq) pairs: per-bucket arrival order kept.
+  size_t tb = 0;
+  HIPCHK(h, rocprim::radix_sort_pairs(nullptr, tb, slot, sslot, idx, sidx, n, 0u, h->L, h->stream));
+  size_t tb2 = 0;
+  HIPCHK(h, rocprim::run_length_encode(nullptr, tb2, sslot, n, uslot, scnt, h->ctr + 6, h->stream));
+  size_t tb3 = 0;
+  HIPCHK(h, rocprim::exclusive_scan(nullptr, tb3, scnt, sstart, 0u, (size_t)n, rocprim::plus<u32>(),
+                                    h->stream));
+  u8* temp;
+  if ((rc = ensure(h, B_TEMP, std::max(tb, std::max(tb2, tb3)), &temp))) return rc;
+  {
+    Launch l(h, "radix_sort_pairs");
+    HIPCHK(h, rocprim::radix_sort_pairs(temp, tb, slot, sslot, idx, sidx, n, 0u, h->L, h->stream));
+  }
+  {
+    Launch l(h, "run_length_encode");
+    HIPCHK(h, rocprim::run_length_encode(temp, tb2, sslot, n, uslot, scnt, h->ctr + 6, h->stream));
+  }
+  if ((rc = read_ctr(h))) return rc;
+  u32 nseg = h->ctr_host[6];
+  {
+    Launch l(h, "exclusive_scan");
+    HIPCHK(h, rocprim::exclusive_scan(temp, tb3, scnt, sstart, 0u, (size_t)nseg, rocprim::plus<u32>(),
+                                      h->stream));
+  }
+  HIPCHK(h, hipMemsetAsync(h->ctr + 6, 0, sizeof(u32), h->stream));
+  {
+    Launch l(h, "k_fold_thread");
+    k_fold_thread<<<grid_for(nseg), kBlock, 0, h->stream>>>(uslot, sstart, scnt, nseg, sidx, h->recs,
+                                                             ov, ow, lng, h->ctr);
+  }
+  HIPCHK(h, hipGetLastError());
+  if ((rc = read_ctr(h))) return rc;
+  u32 nlong = h->ctr_host[6];
+  if (nlong) {
+    Launch l(h, "k_fold_wave");
+    k_fold_wave<<<nlong, 64, 0, h->stream>>>(lng, nlong, uslot, sstart, scnt, sidx, h->recs, ov, ow);
+    HIPCHK(h, hipGetLastError());
+  }
+  (void)n_claimed;  // NEW flags cleared by store_state in the folds
+  return PHIP_OK;
+}
+
+int stage_names(phip_handle* h, const uint8_t* names, const uint32_t* offs, u32 n, bool dev,
+                NamesOffs* src) {
+  const u32* d_offs;
+  int rc;
+  if ((rc = stage(h, B_OFFS, offs, (size_t)n + 1, dev, &d_offs))) return rc;
+  const u8* d_names;
+  size_t nb = 0;
+  if (!dev) nb = offs[n];
+  if ((rc = stage(h, B_NAMES, names, nb, dev, &d_names))) return rc;
+  if (!dev && nb == 0) {
+    u8* p;
+    if ((rc = ensure(h, B_NAMES, 1, &p))) return rc;
+    d_names = p;
+  }
+  src->blob = d_names;
+  src->offs = d_offs;
+  return PHIP_OK;
+}
+
+bool names_ok(const uint32_t* offs, u32 n) {
+  for (u32 i = 0; i < n; ++i) {
+    if (offs[i + 1] < offs[i]) return false;
+    if (offs[i + 1] - offs[i] > PHIP_MAX_NAME_LEN) return false;
+  }
+  return true;
+}
+
+int outputs(phip_handle* h, const phip_results* res, u32 n, bool dev, OutView* ow) {
+  int rc;
+  phip_results r{};
+  if (res) r = *res;
+  if ((rc = out_buf(h, B_STATUS, r.status, n, dev, &ow->status)) ||
+      (rc = out_buf(h, B_REM, r.remaining, n, dev, &ow->remaining)) ||
+      (rc = out_buf(h, B_HAVE, r.have, n, dev, &ow->have)) ||
+      (rc = out_buf(h, B_REPLY, r.reply, n, dev, &ow->reply)))
+    return rc;
+  return PHIP_OK;
+}
+
+int copy_outputs(phip_handle* h, const phip_results* res, u32 n, bool dev, const OutView& ow) {
+  if (!res || dev) {
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    return PHIP_OK;
+  }
+  int rc;
+  if ((rc = copy_back(h, res->status, ow.status, n, dev)) ||
+      (rc = copy_back(h, res->remaining, ow.remaining, n, dev)) ||
+      (rc = copy_back(h, res->have, ow.have, n, dev)) ||
+      (rc = copy_back(h, res->reply, ow.reply, n, dev)))
+    return rc;
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  return PHIP_OK;
+}
+
+// Receive-mode batch (decoded): fast path unless it holds an incast or -0.0.
+template <class Src>
+int receive_decoded(phip_handle* h, Src src, const uint64_t* a, const uint64_t* t,
+                    const int64_t* e, u32 n,
+                    i64 now, const OutView& ow, bool classified) {
+  int rc;
+  if (!classified) {
+    if ((rc = reset_ctr(h))) return rc;
+    Launch l(h, "k_classify");
+    k_classify<<<grid_for(n), kBlock, 0, h->stream>>>(a, t, e, n, h->ctr);
+    HIPCHK(h, hipGetLastError());
+  }
+  if ((rc = read_ctr(h))) return rc;
+  bool dirty = h->ctr_host[0] || h->ctr_host[1];
+  if (!dirty) {
+    if ((rc = reset_ctr(h))) return rc;
+    return fast_receive(h, src, a, t, e, n, now, ow.status);
+  }
+  OpView ov{};
+  ov.kind = nullptr; ov.kind0 = PHIP_OP_RECEIVE;
+  ov.now = nullptr; ov.now0 = now;
+  ov.a = a; ov.t = t; ov.e = e;
+  return ordered(h, src, n, ov, ow);
+}
+
+}  // namespace
+
+// ===================================================================== ABI
+extern "C" {
+
+int phip_abi_version(void) { return PHIP_ABI_VERSION; }
+
+int phip_open(const phip_config* cfg, phip_handle** out) {
+  if (!cfg || !out) return PHIP_ERR_INVALID;
+  *out = nullptr;
+  if (cfg->log2_slots < 4 || cfg->log2_slots > 31) return PHIP_ERR_INVALID;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return PHIP_ERR_NO_DEVICE;
+  if (cfg->device < 0 || cfg->device >= ndev) return PHIP_ERR_NO_DEVICE;
+  phip_handle* h = new phip_handle;
+  h->device = cfg->device;
+  h->L = cfg->log2_slots;
+  h->cap = 1ull << h->L;
+  u32 pct = cfg->max_load_pct ? std::min<u32>(cfg->max_load_pct, 95) : 90;
+  h->max_load = h->cap * pct / 100;
+  h->arena_cap = cfg->arena_bytes ? cfg->arena_bytes : (1ull << 20);
+  if (cfg->debug_tag_bits && cfg->debug_tag_bits < 64) h->tag_mask = (1ull << cfg->debug_tag_bits) - 1;
+  auto fail = [&](hipError_t e) {
+    phip_close(h);
+    (void)e;
+    return PHIP_ERR_HIP;
+  };
+  hipError_t e;
+  if ((e = hipSetDevice(h->device)) != hipSuccess) return fail(e);
+  if ((e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking)) != hipSuccess) return fail(e);
+  if ((e = hipMalloc(&h->tags, h->cap * sizeof(u64))) != hipSuccess) return fail(e);
+  if ((e = hipMalloc(&h->recs, h->cap * sizeof(Rec))) != hipSuccess) return fail(e);
+  if ((e = hipMalloc(&h->arena, h->arena_cap + 64)) != hipSuccess) return fail(e);
+  if ((e = hipMalloc(&h->arena_cursor, 64)) != hipSuccess) return fail(e);
+  if ((e = hipMalloc(&h->ctr, 64)) != hipSuccess) return fail(e);
+  if ((e = hipHostMalloc(&h->ctr_host, 64, 0)) != hipSuccess) return fail(e);
+  if ((e = hipMemsetAsync(h->tags, 0, h->cap * sizeof(u64), h->stream)) != hipSuccess) return fail(e);
+  if ((e = hipMemsetAsync(h->recs, 0, h->cap * sizeof(Rec), h->stream)) != hipSuccess) return fail(e);
+  if ((e = hipMemsetAsync(h->arena_cursor, 0, 64, h->stream)) != hipSuccess) return fail(e);
+  if ((e = hipMemsetAsync(h->ctr, 0, 64, h->stream)) != hipSuccess) return fail(e);
+  if ((e = hipStreamSynchronize(h->stream)) != hipSuccess) return fail(e);
+  *out = h;
+  return PHIP_OK;
+}
+
+void phip_close(phip_handle* h) {
+  if (!h) return;
+  hipSetDevice(h->device);
+  if (h->stream) hipStreamSynchronize(h->stream);
+  for (auto& b : h->buf)
+    if (b.p) hipFree(b.p);
+  for (auto& t : h->event_pool) {
+    hipEventDestroy(t.a);
+    hipEventDestroy(t.b);
+  }
+  if (h->tags) hipFree(h->tags);
+  if (h->recs) hipFree(h->recs);
+  if (h->arena) hipFree(h->arena);
+  if (h->arena_cursor) hipFree(h->arena_cursor);
+  if (h->ctr) hipFree(h->ctr);
+  if (h->ctr_host) hipHostFree(h->ctr_host);
+  if (h->stream) hipStreamDestroy(h->stream);
+  delete h;
+}
+
+const char* phip_last_error(const phip_handle* h) { return h ? h->err.c_str() : "null handle"; }
+
+int phip_flush(phip_handle* h) {
+  if (!h) return PHIP_ERR_INVALID;
+  std::lock_guard<std::mutex> g(h->mu);
+  hipSetDevice(h->device);
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  return PHIP_OK;
+}
+
+uint64_t phip_len(phip_handle* h) { return h ? h->n_buckets : 0; }
+uint64_t phip_capacity(phip_handle* h) { return h ? h->cap : 0; }
+
+int phip_seed(phip_handle* h, const uint8_t* names, const uint32_t* name_offs, uint32_t n,
+              const phip_state* states, uint32_t flags) {
+  if (!h || (n && (!names || !name_offs || !states))) return PHIP_ERR_INVALID;
+  std::lock_guard<std::mutex> g(h->mu);
+  begin_call(h);
+  if (n == 0) return PHIP_OK;
+  bool dev = flags & PHIP_DEVICE_PTRS;
+  if (!dev && !names_ok(name_offs, n)) return set_err(h, PHIP_ERR_NAME_TOO_LARGE, "name > 231 bytes");
+  int rc;
+  NamesOffs src;
+  if ((rc = stage_names(h, names, name_offs, n, dev, &src))) return rc;
+  const phip_state* d_st;
+  if ((rc = stage(h, B_STATES, states, n, dev, &d_st))) return rc;
+  u32* slot;
+  u32 n_claimed = 0;
+  if ((rc = resolve_all(h, src, n, nullptr, 0, &slot, &n_claimed))) return rc;
+  // aux is the per-slot "last writer" scratch: clear, pick the last entry of
+  // each name, apply it, clear again.
+  k_seed_finish<<<grid_for(n), kBlock, 0, h->stream>>>(slot, n, h->recs);
+  k_seed_pick<<<grid_for(n), kBlock, 0, h->stream>>>(slot, n, h->recs);
+  k_seed_apply<<<grid_for(n), kBlock, 0, h->stream>>>(slot, n, d_st, h->recs);
+  k_seed_finish<<<grid_for(n), kBlock, 0, h->stream>>>(slot, n, h->recs);
+  HIPCHK(h, hipGetLastError());
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  return PHIP_OK;
+}
+
+int phip_get(phip_handle* h, const uint8_t* name, uint32_t len, phip_state* out) {
+  if (!h || (!name && len) || !out) return PHIP_ERR_INVALID;
+  if (len > PHIP_MAX_NAME_LEN) return 0;
+  std::lock_guard<std::mutex> g(h->mu);
+  begin_call(h);
+  u8* d_name;
+  Rec* d_rec;
+  int rc;
+  if ((rc = ensure(h, B_NAME1, 256 + sizeof(Rec) + 16, &d_name))) return rc;
+  d_rec = (Rec*)(d_name + 256);
+  int* d_found = (int*)(d_name + 256 + sizeof(Rec));
+  if (len) HIPCHK(h, hipMemcpyAsync(d_name, name, len, hipMemcpyHostToDevice, h->stream));
+  k_get_one<<<1, 64, 0, h->stream>>>(d_name, len, table(h), d_rec, d_found);
+  HIPCHK(h, hipGetLastError());
+  Rec r;
+  int found = 0;
+  HIPCHK(h, hipMemcpyAsync(&r, d_rec, sizeof(Rec), hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(h, hipMemcpyAsync(&found, d_found, sizeof(int), hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  if (!found) return 0;
+  out->added = dec_f64(r.added);
+  out->taken = dec_f64(r.taken);
+  out->elapsed = r.elapsed;
+  out->created = r.created;
+  return 1;
+}
+
+int phip_dump(phip_handle* h, uint8_t* names, uint64_t names_cap, uint64_t* name_offs,
+              phip_state* states, uint64_t max_n, uint64_t* n_out, uint64_t* names_bytes_out) {
+  if (!h) return PHIP_ERR_INVALID;
+  std::lock_guard<std::mutex> g(h->mu);
+  begin_call(h);
+  int rc;
+  u32* list;
+  if ((rc = ensure(h, B_DUMP, h->n_buckets + 1, &list))) return rc;
+  if ((rc = reset_ctr(h))) return rc;
+  k_dump_collect<<<grid_for(h->cap), kBlock, 0, h->stream>>>(h->tags, h->cap, list, h->ctr);
+  HIPCHK(h, hipGetLastError());
+  if ((rc = read_ctr(h))) return rc;
+  u32 n = h->ctr_host[2];
+  Rec* d_out;
+  if ((rc = ensure(h, B_TEMP, (size_t)n * sizeof(Rec), (u8**)&d_out))) return rc;
+  k_dump_gather<<<grid_for(n), kBlock, 0, h->stream>>>(list, n, h->recs, d_out);
+  HIPCHK(h, hipGetLastError());
+  std::vector<Rec> recs(n);
+  if (n) HIPCHK(h, hipMemcpyAsync(recs.data(), d_out, n * sizeof(Rec), hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  // Long names come from the arena.
+  std::vector<u8> arena;
+  u64 cursor = 0;
+  HIPCHK(h, hipMemcpy(&cursor, h->arena_cursor, 8, hipMemcpyDeviceToHost));
+  cursor = std::min(cursor, h->arena_cap);
+  if (cursor) {
+    arena.resize(cursor);
+    HIPCHK(h, hipMemcpy(arena.data(), h->arena, cursor, hipMemcpyDeviceToHost));
+  }
+  u64 total = 0;
+  for (auto& r : recs) total += r.name[0] & 0xFF;
+  if (n_out) *n_out = n;
+  if (names_bytes_out) *names_bytes_out = total;
+  if (!names) return PHIP_OK;
+  if (total > names_cap || n > max_n || !name_offs || !states)
+    return set_err(h, PHIP_ERR_INVALID, "dump buffers too small");
+  u64 o = 0;
+  for (u32 k = 0; k < n; ++k) {
+    const Rec& r = recs[k];
+    u32 len = r.name[0] & 0xFF;
+    name_offs[k] = o;
+    if (len <= 23) {
+      for (u32 j = 0; j < len; ++j) names[o + j] = (u8)(r.name[(j + 1) >> 3] >> (((j + 1) & 7) * 8));
+    } else {
+      u64 aoff = r.name[0] >> 32;
+      if (aoff + len <= arena.size()) std::memcpy(names + o, arena.data() + aoff, len);
+    }
+    o += len;
+    states[k].added = dec_f64(r.added);
+    states[k].taken = dec_f64(r.taken);
+    states[k].elapsed = r.elapsed;
+    states[k].created = r.created;
+  }
+  name_offs[n] = o;
+  return PHIP_OK;
+}
+
+int phip_receive_soa(phip_handle* h, const phip_msgs* m, int64_t now, const phip_results* res,
+                     uint32_t flags) {
+  if (!h || !m) return PHIP_ERR_INVALID;
+  std::lock_guard<std::mutex> g(h->mu);
+  begin_call(h);
+  u32 n = m->n;
+  if (n == 0) return PHIP_OK;
+  if (!m->names || !m->name_offs || !m->added || !m->taken || !m->elapsed) return PHIP_ERR_INVALID;
+  bool dev = flags & PHIP_DEVICE_PTRS;
+  if (!dev && !names_ok(m->name_offs, n)) return set_err(h, PHIP_ERR_NAME_TOO_LARGE, "name > 231 bytes");
+  int rc;
+  NamesOffs src;
+  const uint64_t *a, *t;
+  const int64_t* e;
+  OutView ow{};
+  if ((rc = stage_names(h, m->names, m->name_offs, n, dev, &src)) ||
+      (rc = stage(h, B_A, m->added, n, dev, &a)) || (rc = stage(h, B_T, m->taken, n, dev, &t)) ||
+      (rc = stage(h, B_E, m->elapsed, n, dev, &e)) || (rc = outputs(h, res, n, dev, &ow)))
+    return rc;
+  if ((rc = receive_decoded(h, src, a, t, e, n, now, ow, false))) return rc;
+  return copy_outputs(h, res, n, dev, ow);
+}
+
+int phip_receive_datagrams(phip_handle* h, const uint8_t* bytes, const uint64_t* offs, uint32_t n,
+                           int64_t now, const phip_results* res, uint32_t* stop_index,
+                           uint32_t flags) {
+  if (!h || (n && (!bytes || !offs))) return PHIP_ERR_INVALID;
+  std::lock_guard<std::mutex> g(h->mu);
+  begin_call(h);
+  if (stop_index) *stop_index = n;
+  if (n == 0) return PHIP_OK;
+  bool dev = flags & PHIP_DEVICE_PTRS;
+  int rc;
+  const uint64_t* d_offs;
+  const u8* d_bytes;
+  if ((rc = stage(h, B_DOFFS, offs, (size_t)n + 1, dev, &d_offs))) return rc;
+  size_t nb = dev ? 0 : offs[n];
+  if ((rc = stage(h, B_BYTES, bytes, nb, dev, &d_bytes))) return rc;
+  uint64_t *a, *t, *no;
+  int64_t* e;
+  u8* nl;
+  if ((rc = ensure(h, B_DA, n, &a)) || (rc = ensure(h, B_DT, n, &t)) || (rc = ensure(h, B_DE, n, &e)) ||
+      (rc = ensure(h, B_NOFF, n, &no)) || (rc = ensure(h, B_NLEN, n, &nl)))
+    return rc;
+  OutView ow{};
+  if ((rc = outputs(h, res, n, dev, &ow))) return rc;
+  if ((rc = reset_ctr(h))) return rc;
+  {
+    Launch l(h, "k_decode");
+    k_decode<<<grid_for(n), kBlock, 0, h->stream>>>(d_bytes, d_offs, n, a, t, e, no, nl, h->ctr);
+    HIPCHK(h, hipGetLastError());
+  }
+  if ((rc = read_ctr(h))) return rc;
+  u32 stop = std::min<u32>(h->ctr_host[5], n);
+  // Statuses of the short datagram and everything after it (the Go loop exits).
+  if (ow.status && stop < n) {
+    HIPCHK(h, hipMemsetAsync(ow.status + stop, PHIP_ST_NOT_PROCESSED, n - stop, h->stream));
+    HIPCHK(h, hipMemsetAsync(ow.status + stop, PHIP_ST_SHORT, 1, h->stream));
+  }
+  NamesPairs src{d_bytes, no, nl};
+  if (stop > 0 && (rc = receive_decoded(h, src, a, t, e, stop, now, ow, true))) return rc;
+  if ((rc = copy_outputs(h, res, n, dev, ow))) return rc;
+  if (dev) HIPCHK(h, hipStreamSynchronize(h->stream));
+  if (stop_index) *stop_index = stop;
+  if (stop < n) return set_err(h, PHIP_ERR_SHORT_BUFFER, "short buffer at datagram %u", stop);
+  return PHIP_OK;
+}
+
+int phip_upsert_soa(phip_handle* h, const phip_msgs* m, int64_t now, const phip_results* res,
+                    uint32_t flags) {
+  if (!h || !m) return PHIP_ERR_INVALID;
+  std::lock_guard<std::mutex> g(h->mu);
+  begin_call(h);
+  u32 n = m->n;
+  if (n == 0) return PHIP_OK;
+  if (!m->names || !m->name_offs || !m->added || !m->taken || !m->elapsed) return PHIP_ERR_INVALID;
+  bool dev = flags & PHIP_DEVICE_PTRS;
+  if (!dev && !names_ok(m->name_offs, n)) return set_err(h, PHIP_ERR_NAME_TOO_LARGE, "name > 231 bytes");
+  int rc;
+  NamesOffs src;
+  const uint64_t *a, *t;
+  const int64_t* e;
+  OutView ow{};
+  if ((rc = stage_names(h, m->names, m->name_offs, n, dev, &src)) ||
+      (rc = stage(h, B_A, m->added, n, dev, &a)) || (rc = stage(h, B_T, m->taken, n, dev, &t)) ||
+      (rc = stage(h, B_E, m->elapsed, n, dev, &e)) || (rc = outputs(h, res, n, dev, &ow)))
+    return rc;
+  OpView ov{};
+  ov.kind0 = PHIP_OP_UPSERT;
+  ov.now0 = now;
+  ov.a = a; ov.t = t; ov.e = e;
+  if ((rc = ordered(h, src, n, ov, ow))) return rc;
+  return copy_outputs(h, res, n, dev, ow);
+}
+
+int phip_apply_mixed(phip_handle* h, const phip_ops* ops, const phip_results* res, uint32_t flags) {
+  if (!h || !ops) return PHIP_ERR_INVALID;
+  std::lock_guard<std::mutex> g(h->mu);
+  begin_call(h);
+  u32 n = ops->n;
+  if (n == 0) return PHIP_OK;
+  if (!ops->kind || !ops->names || !ops->name_offs || !ops->now) return PHIP_ERR_INVALID;
+  bool dev = flags & PHIP_DEVICE_PTRS;
+  if (!dev && !names_ok(ops->name_offs, n)) return set_err(h, PHIP_ERR_NAME_TOO_LARGE, "name > 231 bytes");
+  if (!dev) {
+    bool need_take = false, need_state = false;
+    for (u32 i = 0; i < n; ++i) {
+      if (ops->kind[i] > PHIP_OP_UPSERT) return set_err(h, PHIP_ERR_INVALID, "bad op kind at %u", i);
+      if (ops->kind[i] == PHIP_OP_TAKE) need_take = true; else need_state = true;
+    }
+    if (need_take && (!ops->freq || !ops->per || !ops->count)) return PHIP_ERR_INVALID;
+    if (need_state && (!ops->added || !ops->taken || !ops->elapsed)) return PHIP_ERR_INVALID;
+  }
+  int rc;
+  NamesOffs src;
+  OpView ov{};
+  const u8* kind;
+  OutView ow{};
+  if ((rc = stage_names(h, ops->names, ops->name_offs, n, dev, &src)) ||
+      (rc = stage(h, B_KIND, ops->kind, n, dev, &kind)) ||
+      (rc = stage(h, B_NOW, ops->now, n, dev, &ov.now)) ||
+      (rc = stage(h, B_FREQ, ops->freq, n, dev, &ov.freq)) ||
+      (rc = stage(h, B_PER, ops->per, n, dev, &ov.per)) ||
+      (rc = stage(h, B_COUNT, ops->count, n, dev, &ov.count)) ||
+      (rc = stage(h, B_A, ops->added, n, dev, &ov.a)) ||
+      (rc = stage(h, B_T, ops->taken, n, dev, &ov.t)) ||
+      (rc = stage(h, B_E, ops->elapsed, n, dev, &ov.e)) || (rc = outputs(h, res, n, dev, &ow)))
+    return rc;
+  ov.kind = kind;
+  if ((rc = ordered(h, src, n, ov, ow))) return rc;
+  return copy_outputs(h, res, n, dev, ow);
+}
+
+int phip_take(phip_handle* h, const uint8_t* names, const uint32_t* name_offs, uint32_t n,
+              const int64_t* now, const int64_t* freq, const int64_t* per, const uint64_t* count,
+              uint64_t* remaining_out, uint8_t* ok_out, uint32_t flags) {
+  if (!h) return PHIP_ERR_INVALID;
+  if (n == 0) return PHIP_OK;
+  if (flags & PHIP_DEVICE_PTRS) return set_err(h, PHIP_ERR_INVALID, "phip_take: use phip_apply_mixed for device pointers");
+  std::vector<u8> kind(n, PHIP_OP_TAKE), st(n);
+  phip_ops ops{};
+  ops.n = n;
+  ops.kind = kind.data();
+  ops.names = names;
+  ops.name_offs = name_offs;
+  ops.now = now;
+  ops.freq = freq;
+  ops.per = per;
+  ops.count = count;
+  phip_results res{};
+  res.status = st.data();
+  res.remaining = remaining_out;
+  int rc = phip_apply_mixed(h, &ops, &res, flags);
+  if (rc) return rc;
+  if (ok_out)
+    for (u32 i = 0; i < n; ++i) ok_out[i] = (st[i] & 0x7F) == PHIP_ST_TAKE_OK;
+  return PHIP_OK;
+}
+
+int phip_last_timings(phip_handle* h, const char** names, float* ms, int max) {
+  if (!h) return 0;
+  std::lock_guard<std::mutex> g(h->mu);
+  hipSetDevice(h->device);
+  hipStreamSynchronize(h->stream);
+  int k = 0;
+  for (auto& t : h->timings) {
+    if (k >= max) break;
+    float v = 0;
+    hipEventElapsedTime(&v, t.a, t.b);
+    if (names) names[k] = t.name;
+    if (ms) ms[k] = v;
+    ++k;
+  }
+  return k;
+}
+
+void phip_set_timing(phip_handle* h, int on) {
+  if (h) h->timing = on != 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,561 @@
+// HIP kernels of libpatrolhip (gfx950).  Host orchestration: phip_engine.hip.
+//
+// Table: tags[2^L] (u64 FNV-1a tag, 0 = empty) + recs[2^L] (64-byte Rec).
+// Home slot = top L bits of tag * 2^64/phi (Fibonacci hashing), linear probing.
+#pragma once
+#include "phip_device.hpp"
+
+namespace phip {
+
+constexpr int kBlock = 256;
+
+// ---------------------------------------------------------- name sources --
+// Decoded messages: names[offs[i] .. offs[i+1]).
+struct NamesOffs {
+  const u8* blob;
+  const u32* offs;
+  __device__ inline void get(u32 i, u64& off, u32& len) const {
+    u32 a = offs[i], b = offs[i + 1];
+    off = a;
+    len = b - a;
+  }
+};
+// Raw datagrams after decode: name at (off[i], len[i]) inside the datagram blob.
+struct NamesPairs {
+  const u8* blob;
+  const uint64_t* off;
+  const u8* len;
+  __device__ inline void get(u32 i, u64& o, u32& l) const {
+    o = off[i];
+    l = len[i];
+  }
+};
+
+// Wave-aggregated append: returns this lane's position in `list`.
+__device__ inline u32 wave_append(u32* counter, bool pred) {
+  u64 mask = __ballot(pred);
+  if (!pred) return 0;
+  u32 lane = __lane_id();
+  u32 leader = __ffsll((long long)mask) - 1;
+  u32 rank = __popcll(mask & ((1ull << lane) - 1));
+  u32 base = 0;
+  if (lane == leader) base = atomicAdd(counter, (u32)__popcll(mask));
+  base = __shfl(base, leader);
+  return base + rank;
+}
+
+// Full-name equality for a candidate record (names > 23 bytes live in the arena).
+__device__ inline bool name_equal(const Rec& r, const Name& nm, const u8* src, const u8* arena) {
+  if ((r.name[0] & 0xFFu) != (nm.w0 & 0xFFu)) return false;
+  if (nm.len <= 23) return r.name[0] == nm.w0 && r.name[1] == nm.w1 && r.name[2] == nm.w2;
+  if (r.name[1] != nm.w1 || r.name[2] != nm.w2) return false;
+  u64 aoff = r.name[0] >> 32;
+  for (u32 k = 16; k < nm.len; ++k)
+    if (arena[aoff + k] != src[nm.off + k]) return false;
+  return true;
+}
+
+enum ProbeResult : int { kFound = 0, kMiss = 1, kPending = 2, kFull = 3 };
+
+// The device table, passed to kernels by value.
+struct Table {
+  u64* tags;
+  Rec* recs;
+  const u8* arena;
+  u32 L;
+  u64 tag_mask;   // all ones; narrower only in collision tests (phip_config.debug_tag_bits)
+  __device__ inline u64 tag(u64 h) const { return tag_of(h & tag_mask); }
+  __device__ inline u32 home(u64 tag) const {
+    return (u32)((tag * 0x9E3779B97F4A7C15ull) >> (64 - L));
+  }
+  __device__ inline u32 mask() const { return (u32)((1ull << L) - 1); }
+};
+
+// Look the name up.  kFound: *slot = its slot.  kMiss: not present.
+// kPending: a same-tag slot is claimed but not yet published (insert rounds).
+__device__ inline int probe(const Table& T, const Name& nm, const u8* src, u32* slot) {
+  const u64 tag = T.tag(nm.h);
+  const u32 mask = T.mask();
+  u32 s = T.home(tag);
+  for (u32 k = 0; k <= mask; ++k) {
+    u64 t = T.tags[s];
+    if (t == 0) return kMiss;
+    if (t == tag) {
+      const Rec& r = T.recs[s];
+      if (!(r.flags & kRecPublished)) return kPending;
+      if (name_equal(r, nm, src, T.arena)) { *slot = s; return kFound; }
+    }
+    s = (s + 1) & mask;
+  }
+  return kFull;
+}
+
+// ----------------------------------------------------------- classify ----
+// Batch routing: any incast (IsZero remote, repo.go:78) or -0.0 replica
+// field sends the batch to the ordered path.
+__global__ void k_classify(const uint64_t* __restrict__ a, const uint64_t* __restrict__ t,
+                           const int64_t* __restrict__ e, u32 n, u32* ctr) {
+  u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+  bool inc = false, nz = false;
+  if (i < n) {
+    u64 ab = a[i], tb = t[i];
+    i64 eb = e[i];
+    inc = state_is_zero(ab, tb, eb);
+    nz = !inc && (ab == kSign || tb == kSign);
+  }
+  u64 mi = __ballot(inc), mn = __ballot(nz);
+  if (__lane_id() == 0) {
+    if (mi) atomicAdd(&ctr[0], (u32)__popcll(mi));
+    if (mn) atomicAdd(&ctr[1], (u32)__popcll(mn));
+  }
+}
+
+// ------------------------------------------------------- fast receive ----
+// The batched Receive loop (repo.go:54-92) for a batch with no incast and no
+// -0.0: GetBucket(name) + Merge(&remote) for every message.  The merge is a
+// read-then-atomicMax on E-encoded fields: state only grows, so a stale read
+// can only cause a redundant atomic, never a lost update, and once a hot
+// bucket has converged its messages are pure L2-hit reads.
+// Misses are appended to `miss` (insert pipeline, then this kernel again on
+// the miss list with `track_new`).
+template <class Src>
+__global__ __launch_bounds__(kBlock) void k_receive_fast(
+    Src src, const uint64_t* __restrict__ ma, const uint64_t* __restrict__ mt,
+    const int64_t* __restrict__ me,
+    u32 n, const u32* __restrict__ list, Table T, u8* __restrict__ status, u32* miss, u32* ctr,
+    int track_new) {
+  u32 tid = blockIdx.x * blockDim.x + threadIdx.x;
+  bool missed = false;
+  u32 i = 0;
+  if (tid < n) {
+    i = list ? list[tid] : tid;
+    u64 off; u32 len;
+    src.get(i, off, len);
+    Name nm;
+    load_name(src.blob, off, len, nm);
+    u64 ab = ma[i], tb = mt[i];
+    i64 eb = me[i];
+    u32 s;
+    int pr = probe(T, nm, src.blob, &s);
+    if (pr == kFound) {
+      Rec* r = &T.recs[s];
+      u64 ea = enc_replica(ab), et = enc_replica(tb);
+      u64 ca = r->added, ct = r->taken;
+      i64 ce = r->elapsed;
+      if (ea > ca) atomicMax(&r->added, ea);
+      if (et > ct) atomicMax(&r->taken, et);
+      if (eb > ce) atomicMax(&r->elapsed, eb);
+      if (track_new && (r->flags & kRecNew)) atomicMin(&r->aux, i);
+      if (status) status[i] = PHIP_ST_MERGED;
+    } else {
+      missed = true;
+      if (pr == kFull) atomicOr(&ctr[8], 1u);
+    }
+  }
+  u32 pos = wave_append(&ctr[2], missed);
+  if (missed) miss[pos] = i;
+}
+
+// Status of the messages that went through the insert pipeline: the first
+// (lowest-seq) message of a created bucket gets PHIP_ST_CREATED
+// (repo.go:189-211 creates on the first GetBucket).
+template <class Src>
+__global__ void k_mark_created(Src src, u32 n, const u32* __restrict__ list, Table T, u8* status) {
+  u32 tid = blockIdx.x * blockDim.x + threadIdx.x;
+  if (tid >= n || !status) return;
+  u32 i = list[tid];
+  u64 off; u32 len;
+  src.get(i, off, len);
+  Name nm;
+  load_name(src.blob, off, len, nm);
+  u32 s;
+  if (probe(T, nm, src.blob, &s) != kFound) return;
+  const Rec& r = T.recs[s];
+  if ((r.flags & kRecNew) && r.aux == i) status[i] |= 0x80;
+}
+
+// -------------------------------------------------------------- resolve --
+// Name -> slot for every op (ordered path, seed, get).  Misses appended.
+template <class Src>
+__global__ __launch_bounds__(kBlock) void k_resolve(Src src, u32 n, const u32* __restrict__ list,
+                                                    Table T, u32* __restrict__ slot_out, u32* miss,
+                                                    u32* ctr) {
+  u32 tid = blockIdx.x * blockDim.x + threadIdx.x;
+  bool missed = false;
+  u32 i = 0;
+  if (tid < n) {
+    i = list ? list[tid] : tid;
+    u64 off; u32 len;
+    src.get(i, off, len);
+    Name nm;
+    load_name(src.blob, off, len, nm);
+    u32 s;
+    int pr = probe(T, nm, src.blob, &s);
+    if (pr == kFound) slot_out[i] = s;
+    else {
+      missed = true;
+      if (pr == kFull) atomicOr(&ctr[8], 1u);
+    }
+  }
+  if (miss) {
+    u32 pos = wave_append(&ctr[2], missed);
+    if (missed) miss[pos] = i;
+  }
+}
+
+// ------------------------------------------------------------- inserts ---
+// Round of the insert pipeline.  Claim: CAS an empty tag slot.  A same-tag
+// slot claimed in this round (not yet published) cannot be name-checked, so
+// the message waits for the next round (retry list); after the publish
+// kernel the name is visible and the retry either finds it or keeps probing.
+template <class Src>
+__global__ __launch_bounds__(kBlock) void k_claim(Src src, u32 n, const u32* __restrict__ list,
+                                                  Table T, u32* claimed_slot, u32* claimed_msg,
+                                                  u32* retry, u32* ctr) {
+  u32 tid = blockIdx.x * blockDim.x + threadIdx.x;
+  bool won = false, again = false;
+  u32 i = 0, s = 0;
+  if (tid < n) {
+    i = list[tid];
+    u64 off; u32 len;
+    src.get(i, off, len);
+    Name nm;
+    load_name(src.blob, off, len, nm);
+    const u64 tag = T.tag(nm.h);
+    const u32 mask = T.mask();
+    s = T.home(tag);
+    u32 k = 0;
+    for (; k <= mask; ++k) {
+      u64 t = __hip_atomic_load(&T.tags[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (t == 0) {
+        t = atomicCAS(&T.tags[s], 0ull, tag);
+        if (t == 0) { won = true; break; }
+      }
+      if (t == tag) {
+        const Rec& r = T.recs[s];
+        if (!(r.flags & kRecPublished)) { again = true; break; }
+        if (name_equal(r, nm, src.blob, T.arena)) break;   // inserted by an earlier round
+      }
+      s = (s + 1) & mask;
+    }
+    if (k > mask) atomicOr(&ctr[8], 1u);
+  }
+  u32 p = wave_append(&ctr[3], won);
+  if (won) { claimed_slot[p] = s; claimed_msg[p] = i; }
+  u32 q = wave_append(&ctr[4], again);
+  if (again) retry[q] = i;
+}
+
+// Publish claimed slots: canonical name (+arena for long names), zero state
+// (a GetBucket-created Bucket, repo.go:208), created clock, NEW flag.
+template <class Src>
+__global__ void k_publish(Src src, u32 base, u32 n, const u32* __restrict__ claimed_slot,
+                          const u32* __restrict__ claimed_msg, Rec* recs, u8* arena,
+                          u64 arena_cap, u64* arena_cursor, const int64_t* __restrict__ now_arr,
+                          i64 now0, u32* ctr) {
+  u32 tid = blockIdx.x * blockDim.x + threadIdx.x;
+  if (tid >= n) return;
+  u32 s = claimed_slot[base + tid], i = claimed_msg[base + tid];
+  u64 off; u32 len;
+  src.get(i, off, len);
+  Name nm;
+  load_name(src.blob, off, len, nm);
+  Rec r;
+  r.added = kEPosZero;
+  r.taken = kEPosZero;
+  r.elapsed = 0;
+  r.created = now_arr ? now_arr[i] : now0;
+  r.name[0] = nm.w0; r.name[1] = nm.w1; r.name[2] = nm.w2;
+  if (len > 23) {
+    u64 a = atomicAdd(arena_cursor, (u64)len);
+    if (a + len > arena_cap) { atomicOr(&ctr[7], 1u); a = 0; }
+    else for (u32 k = 0; k < len; ++k) arena[a + k] = src.blob[off + k];
+    r.name[0] = (nm.w0 & 0xFFu) | (a << 32);
+  }
+  r.flags = kRecPublished | kRecNew;
+  r.aux = 0xFFFFFFFFu;
+  recs[s] = r;
+}
+
+__global__ void k_clear_new(const u32* __restrict__ claimed_slot, u32 n, Rec* recs) {
+  u32 tid = blockIdx.x * blockDim.x + threadIdx.x;
+  if (tid >= n) return;
+  Rec* r = &recs[claimed_slot[tid]];
+  r->flags = kRecPublished;
+  r->aux = 0;
+}
+
+// --------------------------------------------------------------- decode --
+// UnmarshalBinary (bucket.go:71-91) for a batch of raw datagrams: big-endian
+// fields, name length byte, io.ErrShortBuffer when < 25 bytes or the name is
+// truncated; trailing bytes are ignored.  The first short datagram index is
+// min-reduced into ctr[5] (the Go loop stops there, repo.go:72-73).
+__device__ inline u64 load_be64(const u8* p) {
+  u64 v = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) v = (v << 8) | p[k];
+  return v;
+}
+
+__global__ void k_decode(const u8* __restrict__ bytes, const uint64_t* __restrict__ offs, u32 n,
+                         uint64_t* __restrict__ a, uint64_t* __restrict__ t,
+                         int64_t* __restrict__ e, uint64_t* __restrict__ noff,
+                         u8* __restrict__ nlen, u32* ctr) {
+  u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+  bool inc = false, nz = false;
+  if (i < n) {
+    u64 o = offs[i], sz = offs[i + 1] - o;
+    bool bad = sz < 25;
+    if (!bad) {
+      const u8* p = bytes + o;
+      u64 ab = load_be64(p), tb = load_be64(p + 8);
+      i64 eb = (i64)load_be64(p + 16);
+      u32 l = p[24];
+      bad = sz - 25 < l;
+      a[i] = ab; t[i] = tb; e[i] = eb;
+      noff[i] = o + 25;
+      nlen[i] = (u8)l;
+      inc = !bad && state_is_zero(ab, tb, eb);
+      nz = !bad && !inc && (ab == kSign || tb == kSign);
+    }
+    if (bad) {
+      nlen[i] = 0; noff[i] = o;
+      atomicMin(&ctr[5], i);
+    }
+  }
+  u64 mi = __ballot(inc), mn = __ballot(nz);
+  if (__lane_id() == 0) {
+    if (mi) atomicAdd(&ctr[0], (u32)__popcll(mi));
+    if (mn) atomicAdd(&ctr[1], (u32)__popcll(mn));
+  }
+}
+
+// ------------------------------------------------------------ ordered ----
+// A view of a mixed op stream; null arrays mean "uniform value".
+struct OpView {
+  const u8* kind; u32 kind0;
+  const int64_t* now; i64 now0;
+  const int64_t* freq; const int64_t* per; const uint64_t* count;
+  const uint64_t* a; const uint64_t* t; const int64_t* e;
+};
+
+struct OutView {
+  u8* status;
+  uint64_t* remaining;
+  uint64_t* have;
+  phip_state* reply;
+};
+
+struct FState {
+  double a, t;
+  i64 e, c;
+  bool existed;
+};
+
+struct OpOut {
+  u8 st;
+  bool has_reply;
+  u64 rem, have;
+};
+
+// One op of the ordered stream against state S (result state in S2).
+// Returns whether S2 differs from S (bitwise, or existence).
+__device__ inline bool eval_op(const OpView& ov, u32 i, const FState& S, FState& S2, OpOut& out) {
+  const u32 kind = ov.kind ? ov.kind[i] : ov.kind0;
+  const i64 now = ov.now ? ov.now[i] : ov.now0;
+  S2 = S;
+  u8 cflag = 0;
+  if (!S.existed) { S2.c = now; S2.existed = true; cflag = 0x80; }   // repo.go:208
+  out.has_reply = false; out.rem = 0; out.have = 0;
+  if (kind == PHIP_OP_TAKE) {
+    TakeResult r = take_step(S2.a, S2.t, S2.e, S2.c, now, ov.freq[i], ov.per[i], ov.count[i]);
+    out.st = (r.ok ? PHIP_ST_TAKE_OK : PHIP_ST_TAKE_DENIED) | cflag;
+    out.rem = r.remaining; out.have = r.have_bits;
+  } else {
+    u64 ab = ov.a[i], tb = ov.t[i];
+    i64 eb = ov.e[i];
+    if (kind == PHIP_OP_UPSERT && !S.existed) {               // repo.go:225-230
+      S2.a = as_f64(ab); S2.t = as_f64(tb); S2.e = eb;
+      out.st = PHIP_ST_UPSERT_INSERTED | cflag;
+    } else if (kind == PHIP_OP_RECEIVE && state_is_zero(ab, tb, eb)) {   // repo.go:86-90
+      bool reply = S.existed && !state_is_zero(as_bits(S.a), as_bits(S.t), S.e);
+      out.st = (reply ? PHIP_ST_INCAST_REPLY : PHIP_ST_INCAST_NOREPLY) | cflag;
+      out.has_reply = reply;
+    } else {                                                      // bucket.go:240-263
+      go_merge(S2.a, S2.t, S2.e, as_f64(ab), as_f64(tb), eb);
+      out.st = PHIP_ST_MERGED | cflag;
+    }
+  }
+  return !S.existed || as_bits(S2.a) != as_bits(S.a) || as_bits(S2.t) != as_bits(S.t) ||
+         S2.e != S.e;
+}
+
+__device__ inline void write_out(const OutView& o, u32 i, const OpOut& r, const FState& S) {
+  if (o.status) o.status[i] = r.st;
+  if (o.remaining) o.remaining[i] = r.rem;
+  if (o.have) o.have[i] = r.have;
+  if (o.reply && r.has_reply) {
+    phip_state st;
+    st.added = as_bits(S.a); st.taken = as_bits(S.t); st.elapsed = S.e; st.created = S.c;
+    o.reply[i] = st;
+  }
+}
+
+__device__ inline FState load_state(const Rec& r) {
+  FState S;
+  S.a = as_f64(dec_f64(r.added));
+  S.t = as_f64(dec_f64(r.taken));
+  S.e = r.elapsed;
+  S.c = r.created;
+  S.existed = !(r.flags & kRecNew);
+  return S;
+}
+
+__device__ inline void store_state(Rec* r, const FState& S) {
+  r->added = enc_f64(as_bits(S.a));
+  r->taken = enc_f64(as_bits(S.t));
+  r->elapsed = S.e;
+  r->created = S.c;
+  r->flags = kRecPublished;
+  r->aux = 0;
+}
+
+constexpr u32 kLongSeg = 48;
+
+// One thread folds one bucket's ops in seq order (segments of <= kLongSeg
+// ops); longer segments are handed to k_fold_wave.
+__global__ __launch_bounds__(kBlock) void k_fold_thread(
+    const u32* __restrict__ seg_slot, const u32* __restrict__ seg_start,
+    const u32* __restrict__ seg_count, u32 nseg, const u32* __restrict__ sorted_idx, Rec* recs,
+    OpView ov, OutView ow, u32* long_list, u32* ctr) {
+  u32 g = blockIdx.x * blockDim.x + threadIdx.x;
+  bool is_long = false;
+  if (g < nseg) {
+    u32 cnt = seg_count[g];
+    if (cnt > kLongSeg) is_long = true;
+    else {
+      Rec* r = &recs[seg_slot[g]];
+      FState S = load_state(*r), S2;
+      u32 st = seg_start[g];
+      for (u32 j = 0; j < cnt; ++j) {
+        u32 i = sorted_idx[st + j];
+        OpOut o;
+        eval_op(ov, i, S, S2, o);
+        write_out(ow, i, o, S);
+        S = S2;
+      }
+      store_state(r, S);
+    }
+  }
+  u32 p = wave_append(&ctr[6], is_long);
+  if (is_long) long_list[p] = g;
+}
+
+__device__ inline double shfl_f64(double v, int src) {
+  u64 b = as_bits(v);
+  u32 lo = __shfl((u32)b, src), hi = __shfl((u32)(b >> 32), src);
+  return as_f64(((u64)hi << 32) | lo);
+}
+__device__ inline i64 shfl_i64(i64 v, int src) {
+  u32 lo = __shfl((u32)(u64)v, src), hi = __shfl((u32)((u64)v >> 32), src);
+  return (i64)(((u64)hi << 32) | lo);
+}
+
+// One wave folds one long segment.  Each step evaluates the next 64 ops
+// against the current state in parallel; every op up to and including the
+// first one that changes the state is final (the ones before it saw exactly
+// the state the sequential fold would have shown them).  Deny streaks and
+// no-op merges therefore retire 64 ops per step.
+__global__ __launch_bounds__(64) void k_fold_wave(
+    const u32* __restrict__ long_list, u32 nlong, const u32* __restrict__ seg_slot,
+    const u32* __restrict__ seg_start, const u32* __restrict__ seg_count,
+    const u32* __restrict__ sorted_idx, Rec* recs, OpView ov, OutView ow) {
+  u32 w = blockIdx.x;
+  if (w >= nlong) return;
+  u32 g = long_list[w];
+  const u32 lane = threadIdx.x;
+  Rec* r = &recs[seg_slot[g]];
+  FState S = load_state(*r);
+  const u32 st = seg_start[g], cnt = seg_count[g];
+  u32 j0 = 0;
+  while (j0 < cnt) {
+    const u32 j = j0 + lane;
+    const bool active = j < cnt;
+    u32 i = active ? sorted_idx[st + j] : 0;
+    FState S2 = S;
+    OpOut o;
+    bool ch = false;
+    if (active) ch = eval_op(ov, i, S, S2, o);
+    u64 m = __ballot(ch);
+    u32 p = m ? (u32)(__ffsll((long long)m) - 1) : 64u;
+    if (active && lane <= p) write_out(ow, i, o, S);
+    if (p < 64) {
+      S.a = shfl_f64(S2.a, p);
+      S.t = shfl_f64(S2.t, p);
+      S.e = shfl_i64(S2.e, p);
+      S.c = shfl_i64(S2.c, p);
+      S.existed = true;
+      j0 += p + 1;
+    } else {
+      j0 += 64;
+    }
+  }
+  if (lane == 0) store_state(r, S);
+}
+
+// Sorted-slot segments from run-length output (counts -> starts is a scan).
+__global__ void k_seg_mark(const u32* __restrict__ sorted_slot, u32 n, u32* head) {
+  u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) head[i] = (i == 0 || sorted_slot[i] != sorted_slot[i - 1]) ? 1u : 0u;
+}
+
+// ------------------------------------------------------------ seed/dump --
+// NewLocalRepo(clock, bs...): last entry of a name wins (map assignment).
+__global__ void k_seed_pick(const u32* __restrict__ slot_of, u32 n, Rec* recs) {
+  u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) atomicMax(&recs[slot_of[i]].aux, i + 1);
+}
+__global__ void k_seed_apply(const u32* __restrict__ slot_of, u32 n, const phip_state* st,
+                             Rec* recs) {
+  u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  Rec* r = &recs[slot_of[i]];
+  if (r->aux != i + 1) return;
+  phip_state s = st[i];
+  r->added = enc_f64(s.added);
+  r->taken = enc_f64(s.taken);
+  r->elapsed = s.elapsed;
+  r->created = s.created;
+}
+__global__ void k_seed_finish(const u32* __restrict__ slot_of, u32 n, Rec* recs) {
+  u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  Rec* r = &recs[slot_of[i]];
+  r->aux = 0;
+  r->flags = kRecPublished;
+}
+
+__global__ void k_dump_collect(const u64* __restrict__ tags, u64 cap, u32* list, u32* ctr) {
+  u64 s = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+  bool occ = s < cap && tags[s] != 0;
+  u32 p = wave_append(&ctr[2], occ);
+  if (occ) list[p] = (u32)s;
+}
+__global__ void k_dump_gather(const u32* __restrict__ list, u32 n, const Rec* __restrict__ recs,
+                              Rec* out) {
+  u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = recs[list[i]];
+}
+
+// Single lookup (phip_get).
+__global__ void k_get_one(const u8* name, u32 len, Table T, Rec* out, int* found) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  Name nm;
+  load_name(name, 0, len, nm);
+  u32 s;
+  int pr = probe(T, nm, name, &s);
+  *found = pr == kFound;
+  if (pr == kFound) *out = T.recs[s];
+}
+
+}  // namespace phip

@@ -1,0 +1,286 @@
+"""Python mirror of Patrol's Repo seam over libpatrolhip.
+
+Patrol (Go) exposes its bucket map through the `Repo` interface
+(repo.go:15-18) and drives it from two loops: the UDP `Receive` loop
+(repo.go:54-92) and the HTTP `takeBucket` handler (api.go:51-86).  A
+device-resident table cannot hand out mutable `*Bucket` pointers, so the
+unit of work here is a batch of ops, each with the exact Go semantics in
+batch order (include/patrolhip.h).  This module is a thin ctypes layer used by
+the tests and bench.py; a Go deployment binds the same C ABI with cgo
+(INTEGRATION.md).
+
+Arrays may be numpy (host) or torch CUDA tensors (device, zero-copy: the
+call then passes PHIP_DEVICE_PTRS).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+from typing import Iterable, Sequence
+
+import numpy as np
+
+from . import _lib
+from ._lib import (DEVICE_PTRS, phip_config, phip_msgs, phip_ops, phip_results, phip_state)
+
+
+class PatrolHipError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"libpatrolhip error {code} ({_lib.PHIP_ERR.get(code, '?')}): {msg}")
+        self.code = code
+
+
+def _is_torch(x) -> bool:
+    return type(x).__module__.startswith("torch")
+
+
+def _ptr(x):
+    if x is None:
+        return None
+    if _is_torch(x):
+        return x.data_ptr()
+    return x.ctypes.data
+
+
+def _np(x, dtype):
+    if x is None:
+        return None
+    a = np.ascontiguousarray(x, dtype=dtype)
+    return a if a.size else np.zeros(1, dtype)
+
+
+def names_blob(names: Sequence[bytes]):
+    """list[bytes] -> (blob uint8 (8 bytes of read slack), offsets uint32[n+1])."""
+    offs = np.zeros(len(names) + 1, dtype=np.uint32)
+    if len(names):
+        offs[1:] = np.cumsum(np.fromiter((len(x) for x in names), np.int64, len(names)))
+    blob = np.zeros(int(offs[-1]) + 8, dtype=np.uint8)
+    if offs[-1]:
+        blob[:offs[-1]] = np.frombuffer(b"".join(names), dtype=np.uint8)
+    return blob, offs
+
+
+@dataclass
+class BucketState:
+    """A Bucket's replicated fields plus its local `created` (bucket.go:20-32)."""
+    added: int      # float64 bits
+    taken: int      # float64 bits
+    elapsed: int    # ns
+    created: int    # ns since the Unix epoch
+
+    @property
+    def added_f(self) -> float:
+        return float(np.array([self.added], np.uint64).view(np.float64)[0])
+
+    @property
+    def taken_f(self) -> float:
+        return float(np.array([self.taken], np.uint64).view(np.float64)[0])
+
+
+class GPURepo:
+    """A device-resident bucket map (the LocalRepo of repo.go:171-235)."""
+
+    def __init__(self, device: int = 0, log2_slots: int = 20, arena_bytes: int = 1 << 24,
+                 max_load_pct: int = 90, debug_tag_bits: int = 0):
+        self.L = _lib.load()
+        cfg = phip_config(device, log2_slots, arena_bytes, max_load_pct, debug_tag_bits)
+        h = C.c_void_p()
+        rc = self.L.phip_open(C.byref(cfg), C.byref(h))
+        if rc != 0:
+            raise PatrolHipError(rc, "phip_open failed")
+        self.h = h
+        self.device = device
+
+    # ------------------------------------------------------------ basics --
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.phip_close(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __len__(self):
+        return int(self.L.phip_len(self.h))
+
+    @property
+    def capacity(self) -> int:
+        return int(self.L.phip_capacity(self.h))
+
+    def _check(self, rc: int, allow=()):
+        if rc < 0 and rc not in allow:
+            raise PatrolHipError(rc, self.L.phip_last_error(self.h).decode(errors="replace"))
+        return rc
+
+    def flush(self):
+        self._check(self.L.phip_flush(self.h))
+
+    def set_timing(self, on: bool):
+        self.L.phip_set_timing(self.h, 1 if on else 0)
+
+    def timings(self):
+        names = (C.c_char_p * 256)()
+        ms = (C.c_float * 256)()
+        k = self.L.phip_last_timings(self.h, names, ms, 256)
+        return [(names[i].decode(), float(ms[i])) for i in range(k)]
+
+    # -------------------------------------------------------------- repo --
+    def seed(self, names: Sequence[bytes], added, taken, elapsed, created):
+        """NewLocalRepo(clock, bs...) (repo.go:179-185): buckets as given."""
+        blob, offs = names_blob(names)
+        n = len(names)
+        st = np.zeros(max(n, 1), dtype=[("a", "<u8"), ("t", "<u8"), ("e", "<i8"), ("c", "<i8")])
+        st["a"][:n], st["t"][:n] = np.asarray(added, np.uint64), np.asarray(taken, np.uint64)
+        st["e"][:n], st["c"][:n] = np.asarray(elapsed, np.int64), np.asarray(created, np.int64)
+        self._check(self.L.phip_seed(self.h, blob.ctypes.data, offs.ctypes.data, n,
+                                     st.ctypes.data, 0))
+
+    def seed_device(self, names, name_offs, states, n: int):
+        """phip_seed with device pointers: names (uint8 CUDA tensor), name_offs
+        (n+1 int32/uint32), states (n x 4 int64: added bits, taken bits,
+        elapsed, created)."""
+        self._check(self.L.phip_seed(self.h, _ptr(names), _ptr(name_offs), n, _ptr(states),
+                                     DEVICE_PTRS))
+
+    def get(self, name: bytes):
+        """Lookup without creating (None when absent)."""
+        s = phip_state()
+        rc = self._check(self.L.phip_get(self.h, name, len(name), C.byref(s)))
+        if rc == 0:
+            return None
+        return BucketState(s.added, s.taken, s.elapsed, s.created)
+
+    def dump(self):
+        """{name: BucketState} of every bucket."""
+        n, nb = C.c_uint64(), C.c_uint64()
+        self._check(self.L.phip_dump(self.h, None, 0, None, None, 0, C.byref(n), C.byref(nb)))
+        cnt = n.value
+        names = np.zeros(max(nb.value, 1), np.uint8)
+        offs = np.zeros(cnt + 1, np.uint64)
+        st = np.zeros(max(cnt, 1), dtype=[("a", "<u8"), ("t", "<u8"), ("e", "<i8"), ("c", "<i8")])
+        self._check(self.L.phip_dump(self.h, names.ctypes.data, names.size, offs.ctypes.data,
+                                     st.ctypes.data, cnt, C.byref(n), C.byref(nb)))
+        raw = names.tobytes()
+        return {raw[int(offs[i]):int(offs[i + 1])]:
+                BucketState(int(st["a"][i]), int(st["t"][i]), int(st["e"][i]), int(st["c"][i]))
+                for i in range(n.value)}
+
+    # ---------------------------------------------------------- hot path --
+    @staticmethod
+    def _results(n, want_remaining=False, want_reply=False):
+        status = np.zeros(max(n, 1), np.uint8)
+        rem = np.zeros(max(n, 1), np.uint64) if want_remaining else None
+        have = np.zeros(max(n, 1), np.uint64) if want_remaining else None
+        reply = (np.zeros(max(n, 1), dtype=[("a", "<u8"), ("t", "<u8"), ("e", "<i8"), ("c", "<i8")])
+                 if want_reply else None)
+        res = phip_results(status.ctypes.data, _ptr(rem), _ptr(have), _ptr(reply))
+        return res, status, rem, have, reply
+
+    def receive_datagrams(self, datagrams: Sequence[bytes], now: int):
+        """ReplicatedRepo.Receive over raw datagrams (repo.go:54-92).
+
+        Returns dict(status, reply, stop) — `stop` is the index of the first
+        malformed datagram (the Go loop returns io.ErrShortBuffer there) or n.
+        """
+        n = len(datagrams)
+        offs = np.zeros(n + 1, np.uint64)
+        if n:
+            offs[1:] = np.cumsum([len(d) for d in datagrams])
+        blob = np.zeros(int(offs[-1]) + 8, np.uint8)
+        if offs[-1]:
+            blob[:offs[-1]] = np.frombuffer(b"".join(datagrams), np.uint8)
+        res, status, _, _, reply = self._results(n, want_reply=True)
+        stop = C.c_uint32()
+        self._check(self.L.phip_receive_datagrams(self.h, blob.ctypes.data, offs.ctypes.data, n,
+                                                  int(now), C.byref(res), C.byref(stop), 0),
+                    allow=(-5,))
+        return dict(status=status[:n], reply=reply[:n], stop=stop.value)
+
+    def receive_soa(self, names, added, taken, elapsed, now: int, name_offs=None, n=None,
+                    status=None, device=False):
+        """Receive over decoded states.  With device=True every array is a torch
+        CUDA tensor (names = uint8 blob, name_offs = int32/uint32 offsets)."""
+        if device:
+            m = phip_msgs(n, 0, _ptr(names), _ptr(name_offs), _ptr(added), _ptr(taken), _ptr(elapsed))
+            res = phip_results(_ptr(status), None, None, None)
+            self._check(self.L.phip_receive_soa(self.h, C.byref(m), int(now), C.byref(res),
+                                                DEVICE_PTRS))
+            return None
+        n = len(names)
+        blob, offs = names_blob(names)
+        a, t, e = _np(added, np.uint64), _np(taken, np.uint64), _np(elapsed, np.int64)
+        m = phip_msgs(n, 0, blob.ctypes.data, offs.ctypes.data, a.ctypes.data, t.ctypes.data,
+                      e.ctypes.data)
+        res, st, _, _, reply = self._results(n, want_reply=True)
+        self._check(self.L.phip_receive_soa(self.h, C.byref(m), int(now), C.byref(res), 0))
+        return dict(status=st[:n], reply=reply[:n])
+
+    def upsert_soa(self, names, added, taken, elapsed, now: int):
+        """LocalRepo.UpsertBucket for each state (repo.go:215-235)."""
+        n = len(names)
+        blob, offs = names_blob(names)
+        a, t, e = _np(added, np.uint64), _np(taken, np.uint64), _np(elapsed, np.int64)
+        m = phip_msgs(n, 0, blob.ctypes.data, offs.ctypes.data, a.ctypes.data, t.ctypes.data,
+                      e.ctypes.data)
+        res, st, _, _, _ = self._results(n)
+        self._check(self.L.phip_upsert_soa(self.h, C.byref(m), int(now), C.byref(res), 0))
+        return dict(status=st[:n])
+
+    def apply_mixed(self, kind, names, now, freq=None, per=None, count=None, added=None,
+                    taken=None, elapsed=None):
+        """Ordered TAKE/RECEIVE/UPSERT stream (api.go:67-74, repo.go:78-90, :215-235)."""
+        n = len(names)
+        blob, offs = names_blob(names)
+        arrs = dict(kind=_np(kind, np.uint8), now=_np(now, np.int64), freq=_np(freq, np.int64),
+                    per=_np(per, np.int64), count=_np(count, np.uint64),
+                    added=_np(added, np.uint64), taken=_np(taken, np.uint64),
+                    elapsed=_np(elapsed, np.int64))
+        ops = phip_ops(n, 0, _ptr(arrs["kind"]), blob.ctypes.data, offs.ctypes.data,
+                       _ptr(arrs["now"]), _ptr(arrs["freq"]), _ptr(arrs["per"]), _ptr(arrs["count"]),
+                       _ptr(arrs["added"]), _ptr(arrs["taken"]), _ptr(arrs["elapsed"]))
+        res, st, rem, have, reply = self._results(n, want_remaining=True, want_reply=True)
+        self._check(self.L.phip_apply_mixed(self.h, C.byref(ops), C.byref(res), 0))
+        return dict(status=st[:n], remaining=rem[:n], have=have[:n], reply=reply[:n])
+
+    def take(self, names, now, freq, per, count):
+        """Batched Bucket.Take via GetBucket (create) then Take: (remaining, ok)."""
+        n = len(names)
+        blob, offs = names_blob(names)
+        now, freq, per = _np(now, np.int64), _np(freq, np.int64), _np(per, np.int64)
+        count = _np(count, np.uint64)
+        rem = np.zeros(max(n, 1), np.uint64)
+        ok = np.zeros(max(n, 1), np.uint8)
+        self._check(self.L.phip_take(self.h, blob.ctypes.data, offs.ctypes.data, n, now.ctypes.data,
+                                     freq.ctypes.data, per.ctypes.data, count.ctypes.data,
+                                     rem.ctypes.data, ok.ctypes.data, 0))
+        return rem[:n], ok[:n].astype(bool)
+
+    def api_take(self, name: bytes, rate: bytes, count: bytes, now: int):
+        """API.takeBucket (api.go:51-86): (HTTP status, body)."""
+        body = C.create_string_buffer(64)
+        bl = C.c_uint32()
+        code = self._check(self.L.phip_api_take(self.h, name, len(name), rate, len(rate), count,
+                                                len(count), int(now), body, C.byref(bl)))
+        return code, body.raw[:bl.value].decode()
+
+
+def parse_rate(s: bytes):
+    """ParseRate (bucket.go:102-123): (freq, per_ns, ok) with Go's error values."""
+    L = _lib.load()
+    f, p = C.c_int64(), C.c_int64()
+    rc = L.phip_parse_rate(s, len(s), C.byref(f), C.byref(p))
+    return f.value, p.value, rc == 0
+
+
+def marshal(name: bytes, state: BucketState) -> bytes:
+    """Bucket.MarshalBinary (bucket.go:51-68)."""
+    L = _lib.load()
+    out = C.create_string_buffer(256)
+    st = phip_state(state.added, state.taken, state.elapsed, state.created)
+    n = L.phip_marshal(name, len(name), C.byref(st), out)
+    if n < 0:
+        raise PatrolHipError(n, "bucket name larger than 231")
+    return out.raw[:n]
