@@ -217,8 +217,10 @@ int insert_names(phip_handle* h, Src src, u32* list, u32 nlist, const int64_t* n
   u32* nxt = retry;
   u32* spare = nullptr;
   if ((rc = ensure(h, B_MISS2, nlist, &spare))) return rc;
+  // Every round claims at least one slot while names are pending (a pending
+  // name met a slot claimed in that same round), so this terminates; with a
+  // 64-bit tag a second round is already rare.
   for (int round = 0; ncur > 0; ++round) {
-    if (round > 64) return set_err(h, PHIP_ERR_INVALID, "insert did not converge");
     if (h->n_buckets >= h->max_load)
       return set_err(h, PHIP_ERR_FULL, "table load limit reached: %llu buckets of %llu allowed",
                      (unsigned long long)h->n_buckets, (unsigned long long)h->max_load);
@@ -234,6 +236,8 @@ int insert_names(phip_handle* h, Src src, u32* list, u32 nlist, const int64_t* n
     if ((rc = check_flags(h))) return rc;
     u32 claimed_total = h->ctr_host[3];
     u32 fresh = claimed_total - total;
+    if (fresh == 0 && h->ctr_host[4] != 0)
+      return set_err(h, PHIP_ERR_INVALID, "internal: insert round made no progress");
     if (fresh) {
       Launch l(h, "k_publish");
       k_publish<Src><<<grid_for(fresh), kBlock, 0, h->stream>>>(
