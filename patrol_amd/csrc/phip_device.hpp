@@ -131,24 +131,30 @@ __host__ __device__ inline bool state_is_zero(u64 a_bits, u64 t_bits, i64 e) {
 }
 
 // ------------------------------------------------------------ table -----
-// One 64-byte slot record (one HBM burst): state + canonical name.
+// One 64-byte slot record = one HBM burst holding everything a lookup and a
+// merge touch: probe tag, state, canonical name.
+//   tag          FNV-1a 64 of the name (0 = empty slot; a 0 hash is stored as 1)
 //   added/taken  E-encoded float64
-//   name[0] byte0 = len; len <= 23: bytes 1..len of name[] hold the name;
-//           len > 23: name[0] bytes 4..7 = arena offset, name[1..2] = the
-//           first 16 bytes (fast reject), full name in the arena.
+//   name[0..2]   byte 0 = len, byte 1 = flags (kRec*), then
+//                len <= 22: bytes 2..2+len = the name, zero padded;
+//                len  > 22: bytes 4..7 = arena offset, bytes 8..23 = first 16
+//                bytes (fast reject), full name in the arena.
 struct alignas(64) Rec {
+  u64 tag;
   u64 added;
   u64 taken;
   i64 elapsed;
   i64 created;
   u64 name[3];
-  u32 flags;
-  u32 aux;   // scratch: min seq of the ops of the batch that created it
 };
 static_assert(sizeof(Rec) == 64, "slot record must be one 64-byte burst");
 
-constexpr u32 kRecPublished = 1u;   // name and state written (visible after a kernel boundary)
-constexpr u32 kRecNew = 2u;         // created by the current batch
+constexpr u32 kInlineName = 22;
+constexpr u64 kRecPublished = 1u;   // name and state written (visible after a kernel boundary)
+constexpr u64 kRecNew = 2u;         // created by the current batch
+
+__host__ __device__ inline u32 rec_flags(const Rec& r) { return (u32)((r.name[0] >> 8) & 0xFFu); }
+__host__ __device__ inline u64 with_flags(u64 w0, u64 f) { return (w0 & ~0xFF00ull) | (f << 8); }
 
 constexpr u64 kFnvOffset = 0xcbf29ce484222325ull;
 constexpr u64 kFnvPrime = 0x100000001b3ull;
@@ -162,7 +168,7 @@ __host__ __device__ inline u64 fnv_step(u64 h, u8 c) {
 __host__ __device__ inline u64 tag_of(u64 h) { return h ? h : 1ull; }
 
 struct Name {
-  u64 w0, w1, w2;   // canonical 24-byte field (see Rec)
+  u64 w0, w1, w2;   // canonical 24-byte field (see Rec), flags byte 0
   u64 h;            // FNV-1a 64
   u64 off;          // byte offset of the name in its source blob
   u32 len;
@@ -178,11 +184,11 @@ __host__ __device__ inline void put_name_byte(Name& nm, u32 pos, u8 c) {
 // Reads name bytes src[off .. off+len), hashes and canonicalises them.
 __host__ __device__ inline void load_name(const u8* src, u64 off, u32 len, Name& nm) {
   nm.w0 = len & 0xFFu; nm.w1 = 0; nm.w2 = 0; nm.h = kFnvOffset; nm.off = off; nm.len = len;
-  const bool inl = len <= 23;
+  const bool inl = len <= kInlineName;
   for (u32 k = 0; k < len; ++k) {
     u8 c = src[off + k];
     nm.h = fnv_step(nm.h, c);
-    if (inl) put_name_byte(nm, k + 1, c);
+    if (inl) put_name_byte(nm, k + 2, c);
     else if (k < 16) put_name_byte(nm, k + 8, c);
   }
 }

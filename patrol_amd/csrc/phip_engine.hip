@@ -54,8 +54,8 @@ struct phip_handle {
   u32 L = 0;
   u64 cap = 0;
   u64 max_load = 0;
-  u64* tags = nullptr;
   Rec* recs = nullptr;
+  u32* aux = nullptr;
   u8* arena = nullptr;
   u64 arena_cap = 0;
   u64* arena_cursor = nullptr;
@@ -108,8 +108,8 @@ int ensure(phip_handle* h, BufId id, size_t count, T** out) {
 
 inline Table table(phip_handle* h) {
   Table t;
-  t.tags = h->tags;
   t.recs = h->recs;
+  t.aux = h->aux;
   t.arena = h->arena;
   t.L = h->L;
   t.tag_mask = h->tag_mask;
@@ -241,7 +241,7 @@ int insert_names(phip_handle* h, Src src, u32* list, u32 nlist, const int64_t* n
     if (fresh) {
       Launch l(h, "k_publish");
       k_publish<Src><<<grid_for(fresh), kBlock, 0, h->stream>>>(
-          src, total, fresh, cslot, cmsg, h->recs, h->arena, h->arena_cap, h->arena_cursor, now_arr,
+          src, total, fresh, cslot, cmsg, table(h), h->arena, h->arena_cap, h->arena_cursor, now_arr,
           now0, h->ctr);
     }
     HIPCHK(h, hipGetLastError());
@@ -260,7 +260,7 @@ int clear_new(phip_handle* h, u32 n_claimed) {
   if (!n_claimed) return PHIP_OK;
   u32* cslot = (u32*)h->buf[B_CSLOT].p;
   Launch l(h, "k_clear_new");
-  k_clear_new<<<grid_for(n_claimed), kBlock, 0, h->stream>>>(cslot, n_claimed, h->recs);
+  k_clear_new<<<grid_for(n_claimed), kBlock, 0, h->stream>>>(cslot, n_claimed, table(h));
   HIPCHK(h, hipGetLastError());
   return PHIP_OK;
 }
@@ -512,14 +512,14 @@ int phip_open(const phip_config* cfg, phip_handle** out) {
   hipError_t e;
   if ((e = hipSetDevice(h->device)) != hipSuccess) return fail(e);
   if ((e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking)) != hipSuccess) return fail(e);
-  if ((e = hipMalloc(&h->tags, h->cap * sizeof(u64))) != hipSuccess) return fail(e);
   if ((e = hipMalloc(&h->recs, h->cap * sizeof(Rec))) != hipSuccess) return fail(e);
+  if ((e = hipMalloc(&h->aux, h->cap * sizeof(u32))) != hipSuccess) return fail(e);
   if ((e = hipMalloc(&h->arena, h->arena_cap + 64)) != hipSuccess) return fail(e);
   if ((e = hipMalloc(&h->arena_cursor, 64)) != hipSuccess) return fail(e);
   if ((e = hipMalloc(&h->ctr, 64)) != hipSuccess) return fail(e);
   if ((e = hipHostMalloc(&h->ctr_host, 64, 0)) != hipSuccess) return fail(e);
-  if ((e = hipMemsetAsync(h->tags, 0, h->cap * sizeof(u64), h->stream)) != hipSuccess) return fail(e);
   if ((e = hipMemsetAsync(h->recs, 0, h->cap * sizeof(Rec), h->stream)) != hipSuccess) return fail(e);
+  if ((e = hipMemsetAsync(h->aux, 0, h->cap * sizeof(u32), h->stream)) != hipSuccess) return fail(e);
   if ((e = hipMemsetAsync(h->arena_cursor, 0, 64, h->stream)) != hipSuccess) return fail(e);
   if ((e = hipMemsetAsync(h->ctr, 0, 64, h->stream)) != hipSuccess) return fail(e);
   if ((e = hipStreamSynchronize(h->stream)) != hipSuccess) return fail(e);
@@ -537,8 +537,8 @@ void phip_close(phip_handle* h) {
     hipEventDestroy(t.a);
     hipEventDestroy(t.b);
   }
-  if (h->tags) hipFree(h->tags);
   if (h->recs) hipFree(h->recs);
+  if (h->aux) hipFree(h->aux);
   if (h->arena) hipFree(h->arena);
   if (h->arena_cursor) hipFree(h->arena_cursor);
   if (h->ctr) hipFree(h->ctr);
@@ -578,10 +578,10 @@ int phip_seed(phip_handle* h, const uint8_t* names, const uint32_t* name_offs, u
   if ((rc = resolve_all(h, src, n, nullptr, 0, &slot, &n_claimed))) return rc;
   // aux is the per-slot "last writer" scratch: clear, pick the last entry of
   // each name, apply it, clear again.
-  k_seed_finish<<<grid_for(n), kBlock, 0, h->stream>>>(slot, n, h->recs);
-  k_seed_pick<<<grid_for(n), kBlock, 0, h->stream>>>(slot, n, h->recs);
-  k_seed_apply<<<grid_for(n), kBlock, 0, h->stream>>>(slot, n, d_st, h->recs);
-  k_seed_finish<<<grid_for(n), kBlock, 0, h->stream>>>(slot, n, h->recs);
+  k_seed_finish<<<grid_for(n), kBlock, 0, h->stream>>>(slot, n, table(h));
+  k_seed_pick<<<grid_for(n), kBlock, 0, h->stream>>>(slot, n, table(h));
+  k_seed_apply<<<grid_for(n), kBlock, 0, h->stream>>>(slot, n, d_st, table(h));
+  k_seed_finish<<<grid_for(n), kBlock, 0, h->stream>>>(slot, n, table(h));
   HIPCHK(h, hipGetLastError());
   HIPCHK(h, hipStreamSynchronize(h->stream));
   return PHIP_OK;
@@ -623,7 +623,7 @@ int phip_dump(phip_handle* h, uint8_t* names, uint64_t names_cap, uint64_t* name
   u32* list;
   if ((rc = ensure(h, B_DUMP, h->n_buckets + 1, &list))) return rc;
   if ((rc = reset_ctr(h))) return rc;
-  k_dump_collect<<<grid_for(h->cap), kBlock, 0, h->stream>>>(h->tags, h->cap, list, h->ctr);
+  k_dump_collect<<<grid_for(h->cap), kBlock, 0, h->stream>>>(h->recs, h->cap, list, h->ctr);
   HIPCHK(h, hipGetLastError());
   if ((rc = read_ctr(h))) return rc;
   u32 n = h->ctr_host[2];
@@ -644,7 +644,7 @@ int phip_dump(phip_handle* h, uint8_t* names, uint64_t names_cap, uint64_t* name
     HIPCHK(h, hipMemcpy(arena.data(), h->arena, cursor, hipMemcpyDeviceToHost));
   }
   u64 total = 0;
-  for (auto& r : recs) total += r.name[0] & 0xFF;
+  for (auto& r : recs) total += r.name[0] & 0xFF;   // byte 0 = length
   if (n_out) *n_out = n;
   if (names_bytes_out) *names_bytes_out = total;
   if (!names) return PHIP_OK;
@@ -655,8 +655,8 @@ int phip_dump(phip_handle* h, uint8_t* names, uint64_t names_cap, uint64_t* name
     const Rec& r = recs[k];
     u32 len = r.name[0] & 0xFF;
     name_offs[k] = o;
-    if (len <= 23) {
-      for (u32 j = 0; j < len; ++j) names[o + j] = (u8)(r.name[(j + 1) >> 3] >> (((j + 1) & 7) * 8));
+    if (len <= kInlineName) {
+      for (u32 j = 0; j < len; ++j) names[o + j] = (u8)(r.name[(j + 2) >> 3] >> (((j + 2) & 7) * 8));
     } else {
       u64 aoff = r.name[0] >> 32;
       if (aoff + len <= arena.size()) std::memcpy(names + o, arena.data() + aoff, len);

@@ -1,7 +1,9 @@
 // HIP kernels of libpatrolhip (gfx950).  Host orchestration: phip_engine.hip.
 //
-// Table: tags[2^L] (u64 FNV-1a tag, 0 = empty) + recs[2^L] (64-byte Rec).
-// Home slot = top L bits of tag * 2^64/phi (Fibonacci hashing), linear probing.
+// Table: recs[2^L] 64-byte slot records (tag, state and name in one HBM
+// burst) + aux[2^L] u32 scratch used only by inserting/seeding batches.
+// Home slot = top L bits of tag * 2^64/phi (Fibonacci hashing), linear
+// probing; a lookup touches one 64-byte record per probe step.
 #pragma once
 #include "phip_device.hpp"
 
@@ -44,10 +46,11 @@ __device__ inline u32 wave_append(u32* counter, bool pred) {
   return base + rank;
 }
 
-// Full-name equality for a candidate record (names > 23 bytes live in the arena).
+// Full-name equality for a candidate record (names > 22 bytes live in the arena).
 __device__ inline bool name_equal(const Rec& r, const Name& nm, const u8* src, const u8* arena) {
-  if ((r.name[0] & 0xFFu) != (nm.w0 & 0xFFu)) return false;
-  if (nm.len <= 23) return r.name[0] == nm.w0 && r.name[1] == nm.w1 && r.name[2] == nm.w2;
+  const u64 r0 = r.name[0] & ~0xFF00ull;   // drop the flags byte
+  if ((r0 & 0xFFu) != (nm.w0 & 0xFFu)) return false;
+  if (nm.len <= kInlineName) return r0 == nm.w0 && r.name[1] == nm.w1 && r.name[2] == nm.w2;
   if (r.name[1] != nm.w1 || r.name[2] != nm.w2) return false;
   u64 aoff = r.name[0] >> 32;
   for (u32 k = 16; k < nm.len; ++k)
@@ -59,8 +62,8 @@ enum ProbeResult : int { kFound = 0, kMiss = 1, kPending = 2, kFull = 3 };
 
 // The device table, passed to kernels by value.
 struct Table {
-  u64* tags;
   Rec* recs;
+  u32* aux;
   const u8* arena;
   u32 L;
   u64 tag_mask;   // all ones; narrower only in collision tests (phip_config.debug_tag_bits)
@@ -71,19 +74,36 @@ struct Table {
   __device__ inline u32 mask() const { return (u32)((1ull << L) - 1); }
 };
 
-// Look the name up.  kFound: *slot = its slot.  kMiss: not present.
-// kPending: a same-tag slot is claimed but not yet published (insert rounds).
-__device__ inline int probe(const Table& T, const Name& nm, const u8* src, u32* slot) {
+// Whole-record load: four 16-byte loads issued together (one 64-byte burst),
+// so tag, state and name arrive in one memory round trip.
+__device__ inline Rec load_rec(const Rec* p) {
+  const uint4* q = reinterpret_cast<const uint4*>(p);
+  uint4 a = q[0], b = q[1], c = q[2], d = q[3];
+  Rec r;
+  r.tag = ((u64)a.y << 32) | a.x;
+  r.added = ((u64)a.w << 32) | a.z;
+  r.taken = ((u64)b.y << 32) | b.x;
+  r.elapsed = (i64)(((u64)b.w << 32) | b.z);
+  r.created = (i64)(((u64)c.y << 32) | c.x);
+  r.name[0] = ((u64)c.w << 32) | c.z;
+  r.name[1] = ((u64)d.y << 32) | d.x;
+  r.name[2] = ((u64)d.w << 32) | d.z;
+  return r;
+}
+
+// Look the name up.  kFound: *slot = its slot and *rec = its contents.
+// kMiss: not present.  kPending: a same-tag slot is claimed but not yet
+// published (only seen by insert rounds).
+__device__ inline int probe(const Table& T, const Name& nm, const u8* src, u32* slot, Rec* rec) {
   const u64 tag = T.tag(nm.h);
   const u32 mask = T.mask();
   u32 s = T.home(tag);
   for (u32 k = 0; k <= mask; ++k) {
-    u64 t = T.tags[s];
-    if (t == 0) return kMiss;
-    if (t == tag) {
-      const Rec& r = T.recs[s];
-      if (!(r.flags & kRecPublished)) return kPending;
-      if (name_equal(r, nm, src, T.arena)) { *slot = s; return kFound; }
+    Rec r = load_rec(&T.recs[s]);
+    if (r.tag == 0) return kMiss;
+    if (r.tag == tag) {
+      if (!(rec_flags(r) & kRecPublished)) return kPending;
+      if (name_equal(r, nm, src, T.arena)) { *slot = s; *rec = r; return kFound; }
     }
     s = (s + 1) & mask;
   }
@@ -112,18 +132,36 @@ __global__ void k_classify(const uint64_t* __restrict__ a, const uint64_t* __res
 
 // ------------------------------------------------------- fast receive ----
 // The batched Receive loop (repo.go:54-92) for a batch with no incast and no
-// -0.0: GetBucket(name) + Merge(&remote) for every message.  The merge is a
-// read-then-atomicMax on E-encoded fields: state only grows, so a stale read
-// can only cause a redundant atomic, never a lost update, and once a hot
-// bucket has converged its messages are pure L2-hit reads.
+// -0.0: GetBucket(name) + Merge(&remote) for every message.
+//
+// Each lane resolves its message (one 64-byte record per probe step; the
+// record carries the state too) and compares the replica against the state
+// it just read.  Only fields that would grow go further: they are max-combined
+// per slot in an LDS table shared by the workgroup, and one lane per
+// distinct slot then issues the device-scope atomicMax for the combined
+// value.  State only grows (E-encoding, phip_device.hpp), so a stale read can
+// only cause a redundant atomic, never a lost update; combining first keeps
+// a Zipf-hot bucket at one atomic per workgroup instead of one per message.
 // Misses are appended to `miss` (insert pipeline, then this kernel again on
 // the miss list with `track_new`).
+constexpr u32 kCombSlots = 2 * kBlock;
+constexpr u32 kCombEmpty = 0xFFFFFFFFu;
+
 template <class Src>
 __global__ __launch_bounds__(kBlock) void k_receive_fast(
     Src src, const uint64_t* __restrict__ ma, const uint64_t* __restrict__ mt,
     const int64_t* __restrict__ me,
     u32 n, const u32* __restrict__ list, Table T, u8* __restrict__ status, u32* miss, u32* ctr,
     int track_new) {
+  __shared__ u32 ckey[kCombSlots];
+  __shared__ u64 cmax[3][kCombSlots];   // combined replica maxima (elapsed biased by 2^63)
+  __shared__ u64 cseen[3][kCombSlots];  // state seen by the lane that opened the entry
+  for (u32 j = threadIdx.x; j < kCombSlots; j += kBlock) {
+    ckey[j] = kCombEmpty;
+    cmax[0][j] = 0; cmax[1][j] = 0; cmax[2][j] = 0;
+  }
+  __syncthreads();
+
   u32 tid = blockIdx.x * blockDim.x + threadIdx.x;
   bool missed = false;
   u32 i = 0;
@@ -133,19 +171,30 @@ __global__ __launch_bounds__(kBlock) void k_receive_fast(
     src.get(i, off, len);
     Name nm;
     load_name(src.blob, off, len, nm);
-    u64 ab = ma[i], tb = mt[i];
-    i64 eb = me[i];
+    const u64 ea = enc_replica(ma[i]), et = enc_replica(mt[i]);
+    const u64 ee = (u64)me[i] ^ kSign;
     u32 s;
-    int pr = probe(T, nm, src.blob, &s);
+    Rec cur;
+    int pr = probe(T, nm, src.blob, &s, &cur);
     if (pr == kFound) {
-      Rec* r = &T.recs[s];
-      u64 ea = enc_replica(ab), et = enc_replica(tb);
-      u64 ca = r->added, ct = r->taken;
-      i64 ce = r->elapsed;
-      if (ea > ca) atomicMax(&r->added, ea);
-      if (et > ct) atomicMax(&r->taken, et);
-      if (eb > ce) atomicMax(&r->elapsed, eb);
-      if (track_new && (r->flags & kRecNew)) atomicMin(&r->aux, i);
+      const u64 ua = cur.added, ut = cur.taken, ue = (u64)cur.elapsed ^ kSign;
+      const bool ga = ea > ua, gt = et > ut, ge = ee > ue;
+      if (ga || gt || ge) {
+        u32 h = (s * 2654435761u) >> (32 - 9);
+        for (;;) {
+          u32 old = atomicCAS(&ckey[h], kCombEmpty, s);
+          if (old == kCombEmpty) {
+            cseen[0][h] = ua; cseen[1][h] = ut; cseen[2][h] = ue;
+            break;
+          }
+          if (old == s) break;
+          h = (h + 1) & (kCombSlots - 1);
+        }
+        if (ga) atomicMax(&cmax[0][h], ea);
+        if (gt) atomicMax(&cmax[1][h], et);
+        if (ge) atomicMax(&cmax[2][h], ee);
+      }
+      if (track_new && (rec_flags(cur) & kRecNew)) atomicMin(&T.aux[s], i);
       if (status) status[i] = PHIP_ST_MERGED;
     } else {
       missed = true;
@@ -154,6 +203,16 @@ __global__ __launch_bounds__(kBlock) void k_receive_fast(
   }
   u32 pos = wave_append(&ctr[2], missed);
   if (missed) miss[pos] = i;
+
+  __syncthreads();
+  for (u32 j = threadIdx.x; j < kCombSlots; j += kBlock) {
+    u32 s = ckey[j];
+    if (s == kCombEmpty) continue;
+    Rec* r = &T.recs[s];
+    if (cmax[0][j] > cseen[0][j]) atomicMax(&r->added, cmax[0][j]);
+    if (cmax[1][j] > cseen[1][j]) atomicMax(&r->taken, cmax[1][j]);
+    if (cmax[2][j] > cseen[2][j]) atomicMax(&r->elapsed, (i64)(cmax[2][j] ^ kSign));
+  }
 }
 
 // Status of the messages that went through the insert pipeline: the first
@@ -169,9 +228,9 @@ __global__ void k_mark_created(Src src, u32 n, const u32* __restrict__ list, Tab
   Name nm;
   load_name(src.blob, off, len, nm);
   u32 s;
-  if (probe(T, nm, src.blob, &s) != kFound) return;
-  const Rec& r = T.recs[s];
-  if ((r.flags & kRecNew) && r.aux == i) status[i] |= 0x80;
+  Rec r;
+  if (probe(T, nm, src.blob, &s, &r) != kFound) return;
+  if ((rec_flags(r) & kRecNew) && T.aux[s] == i) status[i] |= 0x80;
 }
 
 // -------------------------------------------------------------- resolve --
@@ -190,7 +249,8 @@ __global__ __launch_bounds__(kBlock) void k_resolve(Src src, u32 n, const u32* _
     Name nm;
     load_name(src.blob, off, len, nm);
     u32 s;
-    int pr = probe(T, nm, src.blob, &s);
+    Rec r;
+    int pr = probe(T, nm, src.blob, &s, &r);
     if (pr == kFound) slot_out[i] = s;
     else {
       missed = true;
@@ -226,14 +286,14 @@ __global__ __launch_bounds__(kBlock) void k_claim(Src src, u32 n, const u32* __r
     s = T.home(tag);
     u32 k = 0;
     for (; k <= mask; ++k) {
-      u64 t = __hip_atomic_load(&T.tags[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      u64 t = __hip_atomic_load(&T.recs[s].tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (t == 0) {
-        t = atomicCAS(&T.tags[s], 0ull, tag);
+        t = atomicCAS(&T.recs[s].tag, 0ull, tag);
         if (t == 0) { won = true; break; }
       }
       if (t == tag) {
-        const Rec& r = T.recs[s];
-        if (!(r.flags & kRecPublished)) { again = true; break; }
+        Rec r = load_rec(&T.recs[s]);
+        if (!(rec_flags(r) & kRecPublished)) { again = true; break; }
         if (name_equal(r, nm, src.blob, T.arena)) break;   // inserted by an earlier round
       }
       s = (s + 1) & mask;
@@ -250,7 +310,7 @@ __global__ __launch_bounds__(kBlock) void k_claim(Src src, u32 n, const u32* __r
 // (a GetBucket-created Bucket, repo.go:208), created clock, NEW flag.
 template <class Src>
 __global__ void k_publish(Src src, u32 base, u32 n, const u32* __restrict__ claimed_slot,
-                          const u32* __restrict__ claimed_msg, Rec* recs, u8* arena,
+                          const u32* __restrict__ claimed_msg, Table T, u8* arena,
                           u64 arena_cap, u64* arena_cursor, const int64_t* __restrict__ now_arr,
                           i64 now0, u32* ctr) {
   u32 tid = blockIdx.x * blockDim.x + threadIdx.x;
@@ -261,28 +321,30 @@ __global__ void k_publish(Src src, u32 base, u32 n, const u32* __restrict__ clai
   Name nm;
   load_name(src.blob, off, len, nm);
   Rec r;
+  r.tag = T.tag(nm.h);
   r.added = kEPosZero;
   r.taken = kEPosZero;
   r.elapsed = 0;
   r.created = now_arr ? now_arr[i] : now0;
   r.name[0] = nm.w0; r.name[1] = nm.w1; r.name[2] = nm.w2;
-  if (len > 23) {
+  if (len > kInlineName) {
     u64 a = atomicAdd(arena_cursor, (u64)len);
     if (a + len > arena_cap) { atomicOr(&ctr[7], 1u); a = 0; }
     else for (u32 k = 0; k < len; ++k) arena[a + k] = src.blob[off + k];
     r.name[0] = (nm.w0 & 0xFFu) | (a << 32);
   }
-  r.flags = kRecPublished | kRecNew;
-  r.aux = 0xFFFFFFFFu;
-  recs[s] = r;
+  r.name[0] = with_flags(r.name[0], kRecPublished | kRecNew);
+  T.recs[s] = r;
+  T.aux[s] = 0xFFFFFFFFu;
 }
 
-__global__ void k_clear_new(const u32* __restrict__ claimed_slot, u32 n, Rec* recs) {
+__global__ void k_clear_new(const u32* __restrict__ claimed_slot, u32 n, Table T) {
   u32 tid = blockIdx.x * blockDim.x + threadIdx.x;
   if (tid >= n) return;
-  Rec* r = &recs[claimed_slot[tid]];
-  r->flags = kRecPublished;
-  r->aux = 0;
+  u32 s = claimed_slot[tid];
+  Rec* r = &T.recs[s];
+  r->name[0] = with_flags(r->name[0], kRecPublished);
+  T.aux[s] = 0;
 }
 
 // --------------------------------------------------------------- decode --
@@ -407,7 +469,7 @@ __device__ inline FState load_state(const Rec& r) {
   S.t = as_f64(dec_f64(r.taken));
   S.e = r.elapsed;
   S.c = r.created;
-  S.existed = !(r.flags & kRecNew);
+  S.existed = !(rec_flags(r) & kRecNew);
   return S;
 }
 
@@ -416,8 +478,7 @@ __device__ inline void store_state(Rec* r, const FState& S) {
   r->taken = enc_f64(as_bits(S.t));
   r->elapsed = S.e;
   r->created = S.c;
-  r->flags = kRecPublished;
-  r->aux = 0;
+  r->name[0] = with_flags(r->name[0], kRecPublished);
 }
 
 constexpr u32 kLongSeg = 48;
@@ -435,7 +496,7 @@ __global__ __launch_bounds__(kBlock) void k_fold_thread(
     if (cnt > kLongSeg) is_long = true;
     else {
       Rec* r = &recs[seg_slot[g]];
-      FState S = load_state(*r), S2;
+      FState S = load_state(load_rec(r)), S2;
       u32 st = seg_start[g];
       for (u32 j = 0; j < cnt; ++j) {
         u32 i = sorted_idx[st + j];
@@ -475,7 +536,7 @@ __global__ __launch_bounds__(64) void k_fold_wave(
   u32 g = long_list[w];
   const u32 lane = threadIdx.x;
   Rec* r = &recs[seg_slot[g]];
-  FState S = load_state(*r);
+  FState S = load_state(load_rec(r));
   const u32 st = seg_start[g], cnt = seg_count[g];
   u32 j0 = 0;
   while (j0 < cnt) {
@@ -511,33 +572,33 @@ __global__ void k_seg_mark(const u32* __restrict__ sorted_slot, u32 n, u32* head
 
 // ------------------------------------------------------------ seed/dump --
 // NewLocalRepo(clock, bs...): last entry of a name wins (map assignment).
-__global__ void k_seed_pick(const u32* __restrict__ slot_of, u32 n, Rec* recs) {
+__global__ void k_seed_pick(const u32* __restrict__ slot_of, u32 n, Table T) {
   u32 i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) atomicMax(&recs[slot_of[i]].aux, i + 1);
+  if (i < n) atomicMax(&T.aux[slot_of[i]], i + 1);
 }
 __global__ void k_seed_apply(const u32* __restrict__ slot_of, u32 n, const phip_state* st,
-                             Rec* recs) {
+                             Table T) {
   u32 i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  Rec* r = &recs[slot_of[i]];
-  if (r->aux != i + 1) return;
+  Rec* r = &T.recs[slot_of[i]];
+  if (T.aux[slot_of[i]] != i + 1) return;
   phip_state s = st[i];
   r->added = enc_f64(s.added);
   r->taken = enc_f64(s.taken);
   r->elapsed = s.elapsed;
   r->created = s.created;
 }
-__global__ void k_seed_finish(const u32* __restrict__ slot_of, u32 n, Rec* recs) {
+__global__ void k_seed_finish(const u32* __restrict__ slot_of, u32 n, Table T) {
   u32 i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  Rec* r = &recs[slot_of[i]];
-  r->aux = 0;
-  r->flags = kRecPublished;
+  u32 s = slot_of[i];
+  T.aux[s] = 0;
+  T.recs[s].name[0] = with_flags(T.recs[s].name[0], kRecPublished);
 }
 
-__global__ void k_dump_collect(const u64* __restrict__ tags, u64 cap, u32* list, u32* ctr) {
+__global__ void k_dump_collect(const Rec* __restrict__ recs, u64 cap, u32* list, u32* ctr) {
   u64 s = (u64)blockIdx.x * blockDim.x + threadIdx.x;
-  bool occ = s < cap && tags[s] != 0;
+  bool occ = s < cap && recs[s].tag != 0;
   u32 p = wave_append(&ctr[2], occ);
   if (occ) list[p] = (u32)s;
 }
@@ -553,9 +614,10 @@ __global__ void k_get_one(const u8* name, u32 len, Table T, Rec* out, int* found
   Name nm;
   load_name(name, 0, len, nm);
   u32 s;
-  int pr = probe(T, nm, name, &s);
+  Rec r;
+  int pr = probe(T, nm, name, &s, &r);
   *found = pr == kFound;
-  if (pr == kFound) *out = T.recs[s];
+  if (pr == kFound) *out = r;
 }
 
 }  // namespace phip
