@@ -45,7 +45,7 @@ def parse():
     p.add_argument("--warmup", type=int, default=2)
     p.add_argument("--keys", type=int, default=10_000_000)
     p.add_argument("--messages", type=int, default=100_000_000)
-    p.add_argument("--log2-slots", type=int, default=24)
+    p.add_argument("--log2-slots", type=int, default=25)
     p.add_argument("--zipf", type=float, default=1.1)
     p.add_argument("--cpu-sample", type=int, default=10_000_000)
     p.add_argument("--cpu-threads", type=int, default=0)

@@ -132,28 +132,34 @@ __host__ __device__ inline bool state_is_zero(u64 a_bits, u64 t_bits, i64 e) {
 
 // ------------------------------------------------------------ table -----
 // One 64-byte slot record = one HBM burst holding everything a lookup and a
-// merge touch: probe tag, state, canonical name.
-//   tag          FNV-1a 64 of the name (0 = empty slot; a 0 hash is stored as 1)
-//   added/taken  E-encoded float64
-//   name[0..2]   byte 0 = len, byte 1 = flags (kRec*), then
-//                len <= 22: bytes 2..2+len = the name, zero padded;
-//                len  > 22: bytes 4..7 = arena offset, bytes 8..23 = first 16
-//                bytes (fast reject), full name in the arena.
+// merge touch, ordered so that the Receive fast path reads only the first
+// 48 bytes (three 16-byte loads) for names of up to 14 bytes:
+//   [ 0,16) tag, added     tag = FNV-1a 64 of the name (0 = empty; a 0 hash is stored as 1)
+//   [16,32) taken, elapsed added/taken are E-encoded float64
+//   [32,48) name0, name1   canonical name words 0-1
+//   [48,64) created, name2 canonical name word 2
+// Canonical name (24 bytes, words name0..name2): byte 0 = len, byte 1 = flags
+// (kRec*), then len <= 22: bytes 2..2+len = the name, zero padded (names of
+// up to 14 bytes end in name1, so name2 = 0); len > 22: bytes 4..7 = arena
+// offset, bytes 8..23 = the first 16 bytes (fast reject), full name in the arena.
 struct alignas(64) Rec {
   u64 tag;
   u64 added;
   u64 taken;
   i64 elapsed;
+  u64 name0;
+  u64 name1;
   i64 created;
-  u64 name[3];
+  u64 name2;
 };
 static_assert(sizeof(Rec) == 64, "slot record must be one 64-byte burst");
 
 constexpr u32 kInlineName = 22;
+constexpr u32 kShortName = 14;     // fits name0/name1: the 48-byte fast path
 constexpr u64 kRecPublished = 1u;   // name and state written (visible after a kernel boundary)
 constexpr u64 kRecNew = 2u;         // created by the current batch
 
-__host__ __device__ inline u32 rec_flags(const Rec& r) { return (u32)((r.name[0] >> 8) & 0xFFu); }
+__host__ __device__ inline u32 rec_flags(const Rec& r) { return (u32)((r.name0 >> 8) & 0xFFu); }
 __host__ __device__ inline u64 with_flags(u64 w0, u64 f) { return (w0 & ~0xFF00ull) | (f << 8); }
 
 constexpr u64 kFnvOffset = 0xcbf29ce484222325ull;

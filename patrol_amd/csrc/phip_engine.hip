@@ -644,7 +644,7 @@ int phip_dump(phip_handle* h, uint8_t* names, uint64_t names_cap, uint64_t* name
     HIPCHK(h, hipMemcpy(arena.data(), h->arena, cursor, hipMemcpyDeviceToHost));
   }
   u64 total = 0;
-  for (auto& r : recs) total += r.name[0] & 0xFF;   // byte 0 = length
+  for (auto& r : recs) total += r.name0 & 0xFF;   // byte 0 = length
   if (n_out) *n_out = n;
   if (names_bytes_out) *names_bytes_out = total;
   if (!names) return PHIP_OK;
@@ -653,12 +653,13 @@ int phip_dump(phip_handle* h, uint8_t* names, uint64_t names_cap, uint64_t* name
   u64 o = 0;
   for (u32 k = 0; k < n; ++k) {
     const Rec& r = recs[k];
-    u32 len = r.name[0] & 0xFF;
+    u32 len = r.name0 & 0xFF;
     name_offs[k] = o;
     if (len <= kInlineName) {
-      for (u32 j = 0; j < len; ++j) names[o + j] = (u8)(r.name[(j + 2) >> 3] >> (((j + 2) & 7) * 8));
+      const u64 w[3] = {r.name0, r.name1, r.name2};
+      for (u32 j = 0; j < len; ++j) names[o + j] = (u8)(w[(j + 2) >> 3] >> (((j + 2) & 7) * 8));
     } else {
-      u64 aoff = r.name[0] >> 32;
+      u64 aoff = r.name0 >> 32;
       if (aoff + len <= arena.size()) std::memcpy(names + o, arena.data() + aoff, len);
     }
     o += len;

@@ -11,13 +11,22 @@ namespace phip {
 
 constexpr int kBlock = 256;
 
+// Streaming loads, optionally non-temporal (read-once batch data should not
+// push hot slot records out of the XCD's L2).
+template <bool NT, class T>
+__device__ inline T ld(const T* p) {
+  if constexpr (NT) return __builtin_nontemporal_load(p);
+  else return *p;
+}
+
 // ---------------------------------------------------------- name sources --
 // Decoded messages: names[offs[i] .. offs[i+1]).
 struct NamesOffs {
   const u8* blob;
   const u32* offs;
+  template <bool NT = false>
   __device__ inline void get(u32 i, u64& off, u32& len) const {
-    u32 a = offs[i], b = offs[i + 1];
+    u32 a = ld<NT>(offs + i), b = ld<NT>(offs + i + 1);
     off = a;
     len = b - a;
   }
@@ -27,11 +36,40 @@ struct NamesPairs {
   const u8* blob;
   const uint64_t* off;
   const u8* len;
+  template <bool NT = false>
   __device__ inline void get(u32 i, u64& o, u32& l) const {
-    o = off[i];
-    l = len[i];
+    o = ld<NT>(off + i);
+    l = ld<NT>(len + i);
   }
 };
+
+// Name read with aligned 8-byte loads (up to 4 per name) instead of one
+// byte load per character.  Needs the blob 8-byte aligned and readable up to
+// the next 8-byte boundary past its last name (the ABI's slack rule).
+template <bool NT>
+__device__ inline void load_name_wide(const u8* src, u64 off, u32 len, Name& nm) {
+  if (len > kInlineName) { load_name(src, off, len, nm); return; }
+  const u32 sh = (u32)(off & 7) * 8;
+  const u32 nw = ((u32)(off & 7) + len + 7) >> 3;
+  const u64* p = reinterpret_cast<const u64*>(src + (off & ~7ull));
+  const u64 w0 = nw > 0 ? ld<NT>(p) : 0, w1 = nw > 1 ? ld<NT>(p + 1) : 0;
+  const u64 w2 = nw > 2 ? ld<NT>(p + 2) : 0, w3 = nw > 3 ? ld<NT>(p + 3) : 0;
+  u64 b0 = sh ? (w0 >> sh) | (w1 << (64 - sh)) : w0;
+  u64 b1 = sh ? (w1 >> sh) | (w2 << (64 - sh)) : w1;
+  u64 b2 = sh ? (w2 >> sh) | (w3 << (64 - sh)) : w2;
+  if (len < 8) { b0 = len ? b0 & ((1ull << (8 * len)) - 1) : 0; b1 = 0; b2 = 0; }
+  else if (len < 16) { b1 = len > 8 ? b1 & ((1ull << (8 * (len - 8))) - 1) : 0; b2 = 0; }
+  else if (len < 24) { b2 = len > 16 ? b2 & ((1ull << (8 * (len - 16))) - 1) : 0; }
+  u64 h = kFnvOffset;
+  for (u32 k = 0; k < len; ++k) {
+    const u64 w = k < 8 ? b0 : (k < 16 ? b1 : b2);
+    h = fnv_step(h, (u8)(w >> ((k & 7) * 8)));
+  }
+  nm.h = h; nm.len = len; nm.off = off;
+  nm.w0 = (u64)len | (b0 << 16);           // name byte k sits at canonical byte k+2
+  nm.w1 = (b0 >> 48) | (b1 << 16);
+  nm.w2 = (b1 >> 48) | (b2 << 16);
+}
 
 // Wave-aggregated append: returns this lane's position in `list`.
 __device__ inline u32 wave_append(u32* counter, bool pred) {
@@ -48,11 +86,11 @@ __device__ inline u32 wave_append(u32* counter, bool pred) {
 
 // Full-name equality for a candidate record (names > 22 bytes live in the arena).
 __device__ inline bool name_equal(const Rec& r, const Name& nm, const u8* src, const u8* arena) {
-  const u64 r0 = r.name[0] & ~0xFF00ull;   // drop the flags byte
+  const u64 r0 = r.name0 & ~0xFF00ull;   // drop the flags byte
   if ((r0 & 0xFFu) != (nm.w0 & 0xFFu)) return false;
-  if (nm.len <= kInlineName) return r0 == nm.w0 && r.name[1] == nm.w1 && r.name[2] == nm.w2;
-  if (r.name[1] != nm.w1 || r.name[2] != nm.w2) return false;
-  u64 aoff = r.name[0] >> 32;
+  if (nm.len <= kInlineName) return r0 == nm.w0 && r.name1 == nm.w1 && r.name2 == nm.w2;
+  if (r.name1 != nm.w1 || r.name2 != nm.w2) return false;
+  u64 aoff = r.name0 >> 32;
   for (u32 k = 16; k < nm.len; ++k)
     if (arena[aoff + k] != src[nm.off + k]) return false;
   return true;
@@ -84,22 +122,41 @@ __device__ inline Rec load_rec(const Rec* p) {
   r.added = ((u64)a.w << 32) | a.z;
   r.taken = ((u64)b.y << 32) | b.x;
   r.elapsed = (i64)(((u64)b.w << 32) | b.z);
-  r.created = (i64)(((u64)c.y << 32) | c.x);
-  r.name[0] = ((u64)c.w << 32) | c.z;
-  r.name[1] = ((u64)d.y << 32) | d.x;
-  r.name[2] = ((u64)d.w << 32) | d.z;
+  r.name0 = ((u64)c.y << 32) | c.x;
+  r.name1 = ((u64)c.w << 32) | c.z;
+  r.created = (i64)(((u64)d.y << 32) | d.x);
+  r.name2 = ((u64)d.w << 32) | d.z;
   return r;
 }
 
-// Look the name up.  kFound: *slot = its slot and *rec = its contents.
+// The first 48 bytes only (tag, state, name words 0-1); name2 and created
+// are left 0.  Enough to find and merge a name of <= kShortName bytes.
+__device__ inline Rec load_rec48(const Rec* p) {
+  const uint4* q = reinterpret_cast<const uint4*>(p);
+  uint4 a = q[0], b = q[1], c = q[2];
+  Rec r;
+  r.tag = ((u64)a.y << 32) | a.x;
+  r.added = ((u64)a.w << 32) | a.z;
+  r.taken = ((u64)b.y << 32) | b.x;
+  r.elapsed = (i64)(((u64)b.w << 32) | b.z);
+  r.name0 = ((u64)c.y << 32) | c.x;
+  r.name1 = ((u64)c.w << 32) | c.z;
+  r.created = 0;
+  r.name2 = 0;
+  return r;
+}
+
+// Look the name up.  kFound: *slot = its slot and *rec = its contents (for
+// names of <= kShortName bytes only the first 48 bytes: created/name2 = 0).
 // kMiss: not present.  kPending: a same-tag slot is claimed but not yet
 // published (only seen by insert rounds).
 __device__ inline int probe(const Table& T, const Name& nm, const u8* src, u32* slot, Rec* rec) {
   const u64 tag = T.tag(nm.h);
   const u32 mask = T.mask();
   u32 s = T.home(tag);
+  const bool shortname = nm.len <= kShortName;
   for (u32 k = 0; k <= mask; ++k) {
-    Rec r = load_rec(&T.recs[s]);
+    Rec r = shortname ? load_rec48(&T.recs[s]) : load_rec(&T.recs[s]);
     if (r.tag == 0) return kMiss;
     if (r.tag == tag) {
       if (!(rec_flags(r) & kRecPublished)) return kPending;
@@ -144,74 +201,107 @@ __global__ void k_classify(const uint64_t* __restrict__ a, const uint64_t* __res
 // a Zipf-hot bucket at one atomic per workgroup instead of one per message.
 // Misses are appended to `miss` (insert pipeline, then this kernel again on
 // the miss list with `track_new`).
-constexpr u32 kCombSlots = 2 * kBlock;
 constexpr u32 kCombEmpty = 0xFFFFFFFFu;
 
-template <class Src>
+// Variant bits (tools/ubench_receive.hip times the combinations).
+constexpr int kFastCombine = 1;   // LDS per-slot combining before atomics
+constexpr int kFastNT = 2;        // non-temporal streaming loads
+constexpr int kFastWide = 4;      // 8-byte-word name loads
+constexpr int kFastSkip = 8;      // skip the flush when no lane of the block needs an atomic
+constexpr int kFastSmall = 16;    // LDS combining table of kBlock entries (else 2*kBlock)
+constexpr int kFastNoSeen = 32;   // flush every contributed field (no per-entry seen state)
+constexpr int kFastOpt = kFastCombine | kFastNT | kFastWide | kFastSkip | kFastSmall | kFastNoSeen;
+
+template <class Src, int OPT = kFastOpt, int PER = 1>
 __global__ __launch_bounds__(kBlock) void k_receive_fast(
     Src src, const uint64_t* __restrict__ ma, const uint64_t* __restrict__ mt,
     const int64_t* __restrict__ me,
     u32 n, const u32* __restrict__ list, Table T, u8* __restrict__ status, u32* miss, u32* ctr,
     int track_new) {
-  __shared__ u32 ckey[kCombSlots];
-  __shared__ u64 cmax[3][kCombSlots];   // combined replica maxima (elapsed biased by 2^63)
-  __shared__ u64 cseen[3][kCombSlots];  // state seen by the lane that opened the entry
-  for (u32 j = threadIdx.x; j < kCombSlots; j += kBlock) {
-    ckey[j] = kCombEmpty;
-    cmax[0][j] = 0; cmax[1][j] = 0; cmax[2][j] = 0;
-  }
-  __syncthreads();
-
-  u32 tid = blockIdx.x * blockDim.x + threadIdx.x;
-  bool missed = false;
-  u32 i = 0;
-  if (tid < n) {
-    i = list ? list[tid] : tid;
-    u64 off; u32 len;
-    src.get(i, off, len);
-    Name nm;
-    load_name(src.blob, off, len, nm);
-    const u64 ea = enc_replica(ma[i]), et = enc_replica(mt[i]);
-    const u64 ee = (u64)me[i] ^ kSign;
-    u32 s;
-    Rec cur;
-    int pr = probe(T, nm, src.blob, &s, &cur);
-    if (pr == kFound) {
-      const u64 ua = cur.added, ut = cur.taken, ue = (u64)cur.elapsed ^ kSign;
-      const bool ga = ea > ua, gt = et > ut, ge = ee > ue;
-      if (ga || gt || ge) {
-        u32 h = (s * 2654435761u) >> (32 - 9);
-        for (;;) {
-          u32 old = atomicCAS(&ckey[h], kCombEmpty, s);
-          if (old == kCombEmpty) {
-            cseen[0][h] = ua; cseen[1][h] = ut; cseen[2][h] = ue;
-            break;
-          }
-          if (old == s) break;
-          h = (h + 1) & (kCombSlots - 1);
-        }
-        if (ga) atomicMax(&cmax[0][h], ea);
-        if (gt) atomicMax(&cmax[1][h], et);
-        if (ge) atomicMax(&cmax[2][h], ee);
-      }
-      if (track_new && (rec_flags(cur) & kRecNew)) atomicMin(&T.aux[s], i);
-      if (status) status[i] = PHIP_ST_MERGED;
-    } else {
-      missed = true;
-      if (pr == kFull) atomicOr(&ctr[8], 1u);
+  constexpr bool kComb = OPT & kFastCombine, kNT = OPT & kFastNT, kWide = OPT & kFastWide;
+  constexpr bool kSkip = OPT & kFastSkip, kSeen = !(OPT & kFastNoSeen);
+  constexpr u32 kSlots = kComb ? ((OPT & kFastSmall) ? kBlock * PER : 2 * kBlock * PER) : 1;
+  constexpr u32 kBits = kSlots >= 2048 ? 11 : kSlots >= 1024 ? 10 : kSlots >= 512 ? 9 : 8;
+  __shared__ u32 ckey[kSlots];
+  __shared__ u64 cmax[3][kSlots];    // combined maxima (elapsed biased by 2^63)
+  __shared__ u64 cseen[3][kSeen ? kSlots : 1];   // state seen by the lane that opened the entry
+  if constexpr (kComb) {
+    for (u32 j = threadIdx.x; j < kSlots; j += kBlock) {
+      ckey[j] = kCombEmpty;
+      cmax[0][j] = 0; cmax[1][j] = 0; cmax[2][j] = 0;
     }
+    __syncthreads();
   }
-  u32 pos = wave_append(&ctr[2], missed);
-  if (missed) miss[pos] = i;
+  bool any_need = false;
+#pragma unroll
+  for (int p = 0; p < PER; ++p) {
+    const u32 tid = (blockIdx.x * PER + p) * kBlock + threadIdx.x;
+    bool missed = false;
+    u32 i = 0;
+    if (tid < n) {
+      i = list ? list[tid] : tid;
+      u64 off; u32 len;
+      src.template get<kNT>(i, off, len);
+      Name nm;
+      if constexpr (kWide) load_name_wide<kNT>(src.blob, off, len, nm);
+      else load_name(src.blob, off, len, nm);
+      const u64 ea = enc_replica(ld<kNT>(ma + i)), et = enc_replica(ld<kNT>(mt + i));
+      const u64 ee = (u64)ld<kNT>(me + i) ^ kSign;
+      u32 s;
+      Rec cur;
+      int pr = probe(T, nm, src.blob, &s, &cur);
+      if (pr == kFound) {
+        const u64 ua = cur.added, ut = cur.taken, ue = (u64)cur.elapsed ^ kSign;
+        const bool ga = ea > ua, gt = et > ut, ge = ee > ue;
+        if (!kComb) {
+          Rec* r = &T.recs[s];
+          if (ga) atomicMax(&r->added, ea);
+          if (gt) atomicMax(&r->taken, et);
+          if (ge) atomicMax(&r->elapsed, (i64)(ee ^ kSign));
+        } else if (ga || gt || ge) {
+          any_need = true;
+          u32 h = (s * 2654435761u) >> (32 - kBits);
+          for (;;) {
+            u32 old = atomicCAS(&ckey[h], kCombEmpty, s);
+            if (old == kCombEmpty) {
+              if constexpr (kSeen) { cseen[0][h] = ua; cseen[1][h] = ut; cseen[2][h] = ue; }
+              break;
+            }
+            if (old == s) break;
+            h = (h + 1) & (kSlots - 1);
+          }
+          if (ga) atomicMax(&cmax[0][h], ea);
+          if (gt) atomicMax(&cmax[1][h], et);
+          if (ge) atomicMax(&cmax[2][h], ee);
+        }
+        if (track_new && (rec_flags(cur) & kRecNew)) atomicMin(&T.aux[s], i);
+        if (status) status[i] = PHIP_ST_MERGED;
+      } else {
+        missed = true;
+        if (pr == kFull) atomicOr(&ctr[8], 1u);
+      }
+    }
+    u32 pos = wave_append(&ctr[2], missed);
+    if (missed) miss[pos] = i;
+  }
 
-  __syncthreads();
-  for (u32 j = threadIdx.x; j < kCombSlots; j += kBlock) {
-    u32 s = ckey[j];
-    if (s == kCombEmpty) continue;
-    Rec* r = &T.recs[s];
-    if (cmax[0][j] > cseen[0][j]) atomicMax(&r->added, cmax[0][j]);
-    if (cmax[1][j] > cseen[1][j]) atomicMax(&r->taken, cmax[1][j]);
-    if (cmax[2][j] > cseen[2][j]) atomicMax(&r->elapsed, (i64)(cmax[2][j] ^ kSign));
+  if constexpr (kComb) {
+    if constexpr (kSkip) {
+      if (!__syncthreads_or(any_need)) return;
+    } else {
+      __syncthreads();
+    }
+    for (u32 j = threadIdx.x; j < kSlots; j += kBlock) {
+      u32 s = ckey[j];
+      if (s == kCombEmpty) continue;
+      Rec* r = &T.recs[s];
+      // A field's maximum is non-zero only if some lane saw it grow.
+      const u64 sa = kSeen ? cseen[0][j] : 0, st = kSeen ? cseen[1][j] : 0;
+      const u64 se = kSeen ? cseen[2][j] : 0;
+      if (cmax[0][j] > sa) atomicMax(&r->added, cmax[0][j]);
+      if (cmax[1][j] > st) atomicMax(&r->taken, cmax[1][j]);
+      if (cmax[2][j] > se) atomicMax(&r->elapsed, (i64)(cmax[2][j] ^ kSign));
+    }
   }
 }
 
@@ -326,14 +416,14 @@ __global__ void k_publish(Src src, u32 base, u32 n, const u32* __restrict__ clai
   r.taken = kEPosZero;
   r.elapsed = 0;
   r.created = now_arr ? now_arr[i] : now0;
-  r.name[0] = nm.w0; r.name[1] = nm.w1; r.name[2] = nm.w2;
+  r.name0 = nm.w0; r.name1 = nm.w1; r.name2 = nm.w2;
   if (len > kInlineName) {
     u64 a = atomicAdd(arena_cursor, (u64)len);
     if (a + len > arena_cap) { atomicOr(&ctr[7], 1u); a = 0; }
     else for (u32 k = 0; k < len; ++k) arena[a + k] = src.blob[off + k];
-    r.name[0] = (nm.w0 & 0xFFu) | (a << 32);
+    r.name0 = (nm.w0 & 0xFFu) | (a << 32);
   }
-  r.name[0] = with_flags(r.name[0], kRecPublished | kRecNew);
+  r.name0 = with_flags(r.name0, kRecPublished | kRecNew);
   T.recs[s] = r;
   T.aux[s] = 0xFFFFFFFFu;
 }
@@ -343,7 +433,7 @@ __global__ void k_clear_new(const u32* __restrict__ claimed_slot, u32 n, Table T
   if (tid >= n) return;
   u32 s = claimed_slot[tid];
   Rec* r = &T.recs[s];
-  r->name[0] = with_flags(r->name[0], kRecPublished);
+  r->name0 = with_flags(r->name0, kRecPublished);
   T.aux[s] = 0;
 }
 
@@ -478,7 +568,7 @@ __device__ inline void store_state(Rec* r, const FState& S) {
   r->taken = enc_f64(as_bits(S.t));
   r->elapsed = S.e;
   r->created = S.c;
-  r->name[0] = with_flags(r->name[0], kRecPublished);
+  r->name0 = with_flags(r->name0, kRecPublished);
 }
 
 constexpr u32 kLongSeg = 48;
@@ -593,7 +683,7 @@ __global__ void k_seed_finish(const u32* __restrict__ slot_of, u32 n, Table T) {
   if (i >= n) return;
   u32 s = slot_of[i];
   T.aux[s] = 0;
-  T.recs[s].name[0] = with_flags(T.recs[s].name[0], kRecPublished);
+  T.recs[s].name0 = with_flags(T.recs[s].name0, kRecPublished);
 }
 
 __global__ void k_dump_collect(const Rec* __restrict__ recs, u64 cap, u32* list, u32* ctr) {
@@ -617,7 +707,7 @@ __global__ void k_get_one(const u8* name, u32 len, Table T, Rec* out, int* found
   Rec r;
   int pr = probe(T, nm, name, &s, &r);
   *found = pr == kFound;
-  if (pr == kFound) *out = r;
+  if (pr == kFound) *out = load_rec(&T.recs[s]);   // probe's copy may be the 48-byte view
 }
 
 }  // namespace phip

@@ -111,68 +111,6 @@ __global__ void v0_count(NamesOffs src, const uint64_t* ma, const uint64_t* mt, 
 }
 
 
-// V7: per-lane probe that loads only the first 16 bytes (tag, added): how much
-// of the resolve cost is the 4x16-byte record load per lane?
-__global__ void v7_tag16(NamesOffs src, u32 n, Table T, u32* slot_out) {
-  u32 i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  u64 off; u32 len;
-  src.get(i, off, len);
-  Name nm;
-  load_name(src.blob, off, len, nm);
-  const u64 tag = T.tag(nm.h);
-  u32 s = T.home(tag);
-  for (u32 k = 0; k < 64; ++k) {
-    uint4 a = reinterpret_cast<const uint4*>(&T.recs[s])[0];
-    u64 t = ((u64)a.y << 32) | a.x;
-    if (t == tag || t == 0) break;
-    s = (s + 1) & T.mask();
-  }
-  slot_out[i] = s;
-}
-
-// V8: quad-cooperative resolve: 4 lanes fetch one 64-byte record with one
-// dwordx4 each (16 records per wave instruction instead of 64 x 4).
-__global__ __launch_bounds__(256) void v8_quad(NamesOffs src, u32 n, Table T, u32* slot_out) {
-  u32 i = blockIdx.x * blockDim.x + threadIdx.x;
-  const u32 lane = __lane_id(), q = lane & 3, qb = lane & ~3u;
-  Name nm;
-  nm.w0 = nm.w1 = nm.w2 = 0; nm.h = 0; nm.len = 0; nm.off = 0;
-  if (i < n) {
-    u64 off; u32 len;
-    src.get(i, off, len);
-    load_name(src.blob, off, len, nm);
-  }
-  const u64 mytag = T.tag(nm.h);
-  const u32 myhome = T.home(mytag);
-  u32 result = 0xFFFFFFFFu;
-  for (u32 r = 0; r < 4; ++r) {
-    const int sl = 16 * r + (lane >> 2);
-    const u64 tag = __shfl(mytag, sl);
-    u32 s = __shfl(myhome, sl);
-    const u64 w0 = __shfl(nm.w0, sl), w1 = __shfl(nm.w1, sl), w2 = __shfl(nm.w2, sl);
-    const bool valid = (blockIdx.x * blockDim.x + (threadIdx.x & ~63u) + sl) < n;
-    bool done = !valid;
-    u32 found = 0xFFFFFFFFu;
-    for (u32 k = 0; k < 64 && __any(!done); ++k) {
-      uint4 c = make_uint4(0, 0, 0, 0);
-      if (!done) c = reinterpret_cast<const uint4*>(&T.recs[s])[q];
-      u64 lo = ((u64)c.y << 32) | c.x, hi = ((u64)c.w << 32) | c.z;
-      u64 rtag = __shfl(lo, qb + 0);
-      u64 n0 = __shfl(hi, qb + 2), n1 = __shfl(lo, qb + 3), n2 = __shfl(hi, qb + 3);
-      if (!done) {
-        if (rtag == 0) done = true;
-        else if (rtag == tag && (n0 & ~0xFF00ull) == w0 && n1 == w1 && n2 == w2) { done = true; found = s; }
-        else s = (s + 1) & T.mask();
-      }
-    }
-    if ((lane >> 2) == (u32)(lane >> 2) && q == 0) { /* quad leader owns the result */ }
-    u32 fr = __shfl(found, (int)(((lane & 15) << 2)));  // message (16r + (lane&15)) lives in quad lane&15
-    if ((lane >> 4) == r) result = fr;
-  }
-  if (i < n) slot_out[i] = result;
-}
-
 static u64 host_fnv(const char* p, size_t n) {
   u64 h = kFnvOffset;
   for (size_t k = 0; k < n; ++k) h = fnv_step(h, (u8)p[k]);
@@ -201,7 +139,7 @@ int main(int argc, char** argv) {
     r.added = kEPosZero; r.taken = kEPosZero; r.elapsed = 0; r.created = 0;
     Name nm;
     load_name((const u8*)buf, 0, len, nm);
-    r.name[0] = with_flags(nm.w0, kRecPublished); r.name[1] = nm.w1; r.name[2] = nm.w2;
+    r.name0 = with_flags(nm.w0, kRecPublished); r.name1 = nm.w1; r.name2 = nm.w2;
   }
   // --- messages
   std::vector<double> cdf(K);
@@ -233,7 +171,7 @@ int main(int argc, char** argv) {
       int len = snprintf(buf, sizeof buf, "b%u", id);
       u64 tag = tag_of(host_fnv(buf, len));
       u32 s = (u32)((tag * 0x9E3779B97F4A7C15ull) >> (64 - L));
-      while (recs[s].tag != tag || ((recs[s].name[0] & 0xFF) != (u64)len)) s = (s + 1) & (cap - 1);
+      while (recs[s].tag != tag || ((recs[s].name0 & 0xFF) != (u64)len)) s = (s + 1) & (cap - 1);
       slot_of_id[id] = s;
     }
     for (u32 i = 0; i < n; ++i) slot[i] = slot_of_id[ids[i]];
@@ -286,7 +224,7 @@ int main(int argc, char** argv) {
   };
   u32* miss; CK(hipMalloc(&miss, n * 4ull));
   u32* dslot2; CK(hipMalloc(&dslot2, n * 4ull));
-  for (int rep = 0; rep < 2; ++rep) {
+  for (int rep = 0; rep < 1; ++rep) {
     timeit("V0 product k_receive_fast", [&] {
       k_receive_fast<NamesOffs><<<G, 256>>>(src, da, dt, de, n, nullptr, T, nullptr, miss, ctr, 0); }, true);
     timeit("V0-old (no combine, counting)", [&] { v0_count<<<G, 256>>>(src, da, dt, de, n, T, ctr); }, true);
@@ -295,15 +233,15 @@ int main(int argc, char** argv) {
     timeit("V2 slot given + atomics", [&] { v2_slot<<<G, 256>>>(dslot, da, dt, de, n, T, ctr); }, true);
     timeit("V3 name+hash only", [&] { v3_hash<<<G, 256>>>(src, n, sink); }, false);
     timeit("V4 resolve only", [&] { v4_resolve<<<G, 256>>>(src, n, T, miss); }, false);
-    timeit("V7 probe loading 16 B only", [&] { v7_tag16<<<G, 256>>>(src, n, T, miss); }, false);
-    timeit("V8 quad-cooperative resolve", [&] { v8_quad<<<G, 256>>>(src, n, T, dslot2); }, false);
-  }
-  {
-    std::vector<u32> got(n);
-    CK(hipMemcpy(got.data(), dslot2, n * 4ull, hipMemcpyDeviceToHost));
-    u64 bad = 0;
-    for (u32 i = 0; i < n; ++i) bad += got[i] != slot[i];
-    printf("V8 slots wrong: %llu of %u\n", (unsigned long long)bad, n);
+#define VAR(OPT, PER, label) \
+    timeit("P" #OPT "x" #PER " " label " fresh", [&] { CK(hipMemset(ctr + 512, 0, 4)); \
+      k_receive_fast<NamesOffs, OPT, PER><<<(n + 256 * PER - 1) / (256 * PER), 256>>>(src, da, dt, de, n, nullptr, T, nullptr, miss, ctr + 512, 0); }, true); \
+    timeit("P" #OPT "x" #PER " " label " no-op", [&] { CK(hipMemset(ctr + 512, 0, 4)); \
+      k_receive_fast<NamesOffs, OPT, PER><<<(n + 256 * PER - 1) / (256 * PER), 256>>>(src, da, dt, de, n, nullptr, T, nullptr, miss, ctr + 512, 0); }, false);
+    VAR(31, 1, "c+nt+wide+skip+small")
+    VAR(63, 1, "c+nt+wide+skip+small+noseen")
+    VAR(61, 1, "c+wide+skip+small+noseen")
+    VAR(47, 1, "c+nt+wide+skip+noseen")
   }
   return 0;
 }
