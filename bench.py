@@ -51,6 +51,8 @@ def parse():
     p.add_argument("--cpu-threads", type=int, default=0)
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--seed", type=int, default=1234)
+    p.add_argument("--dist-backend", default="nccl",
+                   help="nccl (= RCCL on ROCm) for real runs; gloo to rehearse several ranks on one GPU")
     return p.parse_args()
 
 
@@ -160,11 +162,11 @@ def main():
     import torch.distributed as dist
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        dist.init_process_group("nccl", init_method="env://")
+    local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group(args.dist_backend, init_method="env://")
     import patrol_amd
 
     K, n = args.keys, args.messages
@@ -210,7 +212,8 @@ def main():
     el = time.perf_counter() - t0
     repo.set_timing(False)
     if world > 1:
-        tt = torch.tensor([el], dtype=torch.float64, device=dev)
+        tt = torch.tensor([el], dtype=torch.float64,
+                          device=dev if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         el = float(tt.item())
 

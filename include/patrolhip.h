@@ -206,6 +206,13 @@ int phip_api_take(phip_handle* h, const uint8_t* name, uint32_t len, const char*
                   uint32_t rate_len, const char* count, uint32_t count_len, int64_t now,
                   char* body, uint32_t* body_len);
 
+/* ---- shard layer ---- */
+/* FNV-1a 64 of each name (the table's probe key; also the shard map:
+ * owner = ((hash >> 32) * world) >> 32).  Host pointers need no GPU (h may be
+ * NULL); with PHIP_DEVICE_PTRS the hashes are computed on h's GPU. */
+int phip_hash_names(phip_handle* h, const uint8_t* names, const uint32_t* name_offs, uint32_t n,
+                    uint64_t* out, uint32_t flags);
+
 /* ---- diagnostics ---- */
 /* Per-kernel timing of the last hot-path call, measured with HIP events on
  * the handle's stream: writes up to max entries of (name, ms) and returns the

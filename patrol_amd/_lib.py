@@ -17,7 +17,7 @@ EXPORTS = [
     "phip_abi_version", "phip_open", "phip_close", "phip_last_error", "phip_flush", "phip_len",
     "phip_capacity", "phip_seed", "phip_get", "phip_dump", "phip_receive_datagrams",
     "phip_receive_soa", "phip_upsert_soa", "phip_apply_mixed", "phip_take", "phip_parse_rate",
-    "phip_marshal", "phip_api_take", "phip_last_timings", "phip_set_timing",
+    "phip_marshal", "phip_api_take", "phip_last_timings", "phip_set_timing", "phip_hash_names",
 ]
 
 PHIP_OK = 0
@@ -95,6 +95,7 @@ def load(path: str = LIB_PATH):
     L.phip_api_take.argtypes = [vp, C.c_char_p, u32, C.c_char_p, u32, C.c_char_p, u32, i64,
                                 C.c_char_p, C.POINTER(u32)]
     L.phip_last_timings.argtypes = [vp, C.POINTER(C.c_char_p), C.POINTER(C.c_float), C.c_int]
+    L.phip_hash_names.argtypes = [vp, vp, vp, u32, vp, u32]
     L.phip_set_timing.argtypes = [vp, C.c_int]
     L.phip_set_timing.restype = None
     _lib = L

@@ -831,6 +831,27 @@ int phip_take(phip_handle* h, const uint8_t* names, const uint32_t* name_offs, u
   return PHIP_OK;
 }
 
+int phip_hash_names(phip_handle* h, const uint8_t* names, const uint32_t* name_offs, uint32_t n,
+                    uint64_t* out, uint32_t flags) {
+  if ((n && (!names || !name_offs)) || (n && !out)) return PHIP_ERR_INVALID;
+  if (!(flags & PHIP_DEVICE_PTRS)) {
+    for (u32 i = 0; i < n; ++i) {
+      u64 hh = kFnvOffset;
+      for (u32 k = name_offs[i]; k < name_offs[i + 1]; ++k) hh = fnv_step(hh, names[k]);
+      out[i] = hh;
+    }
+    return PHIP_OK;
+  }
+  if (!h) return PHIP_ERR_INVALID;
+  std::lock_guard<std::mutex> g(h->mu);
+  begin_call(h);
+  if (n == 0) return PHIP_OK;
+  k_hash_names<<<grid_for(n), kBlock, 0, h->stream>>>(NamesOffs{names, name_offs}, n, out);
+  HIPCHK(h, hipGetLastError());
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  return PHIP_OK;
+}
+
 int phip_last_timings(phip_handle* h, const char** names, float* ms, int max) {
   if (!h) return 0;
   std::lock_guard<std::mutex> g(h->mu);

@@ -698,6 +698,17 @@ __global__ void k_dump_gather(const u32* __restrict__ list, u32 n, const Rec* __
   if (i < n) out[i] = recs[list[i]];
 }
 
+// FNV-1a 64 of every name (phip_hash_names): the probe key and the shard map.
+__global__ void k_hash_names(NamesOffs src, u32 n, uint64_t* out) {
+  u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  u64 off; u32 len;
+  src.get(i, off, len);
+  Name nm;
+  load_name(src.blob, off, len, nm);
+  out[i] = nm.h;
+}
+
 // Single lookup (phip_get).
 __global__ void k_get_one(const u8* name, u32 len, Table T, Rec* out, int* found) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
