@@ -51,6 +51,9 @@ def parse():
     p.add_argument("--cpu-threads", type=int, default=0)
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--seed", type=int, default=1234)
+    p.add_argument("--workload", default="c2", choices=["c2", "c3"],
+                   help="c2: batched Receive merges (headline); c3: mixed Take+Merge stream")
+    p.add_argument("--ops", type=int, default=50_000_000, help="c3: ops per step")
     p.add_argument("--dist-backend", default="nccl",
                    help="nccl (= RCCL on ROCm) for real runs; gloo to rehearse several ranks on one GPU")
     return p.parse_args()
@@ -156,6 +159,33 @@ def pmc_traffic(workload):
     return None
 
 
+def run_c3(args, torch, dev, repo, rank, K, base, gen):
+    """n ops, 50% Take(rate=100:1s, count=1) / 50% received
+    replica states, interleaved by seq, Zipf over the K buckets; now = t0 +
+    seq*20ns (+1 s per step).  Per-bucket order is the op order."""
+    n = args.ops
+    ids = zipf_ids(torch, gen, n, K, args.zipf, dev)
+    blob, offs = names_for_ids(torch, ids + base)
+    kind = (torch.rand(n, device=dev, generator=gen) < 0.5).to(torch.uint8)   # 0 take, 1 receive
+    freq = torch.full((n,), 100, dtype=torch.int64, device=dev)
+    per = torch.full((n,), 10**9, dtype=torch.int64, device=dev)
+    cnt = torch.ones(n, dtype=torch.int64, device=dev)
+    seq_now = torch.arange(n, dtype=torch.int64, device=dev) * 20
+    steps = []
+    for j in range(args.warmup + args.steps):
+        a, t, e = replica_states(torch, gen, n, j, dev)
+        steps.append((T0 + j * 10**9 + seq_now, a, t, e))
+    status = torch.empty(n, dtype=torch.uint8, device=dev)
+    rem = torch.empty(n, dtype=torch.int64, device=dev)
+    torch.cuda.synchronize()
+
+    def step(j):
+        now, a, t, e = steps[j]
+        repo.apply_mixed_device(n, kind, blob, offs, now, freq, per, cnt, a, t, e,
+                                status=status, remaining=rem)
+    return n, step
+
+
 def main():
     args = parse()
     import torch
@@ -185,14 +215,18 @@ def main():
     del kb, ko, st, keys
     assert len(repo) == K
 
-    ids = zipf_ids(torch, gen, n, K, args.zipf, dev)
-    blob, offs = names_for_ids(torch, ids + base)
-    batches = [replica_states(torch, gen, n, j, dev) for j in range(args.warmup + args.steps)]
-    torch.cuda.synchronize()
+    if args.workload == "c3":
+        n, step = run_c3(args, torch, dev, repo, rank, K, base, gen)
+        ids = None
+    else:
+        ids = zipf_ids(torch, gen, n, K, args.zipf, dev)
+        blob, offs = names_for_ids(torch, ids + base)
+        batches = [replica_states(torch, gen, n, j, dev) for j in range(args.warmup + args.steps)]
+        torch.cuda.synchronize()
 
-    def step(j):
-        a, t, e = batches[j]
-        repo.receive_soa(blob, a, t, e, T0 + j, name_offs=offs, n=n, device=True)
+        def step(j):
+            a, t, e = batches[j]
+            repo.receive_soa(blob, a, t, e, T0 + j, name_offs=offs, n=n, device=True)
 
     for j in range(args.warmup):
         step(j)
@@ -218,15 +252,25 @@ def main():
         el = float(tt.item())
 
     total = world * n * args.steps
-    dom = kern.get(DOMINANT, [float("nan")])
-    dom_ms = float(np.mean(dom))
-    achieved = BYTES_PER_MERGE * n / (dom_ms / 1e3) / 1e9
-    workload = f"C2 merge: {n} replica messages -> {K}-bucket table (2^{args.log2_slots} slots), Zipf({args.zipf})"
+    kms = {k: float(np.mean(v)) for k, v in kern.items()}
+    if args.workload == "c3":
+        # Take 89 B (op 24 + state read 32 + write 24 + result 9), Merge 88 B.
+        bpo = 88.5
+        dom_name, dom_ms = "whole step", el / args.steps * 1e3
+        unit, metric = "ops/s", METRIC + " [C3: mixed Take+Merge ops/sec]"
+        workload = (f"C3 mixed: {n} ops (50% Take 100:1s n=1, 50% Merge), Zipf({args.zipf}) over "
+                    f"{K} buckets (2^{args.log2_slots} slots), per-bucket order kept")
+    else:
+        bpo = BYTES_PER_MERGE
+        dom_name, dom_ms = DOMINANT, float(np.mean(kern.get(DOMINANT, [float("nan")])))
+        unit, metric = "merges/s", METRIC
+        workload = f"C2 merge: {n} replica messages -> {K}-bucket table (2^{args.log2_slots} slots), Zipf({args.zipf})"
+    achieved = bpo * n / (dom_ms / 1e3) / 1e9
     traffic = pmc_traffic(workload)
     out = {
-        "metric": METRIC,
+        "metric": metric,
         "value": total / el,
-        "unit": "merges/s",
+        "unit": unit,
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
@@ -240,11 +284,11 @@ def main():
                    "slots_per_gpu": 1 << args.log2_slots, "parallelism": f"shard{world}"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": DOMINANT, "kernel_ms": dom_ms,
-                     "algorithmic_bytes_per_launch": BYTES_PER_MERGE * n},
-        "kernels_ms": {k: float(np.mean(v)) for k, v in kern.items()},
+                     "kernel": dom_name, "kernel_ms": dom_ms,
+                     "algorithmic_bytes_per_launch": bpo * n},
+        "kernels_ms": kms,
     }
-    if rank == 0 and world == 1 and not args.no_cpu:
+    if rank == 0 and world == 1 and not args.no_cpu and args.workload == "c2":
         threads = args.cpu_threads or min(16, os.cpu_count() or 1)
         try:
             out["cpu_baseline"] = cpu_baseline(args, K, ids.cpu(), threads)

@@ -30,7 +30,7 @@ enum BufId {
   B_STATUS, B_REM, B_HAVE, B_REPLY,
   B_BYTES, B_DOFFS, B_NOFF, B_NLEN, B_DA, B_DT, B_DE,
   B_MISS, B_MISS2, B_RETRY, B_CSLOT, B_CMSG,
-  B_SLOT, B_IDX, B_SSLOT, B_SIDX, B_USLOT, B_SCNT, B_SSTART, B_LONG, B_TEMP, B_DUMP,
+  B_SLOT, B_IDX, B_SSLOT, B_SIDX, B_USLOT, B_SCNT, B_SSTART, B_LONG, B_HUGE, B_TEMP, B_DUMP,
   B_STATES, B_NAME1, B_COUNT_
 };
 
@@ -350,11 +350,11 @@ int ordered(phip_handle* h, Src src, u32 n, const OpView& ov, const OutView& ow)
   u32* slot;
   u32 n_claimed = 0;
   if ((rc = resolve_all(h, src, n, ov.now, ov.now0, &slot, &n_claimed))) return rc;
-  u32 *idx, *sslot, *sidx, *uslot, *scnt, *sstart, *lng;
+  u32 *idx, *sslot, *sidx, *uslot, *scnt, *sstart, *lng, *huge;
   if ((rc = ensure(h, B_IDX, n, &idx)) || (rc = ensure(h, B_SSLOT, n, &sslot)) ||
       (rc = ensure(h, B_SIDX, n, &sidx)) || (rc = ensure(h, B_USLOT, n, &uslot)) ||
       (rc = ensure(h, B_SCNT, n, &scnt)) || (rc = ensure(h, B_SSTART, n, &sstart)) ||
-      (rc = ensure(h, B_LONG, n, &lng)))
+      (rc = ensure(h, B_LONG, n, &lng)) || (rc = ensure(h, B_HUGE, n, &huge)))
     return rc;
   {
     Launch l(h, "k_iota");
@@ -386,14 +386,22 @@ int ordered(phip_handle* h, Src src, u32 n, const OpView& ov, const OutView& ow)
                                       h->stream));
   }
   HIPCHK(h, hipMemsetAsync(h->ctr + 6, 0, sizeof(u32), h->stream));
+  HIPCHK(h, hipMemsetAsync(h->ctr + 9, 0, sizeof(u32), h->stream));
   {
     Launch l(h, "k_fold_thread");
     k_fold_thread<<<grid_for(nseg), kBlock, 0, h->stream>>>(uslot, sstart, scnt, nseg, sidx, h->recs,
-                                                             ov, ow, lng, h->ctr);
+                                                             ov, ow, lng, huge, h->ctr);
   }
   HIPCHK(h, hipGetLastError());
   if ((rc = read_ctr(h))) return rc;
-  u32 nlong = h->ctr_host[6];
+  u32 nlong = h->ctr_host[6], nhuge = h->ctr_host[9];
+  // Different segments touch different slots: the two folds may overlap.
+  if (nhuge) {
+    Launch l(h, "k_fold_block");
+    k_fold_block<<<nhuge, kFoldThreads, 0, h->stream>>>(huge, nhuge, uslot, sstart, scnt, sidx,
+                                                         h->recs, ov, ow);
+    HIPCHK(h, hipGetLastError());
+  }
   if (nlong) {
     Launch l(h, "k_fold_wave");
     k_fold_wave<<<nlong, 64, 0, h->stream>>>(lng, nlong, uslot, sstart, scnt, sidx, h->recs, ov, ow);

@@ -571,19 +571,21 @@ __device__ inline void store_state(Rec* r, const FState& S) {
   r->name0 = with_flags(r->name0, kRecPublished);
 }
 
-constexpr u32 kLongSeg = 48;
+constexpr u32 kLongSeg = 48;        // longer segments: k_fold_wave
+constexpr u32 kHugeSeg = 4096;      // longer still: k_fold_block
 
 // One thread folds one bucket's ops in seq order (segments of <= kLongSeg
 // ops); longer segments are handed to k_fold_wave.
 __global__ __launch_bounds__(kBlock) void k_fold_thread(
     const u32* __restrict__ seg_slot, const u32* __restrict__ seg_start,
     const u32* __restrict__ seg_count, u32 nseg, const u32* __restrict__ sorted_idx, Rec* recs,
-    OpView ov, OutView ow, u32* long_list, u32* ctr) {
+    OpView ov, OutView ow, u32* long_list, u32* huge_list, u32* ctr) {
   u32 g = blockIdx.x * blockDim.x + threadIdx.x;
-  bool is_long = false;
+  bool is_long = false, is_huge = false;
   if (g < nseg) {
     u32 cnt = seg_count[g];
-    if (cnt > kLongSeg) is_long = true;
+    if (cnt > kHugeSeg) is_huge = true;
+    else if (cnt > kLongSeg) is_long = true;
     else {
       Rec* r = &recs[seg_slot[g]];
       FState S = load_state(load_rec(r)), S2;
@@ -600,6 +602,8 @@ __global__ __launch_bounds__(kBlock) void k_fold_thread(
   }
   u32 p = wave_append(&ctr[6], is_long);
   if (is_long) long_list[p] = g;
+  u32 q = wave_append(&ctr[9], is_huge);
+  if (is_huge) huge_list[q] = g;
 }
 
 __device__ inline double shfl_f64(double v, int src) {
@@ -652,6 +656,86 @@ __global__ __launch_bounds__(64) void k_fold_wave(
     }
   }
   if (lane == 0) store_state(r, S);
+}
+
+// One workgroup folds one very long segment (a Zipf-hot bucket).  Same rule
+// as k_fold_wave, over windows of kFoldThreads * kFoldPer ops: every thread
+// evaluates kFoldPer ops of the window against the current state, a
+// workgroup min finds the first op that changes it, every op up to it is
+// final, and that op's result state becomes the current one.  A rate-limited
+// hot bucket mostly denies (no change), so most windows retire all of their
+// kFoldThreads * kFoldPer ops at once.
+constexpr u32 kFoldThreads = 1024;
+constexpr u32 kFoldPer = 8;
+
+__global__ __launch_bounds__(kFoldThreads) void k_fold_block(
+    const u32* __restrict__ huge_list, u32 nhuge, const u32* __restrict__ seg_slot,
+    const u32* __restrict__ seg_start, const u32* __restrict__ seg_count,
+    const u32* __restrict__ sorted_idx, Rec* recs, OpView ov, OutView ow) {
+  __shared__ u32 wave_min[kFoldThreads / 64];
+  __shared__ u64 s_state[4];
+  __shared__ u32 s_first;
+  if (blockIdx.x >= nhuge) return;
+  const u32 g = huge_list[blockIdx.x];
+  const u32 tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  Rec* r = &recs[seg_slot[g]];
+  FState S = load_state(load_rec(r));
+  const u32 st = seg_start[g], cnt = seg_count[g];
+  u32 pos = 0;
+  while (pos < cnt) {
+    u32 idx[kFoldPer];
+    OpOut out[kFoldPer];
+    u32 my_first = 0xFFFFFFFFu;
+    FState mine = S;
+#pragma unroll
+    for (u32 k = 0; k < kFoldPer; ++k) {
+      const u32 j = pos + k * kFoldThreads + tid;
+      idx[k] = 0xFFFFFFFFu;
+      if (j < cnt) {
+        idx[k] = sorted_idx[st + j];
+        FState S2;
+        bool ch = eval_op(ov, idx[k], S, S2, out[k]);
+        if (ch && j < my_first) { my_first = j; mine = S2; }
+      }
+    }
+    // workgroup min of the first changing position
+    u32 m = my_first;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) m = min(m, (u32)__shfl_xor((int)m, off));
+    if (lane == 0) wave_min[wv] = m;
+    __syncthreads();
+    if (tid == 0) {
+      u32 f = 0xFFFFFFFFu;
+      for (u32 w = 0; w < kFoldThreads / 64; ++w) f = min(f, wave_min[w]);
+      s_first = f;
+    }
+    __syncthreads();
+    const u32 first = s_first;
+#pragma unroll
+    for (u32 k = 0; k < kFoldPer; ++k) {
+      const u32 j = pos + k * kFoldThreads + tid;
+      if (idx[k] != 0xFFFFFFFFu && j <= first) write_out(ow, idx[k], out[k], S);
+    }
+    if (first == 0xFFFFFFFFu) {
+      pos += kFoldThreads * kFoldPer;
+    } else {
+      if (my_first == first) {
+        s_state[0] = as_bits(mine.a);
+        s_state[1] = as_bits(mine.t);
+        s_state[2] = (u64)mine.e;
+        s_state[3] = (u64)mine.c;
+      }
+      __syncthreads();
+      S.a = as_f64(s_state[0]);
+      S.t = as_f64(s_state[1]);
+      S.e = (i64)s_state[2];
+      S.c = (i64)s_state[3];
+      S.existed = true;
+      pos = first + 1;
+    }
+    __syncthreads();   // s_first / s_state reuse in the next window
+  }
+  if (tid == 0) store_state(r, S);
 }
 
 // Sorted-slot segments from run-length output (counts -> starts is a scan).

@@ -245,6 +245,15 @@ class GPURepo:
         self._check(self.L.phip_apply_mixed(self.h, C.byref(ops), C.byref(res), 0))
         return dict(status=st[:n], remaining=rem[:n], have=have[:n], reply=reply[:n])
 
+    def apply_mixed_device(self, n, kind, names, name_offs, now, freq=None, per=None, count=None,
+                           added=None, taken=None, elapsed=None, status=None, remaining=None,
+                           have=None):
+        """apply_mixed with every array a torch CUDA tensor (PHIP_DEVICE_PTRS)."""
+        ops = phip_ops(n, 0, _ptr(kind), _ptr(names), _ptr(name_offs), _ptr(now), _ptr(freq),
+                       _ptr(per), _ptr(count), _ptr(added), _ptr(taken), _ptr(elapsed))
+        res = phip_results(_ptr(status), _ptr(remaining), _ptr(have), None)
+        self._check(self.L.phip_apply_mixed(self.h, C.byref(ops), C.byref(res), DEVICE_PTRS))
+
     def take(self, names, now, freq, per, count):
         """Batched Bucket.Take via GetBucket (create) then Take: (remaining, ok)."""
         n = len(names)

@@ -223,6 +223,23 @@ def test_mixed_stream_vs_oracle(pa, hot):
     assert_same_dump(gpu_dump(g), o.dump())
 
 
+def test_mixed_stream_hot_buckets_block_fold(pa):
+    """Several buckets with 10^4..10^5 ops each (k_fold_block windows), rate
+    changes and merges interleaved: exact vs the oracle."""
+    rng = np.random.default_rng(77)
+    n, K = 300000, 50
+    args = list(_mixed_stream(rng, n, K, 0.4))
+    g = pa.GPURepo(log2_slots=10)
+    o = O.Repo()
+    out = g.apply_mixed(*args)
+    ref = o.apply_mixed(*args)
+    assert np.array_equal(out["status"], ref["status"])
+    assert np.array_equal(out["remaining"], ref["remaining"])
+    take = args[0] == 0
+    assert np.array_equal(out["have"][take], ref["have"][take])
+    assert_same_dump(gpu_dump(g), o.dump())
+
+
 def test_tag_collisions_names_always_compared(pa):
     """With the probe tag cut to 3 bits nearly every lookup meets other names
     with an equal tag: results must still be exact."""
