@@ -291,6 +291,7 @@ class Bucket:                     # bucket.go:20-32 (created: int64 ns)
 
 # Status codes (mirror include/patrolhip.h).
 MERGED, INCAST_REPLY, INCAST_NOREPLY, SHORT, NOT_PROCESSED, TAKE_OK, TAKE_DENIED = 1, 2, 3, 4, 5, 6, 7
+UPSERT_INSERTED = 8
 CREATED = 0x80
 
 
@@ -347,6 +348,28 @@ class LocalRepo:                  # repo.go:171-235
         b, existed = self.get_bucket(name, now)
         rem, ok, have = b.take(now, r, n)
         return (TAKE_OK if ok else TAKE_DENIED) | (0 if existed else CREATED), rem, have
+
+    def upsert(self, remote: Bucket, now: int):      # repo.go:215-235, a distinct state
+        _, merged = self.upsert_bucket(remote, now)
+        return MERGED if merged else (UPSERT_INSERTED | CREATED)
+
+    def apply_mixed(self, ops):
+        """ops: (kind, name, now, freq, per, count, added_bits, taken_bits, elapsed)
+        in index order; kind 0 Take, 1 Receive, 2 Upsert.  Returns per op
+        (status, remaining, have_bits, reply)."""
+        out = []
+        for kind, name, now, freq, per, count, ab, tb, e in ops:
+            if kind == 0:
+                st, rem, have = self.take(name, now, Rate(freq, per), count)
+                out.append((st, rem, f2b(have), None))
+                continue
+            remote = Bucket(name=name, added=b2f(ab), taken=b2f(tb), elapsed=e)
+            if kind == 2:
+                out.append((self.upsert(remote, now), 0, 0, None))
+            else:
+                st, reply = self.receive_one(remote, now)
+                out.append((st, 0, 0, reply))
+        return out
 
 
 def api_take(repo: LocalRepo, name: str, rate: str, count: str, now: int):

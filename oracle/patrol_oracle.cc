@@ -393,6 +393,7 @@ enum {
   ST_NOT_PROCESSED = 5,   // after a ST_SHORT (the Go loop has exited)
   ST_TAKE_OK = 6,
   ST_TAKE_DENIED = 7,
+  ST_UPSERT_INSERTED = 8, // UpsertBucket inserted the state as-is          repo.go:225-230
   ST_CREATED = 0x80,      // flag: this op created the bucket (GetBucket miss)
 };
 
@@ -489,7 +490,7 @@ void orc_upsert_soa(void* r, const uint8_t* names, const uint32_t* offs, uint32_
 }
 
 // Mixed ordered stream: kind 0 = Take (api.go:67-74 minus HTTP), kind 1 =
-// received replica state (repo.go:78-90).  Ops apply in index order; each op
+// received replica state (repo.go:78-90), kind 2 = UpsertBucket (repo.go:215-235).  Ops apply in index order; each op
 // carries its own clock reading `now`, also used as `created` on a miss.
 void orc_apply_mixed(void* r, const uint8_t* kind, const uint8_t* names, const uint32_t* offs,
                      uint32_t n, const int64_t* now, const int64_t* freq, const int64_t* per,
@@ -501,6 +502,17 @@ void orc_apply_mixed(void* r, const uint8_t* kind, const uint8_t* names, const u
   Bucket remote;
   for (uint32_t i = 0; i < n; ++i) {
     std::string_view name((const char*)names + offs[i], offs[i + 1] - offs[i]);
+    if (kind[i] == 2) {   // LocalRepo.UpsertBucket of a distinct state (repo.go:215-235)
+      Bucket up;
+      up.name.assign(name);
+      up.added = b2f(added[i]); up.taken = b2f(taken[i]); up.elapsed = elapsed[i];
+      bool merged;
+      repo->upsert_bucket(up, now[i], &merged);
+      status[i] = merged ? ST_MERGED : (ST_UPSERT_INSERTED | ST_CREATED);
+      if (remaining) remaining[i] = 0;
+      if (have_bits) have_bits[i] = 0;
+      continue;
+    }
     bool existed;
     Bucket* b = repo->get_bucket(name, now[i], &existed);
     uint8_t st;

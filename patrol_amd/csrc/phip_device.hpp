@@ -77,13 +77,33 @@ __device__ inline u64 go_u64(double x) {
   return (u64)cvttsd2sq(x - 9223372036854775808.0) | kSign;
 }
 
-// Rate.Tokens (bucket.go:132-143) with Rate.Interval (bucket.go:146-148).
-__device__ inline double rate_tokens(i64 freq, i64 per, i64 d) {
-  if (freq == 0 || per == 0) return 0.0;
-  i64 interval = (freq == -1 && per == (i64)kSign) ? (i64)kSign : per / freq;
-  if (interval == 0) return 0.0;
-  return (double)d / (double)interval;
+// Rate.Interval (bucket.go:146-148) folded with the zero tests of
+// Rate.Tokens (bucket.go:132-137): 0 means "Tokens() returns 0".  Computed
+// once per op when the ordered stream is gathered (k_gather_ops).
+__host__ __device__ inline i64 rate_interval(i64 freq, i64 per) {
+  if (freq == 0 || per == 0) return 0;
+  if (freq == -1 && per == (i64)kSign) return (i64)kSign;   // Go's MinInt64 / -1 wraps
+  return per / freq;
 }
+
+// Go float64 + and - as amd64 executes them (ADDSD/SUBSD, the left Go
+// operand in the destination register), down to the NaN bits: a NaN operand
+// comes back quieted with its sign and payload, the left one first, and an
+// invalid operation (Inf - Inf) gives the x86 default NaN 0xFFF8000000000000.
+// gfx950 computes a - b as a + (-b), which flips the sign of a NaN b and
+// returns the positive default NaN, so results that are NaN are rebuilt here.
+constexpr u64 kQuietBit = 0x0008000000000000ull;
+constexpr u64 kX86DefaultNaN = 0xFFF8000000000000ull;
+
+__device__ inline double x86_nan_fix(double r, double a, double b) {
+  if (__builtin_expect(r == r, 1)) return r;
+  const u64 ab = as_bits(a), bb = as_bits(b);
+  if (is_nan_bits(ab)) return as_f64(ab | kQuietBit);
+  if (is_nan_bits(bb)) return as_f64(bb | kQuietBit);
+  return as_f64(kX86DefaultNaN);
+}
+__device__ inline double go_add(double a, double b) { return x86_nan_fix(a + b, a, b); }
+__device__ inline double go_sub(double a, double b) { return x86_nan_fix(a - b, a, b); }
 
 struct TakeResult {
   u64 remaining;
@@ -91,30 +111,31 @@ struct TakeResult {
   bool ok;
 };
 
-// Bucket.Take (bucket.go:186-225), in the reference's exact operation order.
-// `created` and `now` are int64 ns; created.Add(elapsed) is exact (128-bit,
-// as time.Time cannot overflow here), now.Sub(last) saturates like
-// time.Time.Sub, and elapsed += dt wraps like Go int64.
+// Bucket.Take (bucket.go:186-225), in the reference's exact operation order,
+// with Rate.Interval precomputed (rate_interval).  `created` and `now` are
+// int64 ns; created.Add(elapsed) is exact (128-bit, as time.Time cannot
+// overflow here), now.Sub(last) saturates like time.Time.Sub, and
+// elapsed += dt wraps like Go int64.
 __device__ inline TakeResult take_step(double& added, double& taken, i64& elapsed, i64 created,
-                                       i64 now, i64 freq, i64 per, u64 n) {
+                                       i64 now, i64 interval, i64 freq, u64 n) {
   double capacity = (double)freq;                              // :192
   if (added == 0) added = capacity;                            // :194-196
   __int128 last = (__int128)created + (__int128)elapsed;       // :198
   if ((__int128)now < last) last = now;                        // :199-201
-  double tokens = added - taken;                               // :204
+  double tokens = go_sub(added, taken);                        // :204
   __int128 dd = (__int128)now - last;                          // :207
   i64 dt = dd > (__int128)0x7FFFFFFFFFFFFFFFll ? 0x7FFFFFFFFFFFFFFFll
          : (dd < -(__int128)0x7FFFFFFFFFFFFFFFll - 1 ? (i64)kSign : (i64)dd);
-  double add = rate_tokens(freq, per, dt);                     // :210
-  double missing = capacity - tokens;                          // :211
+  double add = interval ? (double)dt / (double)interval : 0.0;  // :210, bucket.go:132-143
+  double missing = go_sub(capacity, tokens);                   // :211
   if (add > missing) add = missing;                            // :211-213
   double t = (double)n;                                        // :215
-  double have = tokens + add;                                  // :216
+  double have = go_add(tokens, add);                           // :216
   if (t > have) return TakeResult{go_u64(have), as_bits(have), false};   // :216-218
   elapsed = (i64)((u64)elapsed + (u64)dt);                     // :220
-  added = added + add;                                         // :221
-  taken = taken + t;                                           // :222
-  double rem = added - taken;
+  added = go_add(added, add);                                  // :221
+  taken = go_add(taken, t);                                    // :222
+  double rem = go_sub(added, taken);
   return TakeResult{go_u64(rem), as_bits(rem), true};          // :224
 }
 

@@ -3,7 +3,8 @@
 // Pipelines:
 //   fast receive  classify -> k_receive_fast -> [insert rounds -> k_receive_fast(miss list)]
 //   ordered       resolve -> [insert rounds -> resolve(miss)] -> sort(slot, seq)
-//                 -> run-length segments -> k_fold_thread / k_fold_wave
+//                 -> run-length segments -> gather ops in (slot, seq) order
+//                 -> k_fold_thread / k_fold_wave / k_fold_block (stream2)
 // Everything runs on the handle's own HIP stream; host synchronisation only
 // reads back small counters (miss count, segment count) between stages.
 #include <cstring>
@@ -31,6 +32,7 @@ enum BufId {
   B_BYTES, B_DOFFS, B_NOFF, B_NLEN, B_DA, B_DT, B_DE,
   B_MISS, B_MISS2, B_RETRY, B_CSLOT, B_CMSG,
   B_SLOT, B_IDX, B_SSLOT, B_SIDX, B_USLOT, B_SCNT, B_SSTART, B_LONG, B_HUGE, B_TEMP, B_DUMP,
+  B_SO_NOW, B_SO_X, B_SO_Y, B_SO_Z, B_SO_KIND,
   B_STATES, B_NAME1, B_COUNT_
 };
 
@@ -49,6 +51,8 @@ struct Timing {
 struct phip_handle {
   int device = 0;
   hipStream_t stream = nullptr;
+  hipStream_t stream2 = nullptr;   // second stream: the hot-bucket fold overlaps the others
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   std::mutex mu;
   std::string err;
   u32 L = 0;
@@ -125,7 +129,9 @@ struct Launch {
   phip_handle* h;
   const char* name;
   Timing* t = nullptr;
-  Launch(phip_handle* h_, const char* n) : h(h_), name(n) {
+  hipStream_t s;
+  Launch(phip_handle* h_, const char* n, hipStream_t st = nullptr)
+      : h(h_), name(n), s(st ? st : h_->stream) {
     if (!h->timing) return;
     if (h->pool_used == h->event_pool.size()) {
       Timing tm{n, nullptr, nullptr};
@@ -135,11 +141,11 @@ struct Launch {
     }
     t = &h->event_pool[h->pool_used++];
     t->name = n;
-    hipEventRecord(t->a, h->stream);
+    hipEventRecord(t->a, s);
   }
   ~Launch() {
     if (t) {
-      hipEventRecord(t->b, h->stream);
+      hipEventRecord(t->b, s);
       h->timings.push_back(*t);
     }
   }
@@ -385,27 +391,49 @@ int ordered(phip_handle* h, Src src, u32 n, const OpView& ov, const OutView& ow)
     HIPCHK(h, rocprim::exclusive_scan(temp, tb3, scnt, sstart, 0u, (size_t)nseg, rocprim::plus<u32>(),
                                       h->stream));
   }
+  SortedOps so;
+  if ((rc = ensure(h, B_SO_NOW, n, &so.now)) || (rc = ensure(h, B_SO_X, n, &so.x)) ||
+      (rc = ensure(h, B_SO_Y, n, &so.y)) || (rc = ensure(h, B_SO_Z, n, &so.z)) ||
+      (rc = ensure(h, B_SO_KIND, n, &so.kind)))
+    return rc;
+  so.idx = sidx;
+  {
+    Launch l(h, "k_gather_ops");
+    k_gather_ops<<<grid_for(n), kBlock, 0, h->stream>>>(sidx, n, ov, so);
+  }
   HIPCHK(h, hipMemsetAsync(h->ctr + 6, 0, sizeof(u32), h->stream));
   HIPCHK(h, hipMemsetAsync(h->ctr + 9, 0, sizeof(u32), h->stream));
   {
-    Launch l(h, "k_fold_thread");
-    k_fold_thread<<<grid_for(nseg), kBlock, 0, h->stream>>>(uslot, sstart, scnt, nseg, sidx, h->recs,
-                                                             ov, ow, lng, huge, h->ctr);
+    Launch l(h, "k_seg_classify");
+    k_seg_classify<<<grid_for(nseg), kBlock, 0, h->stream>>>(scnt, nseg, lng, huge, h->ctr);
   }
   HIPCHK(h, hipGetLastError());
   if ((rc = read_ctr(h))) return rc;
   u32 nlong = h->ctr_host[6], nhuge = h->ctr_host[9];
-  // Different segments touch different slots: the two folds may overlap.
+  // Different segments touch different slots, so the folds may overlap: the
+  // hot-bucket workgroups run on stream2 beside the wave and thread folds.
   if (nhuge) {
-    Launch l(h, "k_fold_block");
-    k_fold_block<<<nhuge, kFoldThreads, 0, h->stream>>>(huge, nhuge, uslot, sstart, scnt, sidx,
-                                                         h->recs, ov, ow);
+    HIPCHK(h, hipEventRecord(h->ev_fork, h->stream));
+    HIPCHK(h, hipStreamWaitEvent(h->stream2, h->ev_fork, 0));
+    Launch l(h, "k_fold_block", h->stream2);
+    k_fold_block<<<nhuge, kFoldThreads, 0, h->stream2>>>(huge, nhuge, uslot, sstart, scnt, so,
+                                                          h->recs, ow);
     HIPCHK(h, hipGetLastError());
   }
   if (nlong) {
     Launch l(h, "k_fold_wave");
-    k_fold_wave<<<nlong, 64, 0, h->stream>>>(lng, nlong, uslot, sstart, scnt, sidx, h->recs, ov, ow);
+    k_fold_wave<<<nlong, 64, 0, h->stream>>>(lng, nlong, uslot, sstart, scnt, so, h->recs, ow);
     HIPCHK(h, hipGetLastError());
+  }
+  {
+    Launch l(h, "k_fold_thread");
+    k_fold_thread<<<grid_for(nseg), kBlock, 0, h->stream>>>(uslot, sstart, scnt, nseg, so,
+                                                             h->recs, ow);
+    HIPCHK(h, hipGetLastError());
+  }
+  if (nhuge) {
+    HIPCHK(h, hipEventRecord(h->ev_join, h->stream2));
+    HIPCHK(h, hipStreamWaitEvent(h->stream, h->ev_join, 0));
   }
   (void)n_claimed;  // NEW flags cleared by store_state in the folds
   return PHIP_OK;
@@ -520,6 +548,9 @@ int phip_open(const phip_config* cfg, phip_handle** out) {
   hipError_t e;
   if ((e = hipSetDevice(h->device)) != hipSuccess) return fail(e);
   if ((e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking)) != hipSuccess) return fail(e);
+  if ((e = hipStreamCreateWithFlags(&h->stream2, hipStreamNonBlocking)) != hipSuccess) return fail(e);
+  if ((e = hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming)) != hipSuccess) return fail(e);
+  if ((e = hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming)) != hipSuccess) return fail(e);
   if ((e = hipMalloc(&h->recs, h->cap * sizeof(Rec))) != hipSuccess) return fail(e);
   if ((e = hipMalloc(&h->aux, h->cap * sizeof(u32))) != hipSuccess) return fail(e);
   if ((e = hipMalloc(&h->arena, h->arena_cap + 64)) != hipSuccess) return fail(e);
@@ -539,6 +570,7 @@ void phip_close(phip_handle* h) {
   if (!h) return;
   hipSetDevice(h->device);
   if (h->stream) hipStreamSynchronize(h->stream);
+  if (h->stream2) hipStreamSynchronize(h->stream2);
   for (auto& b : h->buf)
     if (b.p) hipFree(b.p);
   for (auto& t : h->event_pool) {
@@ -551,6 +583,9 @@ void phip_close(phip_handle* h) {
   if (h->arena_cursor) hipFree(h->arena_cursor);
   if (h->ctr) hipFree(h->ctr);
   if (h->ctr_host) hipHostFree(h->ctr_host);
+  if (h->ev_fork) hipEventDestroy(h->ev_fork);
+  if (h->ev_join) hipEventDestroy(h->ev_join);
+  if (h->stream2) hipStreamDestroy(h->stream2);
   if (h->stream) hipStreamDestroy(h->stream);
   delete h;
 }

@@ -483,7 +483,8 @@ __global__ void k_decode(const u8* __restrict__ bytes, const uint64_t* __restric
 }
 
 // ------------------------------------------------------------ ordered ----
-// A view of a mixed op stream; null arrays mean "uniform value".
+// A view of a mixed op stream as the ABI hands it over; null arrays mean
+// "uniform value" (kind0 / now0).
 struct OpView {
   const u8* kind; u32 kind0;
   const int64_t* now; i64 now0;
@@ -497,6 +498,56 @@ struct OutView {
   uint64_t* have;
   phip_state* reply;
 };
+
+// The op stream regathered in (slot, seq) order, one column per field, so
+// that every fold reads its bucket's ops as contiguous, coalesced runs.
+//   TAKE:            x = Rate.Interval (0 = Tokens() is always 0), y = Freq, z = n
+//   RECEIVE/UPSERT:  x = added bits, y = taken bits, z = elapsed
+struct SortedOps {
+  int64_t* now;
+  uint64_t* x;
+  uint64_t* y;
+  uint64_t* z;
+  const u32* idx;   // original op index (output position) = the sorted permutation
+  u8* kind;
+};
+
+struct SOp {
+  i64 now;
+  u64 x, y, z;
+  u32 idx;
+  u32 kind;
+};
+
+__device__ inline SOp load_sop(const SortedOps& so, u32 j) {
+  SOp o;
+  o.now = so.now[j]; o.x = so.x[j]; o.y = so.y[j]; o.z = so.z[j];
+  o.idx = so.idx[j]; o.kind = so.kind[j];
+  return o;
+}
+
+// Gather: sorted position j <- original op sidx[j] (random reads, coalesced
+// writes; every later pass streams).  The per-op integer division of
+// Rate.Interval is done here, once, instead of in every fold evaluation.
+__global__ __launch_bounds__(kBlock) void k_gather_ops(const u32* __restrict__ sidx, u32 n,
+                                                       OpView ov, SortedOps so) {
+  u32 j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  const u32 i = sidx[j];
+  const u32 kind = ov.kind ? ov.kind[i] : ov.kind0;
+  so.now[j] = ov.now ? ov.now[i] : ov.now0;
+  if (kind == PHIP_OP_TAKE) {
+    const i64 f = ov.freq[i], p = ov.per[i];
+    so.x[j] = (u64)rate_interval(f, p);
+    so.y[j] = (u64)f;
+    so.z[j] = ov.count[i];
+  } else {
+    so.x[j] = ov.a[i];
+    so.y[j] = ov.t[i];
+    so.z[j] = (u64)ov.e[i];
+  }
+  so.kind[j] = (u8)kind;   // so.idx is sidx itself
+}
 
 struct FState {
   double a, t;
@@ -512,24 +563,22 @@ struct OpOut {
 
 // One op of the ordered stream against state S (result state in S2).
 // Returns whether S2 differs from S (bitwise, or existence).
-__device__ inline bool eval_op(const OpView& ov, u32 i, const FState& S, FState& S2, OpOut& out) {
-  const u32 kind = ov.kind ? ov.kind[i] : ov.kind0;
-  const i64 now = ov.now ? ov.now[i] : ov.now0;
+__device__ inline bool eval_sop(const SOp& op, const FState& S, FState& S2, OpOut& out) {
   S2 = S;
   u8 cflag = 0;
-  if (!S.existed) { S2.c = now; S2.existed = true; cflag = 0x80; }   // repo.go:208
+  if (!S.existed) { S2.c = op.now; S2.existed = true; cflag = 0x80; }   // repo.go:208
   out.has_reply = false; out.rem = 0; out.have = 0;
-  if (kind == PHIP_OP_TAKE) {
-    TakeResult r = take_step(S2.a, S2.t, S2.e, S2.c, now, ov.freq[i], ov.per[i], ov.count[i]);
+  if (op.kind == PHIP_OP_TAKE) {
+    TakeResult r = take_step(S2.a, S2.t, S2.e, S2.c, op.now, (i64)op.x, (i64)op.y, op.z);
     out.st = (r.ok ? PHIP_ST_TAKE_OK : PHIP_ST_TAKE_DENIED) | cflag;
     out.rem = r.remaining; out.have = r.have_bits;
   } else {
-    u64 ab = ov.a[i], tb = ov.t[i];
-    i64 eb = ov.e[i];
-    if (kind == PHIP_OP_UPSERT && !S.existed) {               // repo.go:225-230
+    const u64 ab = op.x, tb = op.y;
+    const i64 eb = (i64)op.z;
+    if (op.kind == PHIP_OP_UPSERT && !S.existed) {               // repo.go:225-230
       S2.a = as_f64(ab); S2.t = as_f64(tb); S2.e = eb;
       out.st = PHIP_ST_UPSERT_INSERTED | cflag;
-    } else if (kind == PHIP_OP_RECEIVE && state_is_zero(ab, tb, eb)) {   // repo.go:86-90
+    } else if (op.kind == PHIP_OP_RECEIVE && state_is_zero(ab, tb, eb)) {   // repo.go:86-90
       bool reply = S.existed && !state_is_zero(as_bits(S.a), as_bits(S.t), S.e);
       out.st = (reply ? PHIP_ST_INCAST_REPLY : PHIP_ST_INCAST_NOREPLY) | cflag;
       out.has_reply = reply;
@@ -542,6 +591,7 @@ __device__ inline bool eval_op(const OpView& ov, u32 i, const FState& S, FState&
          S2.e != S.e;
 }
 
+// S is the state the op saw (an incast reply carries it, repo.go:86-90).
 __device__ inline void write_out(const OutView& o, u32 i, const OpOut& r, const FState& S) {
   if (o.status) o.status[i] = r.st;
   if (o.remaining) o.remaining[i] = r.rem;
@@ -571,39 +621,47 @@ __device__ inline void store_state(Rec* r, const FState& S) {
   r->name0 = with_flags(r->name0, kRecPublished);
 }
 
-constexpr u32 kLongSeg = 48;        // longer segments: k_fold_wave
-constexpr u32 kHugeSeg = 4096;      // longer still: k_fold_block
+constexpr u32 kLongSeg = 32;        // longer segments: one wave each (k_fold_wave)
+constexpr u32 kHugeSeg = 16384;     // longer still: one workgroup each (k_fold_block)
 
-// One thread folds one bucket's ops in seq order (segments of <= kLongSeg
-// ops); longer segments are handed to k_fold_wave.
-__global__ __launch_bounds__(kBlock) void k_fold_thread(
-    const u32* __restrict__ seg_slot, const u32* __restrict__ seg_start,
-    const u32* __restrict__ seg_count, u32 nseg, const u32* __restrict__ sorted_idx, Rec* recs,
-    OpView ov, OutView ow, u32* long_list, u32* huge_list, u32* ctr) {
+// Segment classes: small ones are folded by k_fold_thread, the others listed.
+__global__ void k_seg_classify(const u32* __restrict__ seg_count, u32 nseg, u32* long_list,
+                               u32* huge_list, u32* ctr) {
   u32 g = blockIdx.x * blockDim.x + threadIdx.x;
   bool is_long = false, is_huge = false;
   if (g < nseg) {
     u32 cnt = seg_count[g];
-    if (cnt > kHugeSeg) is_huge = true;
-    else if (cnt > kLongSeg) is_long = true;
-    else {
-      Rec* r = &recs[seg_slot[g]];
-      FState S = load_state(load_rec(r)), S2;
-      u32 st = seg_start[g];
-      for (u32 j = 0; j < cnt; ++j) {
-        u32 i = sorted_idx[st + j];
-        OpOut o;
-        eval_op(ov, i, S, S2, o);
-        write_out(ow, i, o, S);
-        S = S2;
-      }
-      store_state(r, S);
-    }
+    is_huge = cnt > kHugeSeg;
+    is_long = !is_huge && cnt > kLongSeg;
   }
   u32 p = wave_append(&ctr[6], is_long);
   if (is_long) long_list[p] = g;
   u32 q = wave_append(&ctr[9], is_huge);
   if (is_huge) huge_list[q] = g;
+}
+
+// One thread folds one short bucket segment in seq order.
+__global__ __launch_bounds__(kBlock) void k_fold_thread(
+    const u32* __restrict__ seg_slot, const u32* __restrict__ seg_start,
+    const u32* __restrict__ seg_count, u32 nseg, SortedOps so, Rec* recs, OutView ow) {
+  u32 g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= nseg) return;
+  const u32 cnt = seg_count[g];
+  if (cnt > kLongSeg) return;
+  Rec* r = &recs[seg_slot[g]];
+  FState S = load_state(load_rec(r)), S2;
+  const u32 st = seg_start[g];
+  SOp op = load_sop(so, st);
+  for (u32 j = 0; j < cnt; ++j) {
+    SOp nx = op;
+    if (j + 1 < cnt) nx = load_sop(so, st + j + 1);   // next op in flight during this one
+    OpOut o;
+    eval_sop(op, S, S2, o);
+    write_out(ow, op.idx, o, S);
+    S = S2;
+    op = nx;
+  }
+  store_state(r, S);
 }
 
 __device__ inline double shfl_f64(double v, int src) {
@@ -616,124 +674,183 @@ __device__ inline i64 shfl_i64(i64 v, int src) {
   return (i64)(((u64)hi << 32) | lo);
 }
 
-// One wave folds one long segment.  Each step evaluates the next 64 ops
-// against the current state in parallel; every op up to and including the
-// first one that changes the state is final (the ones before it saw exactly
-// the state the sequential fold would have shown them).  Deny streaks and
-// no-op merges therefore retire 64 ops per step.
+// One wave folds one long segment, 64 ops per window, the window held in
+// registers (lane k owns op base+k) and the next window's ops already in
+// flight.  A round evaluates every unretired op of the window against the
+// current state; every op up to and including the first one that changes the
+// state is final (the ops before it saw exactly the state a sequential fold
+// would have shown them), and that op's result state becomes the current
+// one.  A round costs one op evaluation, so a change costs what a sequential
+// fold step costs, and a run of unchanged ops (denied Takes, no-op merges)
+// retires up to 64 ops in one step.
 __global__ __launch_bounds__(64) void k_fold_wave(
     const u32* __restrict__ long_list, u32 nlong, const u32* __restrict__ seg_slot,
-    const u32* __restrict__ seg_start, const u32* __restrict__ seg_count,
-    const u32* __restrict__ sorted_idx, Rec* recs, OpView ov, OutView ow) {
+    const u32* __restrict__ seg_start, const u32* __restrict__ seg_count, SortedOps so,
+    Rec* recs, OutView ow) {
   u32 w = blockIdx.x;
   if (w >= nlong) return;
-  u32 g = long_list[w];
+  const u32 g = long_list[w];
   const u32 lane = threadIdx.x;
   Rec* r = &recs[seg_slot[g]];
   FState S = load_state(load_rec(r));
   const u32 st = seg_start[g], cnt = seg_count[g];
-  u32 j0 = 0;
-  while (j0 < cnt) {
-    const u32 j = j0 + lane;
-    const bool active = j < cnt;
-    u32 i = active ? sorted_idx[st + j] : 0;
-    FState S2 = S;
-    OpOut o;
-    bool ch = false;
-    if (active) ch = eval_op(ov, i, S, S2, o);
-    u64 m = __ballot(ch);
-    u32 p = m ? (u32)(__ffsll((long long)m) - 1) : 64u;
-    if (active && lane <= p) write_out(ow, i, o, S);
-    if (p < 64) {
+  SOp op{};
+  if (lane < cnt) op = load_sop(so, st + lane);
+  for (u32 base = 0; base < cnt; base += 64) {
+    SOp nx{};
+    if (base + 64 + lane < cnt) nx = load_sop(so, st + base + 64 + lane);
+    const u32 lim = min(64u, cnt - base);
+    u32 c = 0;
+    while (c < lim) {
+      const bool active = lane >= c && lane < lim;
+      FState S2;
+      OpOut o;
+      bool ch = false;
+      if (active) ch = eval_sop(op, S, S2, o);
+      const u64 m = __ballot(ch);
+      const u32 p = m ? (u32)(__ffsll((long long)m) - 1) : 64u;
+      if (active && lane <= p) write_out(ow, op.idx, o, S);
+      if (p >= 64) break;
       S.a = shfl_f64(S2.a, p);
       S.t = shfl_f64(S2.t, p);
       S.e = shfl_i64(S2.e, p);
       S.c = shfl_i64(S2.c, p);
       S.existed = true;
-      j0 += p + 1;
-    } else {
-      j0 += 64;
+      c = p + 1;
     }
+    op = nx;
   }
   if (lane == 0) store_state(r, S);
 }
 
-// One workgroup folds one very long segment (a Zipf-hot bucket).  Same rule
-// as k_fold_wave, over windows of kFoldThreads * kFoldPer ops: every thread
-// evaluates kFoldPer ops of the window against the current state, a
-// workgroup min finds the first op that changes it, every op up to it is
-// final, and that op's result state becomes the current one.  A rate-limited
-// hot bucket mostly denies (no change), so most windows retire all of their
-// kFoldThreads * kFoldPer ops at once.
-constexpr u32 kFoldThreads = 1024;
-constexpr u32 kFoldPer = 8;
+// One workgroup folds one very long segment (a Zipf-hot bucket).  Windows of
+// kFoldThreads * kFoldPer ops are staged in LDS (the next window's ops are
+// loaded into registers while the current one is folded).  Per window:
+//  * parallel round: every thread evaluates its unretired ops of the window
+//    against the current state; a workgroup min finds the first op that
+//    changes it; ops up to it are final (same rule as k_fold_wave);
+//  * sequential burst: wave 0 continues op by op from there, straight out of
+//    LDS, until kBurstQuiet ops in a row leave the state unchanged.  Changes
+//    cluster (a refill or a merge that raises `added` is followed by a run
+//    of successful Takes), and a parallel round costs far more than one op,
+//    so each cluster costs about one round plus its ops at sequential speed,
+//    and the long unchanged stretches between clusters go at window speed.
+constexpr u32 kFoldThreads = 512;
+constexpr u32 kFoldPer = 4;
+constexpr u32 kFoldWin = kFoldThreads * kFoldPer;
+constexpr u32 kBurstQuiet = 16;
 
 __global__ __launch_bounds__(kFoldThreads) void k_fold_block(
     const u32* __restrict__ huge_list, u32 nhuge, const u32* __restrict__ seg_slot,
-    const u32* __restrict__ seg_start, const u32* __restrict__ seg_count,
-    const u32* __restrict__ sorted_idx, Rec* recs, OpView ov, OutView ow) {
+    const u32* __restrict__ seg_start, const u32* __restrict__ seg_count, SortedOps so,
+    Rec* recs, OutView ow) {
+  __shared__ i64 l_now[kFoldWin];
+  __shared__ u64 l_x[kFoldWin], l_y[kFoldWin], l_z[kFoldWin];
+  __shared__ u32 l_idx[kFoldWin];
+  __shared__ u8 l_kind[kFoldWin];
   __shared__ u32 wave_min[kFoldThreads / 64];
   __shared__ u64 s_state[4];
-  __shared__ u32 s_first;
+  __shared__ u32 s_cur;
   if (blockIdx.x >= nhuge) return;
   const u32 g = huge_list[blockIdx.x];
   const u32 tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   Rec* r = &recs[seg_slot[g]];
   FState S = load_state(load_rec(r));
   const u32 st = seg_start[g], cnt = seg_count[g];
-  u32 pos = 0;
-  while (pos < cnt) {
-    u32 idx[kFoldPer];
-    OpOut out[kFoldPer];
-    u32 my_first = 0xFFFFFFFFu;
-    FState mine = S;
+
+  SOp pre[kFoldPer];
+#pragma unroll
+  for (u32 k = 0; k < kFoldPer; ++k) {
+    const u32 j = k * kFoldThreads + tid;
+    if (j < cnt) pre[k] = load_sop(so, st + j);
+  }
+  for (u32 pos = 0; pos < cnt; pos += kFoldWin) {
+    const u32 lim = min(kFoldWin, cnt - pos);
+    __syncthreads();   // the previous window's LDS readers are done
 #pragma unroll
     for (u32 k = 0; k < kFoldPer; ++k) {
-      const u32 j = pos + k * kFoldThreads + tid;
-      idx[k] = 0xFFFFFFFFu;
-      if (j < cnt) {
-        idx[k] = sorted_idx[st + j];
-        FState S2;
-        bool ch = eval_op(ov, idx[k], S, S2, out[k]);
-        if (ch && j < my_first) { my_first = j; mine = S2; }
+      const u32 w = k * kFoldThreads + tid;
+      if (w < lim) {
+        l_now[w] = pre[k].now; l_x[w] = pre[k].x; l_y[w] = pre[k].y; l_z[w] = pre[k].z;
+        l_idx[w] = pre[k].idx; l_kind[w] = (u8)pre[k].kind;
       }
     }
-    // workgroup min of the first changing position
-    u32 m = my_first;
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) m = min(m, (u32)__shfl_xor((int)m, off));
-    if (lane == 0) wave_min[wv] = m;
     __syncthreads();
-    if (tid == 0) {
-      u32 f = 0xFFFFFFFFu;
-      for (u32 w = 0; w < kFoldThreads / 64; ++w) f = min(f, wave_min[w]);
-      s_first = f;
-    }
-    __syncthreads();
-    const u32 first = s_first;
 #pragma unroll
     for (u32 k = 0; k < kFoldPer; ++k) {
-      const u32 j = pos + k * kFoldThreads + tid;
-      if (idx[k] != 0xFFFFFFFFu && j <= first) write_out(ow, idx[k], out[k], S);
+      const u32 j = pos + kFoldWin + k * kFoldThreads + tid;
+      if (j < cnt) pre[k] = load_sop(so, st + j);
     }
-    if (first == 0xFFFFFFFFu) {
-      pos += kFoldThreads * kFoldPer;
-    } else {
+    u32 cur = 0;
+    while (cur < lim) {
+      // ---- parallel round over [cur, lim)
+      OpOut out[kFoldPer];
+      u32 my_first = 0xFFFFFFFFu;
+      FState mine = S;
+#pragma unroll
+      for (u32 k = 0; k < kFoldPer; ++k) {
+        const u32 w = cur + k * kFoldThreads + tid;
+        if (w < lim) {
+          SOp op;
+          op.now = l_now[w]; op.x = l_x[w]; op.y = l_y[w]; op.z = l_z[w];
+          op.idx = l_idx[w]; op.kind = l_kind[w];
+          FState S2;
+          bool ch = eval_sop(op, S, S2, out[k]);
+          if (ch && my_first == 0xFFFFFFFFu) { my_first = w; mine = S2; }
+        }
+      }
+      u32 m = my_first;
+#pragma unroll
+      for (int off = 32; off >= 1; off >>= 1) m = min(m, (u32)__shfl_xor((int)m, off));
+      if (lane == 0) wave_min[wv] = m;
+      __syncthreads();
+      u32 first = 0xFFFFFFFFu;
+#pragma unroll
+      for (u32 x = 0; x < kFoldThreads / 64; ++x) first = min(first, wave_min[x]);
+#pragma unroll
+      for (u32 k = 0; k < kFoldPer; ++k) {
+        const u32 w = cur + k * kFoldThreads + tid;
+        if (w < lim && w <= first) write_out(ow, l_idx[w], out[k], S);
+      }
+      if (first == 0xFFFFFFFFu) {
+        cur = lim;
+        break;   // the loop-top barrier of the next window orders wave_min reuse
+      }
       if (my_first == first) {
-        s_state[0] = as_bits(mine.a);
-        s_state[1] = as_bits(mine.t);
-        s_state[2] = (u64)mine.e;
-        s_state[3] = (u64)mine.c;
+        s_state[0] = as_bits(mine.a); s_state[1] = as_bits(mine.t);
+        s_state[2] = (u64)mine.e; s_state[3] = (u64)mine.c;
       }
       __syncthreads();
-      S.a = as_f64(s_state[0]);
-      S.t = as_f64(s_state[1]);
-      S.e = (i64)s_state[2];
-      S.c = (i64)s_state[3];
-      S.existed = true;
-      pos = first + 1;
+      // ---- sequential burst (wave 0) from first + 1
+      if (wv == 0) {
+        FState T;
+        T.a = as_f64(s_state[0]); T.t = as_f64(s_state[1]);
+        T.e = (i64)s_state[2]; T.c = (i64)s_state[3]; T.existed = true;
+        u32 j = first + 1, quiet = 0;
+        while (j < lim && quiet < kBurstQuiet) {
+          SOp op;
+          op.now = l_now[j]; op.x = l_x[j]; op.y = l_y[j]; op.z = l_z[j];
+          op.idx = l_idx[j]; op.kind = l_kind[j];
+          FState T2;
+          OpOut o;
+          const bool ch = eval_sop(op, T, T2, o);
+          if (lane == 0) write_out(ow, op.idx, o, T);
+          T = T2;
+          quiet = ch ? 0 : quiet + 1;
+          ++j;
+        }
+        if (lane == 0) {
+          s_state[0] = as_bits(T.a); s_state[1] = as_bits(T.t);
+          s_state[2] = (u64)T.e; s_state[3] = (u64)T.c;
+          s_cur = j;
+        }
+      }
+      __syncthreads();
+      S.a = as_f64(s_state[0]); S.t = as_f64(s_state[1]);
+      S.e = (i64)s_state[2]; S.c = (i64)s_state[3]; S.existed = true;
+      cur = s_cur;
+      __syncthreads();   // s_state / s_cur / wave_min are rewritten by the next round
     }
-    __syncthreads();   // s_first / s_state reuse in the next window
   }
   if (tid == 0) store_state(r, S);
 }

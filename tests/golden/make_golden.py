@@ -152,12 +152,13 @@ def api_table():
 
 
 def mixed_traces(rng):
-    """Ordered Take/Merge streams over a few buckets (api.go:67-74, repo.go:78-90)."""
+    """Ordered Take/Merge streams over a few buckets (api.go:67-74, repo.go:78-90);
+    traces 40.. also carry UpsertBucket ops (kind 2, repo.go:215-235)."""
     traces = []
     rates = [(100, SEC), (5, SEC), (3, SEC), (0, SEC), (7, 0), (2, 3), (1, MS), (-5, SEC),
              (10, -SEC), (-1, -(1 << 63)), (1 << 62, SEC), (9, 60 * SEC)]
     sp = special_floats()
-    for k in range(40):
+    for k in range(52):
         names = ["k%d" % j for j in range(rng.randrange(1, 5))]
         now = T0 + rng.randrange(0, 10**12)
         ops = []
@@ -177,7 +178,8 @@ def mixed_traces(rng):
                     t = float(rng.randrange(0, 50))
                     a = t + rng.random() * 10
                     e = rng.randrange(0, 10 * SEC)
-                ops.append(dict(kind=1, name=name, now=now, added=bits(a), taken=bits(t),
+                kind = 2 if k >= 40 and rng.random() < 0.35 else 1
+                ops.append(dict(kind=kind, name=name, now=now, added=bits(a), taken=bits(t),
                                 elapsed=e))
         repo = G.LocalRepo()
         res = []
@@ -186,6 +188,10 @@ def mixed_traces(rng):
                 st, rem, have = repo.take(op["name"], op["now"], G.Rate(op["freq"], op["per"]),
                                           op["count"])
                 res.append(dict(status=st, remaining=rem, have=bits(have)))
+            elif op["kind"] == 2:
+                remote = G.Bucket(name=op["name"], added=G.b2f(int(op["added"], 16)),
+                                  taken=G.b2f(int(op["taken"], 16)), elapsed=op["elapsed"])
+                res.append(dict(status=repo.upsert(remote, op["now"])))
             else:
                 remote = G.Bucket(name=op["name"], added=G.b2f(int(op["added"], 16)),
                                   taken=G.b2f(int(op["taken"], 16)), elapsed=op["elapsed"])

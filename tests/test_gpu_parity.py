@@ -240,6 +240,61 @@ def test_mixed_stream_hot_buckets_block_fold(pa):
     assert_same_dump(gpu_dump(g), o.dump())
 
 
+def _check_mixed(pa, args, log2_slots, reply=False):
+    g = pa.GPURepo(log2_slots=log2_slots)
+    o = O.Repo()
+    out = g.apply_mixed(*args)
+    ref = o.apply_mixed(*args)
+    assert np.array_equal(out["status"], ref["status"])
+    assert np.array_equal(out["remaining"], ref["remaining"])
+    take = args[0] == 0
+    assert np.array_equal(out["have"][take], ref["have"][take])
+    if reply:
+        rep = (ref["status"] & 0x7F) == 2
+        assert rep.any()
+        r = out["reply"][rep]
+        assert np.array_equal(r["a"], ref["reply_added"][rep])
+        assert np.array_equal(r["t"], ref["reply_taken"][rep])
+        assert np.array_equal(r["e"], ref["reply_elapsed"][rep])
+    assert_same_dump(gpu_dump(g), o.dump())
+
+
+def test_mixed_hot_adversarial_all_fold_kinds(pa):
+    """Thread, wave and workgroup folds on one stream with every op kind:
+    Take (odd rates), Receive of dirty states (incast replies, -0.0, NaN,
+    negatives) and Upsert, with 3 buckets hot enough for k_fold_block."""
+    rng = np.random.default_rng(5150)
+    n, K = 200000, 3000
+    args = list(_mixed_stream(rng, n, K))
+    ids = _gen.zipf_ids(rng, n, K)
+    hot = rng.random(n)
+    ids[hot < 0.15] = 11
+    ids[(hot >= 0.15) & (hot < 0.25)] = 12
+    ids[(hot >= 0.25) & (hot < 0.32)] = 13
+    args[1] = _gen.key_names(ids)
+    args[0] = rng.choice(np.array([0, 1, 2], np.uint8), n, p=[0.5, 0.4, 0.1])
+    a, t, e = _gen.dirty_states(rng, n, 0.1)
+    args[6], args[7], args[8] = a, t, e
+    _check_mixed(pa, args, 13, reply=True)
+
+
+def test_mixed_c3_shape_clamped_clock(pa):
+    """The bench's C3 shape: replica elapsed far ahead of the local clock, so
+    Take's `last` is clamped to now (bucket.go:199-201) and tokens come only
+    from merged added/taken; one bucket carries ~12% of 250k ops."""
+    rng = np.random.default_rng(31337)
+    n, K = 250000, 20000
+    ids = _gen.zipf_ids(rng, n, K)
+    names = _gen.key_names(ids)
+    kind = (rng.random(n) < 0.5).astype(np.uint8)
+    now = _gen.T0 + np.arange(n, dtype=np.int64) * 20
+    freq = np.full(n, 100, np.int64)
+    per = np.full(n, SEC, np.int64)
+    cnt = np.ones(n, np.uint64)
+    a, t, e = _gen.clean_states(rng, n)
+    _check_mixed(pa, [kind, names, now, freq, per, cnt, a, t, e], 16)
+
+
 def test_tag_collisions_names_always_compared(pa):
     """With the probe tag cut to 3 bits nearly every lookup meets other names
     with an equal tag: results must still be exact."""
