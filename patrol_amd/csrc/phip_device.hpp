@@ -105,6 +105,22 @@ __device__ inline double x86_nan_fix(double r, double a, double b) {
 __device__ inline double go_add(double a, double b) { return x86_nan_fix(a + b, a, b); }
 __device__ inline double go_sub(double a, double b) { return x86_nan_fix(a - b, a, b); }
 
+// dt of Take (bucket.go:198-207): last = created.Add(elapsed) (exact),
+// clamped to now, then now.Sub(last) saturating to the int64 range.  The
+// int64 fast path is exact whenever created + elapsed does not overflow.
+__device__ inline i64 take_dt(i64 created, i64 elapsed, i64 now) {
+  i64 last;
+  if (__builtin_expect(!__builtin_add_overflow(created, elapsed, &last), 1)) {
+    if (now < last) return 0;
+    i64 d;
+    return __builtin_sub_overflow(now, last, &d) ? 0x7FFFFFFFFFFFFFFFll : d;
+  }
+  __int128 l = (__int128)created + (__int128)elapsed;
+  if ((__int128)now < l) return 0;
+  __int128 dd = (__int128)now - l;
+  return dd > (__int128)0x7FFFFFFFFFFFFFFFll ? 0x7FFFFFFFFFFFFFFFll : (i64)dd;
+}
+
 struct TakeResult {
   u64 remaining;
   u64 have_bits;
@@ -116,20 +132,18 @@ struct TakeResult {
 // int64 ns; created.Add(elapsed) is exact (128-bit, as time.Time cannot
 // overflow here), now.Sub(last) saturates like time.Time.Sub, and
 // elapsed += dt wraps like Go int64.
+// capacity = float64(Freq) and t = float64(n) come precomputed (k_pack_ops).
 __device__ inline TakeResult take_step(double& added, double& taken, i64& elapsed, i64 created,
-                                       i64 now, i64 interval, i64 freq, u64 n) {
-  double capacity = (double)freq;                              // :192
+                                       i64 now, i64 interval, double capacity, double t) {
+  //                                                              :192 capacity
   if (added == 0) added = capacity;                            // :194-196
-  __int128 last = (__int128)created + (__int128)elapsed;       // :198
-  if ((__int128)now < last) last = now;                        // :199-201
+  const i64 dt = take_dt(created, elapsed, now);                // :198-207
   double tokens = go_sub(added, taken);                        // :204
-  __int128 dd = (__int128)now - last;                          // :207
-  i64 dt = dd > (__int128)0x7FFFFFFFFFFFFFFFll ? 0x7FFFFFFFFFFFFFFFll
-         : (dd < -(__int128)0x7FFFFFFFFFFFFFFFll - 1 ? (i64)kSign : (i64)dd);
-  double add = interval ? (double)dt / (double)interval : 0.0;  // :210, bucket.go:132-143
+  // :210, bucket.go:132-143; 0/interval is a zero with interval's sign
+  double add = !interval ? 0.0 : dt ? (double)dt / (double)interval : (interval < 0 ? -0.0 : 0.0);
   double missing = go_sub(capacity, tokens);                   // :211
   if (add > missing) add = missing;                            // :211-213
-  double t = (double)n;                                        // :215
+  //                                                              :215 t
   double have = go_add(tokens, add);                           // :216
   if (t > have) return TakeResult{go_u64(have), as_bits(have), false};   // :216-218
   elapsed = (i64)((u64)elapsed + (u64)dt);                     // :220

@@ -3,10 +3,12 @@
 // Pipelines:
 //   fast receive  classify -> k_receive_fast -> [insert rounds -> k_receive_fast(miss list)]
 //   ordered       resolve -> [insert rounds -> resolve(miss)] -> sort(slot, seq)
-//                 -> run-length segments -> gather ops in (slot, seq) order
+//                 (ops packed to 32-byte records, kind in the sort value)
+//                 -> run-length segments
 //                 -> k_fold_thread / k_fold_wave / k_fold_block (stream2)
 // Everything runs on the handle's own HIP stream; host synchronisation only
 // reads back small counters (miss count, segment count) between stages.
+#include <cstdlib>
 #include <cstring>
 #include <hip/hip_runtime.h>
 #include <rocprim/rocprim.hpp>
@@ -32,7 +34,7 @@ enum BufId {
   B_BYTES, B_DOFFS, B_NOFF, B_NLEN, B_DA, B_DT, B_DE,
   B_MISS, B_MISS2, B_RETRY, B_CSLOT, B_CMSG,
   B_SLOT, B_IDX, B_SSLOT, B_SIDX, B_USLOT, B_SCNT, B_SSTART, B_LONG, B_HUGE, B_TEMP, B_DUMP,
-  B_SO_NOW, B_SO_X, B_SO_Y, B_SO_Z, B_SO_KIND,
+  B_OPS, B_HOFF, B_HOP, B_HVAL, B_RPOS, B_RST, B_RUNN, B_SEGEX, B_WOFF, B_SUMS, B_WRUN,
   B_STATES, B_NAME1, B_COUNT_
 };
 
@@ -313,10 +315,6 @@ int fast_receive(phip_handle* h, Src src, const uint64_t* a, const uint64_t* t, 
 }
 
 // ------------------------------------------------------------ ordered ----
-__global__ void k_iota(u32* p, u32 n) {
-  u32 i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) p[i] = i;
-}
 
 template <class Src>
 int resolve_all(phip_handle* h, Src src, u32 n, const int64_t* now_arr, i64 now0, u32** slot_out,
@@ -352,6 +350,8 @@ int resolve_all(phip_handle* h, Src src, u32 n, const int64_t* now_arr, i64 now0
 template <class Src>
 int ordered(phip_handle* h, Src src, u32 n, const OpView& ov, const OutView& ow) {
   if (n == 0) return PHIP_OK;
+  if (n > kMaxOrderedOps)
+    return set_err(h, PHIP_ERR_INVALID, "ordered batch of %u ops exceeds 2^30", n);
   int rc;
   u32* slot;
   u32 n_claimed = 0;
@@ -362,9 +362,11 @@ int ordered(phip_handle* h, Src src, u32 n, const OpView& ov, const OutView& ow)
       (rc = ensure(h, B_SCNT, n, &scnt)) || (rc = ensure(h, B_SSTART, n, &sstart)) ||
       (rc = ensure(h, B_LONG, n, &lng)) || (rc = ensure(h, B_HUGE, n, &huge)))
     return rc;
+  OpRec* opr;
+  if ((rc = ensure(h, B_OPS, n, &opr))) return rc;
   {
-    Launch l(h, "k_iota");
-    k_iota<<<grid_for(n), kBlock, 0, h->stream>>>(idx, n);
+    Launch l(h, "k_pack_ops");
+    k_pack_ops<<<grid_for(n), kBlock, 0, h->stream>>>(ov, n, opr, idx);
   }
   // Stable radix sort of (slot, seq) pairs: per-bucket arrival order kept.
   size_t tb = 0;
@@ -391,44 +393,75 @@ int ordered(phip_handle* h, Src src, u32 n, const OpView& ov, const OutView& ow)
     HIPCHK(h, rocprim::exclusive_scan(temp, tb3, scnt, sstart, 0u, (size_t)nseg, rocprim::plus<u32>(),
                                       h->stream));
   }
-  SortedOps so;
-  if ((rc = ensure(h, B_SO_NOW, n, &so.now)) || (rc = ensure(h, B_SO_X, n, &so.x)) ||
-      (rc = ensure(h, B_SO_Y, n, &so.y)) || (rc = ensure(h, B_SO_Z, n, &so.z)) ||
-      (rc = ensure(h, B_SO_KIND, n, &so.kind)))
-    return rc;
-  so.idx = sidx;
   {
-    Launch l(h, "k_gather_ops");
-    k_gather_ops<<<grid_for(n), kBlock, 0, h->stream>>>(sidx, n, ov, so);
+    // long / huge segment lists (order-preserving compaction, no atomics)
+    Launch l(h, "select_segments");
+    size_t tb4 = 0, tb5 = 0;
+    rocprim::counting_iterator<u32> segs(0u);
+    HIPCHK(h, rocprim::select(nullptr, tb4, segs, lng, h->ctr + 6, (size_t)nseg, LongSeg{scnt},
+                              h->stream));
+    HIPCHK(h, rocprim::select(nullptr, tb5, segs, huge, h->ctr + 9, (size_t)nseg, HugeSeg{scnt},
+                              h->stream));
+    if ((rc = ensure(h, B_TEMP, std::max(tb4, tb5), &temp))) return rc;
+    HIPCHK(h, rocprim::select(temp, tb4, segs, lng, h->ctr + 6, (size_t)nseg, LongSeg{scnt},
+                              h->stream));
+    HIPCHK(h, rocprim::select(temp, tb5, segs, huge, h->ctr + 9, (size_t)nseg, HugeSeg{scnt},
+                              h->stream));
   }
-  HIPCHK(h, hipMemsetAsync(h->ctr + 6, 0, sizeof(u32), h->stream));
-  HIPCHK(h, hipMemsetAsync(h->ctr + 9, 0, sizeof(u32), h->stream));
-  {
-    Launch l(h, "k_seg_classify");
-    k_seg_classify<<<grid_for(nseg), kBlock, 0, h->stream>>>(scnt, nseg, lng, huge, h->ctr);
-  }
-  HIPCHK(h, hipGetLastError());
   if ((rc = read_ctr(h))) return rc;
   u32 nlong = h->ctr_host[6], nhuge = h->ctr_host[9];
   // Different segments touch different slots, so the folds may overlap: the
   // hot-bucket workgroups run on stream2 beside the wave and thread folds.
   if (nhuge) {
+    u64 *hoff, *woff;
+    OpRec* hop;
+    u32 *hval, *rpos, *runn, *wrun;
+    RunState* rst;
+    u8* segex;
+    WinSum* sums;
+    const size_t nwin_max = (size_t)n / kFoldWin + nhuge + 1;
+    if ((rc = ensure(h, B_WOFF, (size_t)nhuge + 1, &woff)) ||
+        (rc = ensure(h, B_SUMS, nwin_max, &sums)) || (rc = ensure(h, B_WRUN, nwin_max, &wrun)) ||
+        (rc = ensure(h, B_HOFF, nhuge, &hoff)) || (rc = ensure(h, B_HOP, n, &hop)) ||
+        (rc = ensure(h, B_HVAL, n, &hval)) || (rc = ensure(h, B_RPOS, (size_t)n + nhuge, &rpos)) ||
+        (rc = ensure(h, B_RST, (size_t)n + nhuge, &rst)) || (rc = ensure(h, B_RUNN, nhuge, &runn)) ||
+        (rc = ensure(h, B_SEGEX, nhuge, &segex)))
+      return rc;
     HIPCHK(h, hipEventRecord(h->ev_fork, h->stream));
     HIPCHK(h, hipStreamWaitEvent(h->stream2, h->ev_fork, 0));
-    Launch l(h, "k_fold_block", h->stream2);
-    k_fold_block<<<nhuge, kFoldThreads, 0, h->stream2>>>(huge, nhuge, uslot, sstart, scnt, so,
-                                                          h->recs, ow);
+    {
+      Launch l(h, "k_gather_huge", h->stream2);
+      k_huge_offsets<<<1, 1024, 0, h->stream2>>>(huge, nhuge, scnt, hoff, woff);
+      k_gather_huge<<<(unsigned)nwin_max, kBlock, 0, h->stream2>>>(huge, nhuge, hoff, woff, sstart,
+                                                                    scnt, sidx, opr, hop, hval, sums);
+    }
+    HIPCHK(h, hipGetLastError());
+    static const int variant = getenv("PHIP_FOLD_VARIANT") ? atoi(getenv("PHIP_FOLD_VARIANT")) : 0;
+    auto kb = variant == 1 ? k_fold_block<1> : k_fold_block<0>;
+    {
+      Launch l(h, "k_fold_block", h->stream2);
+      kb<<<nhuge, kFoldThreads, 0, h->stream2>>>(huge, nhuge, uslot, hoff, scnt, hval, hop,
+                                                  h->recs, rpos, rst, runn, segex, woff, sums,
+                                                  wrun);
+    }
+    HIPCHK(h, hipGetLastError());
+    {
+      Launch l(h, "k_huge_outputs", h->stream2);
+      k_huge_outputs<<<(unsigned)nwin_max, kBlock, 0, h->stream2>>>(
+          huge, nhuge, hoff, woff, scnt, hval, hop, rpos, rst, runn, segex, wrun, ow);
+    }
     HIPCHK(h, hipGetLastError());
   }
   if (nlong) {
     Launch l(h, "k_fold_wave");
-    k_fold_wave<<<nlong, 64, 0, h->stream>>>(lng, nlong, uslot, sstart, scnt, so, h->recs, ow);
+    k_fold_wave<<<nlong, 64, 0, h->stream>>>(lng, nlong, uslot, sstart, scnt, sidx, opr, h->recs,
+                                             ow);
     HIPCHK(h, hipGetLastError());
   }
   {
     Launch l(h, "k_fold_thread");
-    k_fold_thread<<<grid_for(nseg), kBlock, 0, h->stream>>>(uslot, sstart, scnt, nseg, so,
-                                                             h->recs, ow);
+    k_fold_thread<<<grid_for(nseg), kBlock, 0, h->stream>>>(uslot, sstart, scnt, nseg, sidx,
+                                                             opr, h->recs, ow);
     HIPCHK(h, hipGetLastError());
   }
   if (nhuge) {

@@ -499,18 +499,20 @@ struct OutView {
   phip_state* reply;
 };
 
-// The op stream regathered in (slot, seq) order, one column per field, so
-// that every fold reads its bucket's ops as contiguous, coalesced runs.
-//   TAKE:            x = Rate.Interval (0 = Tokens() is always 0), y = Freq, z = n
+// One op packed into 32 bytes (one aligned sector), in original order:
+//   TAKE:            x = Rate.Interval (0 = Tokens() is always 0),
+//                    y = float64(Freq) bits (capacity), z = float64(n) bits
 //   RECEIVE/UPSERT:  x = added bits, y = taken bits, z = elapsed
-struct SortedOps {
-  int64_t* now;
-  uint64_t* x;
-  uint64_t* y;
-  uint64_t* z;
-  const u32* idx;   // original op index (output position) = the sorted permutation
-  u8* kind;
+// The op kind rides in the top 2 bits of the radix-sort value (kOpIdxMask
+// below it is the op index), so a fold reads the sorted value stream
+// coalesced and then one 32-byte record per op.
+struct alignas(32) OpRec {
+  i64 now;
+  u64 x, y, z;
 };
+constexpr u32 kOpIdxBits = 30;
+constexpr u32 kOpIdxMask = (1u << kOpIdxBits) - 1;
+constexpr u32 kMaxOrderedOps = 1u << kOpIdxBits;
 
 struct SOp {
   i64 now;
@@ -519,34 +521,42 @@ struct SOp {
   u32 kind;
 };
 
-__device__ inline SOp load_sop(const SortedOps& so, u32 j) {
-  SOp o;
-  o.now = so.now[j]; o.x = so.x[j]; o.y = so.y[j]; o.z = so.z[j];
-  o.idx = so.idx[j]; o.kind = so.kind[j];
-  return o;
+__device__ inline OpRec load_oprec(const OpRec* p) {
+  const ulonglong2* q = reinterpret_cast<const ulonglong2*>(p);
+  ulonglong2 a = q[0], b = q[1];
+  return OpRec{(i64)a.x, a.y, b.x, b.y};
+}
+__device__ inline SOp make_sop(const OpRec& r, u32 v) {
+  return SOp{r.now, r.x, r.y, r.z, v & kOpIdxMask, v >> kOpIdxBits};
+}
+__device__ inline SOp load_sop(const OpRec* ops, u32 v) {
+  return make_sop(load_oprec(ops + (v & kOpIdxMask)), v);
 }
 
-// Gather: sorted position j <- original op sidx[j] (random reads, coalesced
-// writes; every later pass streams).  The per-op integer division of
-// Rate.Interval is done here, once, instead of in every fold evaluation.
-__global__ __launch_bounds__(kBlock) void k_gather_ops(const u32* __restrict__ sidx, u32 n,
-                                                       OpView ov, SortedOps so) {
-  u32 j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= n) return;
-  const u32 i = sidx[j];
+// Pack: op i -> ops[i] (coalesced reads of the ABI columns, coalesced
+// 32-byte writes) and the sort value i | kind << 30.  The per-op integer
+// division of Rate.Interval happens here, once, not in every fold round.
+__global__ __launch_bounds__(kBlock) void k_pack_ops(OpView ov, u32 n, OpRec* __restrict__ ops,
+                                                     u32* __restrict__ val) {
+  u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
   const u32 kind = ov.kind ? ov.kind[i] : ov.kind0;
-  so.now[j] = ov.now ? ov.now[i] : ov.now0;
+  OpRec r;
+  r.now = ov.now ? ov.now[i] : ov.now0;
   if (kind == PHIP_OP_TAKE) {
     const i64 f = ov.freq[i], p = ov.per[i];
-    so.x[j] = (u64)rate_interval(f, p);
-    so.y[j] = (u64)f;
-    so.z[j] = ov.count[i];
+    r.x = (u64)rate_interval(f, p);
+    r.y = as_bits((double)f);             // bucket.go:192
+    r.z = as_bits((double)ov.count[i]);   // bucket.go:215
   } else {
-    so.x[j] = ov.a[i];
-    so.y[j] = ov.t[i];
-    so.z[j] = (u64)ov.e[i];
+    r.x = ov.a[i];
+    r.y = ov.t[i];
+    r.z = (u64)ov.e[i];
   }
-  so.kind[j] = (u8)kind;   // so.idx is sidx itself
+  ulonglong2* q = reinterpret_cast<ulonglong2*>(ops + i);
+  q[0] = ulonglong2{(u64)r.now, r.x};
+  q[1] = ulonglong2{r.y, r.z};
+  val[i] = i | (kind << kOpIdxBits);
 }
 
 struct FState {
@@ -562,33 +572,46 @@ struct OpOut {
 };
 
 // One op of the ordered stream against state S (result state in S2).
-// Returns whether S2 differs from S (bitwise, or existence).
-__device__ inline bool eval_sop(const SOp& op, const FState& S, FState& S2, OpOut& out) {
+// Returns whether S2 differs from S (bitwise, or existence).  kOut: also
+// fill the op's results (the state test alone lets the compiler drop them).
+template <bool kOut>
+__device__ inline bool step_sop(const SOp& op, const FState& S, FState& S2, OpOut& out) {
   S2 = S;
   u8 cflag = 0;
   if (!S.existed) { S2.c = op.now; S2.existed = true; cflag = 0x80; }   // repo.go:208
-  out.has_reply = false; out.rem = 0; out.have = 0;
+  if (kOut) { out.has_reply = false; out.rem = 0; out.have = 0; }
   if (op.kind == PHIP_OP_TAKE) {
-    TakeResult r = take_step(S2.a, S2.t, S2.e, S2.c, op.now, (i64)op.x, (i64)op.y, op.z);
-    out.st = (r.ok ? PHIP_ST_TAKE_OK : PHIP_ST_TAKE_DENIED) | cflag;
-    out.rem = r.remaining; out.have = r.have_bits;
+    TakeResult r = take_step(S2.a, S2.t, S2.e, S2.c, op.now, (i64)op.x, as_f64(op.y), as_f64(op.z));
+    if (kOut) {
+      out.st = (r.ok ? PHIP_ST_TAKE_OK : PHIP_ST_TAKE_DENIED) | cflag;
+      out.rem = r.remaining; out.have = r.have_bits;
+    }
   } else {
     const u64 ab = op.x, tb = op.y;
     const i64 eb = (i64)op.z;
     if (op.kind == PHIP_OP_UPSERT && !S.existed) {               // repo.go:225-230
       S2.a = as_f64(ab); S2.t = as_f64(tb); S2.e = eb;
-      out.st = PHIP_ST_UPSERT_INSERTED | cflag;
+      if (kOut) out.st = PHIP_ST_UPSERT_INSERTED | cflag;
     } else if (op.kind == PHIP_OP_RECEIVE && state_is_zero(ab, tb, eb)) {   // repo.go:86-90
-      bool reply = S.existed && !state_is_zero(as_bits(S.a), as_bits(S.t), S.e);
-      out.st = (reply ? PHIP_ST_INCAST_REPLY : PHIP_ST_INCAST_NOREPLY) | cflag;
-      out.has_reply = reply;
+      if (kOut) {
+        bool reply = S.existed && !state_is_zero(as_bits(S.a), as_bits(S.t), S.e);
+        out.st = (reply ? PHIP_ST_INCAST_REPLY : PHIP_ST_INCAST_NOREPLY) | cflag;
+        out.has_reply = reply;
+      }
     } else {                                                      // bucket.go:240-263
       go_merge(S2.a, S2.t, S2.e, as_f64(ab), as_f64(tb), eb);
-      out.st = PHIP_ST_MERGED | cflag;
+      if (kOut) out.st = PHIP_ST_MERGED | cflag;
     }
   }
   return !S.existed || as_bits(S2.a) != as_bits(S.a) || as_bits(S2.t) != as_bits(S.t) ||
          S2.e != S.e;
+}
+__device__ inline bool eval_sop(const SOp& op, const FState& S, FState& S2, OpOut& out) {
+  return step_sop<true>(op, S, S2, out);
+}
+__device__ inline bool apply_sop(const SOp& op, const FState& S, FState& S2) {
+  OpOut unused;
+  return step_sop<false>(op, S, S2, unused);
 }
 
 // S is the state the op saw (an incast reply carries it, repo.go:86-90).
@@ -623,38 +646,27 @@ __device__ inline void store_state(Rec* r, const FState& S) {
 
 constexpr u32 kLongSeg = 32;        // longer segments: one wave each (k_fold_wave)
 constexpr u32 kHugeSeg = 16384;     // longer still: one workgroup each (k_fold_block)
-
-// Segment classes: small ones are folded by k_fold_thread, the others listed.
-__global__ void k_seg_classify(const u32* __restrict__ seg_count, u32 nseg, u32* long_list,
-                               u32* huge_list, u32* ctr) {
-  u32 g = blockIdx.x * blockDim.x + threadIdx.x;
-  bool is_long = false, is_huge = false;
-  if (g < nseg) {
-    u32 cnt = seg_count[g];
-    is_huge = cnt > kHugeSeg;
-    is_long = !is_huge && cnt > kLongSeg;
-  }
-  u32 p = wave_append(&ctr[6], is_long);
-  if (is_long) long_list[p] = g;
-  u32 q = wave_append(&ctr[9], is_huge);
-  if (is_huge) huge_list[q] = g;
-}
+constexpr u32 kFoldThreads = 512;   // k_fold_block: threads, ops per thread per window
+constexpr u32 kFoldPer = 4;
+constexpr u32 kFoldWin = kFoldThreads * kFoldPer;
+constexpr u32 kBurstQuiet = 16;     // a sequential burst ends after this many unchanged ops
 
 // One thread folds one short bucket segment in seq order.
 __global__ __launch_bounds__(kBlock) void k_fold_thread(
     const u32* __restrict__ seg_slot, const u32* __restrict__ seg_start,
-    const u32* __restrict__ seg_count, u32 nseg, SortedOps so, Rec* recs, OutView ow) {
+    const u32* __restrict__ seg_count, u32 nseg, const u32* __restrict__ sval,
+    const OpRec* __restrict__ ops, Rec* recs, OutView ow) {
   u32 g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= nseg) return;
   const u32 cnt = seg_count[g];
   if (cnt > kLongSeg) return;
   Rec* r = &recs[seg_slot[g]];
-  FState S = load_state(load_rec(r)), S2;
   const u32 st = seg_start[g];
-  SOp op = load_sop(so, st);
+  SOp op = load_sop(ops, sval[st]);
+  FState S = load_state(load_rec(r)), S2;
   for (u32 j = 0; j < cnt; ++j) {
-    SOp nx = op;
-    if (j + 1 < cnt) nx = load_sop(so, st + j + 1);   // next op in flight during this one
+    // next op in flight during this one (unconditional, clamped: see k_fold_block)
+    SOp nx = load_sop(ops, sval[st + min(j + 1, cnt - 1)]);
     OpOut o;
     eval_sop(op, S, S2, o);
     write_out(ow, op.idx, o, S);
@@ -675,30 +687,32 @@ __device__ inline i64 shfl_i64(i64 v, int src) {
 }
 
 // One wave folds one long segment, 64 ops per window, the window held in
-// registers (lane k owns op base+k) and the next window's ops already in
-// flight.  A round evaluates every unretired op of the window against the
-// current state; every op up to and including the first one that changes the
-// state is final (the ops before it saw exactly the state a sequential fold
-// would have shown them), and that op's result state becomes the current
-// one.  A round costs one op evaluation, so a change costs what a sequential
-// fold step costs, and a run of unchanged ops (denied Takes, no-op merges)
-// retires up to 64 ops in one step.
+// registers (lane k owns op base+k), the next window's records and the
+// sort values of the one after already in flight.  A round evaluates every
+// unretired op of the window against the current state; every op up to and
+// including the first one that changes the state is final (the ops before
+// it saw exactly the state a sequential fold would have shown them), and
+// that op's result state becomes the current one.  A round costs one op
+// evaluation, so a change costs what a sequential fold step costs, and a run
+// of unchanged ops (denied Takes, no-op merges) retires up to 64 ops at once.
 __global__ __launch_bounds__(64) void k_fold_wave(
     const u32* __restrict__ long_list, u32 nlong, const u32* __restrict__ seg_slot,
-    const u32* __restrict__ seg_start, const u32* __restrict__ seg_count, SortedOps so,
-    Rec* recs, OutView ow) {
+    const u32* __restrict__ seg_start, const u32* __restrict__ seg_count,
+    const u32* __restrict__ sval, const OpRec* __restrict__ ops, Rec* recs, OutView ow) {
   u32 w = blockIdx.x;
   if (w >= nlong) return;
   const u32 g = long_list[w];
   const u32 lane = threadIdx.x;
   Rec* r = &recs[seg_slot[g]];
-  FState S = load_state(load_rec(r));
   const u32 st = seg_start[g], cnt = seg_count[g];
-  SOp op{};
-  if (lane < cnt) op = load_sop(so, st + lane);
+  // unconditional loads, index clamped into the segment (see k_fold_block)
+  const u32 last = st + cnt - 1;
+  SOp op = load_sop(ops, sval[min(st + lane, last)]);
+  u32 v_nx = sval[min(st + 64 + lane, last)];
+  FState S = load_state(load_rec(r));
   for (u32 base = 0; base < cnt; base += 64) {
-    SOp nx{};
-    if (base + 64 + lane < cnt) nx = load_sop(so, st + base + 64 + lane);
+    SOp nx = load_sop(ops, v_nx);
+    v_nx = sval[min(st + base + 128 + lane, last)];
     const u32 lim = min(64u, cnt - base);
     u32 c = 0;
     while (c < lim) {
@@ -723,137 +737,430 @@ __global__ __launch_bounds__(64) void k_fold_wave(
   if (lane == 0) store_state(r, S);
 }
 
-// One workgroup folds one very long segment (a Zipf-hot bucket).  Windows of
-// kFoldThreads * kFoldPer ops are staged in LDS (the next window's ops are
-// loaded into registers while the current one is folded).  Per window:
-//  * parallel round: every thread evaluates its unretired ops of the window
-//    against the current state; a workgroup min finds the first op that
-//    changes it; ops up to it are final (same rule as k_fold_wave);
-//  * sequential burst: wave 0 continues op by op from there, straight out of
-//    LDS, until kBurstQuiet ops in a row leave the state unchanged.  Changes
-//    cluster (a refill or a merge that raises `added` is followed by a run
-//    of successful Takes), and a parallel round costs far more than one op,
-//    so each cluster costs about one round plus its ops at sequential speed,
-//    and the long unchanged stretches between clusters go at window speed.
-constexpr u32 kFoldThreads = 512;
-constexpr u32 kFoldPer = 4;
-constexpr u32 kFoldWin = kFoldThreads * kFoldPer;
-constexpr u32 kBurstQuiet = 16;
+// ---- window summaries: skip provably quiet windows of a hot bucket -------
+// For window w of a huge segment (ops [w*kFoldWin, (w+1)*kFoldWin)):
+//   merge-applied ops (RECEIVE of a non-zero state, UPSERT): field maxima in
+//   replica E order (enc_replica, elapsed biased);
+//   TAKE ops: the now range, and whether all share (interval, capacity, t).
+// window_quiet(S) proves that no op of the window changes S:
+//   * a merge changes nothing when E'(o) <= E(b) field by field (the
+//     E-encoding identity of phip_device.hpp; for o = -0.0, E'(o) <= E(b)
+//     means b is -0.0, positive or NaN, and Go's b < -0.0 is false);
+//   * an incast request never changes an existing bucket;
+//   * with added != 0 a denied Take changes nothing, and for one (interval,
+//     capacity, t) Take's `have` is monotone in now (dt = now - last is, and
+//     every later step is a correctly rounded monotone operation), so one
+//     denial at the extreme now of the window (max now for interval >= 0,
+//     min now for interval < 0) proves every Take of the window is denied.
+struct alignas(16) WinSum {
+  u64 ea, et, ee;        // maxima (0 = none)
+  i64 now_min, now_max;
+  u64 interval, cap, t;  // the shared Take parameters (kind bit kSumMixed if not shared)
+  u32 flags, pad;
+};
+constexpr u32 kSumTake = 1, kSumMixed = 2, kSumMerge = 4;
 
-__global__ __launch_bounds__(kFoldThreads) void k_fold_block(
-    const u32* __restrict__ huge_list, u32 nhuge, const u32* __restrict__ seg_slot,
-    const u32* __restrict__ seg_start, const u32* __restrict__ seg_count, SortedOps so,
-    Rec* recs, OutView ow) {
-  __shared__ i64 l_now[kFoldWin];
-  __shared__ u64 l_x[kFoldWin], l_y[kFoldWin], l_z[kFoldWin];
-  __shared__ u32 l_idx[kFoldWin];
-  __shared__ u8 l_kind[kFoldWin];
-  __shared__ u32 wave_min[kFoldThreads / 64];
-  __shared__ u64 s_state[4];
-  __shared__ u32 s_cur;
-  if (blockIdx.x >= nhuge) return;
-  const u32 g = huge_list[blockIdx.x];
-  const u32 tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  Rec* r = &recs[seg_slot[g]];
-  FState S = load_state(load_rec(r));
+__device__ inline bool window_quiet(const WinSum& q, const FState& S) {
+  if (!S.existed) return false;
+  if (q.flags & kSumMerge) {
+    if (q.ea > enc_f64(as_bits(S.a)) || q.et > enc_f64(as_bits(S.t)) ||
+        q.ee > ((u64)S.e ^ kSign))
+      return false;
+  }
+  if (q.flags & kSumTake) {
+    if ((q.flags & kSumMixed) || S.a == 0) return false;
+    double a = S.a, t = S.t;
+    i64 e = S.e;
+    const i64 now = (i64)q.interval < 0 ? q.now_min : q.now_max;
+    TakeResult r = take_step(a, t, e, S.c, now, (i64)q.interval, as_f64(q.cap), as_f64(q.t));
+    if (r.ok) return false;
+  }
+  return true;
+}
+
+template <u32 kDiv>
+__device__ inline void huge_scan(const u32* __restrict__ huge_list, u32 nhuge,
+                                 const u32* __restrict__ seg_count, u64* __restrict__ out,
+                                 u64* part) {
+  const u32 tid = threadIdx.x;
+  const u32 per = (nhuge + 1023) / 1024;
+  u64 sum = 0;
+  for (u32 k = 0; k < per; ++k) {
+    const u32 h = tid * per + k;
+    if (h < nhuge) sum += (seg_count[huge_list[h]] + kDiv - 1) / kDiv;
+  }
+  part[tid] = sum;
+  __syncthreads();
+  for (u32 off = 1; off < 1024; off <<= 1) {
+    u64 v = tid >= off ? part[tid - off] : 0;
+    __syncthreads();
+    part[tid] += v;
+    __syncthreads();
+  }
+  u64 base = part[tid] - sum;
+  for (u32 k = 0; k < per; ++k) {
+    const u32 h = tid * per + k;
+    if (h < nhuge) { out[h] = base; base += (seg_count[huge_list[h]] + kDiv - 1) / kDiv; }
+  }
+  __syncthreads();
+}
+
+// Offsets of the huge segments in the contiguous staging arrays (ops) and in
+// the window-summary array (one block).
+__global__ __launch_bounds__(1024) void k_huge_offsets(const u32* __restrict__ huge_list, u32 nhuge,
+                                                       const u32* __restrict__ seg_count,
+                                                       u64* __restrict__ hoff, u64* __restrict__ woff) {
+  __shared__ u64 part[1024];
+  huge_scan<1>(huge_list, nhuge, seg_count, hoff, part);
+  huge_scan<kFoldWin>(huge_list, nhuge, seg_count, woff, part);
+  if (threadIdx.x == 0 && nhuge)
+    woff[nhuge] = woff[nhuge - 1] + (seg_count[huge_list[nhuge - 1]] + kFoldWin - 1) / kFoldWin;
+}
+
+// Window b of the flat window index space -> (huge segment h, window w).
+__device__ inline bool huge_window(const u64* __restrict__ woff, u32 nhuge, u32 b, u32& h, u32& w) {
+  if (b >= woff[nhuge]) return false;
+  u32 lo = 0, hi = nhuge - 1;   // last h with woff[h] <= b
+  while (lo < hi) {
+    const u32 mid = (lo + hi + 1) >> 1;
+    if (woff[mid] <= b) lo = mid; else hi = mid - 1;
+  }
+  h = lo;
+  w = b - (u32)woff[lo];
+  return true;
+}
+
+// The ops of every huge segment gathered into contiguous (slot, seq) order
+// by the whole chip, one block per fold window, so that the one workgroup
+// folding a hot bucket streams its input instead of chasing one random
+// record per op (a single CU cannot keep enough random misses in flight).
+// The same pass writes the window's summary (WinSum).
+constexpr u32 kGatherPer = kFoldWin / kBlock;
+
+__global__ __launch_bounds__(kBlock) void k_gather_huge(
+    const u32* __restrict__ huge_list, u32 nhuge, const u64* __restrict__ hoff,
+    const u64* __restrict__ woff, const u32* __restrict__ seg_start,
+    const u32* __restrict__ seg_count, const u32* __restrict__ sval,
+    const OpRec* __restrict__ ops, OpRec* __restrict__ hop, u32* __restrict__ hval,
+    WinSum* __restrict__ sums) {
+  __shared__ u64 red[6][kBlock / 64];
+  __shared__ u32 s_first;
+  __shared__ u64 s_par[3];
+  u32 h, w;
+  if (!huge_window(woff, nhuge, blockIdx.x, h, w)) return;
+  const u32 g = huge_list[h];
   const u32 st = seg_start[g], cnt = seg_count[g];
+  const u64 dst = hoff[h];
+  const u32 tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const u32 p0 = w * kFoldWin, p1 = min(cnt, p0 + kFoldWin);
+  if (tid == 0) s_first = 0xFFFFFFFFu;
+  u32 v[kGatherPer];
+  OpRec r[kGatherPer];
+#pragma unroll
+  for (u32 k = 0; k < kGatherPer; ++k) v[k] = sval[st + min(p0 + k * kBlock + tid, p1 - 1)];
+#pragma unroll
+  for (u32 k = 0; k < kGatherPer; ++k) r[k] = load_oprec(ops + (v[k] & kOpIdxMask));
+  u64 ea = 0, et = 0, ee = 0, nmin = ~0ull, nmax = 0;
+  u32 first_take = 0xFFFFFFFFu;
+  bool merge = false;
+#pragma unroll
+  for (u32 k = 0; k < kGatherPer; ++k) {
+    const u32 j = p0 + k * kBlock + tid;
+    if (j >= p1) continue;
+    ulonglong2* q = reinterpret_cast<ulonglong2*>(hop + dst + j);
+    q[0] = ulonglong2{(u64)r[k].now, r[k].x};
+    q[1] = ulonglong2{r[k].y, r[k].z};
+    hval[dst + j] = v[k];
+    const u32 kind = v[k] >> kOpIdxBits;
+    if (kind == PHIP_OP_TAKE) {
+      const u64 nb = (u64)r[k].now ^ kSign;
+      nmin = min(nmin, nb); nmax = max(nmax, nb);
+      first_take = min(first_take, j);
+    } else if (kind == PHIP_OP_UPSERT || !state_is_zero(r[k].x, r[k].y, (i64)r[k].z)) {
+      merge = true;
+      ea = max(ea, enc_replica(r[k].x)); et = max(et, enc_replica(r[k].y));
+      ee = max(ee, r[k].z ^ kSign);
+    }
+  }
+  __syncthreads();
+  if (first_take != 0xFFFFFFFFu) atomicMin(&s_first, first_take);
+  __syncthreads();
+  const u32 ft = s_first;
+#pragma unroll
+  for (u32 k = 0; k < kGatherPer; ++k)
+    if (p0 + k * kBlock + tid == ft) { s_par[0] = r[k].x; s_par[1] = r[k].y; s_par[2] = r[k].z; }
+  __syncthreads();
+  bool mixed = false;
+  if (ft != 0xFFFFFFFFu) {
+    const u64 iv = s_par[0], cp = s_par[1], tb = s_par[2];
+#pragma unroll
+    for (u32 k = 0; k < kGatherPer; ++k) {
+      const u32 j = p0 + k * kBlock + tid;
+      if (j < p1 && (v[k] >> kOpIdxBits) == PHIP_OP_TAKE)
+        mixed |= r[k].x != iv || r[k].y != cp || r[k].z != tb;
+    }
+  }
+  u64 x[6] = {ea, et, ee, ~nmin, nmax, (u64)(merge ? 1 : 0) | (mixed ? 2 : 0)};
+#pragma unroll
+  for (int k = 0; k < 6; ++k)
+    for (int off = 32; off >= 1; off >>= 1) {
+      const u64 o = (u64)__shfl_xor((long long)x[k], off);
+      x[k] = k == 5 ? (x[k] | o) : max(x[k], o);
+    }
+  if (lane == 0)
+    for (int k = 0; k < 6; ++k) red[k][wv] = x[k];
+  __syncthreads();
+  if (tid == 0) {
+    for (u32 y = 1; y < kBlock / 64; ++y) {
+      for (int k = 0; k < 5; ++k) x[k] = max(x[k], red[k][y]);
+      x[5] |= red[5][y];
+    }
+    WinSum q;
+    q.ea = x[0]; q.et = x[1]; q.ee = x[2];
+    q.now_min = (i64)(~x[3] ^ kSign); q.now_max = (i64)(x[4] ^ kSign);
+    q.interval = ft != 0xFFFFFFFFu ? s_par[0] : 0;
+    q.cap = ft != 0xFFFFFFFFu ? s_par[1] : 0;
+    q.t = ft != 0xFFFFFFFFu ? s_par[2] : 0;
+    q.flags = (ft != 0xFFFFFFFFu ? kSumTake : 0) | ((x[5] & 2) ? kSumMixed : 0) |
+              ((x[5] & 1) ? kSumMerge : 0);
+    q.pad = 0;
+    sums[woff[h] + w] = q;
+  }
+}
 
-  SOp pre[kFoldPer];
+// The hot-bucket fold records the bucket's state history as runs instead of
+// per-op results: run k says "ops [pos_k, pos_{k+1}) of the segment all saw
+// state state_k".  k_huge_outputs then evaluates every op against its run's
+// state on the whole chip and writes the results, so the one workgroup on
+// the sequential critical path only streams ops and tests "does this op
+// change the state?".
+struct RunState {
+  u64 a, t;   // float64 bits
+  i64 e, c;
+};
+
+__device__ inline void put_run(u32* run_pos, RunState* run_st, u32 k, u32 pos, const FState& S) {
+  run_pos[k] = pos;
+  run_st[k] = RunState{as_bits(S.a), as_bits(S.t), S.e, S.c};
+}
+
+// One workgroup folds one very long segment (a Zipf-hot bucket) from the
+// contiguous copy k_gather_huge made.  Thread t owns ops k*kFoldThreads + t
+// (k < kFoldPer) of each window of kFoldWin ops; two windows are held in
+// registers (buffers A and B, the loop unrolled by two so the loads of the
+// window after next are in flight while one is folded).  Per window:
+//  * parallel round: every thread tests its unretired ops against the
+//    current state; a workgroup min finds the first op that changes it; the
+//    ops before it are retired (they saw the current state);
+//  * sequential burst (only when a round found a change): the window is
+//    staged in LDS and wave 0 applies ops one by one from that op, appending
+//    a run at every change, until kBurstQuiet ops in a row leave the state
+//    unchanged.  Changes cluster (a merge that raises `added` is followed by a
+//    run of successful Takes) and a round costs far more than one op, so a
+//    cluster costs about one round plus its ops at sequential speed, and the
+//    long unchanged stretches between clusters cost one round per window.
+
+struct FoldWin {
+  u32 v[kFoldPer];
+  OpRec r[kFoldPer];
+};
+
+constexpr u32 kSumChunk = kFoldThreads;   // window summaries staged in LDS at a time
+
+struct FoldShared {
+  OpRec op[kFoldWin];
+  u32 val[kFoldWin];
+  WinSum sum[kSumChunk];
+  u32 wave_min[2][kFoldThreads / 64];
+  u64 state[4];
+  u32 cur, nrun;
+};
+
+// Loads are unconditional (index clamped into the segment): a load under a
+// runtime condition makes hipcc branch around it and wait for it on the spot
+// (cdna_hip_programming.md, "traps that silently de-pipeline").
+__device__ inline void fold_load(FoldWin& W, const u32* __restrict__ sv,
+                                 const OpRec* __restrict__ so, u32 pos, u32 last, u32 tid) {
 #pragma unroll
   for (u32 k = 0; k < kFoldPer; ++k) {
-    const u32 j = k * kFoldThreads + tid;
-    if (j < cnt) pre[k] = load_sop(so, st + j);
+    const u32 j = min(pos + k * kFoldThreads + tid, last);
+    W.v[k] = sv[j];
+    W.r[k] = load_oprec(so + j);
   }
-  for (u32 pos = 0; pos < cnt; pos += kFoldWin) {
-    const u32 lim = min(kFoldWin, cnt - pos);
-    __syncthreads();   // the previous window's LDS readers are done
+}
+
+template <int V>
+__device__ inline void fold_window(const FoldWin& W, u32 pos, u32 lim, FState& S, u32& round,
+                                   FoldShared& sh, u32* rp, RunState* rs, u32 tid) {
+  const u32 lane = tid & 63, wv = tid >> 6;
+  u32 cur = 0;
+  bool staged = false;
+  while (cur < lim) {
+    u32 my_first = 0xFFFFFFFFu;
+    if constexpr (!(V & 1)) {
 #pragma unroll
-    for (u32 k = 0; k < kFoldPer; ++k) {
-      const u32 w = k * kFoldThreads + tid;
-      if (w < lim) {
-        l_now[w] = pre[k].now; l_x[w] = pre[k].x; l_y[w] = pre[k].y; l_z[w] = pre[k].z;
-        l_idx[w] = pre[k].idx; l_kind[w] = (u8)pre[k].kind;
+      for (u32 k = 0; k < kFoldPer; ++k) {
+        const u32 w = k * kFoldThreads + tid;
+        if (w >= cur && w < lim && my_first == 0xFFFFFFFFu) {
+          FState S2;
+          if (apply_sop(make_sop(W.r[k], W.v[k]), S, S2)) my_first = w;
+        }
+      }
+    }
+    u32 m = my_first;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) m = min(m, (u32)__shfl_xor((int)m, off));
+    u32* wm = sh.wave_min[round & 1];   // alternating: one barrier per round suffices
+    ++round;
+    if (lane == 0) wm[wv] = m;
+    __syncthreads();
+    u32 first = 0xFFFFFFFFu;
+#pragma unroll
+    for (u32 x = 0; x < kFoldThreads / 64; ++x) first = min(first, wm[x]);
+    if (first == 0xFFFFFFFFu) return;
+    if (!staged) {
+#pragma unroll
+      for (u32 k = 0; k < kFoldPer; ++k) {
+        const u32 w = k * kFoldThreads + tid;
+        sh.op[w] = W.r[k];
+        sh.val[w] = W.v[k];
+      }
+      staged = true;
+      __syncthreads();
+    }
+    // ---- sequential burst (wave 0) from `first`, which changes the state
+    if (wv == 0) {
+      FState T = S;
+      u32 j = first, quiet = 0, nrun = sh.nrun;
+      while (j < lim && quiet < kBurstQuiet) {
+        FState T2;
+        if (apply_sop(make_sop(sh.op[j], sh.val[j]), T, T2)) {
+          T = T2;
+          if (lane == 0) put_run(rp, rs, nrun, pos + j + 1, T);
+          ++nrun;
+          quiet = 0;
+        } else {
+          ++quiet;
+        }
+        ++j;
+      }
+      if (lane == 0) {
+        sh.state[0] = as_bits(T.a); sh.state[1] = as_bits(T.t);
+        sh.state[2] = (u64)T.e; sh.state[3] = (u64)T.c;
+        sh.cur = j;
+        sh.nrun = nrun;
       }
     }
     __syncthreads();
-#pragma unroll
-    for (u32 k = 0; k < kFoldPer; ++k) {
-      const u32 j = pos + kFoldWin + k * kFoldThreads + tid;
-      if (j < cnt) pre[k] = load_sop(so, st + j);
-    }
-    u32 cur = 0;
-    while (cur < lim) {
-      // ---- parallel round over [cur, lim)
-      OpOut out[kFoldPer];
-      u32 my_first = 0xFFFFFFFFu;
-      FState mine = S;
-#pragma unroll
-      for (u32 k = 0; k < kFoldPer; ++k) {
-        const u32 w = cur + k * kFoldThreads + tid;
-        if (w < lim) {
-          SOp op;
-          op.now = l_now[w]; op.x = l_x[w]; op.y = l_y[w]; op.z = l_z[w];
-          op.idx = l_idx[w]; op.kind = l_kind[w];
-          FState S2;
-          bool ch = eval_sop(op, S, S2, out[k]);
-          if (ch && my_first == 0xFFFFFFFFu) { my_first = w; mine = S2; }
-        }
-      }
-      u32 m = my_first;
-#pragma unroll
-      for (int off = 32; off >= 1; off >>= 1) m = min(m, (u32)__shfl_xor((int)m, off));
-      if (lane == 0) wave_min[wv] = m;
-      __syncthreads();
-      u32 first = 0xFFFFFFFFu;
-#pragma unroll
-      for (u32 x = 0; x < kFoldThreads / 64; ++x) first = min(first, wave_min[x]);
-#pragma unroll
-      for (u32 k = 0; k < kFoldPer; ++k) {
-        const u32 w = cur + k * kFoldThreads + tid;
-        if (w < lim && w <= first) write_out(ow, l_idx[w], out[k], S);
-      }
-      if (first == 0xFFFFFFFFu) {
-        cur = lim;
-        break;   // the loop-top barrier of the next window orders wave_min reuse
-      }
-      if (my_first == first) {
-        s_state[0] = as_bits(mine.a); s_state[1] = as_bits(mine.t);
-        s_state[2] = (u64)mine.e; s_state[3] = (u64)mine.c;
-      }
-      __syncthreads();
-      // ---- sequential burst (wave 0) from first + 1
-      if (wv == 0) {
-        FState T;
-        T.a = as_f64(s_state[0]); T.t = as_f64(s_state[1]);
-        T.e = (i64)s_state[2]; T.c = (i64)s_state[3]; T.existed = true;
-        u32 j = first + 1, quiet = 0;
-        while (j < lim && quiet < kBurstQuiet) {
-          SOp op;
-          op.now = l_now[j]; op.x = l_x[j]; op.y = l_y[j]; op.z = l_z[j];
-          op.idx = l_idx[j]; op.kind = l_kind[j];
-          FState T2;
-          OpOut o;
-          const bool ch = eval_sop(op, T, T2, o);
-          if (lane == 0) write_out(ow, op.idx, o, T);
-          T = T2;
-          quiet = ch ? 0 : quiet + 1;
-          ++j;
-        }
-        if (lane == 0) {
-          s_state[0] = as_bits(T.a); s_state[1] = as_bits(T.t);
-          s_state[2] = (u64)T.e; s_state[3] = (u64)T.c;
-          s_cur = j;
-        }
-      }
-      __syncthreads();
-      S.a = as_f64(s_state[0]); S.t = as_f64(s_state[1]);
-      S.e = (i64)s_state[2]; S.c = (i64)s_state[3]; S.existed = true;
-      cur = s_cur;
-      __syncthreads();   // s_state / s_cur / wave_min are rewritten by the next round
-    }
+    S.a = as_f64(sh.state[0]); S.t = as_f64(sh.state[1]);
+    S.e = (i64)sh.state[2]; S.c = (i64)sh.state[3]; S.existed = true;
+    cur = sh.cur;
+    __syncthreads();   // state / cur are rewritten by the next burst
   }
-  if (tid == 0) store_state(r, S);
 }
+
+// Ablation variants (tools only, PHIP_FOLD_VARIANT): 1 = no state test
+// (every op unchanged: streaming cost alone).
+template <int V = 0>
+__global__ __launch_bounds__(kFoldThreads) void k_fold_block(
+    const u32* __restrict__ huge_list, u32 nhuge, const u32* __restrict__ seg_slot,
+    const u64* __restrict__ hoff, const u32* __restrict__ seg_count,
+    const u32* __restrict__ hval, const OpRec* __restrict__ hop, Rec* recs,
+    u32* __restrict__ run_pos, RunState* __restrict__ run_st, u32* __restrict__ run_n,
+    u8* __restrict__ seg_existed, const u64* __restrict__ woff, const WinSum* __restrict__ sums,
+    u32* __restrict__ win_run) {
+  __shared__ FoldShared sh;
+  if (blockIdx.x >= nhuge) return;
+  const u32 g = huge_list[blockIdx.x];
+  const u32 tid = threadIdx.x;
+  Rec* r = &recs[seg_slot[g]];
+  const u32 cnt = seg_count[g], last = cnt - 1;
+  const u64 base = hoff[blockIdx.x];
+  const u32* __restrict__ sv = hval + base;
+  const OpRec* __restrict__ so = hop + base;
+  // this segment's runs: at most one per op plus the initial one
+  u32* rp = run_pos + base + blockIdx.x;
+  RunState* rs = run_st + base + blockIdx.x;
+
+  FState S = load_state(load_rec(r));
+  if (tid == 0) {
+    put_run(rp, rs, 0, 0, S);
+    seg_existed[blockIdx.x] = S.existed;
+    sh.nrun = 1;
+  }
+  const u32 nwin = (cnt + kFoldWin - 1) / kFoldWin;
+  const WinSum* __restrict__ ws = sums + woff[blockIdx.x];
+  u32* __restrict__ wr = win_run + woff[blockIdx.x];
+  u32 round = 0;
+  FoldWin A;
+  for (u32 w = 0; w < nwin; ++w) {
+    if (tid == 0) wr[w] = sh.nrun - 1;   // run in effect at the window's first op
+    if (w % kSumChunk == 0) {
+      __syncthreads();   // previous chunk's readers are done
+      if (w + tid < nwin) sh.sum[tid] = ws[w + tid];
+      __syncthreads();
+    }
+    if (window_quiet(sh.sum[w % kSumChunk], S)) continue;   // uniform decision
+    const u32 pos = w * kFoldWin;
+    fold_load(A, sv, so, pos, last, tid);
+    fold_window<V>(A, pos, min(kFoldWin, cnt - pos), S, round, sh, rp, rs, tid);
+  }
+  if (tid == 0) {
+    store_state(r, S);
+    run_n[blockIdx.x] = sh.nrun;
+  }
+}
+
+// Results of every op of the huge segments: op j of segment h saw the state
+// of the last run of h starting at or before j.  One block per fold window;
+// the fold recorded the run in effect at each window start, so the search
+// only spans the runs that begin inside the window (usually none).
+__global__ __launch_bounds__(kBlock) void k_huge_outputs(
+    const u32* __restrict__ huge_list, u32 nhuge, const u64* __restrict__ hoff,
+    const u64* __restrict__ woff, const u32* __restrict__ seg_count,
+    const u32* __restrict__ hval, const OpRec* __restrict__ hop,
+    const u32* __restrict__ run_pos, const RunState* __restrict__ run_st,
+    const u32* __restrict__ run_n, const u8* __restrict__ seg_existed,
+    const u32* __restrict__ win_run, OutView ow) {
+  u32 h, w;
+  if (!huge_window(woff, nhuge, blockIdx.x, h, w)) return;
+  const u32 cnt = seg_count[huge_list[h]];
+  const u64 base = hoff[h];
+  const u32* rp = run_pos + base + h;
+  const RunState* rs = run_st + base + h;
+  const u32 nwin = (u32)(woff[h + 1] - woff[h]);
+  const u32 k0 = win_run[woff[h] + w];
+  const u32 k1 = w + 1 < nwin ? win_run[woff[h] + w + 1] : run_n[h] - 1;
+  const bool existed0 = seg_existed[h];
+  const u32 p0 = w * kFoldWin, p1 = min(cnt, p0 + kFoldWin);
+  for (u32 j = p0 + threadIdx.x; j < p1; j += kBlock) {
+    u32 lo = k0, hi = k1;   // last k in [k0, k1] with rp[k] <= j
+    while (lo < hi) {
+      const u32 mid = (lo + hi + 1) >> 1;
+      if (rp[mid] <= j) lo = mid; else hi = mid - 1;
+    }
+    const RunState q = rs[lo];
+    FState S;
+    S.a = as_f64(q.a); S.t = as_f64(q.t); S.e = q.e; S.c = q.c;
+    S.existed = lo > 0 || existed0;
+    const SOp op = make_sop(load_oprec(hop + base + j), hval[base + j]);
+    FState S2;
+    OpOut o;
+    eval_sop(op, S, S2, o);
+    write_out(ow, op.idx, o, S);
+  }
+}
+
+// Segment classes for rocprim::select (segments are folded by k_fold_thread
+// unless listed here).
+struct LongSeg {
+  const u32* cnt;
+  __device__ bool operator()(u32 g) const { return cnt[g] > kLongSeg && cnt[g] <= kHugeSeg; }
+};
+struct HugeSeg {
+  const u32* cnt;
+  __device__ bool operator()(u32 g) const { return cnt[g] > kHugeSeg; }
+};
 
 // Sorted-slot segments from run-length output (counts -> starts is a scan).
 __global__ void k_seg_mark(const u32* __restrict__ sorted_slot, u32 n, u32* head) {

@@ -295,6 +295,70 @@ def test_mixed_c3_shape_clamped_clock(pa):
     _check_mixed(pa, [kind, names, now, freq, per, cnt, a, t, e], 16)
 
 
+def test_take_clock_extremes(pa):
+    """Take's clock arithmetic at the int64 edges (bucket.go:198-207):
+    created + elapsed overflowing either way, now.Sub saturating, negative
+    clocks, with every fold kind (1, 40 and 20000 ops per bucket)."""
+    rng = np.random.default_rng(2718)
+    I64 = np.iinfo(np.int64)
+    edge = np.array([I64.min, I64.min + 1, -(1 << 62), -SEC, -1, 0, 1, SEC, 1 << 62,
+                     I64.max - 1, I64.max], np.int64)
+    K = 60
+    names = [b"edge%d" % k for k in range(K)]
+    created = edge[rng.integers(0, len(edge), K)]
+    elapsed = edge[rng.integers(0, len(edge), K)]
+    added = (rng.random(K) * 50).view(np.uint64)
+    taken = (rng.random(K) * 10).view(np.uint64)
+    reps = np.concatenate([np.full(20, 1), np.full(30, 40), np.full(10, 20000)])
+    ids = np.repeat(np.arange(K), reps)
+    rng.shuffle(ids)
+    n = len(ids)
+    nm = [names[i] for i in ids]
+    kind = (rng.random(n) < 0.8).astype(np.uint8) ^ 1        # mostly Take
+    now = edge[rng.integers(0, len(edge), n)].copy()
+    mid = rng.random(n) < 0.5
+    now[mid] = rng.integers(-(1 << 62), 1 << 62, int(mid.sum()))
+    freq = rng.choice(np.array([1, 3, 100, 1 << 40, -7], np.int64), n)
+    per = rng.choice(np.array([SEC, 1, 3 * SEC, I64.max, I64.min], np.int64), n)
+    cnt = rng.choice(np.array([0, 1, 2, 5], np.uint64), n)
+    a = (rng.random(n) * 60).view(np.uint64)
+    t = (rng.random(n) * 20).view(np.uint64)
+    e = edge[rng.integers(0, len(edge), n)]
+    g = pa.GPURepo(log2_slots=10)
+    o = O.Repo()
+    g.seed(names, added, taken, elapsed, created)
+    o.seed(names, added, taken, elapsed, created)
+    out = g.apply_mixed(kind, nm, now, freq, per, cnt, a, t, e)
+    ref = o.apply_mixed(kind, nm, now, freq, per, cnt, a, t, e)
+    assert np.array_equal(out["status"], ref["status"])
+    assert np.array_equal(out["remaining"], ref["remaining"])
+    tk = kind == 0
+    assert np.array_equal(out["have"][tk], ref["have"][tk])
+    assert_same_dump(gpu_dump(g), o.dump())
+
+
+@pytest.mark.parametrize("freq,per", [(100, SEC), (-5, SEC), (7, 0), (3, -SEC)])
+def test_hot_bucket_quiet_window_skips(pa, freq, per):
+    """k_fold_block skips windows its summary proves quiet: one uniform rate
+    per run (positive, negative and zero intervals), jittered clocks (now not
+    monotone), merges carrying -0.0, NaN and negatives, an incast now and
+    then; 3 buckets of ~40k ops each (about 20 windows of 2048)."""
+    rng = np.random.default_rng(abs(freq) * 7 + 3)
+    n = 120000
+    ids = rng.integers(0, 3, n)
+    names = [b"hot%d" % i for i in ids]
+    kind = (rng.random(n) < 0.3).astype(np.uint8)          # 70% Take
+    now = _gen.T0 + np.arange(n, dtype=np.int64) * 50_000 + rng.integers(-2 * MS, 2 * MS, n)
+    fr = np.full(n, freq, np.int64)
+    pe = np.full(n, per, np.int64)
+    cnt = np.ones(n, np.uint64)
+    a, t, e = _gen.dirty_states(rng, n, 0.02)
+    a = (np.abs(a.view(np.float64)) / 1e5).view(np.uint64).copy()
+    t = (np.abs(t.view(np.float64)) / 1e5).view(np.uint64).copy()
+    e = e >> 20
+    _check_mixed(pa, [kind, names, now, fr, pe, cnt, a, t, e], 10, reply=True)
+
+
 def test_tag_collisions_names_always_compared(pa):
     """With the probe tag cut to 3 bits nearly every lookup meets other names
     with an equal tag: results must still be exact."""
