@@ -220,6 +220,10 @@ int phip_hash_names(phip_handle* h, const uint8_t* names, const uint32_t* name_o
 int phip_last_timings(phip_handle* h, const char** names, float* ms, int max);
 /* Enable (1) or disable (0) event timing (off by default). */
 void phip_set_timing(phip_handle* h, int on);
+/* Counters of the last fast-path Receive batch: out[0] hot-directory
+ * entries, out[1] messages folded through the directory, out[2] messages
+ * that missed the table (inserted).  Returns the number written (<= 3). */
+int phip_last_stats(phip_handle* h, uint64_t* out, int max);
 
 #ifdef __cplusplus
 }

@@ -17,7 +17,7 @@ EXPORTS = [
     "phip_abi_version", "phip_open", "phip_close", "phip_last_error", "phip_flush", "phip_len",
     "phip_capacity", "phip_seed", "phip_get", "phip_dump", "phip_receive_datagrams",
     "phip_receive_soa", "phip_upsert_soa", "phip_apply_mixed", "phip_take", "phip_parse_rate",
-    "phip_marshal", "phip_api_take", "phip_last_timings", "phip_set_timing", "phip_hash_names",
+    "phip_marshal", "phip_api_take", "phip_last_timings", "phip_set_timing", "phip_last_stats", "phip_hash_names",
 ]
 
 PHIP_OK = 0
@@ -98,5 +98,7 @@ def load(path: str = LIB_PATH):
     L.phip_hash_names.argtypes = [vp, vp, vp, u32, vp, u32]
     L.phip_set_timing.argtypes = [vp, C.c_int]
     L.phip_set_timing.restype = None
+    L.phip_last_stats.argtypes = [vp, C.POINTER(C.c_uint64), C.c_int]
+    L.phip_last_stats.restype = C.c_int
     _lib = L
     return L

@@ -1,7 +1,8 @@
 // libpatrolhip host orchestration: the C ABI of include/patrolhip.h.
 //
 // Pipelines:
-//   fast receive  classify -> k_receive_fast -> [insert rounds -> k_receive_fast(miss list)]
+//   fast receive  classify -> hot directory -> k_receive_fast
+//                 -> [insert rounds -> k_receive_list(miss list)]
 //   ordered       resolve -> [insert rounds -> resolve(miss)] -> sort(slot, seq)
 //                 (ops packed to 32-byte records, kind in the sort value)
 //                 -> run-length segments
@@ -35,7 +36,7 @@ enum BufId {
   B_MISS, B_MISS2, B_RETRY, B_CSLOT, B_CMSG,
   B_SLOT, B_IDX, B_SSLOT, B_SIDX, B_USLOT, B_SCNT, B_SSTART, B_LONG, B_HUGE, B_TEMP, B_DUMP,
   B_OPS, B_HOFF, B_HOP, B_HVAL, B_RPOS, B_RST, B_RUNN, B_SEGEX, B_WOFF, B_SUMS, B_WRUN,
-  B_STATES, B_NAME1, B_COUNT_
+  B_STATES, B_NAME1, B_HOT, B_COUNT_
 };
 
 struct DevBuf {
@@ -52,6 +53,8 @@ struct Timing {
 
 struct phip_handle {
   int device = 0;
+  int ncu = 256;             // compute units (persistent grid size)
+  uint64_t stats[3] = {0, 0, 0};   // last fast batch: hot entries, hot hits, misses
   hipStream_t stream = nullptr;
   hipStream_t stream2 = nullptr;   // second stream: the hot-bucket fold overlaps the others
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
@@ -274,6 +277,49 @@ int clear_new(phip_handle* h, u32 n_claimed) {
 }
 
 // ------------------------------------------------------- fast receive ----
+// Hot directory of a fast batch (phip_kernels.hpp): sample -> count ->
+// threshold -> directory, all on the stream (no host round trip).  Returns
+// the header/directory to hand to k_receive_fast (nullptr: none).
+template <class Src>
+int build_hot(phip_handle* h, Src src, u32 n, const HotHdr** hdr_out, const HotEntry** dir_out) {
+  *hdr_out = nullptr;
+  *dir_out = nullptr;
+  if (n < kHotMinBatch) return PHIP_OK;
+  constexpr size_t kCnt = size_t(1) << kHotCntBits;
+  const size_t zero_bytes = 2 * kCnt * sizeof(u32) + kHotHist * sizeof(u32) + sizeof(HotHdr);
+  u8* base;
+  int rc;
+  if ((rc = ensure(h, B_HOT, zero_bytes + kHotMax * sizeof(HotEntry), &base))) return rc;
+  u32* ckeys = (u32*)base;
+  u32* ccnt = ckeys + kCnt;
+  u32* hist = ccnt + kCnt;
+  HotHdr* hdr = (HotHdr*)(hist + kHotHist);
+  HotEntry* dir = (HotEntry*)(hdr + 1);
+  HIPCHK(h, hipMemsetAsync(base, 0, zero_bytes, h->stream));
+  const u32 stride = std::max<u32>(64, (n + kHotSampleMax - 1) / kHotSampleMax);
+  const u32 nsample = (n + stride - 1) / stride;
+  {
+    Launch l(h, "k_hot_sample");
+    k_hot_sample<Src><<<grid_for(nsample, 256), 256, 0, h->stream>>>(src, n, stride, nsample, table(h),
+                                                                    ckeys, ccnt);
+  }
+  {
+    Launch l(h, "k_hot_select");
+    k_hot_hist<<<grid_for(kCnt), kBlock, 0, h->stream>>>(ccnt, hist);
+    k_hot_select<<<1, 256, 0, h->stream>>>(hist, hdr);
+    k_hot_build<<<grid_for(kCnt), kBlock, 0, h->stream>>>(ckeys, ccnt, hdr, table(h), dir);
+  }
+  HIPCHK(h, hipGetLastError());
+  *hdr_out = hdr;
+  *dir_out = dir;
+  return PHIP_OK;
+}
+
+inline unsigned fast_grid(phip_handle* h, u32 n) {
+  const u64 tiles = (n + kFastBlock - 1) / kFastBlock;
+  return (unsigned)std::max<u64>(1, std::min<u64>(tiles, (u64)h->ncu * kFastPerCU));
+}
+
 template <class Src>
 int fast_receive(phip_handle* h, Src src, const uint64_t* a, const uint64_t* t, const int64_t* e,
                  u32 n, i64 now,
@@ -281,15 +327,21 @@ int fast_receive(phip_handle* h, Src src, const uint64_t* a, const uint64_t* t, 
   u32* miss;
   int rc;
   if ((rc = ensure(h, B_MISS, n, &miss))) return rc;
+  const HotHdr* hot;
+  const HotEntry* hot_dir;
+  if ((rc = build_hot(h, src, n, &hot, &hot_dir))) return rc;
   {
     Launch l(h, "k_receive_fast");
-    k_receive_fast<Src><<<grid_for(n), kBlock, 0, h->stream>>>(src, a, t, e, n, nullptr, table(h),
-                                                                status, miss, h->ctr, 0);
+    k_receive_fast<Src><<<fast_grid(h, n), kFastBlock, 0, h->stream>>>(
+        src, a, t, e, n, table(h), status, miss, h->ctr, hot, hot_dir);
   }
   HIPCHK(h, hipGetLastError());
   if ((rc = read_ctr(h))) return rc;
   if ((rc = check_flags(h))) return rc;
   u32 nmiss = h->ctr_host[2];
+  h->stats[0] = h->ctr_host[11];
+  h->stats[1] = h->ctr_host[10];
+  h->stats[2] = nmiss;
   if (nmiss == 0) return PHIP_OK;
   u32 n_claimed = 0;
   if ((rc = insert_names(h, src, miss, nmiss, nullptr, now, &n_claimed))) return rc;
@@ -298,9 +350,9 @@ int fast_receive(phip_handle* h, Src src, const uint64_t* a, const uint64_t* t, 
   u32* miss2;
   if ((rc = ensure(h, B_MISS2, nmiss, &miss2))) return rc;
   {
-    Launch l(h, "k_receive_fast_miss");
-    k_receive_fast<Src><<<grid_for(nmiss), kBlock, 0, h->stream>>>(
-        src, a, t, e, nmiss, miss, table(h), status, miss2, h->ctr, 1);
+    Launch l(h, "k_receive_list");
+    k_receive_list<Src><<<grid_for(nmiss), kBlock, 0, h->stream>>>(
+        src, a, t, e, nmiss, miss, table(h), status, miss2, h->ctr);
   }
   HIPCHK(h, hipGetLastError());
   {
@@ -580,6 +632,9 @@ int phip_open(const phip_config* cfg, phip_handle** out) {
   };
   hipError_t e;
   if ((e = hipSetDevice(h->device)) != hipSuccess) return fail(e);
+  if ((e = hipDeviceGetAttribute(&h->ncu, hipDeviceAttributeMultiprocessorCount, h->device)) !=
+      hipSuccess)
+    return fail(e);
   if ((e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking)) != hipSuccess) return fail(e);
   if ((e = hipStreamCreateWithFlags(&h->stream2, hipStreamNonBlocking)) != hipSuccess) return fail(e);
   if ((e = hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming)) != hipSuccess) return fail(e);
@@ -947,6 +1002,14 @@ int phip_last_timings(phip_handle* h, const char** names, float* ms, int max) {
 
 void phip_set_timing(phip_handle* h, int on) {
   if (h) h->timing = on != 0;
+}
+
+int phip_last_stats(phip_handle* h, uint64_t* out, int max) {
+  if (!h || !out) return 0;
+  std::lock_guard<std::mutex> g(h->mu);
+  int k = 0;
+  for (; k < max && k < 3; ++k) out[k] = h->stats[k];
+  return k;
 }
 
 }  // extern "C"

@@ -191,118 +191,375 @@ __global__ void k_classify(const uint64_t* __restrict__ a, const uint64_t* __res
 // The batched Receive loop (repo.go:54-92) for a batch with no incast and no
 // -0.0: GetBucket(name) + Merge(&remote) for every message.
 //
-// Each lane resolves its message (one 64-byte record per probe step; the
-// record carries the state too) and compares the replica against the state
-// it just read.  Only fields that would grow go further: they are max-combined
-// per slot in an LDS table shared by the workgroup, and one lane per
-// distinct slot then issues the device-scope atomicMax for the combined
-// value.  State only grows (E-encoding, phip_device.hpp), so a stale read can
-// only cause a redundant atomic, never a lost update; combining first keeps
-// a Zipf-hot bucket at one atomic per workgroup instead of one per message.
-// Misses are appended to `miss` (insert pipeline, then this kernel again on
-// the miss list with `track_new`).
+// One lane per message.  The kernel is bound by memory latency, so every
+// lane issues its loads in as few dependent rounds as possible:
+//   round 1  name offsets + the three replica fields (all independent);
+//   round 2  the name as three aligned 8-byte words, each address clamped to
+//            the name's own last word (always in bounds, so no branches);
+//   round 3  the home slot's first 48 bytes (tag, state, name words 0-1).
+// Names of more than kShortName bytes and probe chains longer than one slot
+// take a divergent slow path (rare: C2's names are <= 8 bytes, load 0.3).
+//
+// The lane then compares the replica against the state it just read.  Only
+// fields that would grow go further: they are max-combined per slot in an LDS
+// table shared by the workgroup, and one lane per distinct slot issues the
+// device-scope atomicMax for the combined value.  State only grows
+// (E-encoding, phip_device.hpp), so a stale read can only cause a redundant
+// atomic, never a lost update; combining keeps a Zipf-hot bucket at one
+// atomic per workgroup instead of one per message, and a workgroup in which
+// no field grows skips the flush.  Misses are appended to `miss` (insert
+// pipeline, then this kernel again on the miss list with `track_new`).
 constexpr u32 kCombEmpty = 0xFFFFFFFFu;
+constexpr u32 kCombSlots = 256;
+constexpr u32 kCombBits = 8;
+static_assert((1u << kCombBits) == kCombSlots, "combining table size");
 
-// Variant bits (tools/ubench_receive.hip times the combinations).
-constexpr int kFastCombine = 1;   // LDS per-slot combining before atomics
-constexpr int kFastNT = 2;        // non-temporal streaming loads
-constexpr int kFastWide = 4;      // 8-byte-word name loads
-constexpr int kFastSkip = 8;      // skip the flush when no lane of the block needs an atomic
-constexpr int kFastSmall = 16;    // LDS combining table of kBlock entries (else 2*kBlock)
-constexpr int kFastNoSeen = 32;   // flush every contributed field (no per-entry seen state)
-constexpr int kFastOpt = kFastCombine | kFastNT | kFastWide | kFastSkip | kFastSmall | kFastNoSeen;
+// Name words for a name of <= kShortName bytes: the three aligned words that
+// can hold it, with each address clamped to the word holding its last byte
+// (so all three loads issue unconditionally and stay inside the name).
+template <bool NT>
+__device__ inline void load_words3(const u8* blob, u64 off, u32 len, u64& w0, u64& w1, u64& w2) {
+  const u64* p = reinterpret_cast<const u64*>(blob);
+  const u64 wb = off >> 3;
+  const u64 we = (off + (len ? len : 1u) - 1) >> 3;
+  w0 = ld<NT>(p + wb);
+  w1 = ld<NT>(p + (wb + 1 < we ? wb + 1 : we));
+  w2 = ld<NT>(p + (wb + 2 < we ? wb + 2 : we));
+}
 
-template <class Src, int OPT = kFastOpt, int PER = 1>
-__global__ __launch_bounds__(kBlock) void k_receive_fast(
-    Src src, const uint64_t* __restrict__ ma, const uint64_t* __restrict__ mt,
-    const int64_t* __restrict__ me,
-    u32 n, const u32* __restrict__ list, Table T, u8* __restrict__ status, u32* miss, u32* ctr,
-    int track_new) {
-  constexpr bool kComb = OPT & kFastCombine, kNT = OPT & kFastNT, kWide = OPT & kFastWide;
-  constexpr bool kSkip = OPT & kFastSkip, kSeen = !(OPT & kFastNoSeen);
-  constexpr u32 kSlots = kComb ? ((OPT & kFastSmall) ? kBlock * PER : 2 * kBlock * PER) : 1;
-  constexpr u32 kBits = kSlots >= 2048 ? 11 : kSlots >= 1024 ? 10 : kSlots >= 512 ? 9 : 8;
-  __shared__ u32 ckey[kSlots];
-  __shared__ u64 cmax[3][kSlots];    // combined maxima (elapsed biased by 2^63)
-  __shared__ u64 cseen[3][kSeen ? kSlots : 1];   // state seen by the lane that opened the entry
-  if constexpr (kComb) {
-    for (u32 j = threadIdx.x; j < kSlots; j += kBlock) {
-      ckey[j] = kCombEmpty;
-      cmax[0][j] = 0; cmax[1][j] = 0; cmax[2][j] = 0;
-    }
-    __syncthreads();
-  }
-  bool any_need = false;
+// One FNV-1a step on the hash held as 32-bit halves:
+// h*0x100000001b3 = h*0x1b3 + (h << 40), so hi' = hi*0x1b3 + carry + (lo << 8).
+__device__ inline void fnv_step32(u32& lo, u32& hi, u32 c) {
+  lo ^= c;
+  const u64 p = (u64)lo * 0x1b3u;
+  hi = (u32)((u64)hi * 0x1b3u + (p >> 32)) + (lo << 8);
+  lo = (u32)p;
+}
+
+// FNV-1a and the canonical words of a name of <= kShortName bytes from the
+// words load_words3 returned (bytes past the name's end are ignored).
+__device__ inline void short_name(u64 w0, u64 w1, u64 w2, u64 off, u32 len, Name& nm) {
+  const u32 sh = (u32)(off & 7) * 8;
+  u64 b0 = (w0 >> sh) | ((w1 << 1) << (63 - sh));
+  u64 b1 = (w1 >> sh) | ((w2 << 1) << (63 - sh));
+  b0 = len >= 8 ? b0 : (b0 & ((1ull << (8 * len)) - 1));
+  b1 = len > 8 ? (b1 & ((1ull << (8 * (len - 8))) - 1)) : 0;
+  u32 lo = (u32)kFnvOffset, hi = (u32)(kFnvOffset >> 32);
+  const u32 q[4] = {(u32)b0, (u32)(b0 >> 32), (u32)b1, (u32)(b1 >> 32)};
 #pragma unroll
-  for (int p = 0; p < PER; ++p) {
-    const u32 tid = (blockIdx.x * PER + p) * kBlock + threadIdx.x;
-    bool missed = false;
-    u32 i = 0;
-    if (tid < n) {
-      i = list ? list[tid] : tid;
-      u64 off; u32 len;
-      src.template get<kNT>(i, off, len);
+  for (u32 k = 0; k < kShortName; ++k)
+    if (k < len) fnv_step32(lo, hi, (q[k >> 2] >> (8 * (k & 3))) & 0xFFu);
+  nm.h = ((u64)hi << 32) | lo; nm.len = len; nm.off = off;
+  nm.w0 = (u64)len | (b0 << 16);     // name byte k sits at canonical byte k+2
+  nm.w1 = (b0 >> 48) | (b1 << 16);
+  nm.w2 = 0;
+}
+
+// enc_replica for a replica field that is not -0.0 (the fast path's batches
+// hold none), without branches.
+__device__ inline u64 enc_replica_nz(u64 b) {
+  const u64 mag = b & ~kSign;
+  const u64 e = (b >> 63) ? kInfBits - mag : kInfBits + mag + (mag != 0);
+  return mag > kInfBits ? 0ull : e;
+}
+
+// ------------------------------------------------- hot-bucket directory --
+// Zipf-skewed batches put most messages on a few buckets (C2: the top 512 of
+// 10M buckets carry 61% of the messages).  Before the fast kernel runs, a
+// strided sample of the batch is resolved and counted; the (at most kHotMax)
+// buckets sampled most often form the batch's hot directory.  Every fast
+// workgroup keeps the directory in LDS and folds the messages of those
+// buckets into per-workgroup maxima there, with no record read, flushing them
+// with one atomicMax per field at the end.  Merge is an order-free max on the
+// fast path, so this is exact; the directory only decides which messages skip
+// the table read.
+constexpr u32 kHotMax = 512;          // directory entries
+constexpr u32 kHotLds = 1024;         // LDS lookup slots (power of 2, >= 2 * kHotMax)
+constexpr u32 kHotCntBits = 18;       // sample count table: 2^18 (slot+1, count) pairs
+constexpr u32 kHotSampleMax = 1u << 17;   // samples per batch (half the count table)
+constexpr u32 kHotHist = 4096;        // histogram bins of sample counts
+constexpr u32 kHotMinCount = 8;       // sample hits for a bucket to qualify
+constexpr u32 kHotMinBatch = 1u << 20;    // smaller batches skip the directory
+
+struct HotEntry {
+  u64 tag, w0, w1;   // table tag and canonical name words 0-1 (flags byte cleared)
+  u32 slot, pad;
+};
+struct HotHdr {
+  u32 n;             // directory entries
+  u32 thresh;        // sample count threshold that selected them
+  u32 pad[14];
+};
+
+__device__ inline u32 hot_home(u64 tag) { return (u32)(tag ^ (tag >> 29)) & (kHotLds - 1); }
+
+// Sample j = message j*stride: resolve it (short names only) and count its
+// slot, aggregated per workgroup in LDS first (a hot slot is sampled by most
+// lanes; one global atomic per workgroup and slot keeps it off one address).
+template <class Src>
+__global__ __launch_bounds__(256) void k_hot_sample(Src src, u32 n, u32 stride, u32 nsample, Table T,
+                                                    u32* __restrict__ ckeys, u32* __restrict__ ccnt) {
+  constexpr u32 kL = 512;
+  __shared__ u32 lkey[kL], lcnt[kL];
+  lkey[threadIdx.x] = 0; lkey[threadIdx.x + 256] = 0;
+  lcnt[threadIdx.x] = 0; lcnt[threadIdx.x + 256] = 0;
+  __syncthreads();
+  const u32 j = blockIdx.x * blockDim.x + threadIdx.x;
+  const u32 i = j * stride;
+  if (j < nsample && i < n) {
+    u64 off; u32 len;
+    src.template get<true>(i, off, len);
+    if (len <= kShortName) {
       Name nm;
-      if constexpr (kWide) load_name_wide<kNT>(src.blob, off, len, nm);
-      else load_name(src.blob, off, len, nm);
-      const u64 ea = enc_replica(ld<kNT>(ma + i)), et = enc_replica(ld<kNT>(mt + i));
-      const u64 ee = (u64)ld<kNT>(me + i) ^ kSign;
+      load_name_wide<true>(src.blob, off, len, nm);
       u32 s;
-      Rec cur;
-      int pr = probe(T, nm, src.blob, &s, &cur);
-      if (pr == kFound) {
-        const u64 ua = cur.added, ut = cur.taken, ue = (u64)cur.elapsed ^ kSign;
-        const bool ga = ea > ua, gt = et > ut, ge = ee > ue;
-        if (!kComb) {
-          Rec* r = &T.recs[s];
-          if (ga) atomicMax(&r->added, ea);
-          if (gt) atomicMax(&r->taken, et);
-          if (ge) atomicMax(&r->elapsed, (i64)(ee ^ kSign));
-        } else if (ga || gt || ge) {
-          any_need = true;
-          u32 h = (s * 2654435761u) >> (32 - kBits);
-          for (;;) {
-            u32 old = atomicCAS(&ckey[h], kCombEmpty, s);
-            if (old == kCombEmpty) {
-              if constexpr (kSeen) { cseen[0][h] = ua; cseen[1][h] = ut; cseen[2][h] = ue; }
-              break;
-            }
-            if (old == s) break;
-            h = (h + 1) & (kSlots - 1);
-          }
-          if (ga) atomicMax(&cmax[0][h], ea);
-          if (gt) atomicMax(&cmax[1][h], et);
-          if (ge) atomicMax(&cmax[2][h], ee);
+      Rec r;
+      if (probe(T, nm, src.blob, &s, &r) == kFound) {
+        u32 h = (s * 2654435761u) >> (32 - 9);
+        for (;;) {   // <= 256 distinct keys in a 512-entry table: always terminates
+          const u32 old = atomicCAS(&lkey[h], 0u, s + 1);
+          if (old == 0 || old == s + 1) { atomicAdd(&lcnt[h], 1u); break; }
+          h = (h + 1) & (kL - 1);
         }
-        if (track_new && (rec_flags(cur) & kRecNew)) atomicMin(&T.aux[s], i);
-        if (status) status[i] = PHIP_ST_MERGED;
-      } else {
-        missed = true;
-        if (pr == kFull) atomicOr(&ctr[8], 1u);
       }
     }
-    u32 pos = wave_append(&ctr[2], missed);
+  }
+  __syncthreads();
+  constexpr u32 mask = (1u << kHotCntBits) - 1;
+  for (u32 e = threadIdx.x; e < kL; e += 256) {
+    const u32 key = lkey[e];
+    if (!key) continue;
+    u32 h = ((key - 1) * 2654435761u) >> (32 - kHotCntBits);
+    for (u32 k = 0; k <= mask; ++k) {
+      const u32 old = atomicCAS(&ckeys[h], 0u, key);
+      if (old == 0 || old == key) { atomicAdd(&ccnt[h], lcnt[e]); break; }
+      h = (h + 1) & mask;
+    }
+  }
+}
+
+__global__ void k_hot_hist(const u32* __restrict__ ccnt, u32* __restrict__ hist) {
+  const u32 e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (1u << kHotCntBits)) return;
+  const u32 c = ccnt[e];
+  if (c >= kHotMinCount) atomicAdd(&hist[c < kHotHist ? c : kHotHist - 1], 1u);
+}
+
+// One workgroup of 256: the lowest threshold t >= kHotMinCount with at most
+// kHotMax sampled slots counted t or more times.
+__global__ __launch_bounds__(256) void k_hot_select(const u32* __restrict__ hist, HotHdr* hdr) {
+  constexpr u32 kPer = kHotHist / 256;
+  __shared__ u32 part[256];
+  __shared__ u32 best;
+  const u32 t = threadIdx.x;
+  u32 s = 0;
+  for (u32 k = 0; k < kPer; ++k) s += hist[t * kPer + k];
+  part[t] = s;
+  if (t == 0) best = kHotHist;
+  __syncthreads();
+  u32 run = 0;   // slots counted in later chunks
+  for (u32 u = t + 1; u < 256; ++u) run += part[u];
+  u32 lo = kHotHist;
+  for (int b = (int)kPer - 1; b >= 0; --b) {
+    run += hist[t * kPer + b];
+    if (run <= kHotMax) lo = t * kPer + b;
+  }
+  atomicMin(&best, lo);
+  __syncthreads();
+  if (t == 0) {
+    hdr->n = 0;
+    hdr->thresh = best > kHotMinCount ? best : kHotMinCount;
+  }
+}
+
+__global__ void k_hot_build(const u32* __restrict__ ckeys, const u32* __restrict__ ccnt, HotHdr* hdr,
+                            Table T, HotEntry* __restrict__ dir) {
+  const u32 e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (1u << kHotCntBits)) return;
+  const u32 c = ccnt[e];
+  if (c < kHotMinCount || c < hdr->thresh) return;
+  const u32 idx = atomicAdd(&hdr->n, 1u);
+  if (idx >= kHotMax) return;   // cannot happen: the threshold bounds the count
+  const u32 s = ckeys[e] - 1;
+  const Rec r = load_rec(&T.recs[s]);
+  HotEntry d;
+  d.tag = r.tag;
+  d.w0 = r.name0 & ~0xFF00ull;
+  d.w1 = r.name1;
+  d.slot = s;
+  d.pad = 0;
+  dir[idx] = d;
+}
+
+// ----------------------------------------------------- fast receive --------
+// Persistent workgroups; every wave walks its own 64-message chunks
+// (grid-stride over waves, no workgroup barrier inside the loop, so a wave
+// waiting on a table read never holds up another).  Per message:
+//   hot directory hit  -> fold into the workgroup's LDS maxima (no table read);
+//   otherwise          -> read the home slot's first 48 bytes, compare, and
+//                         atomicMax the fields that grow.
+// Cold buckets almost never repeat inside a chunk once the hot ones are in
+// the directory, so there is no workgroup-wide combining table.  State only
+// grows (E-encoding, phip_device.hpp), so a stale read can only cause a
+// redundant atomic, never a lost update.  Misses are appended to `miss`; the
+// insert pipeline then creates their buckets and k_receive_list merges them.
+constexpr u32 kFastBlock = 512;
+constexpr u32 kFastPerCU = 4;         // resident workgroups per CU (LDS ~30 KB each)
+
+template <class Src>
+__global__ __launch_bounds__(kFastBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_receive_fast(
+    Src src, const uint64_t* __restrict__ ma, const uint64_t* __restrict__ mt,
+    const int64_t* __restrict__ me, u32 n, Table T,
+    u8* __restrict__ status, u32* miss, u32* ctr, const HotHdr* __restrict__ hot,
+    const HotEntry* __restrict__ hot_dir) {
+  __shared__ u32 hslot[kHotLds];        // directory index + 1 (0 = empty)
+  __shared__ u64 htag[kHotMax], hw0[kHotMax], hw1[kHotMax];
+  __shared__ u32 hrec[kHotMax];
+  __shared__ u64 hmax[3][kHotMax];      // per-workgroup maxima (elapsed biased by 2^63)
+  __shared__ u32 hhits;
+
+  const u32 nh = hot ? min(hot->n, kHotMax) : 0u;
+  for (u32 j = threadIdx.x; j < kHotLds; j += kFastBlock) hslot[j] = 0;
+  for (u32 j = threadIdx.x; j < kHotMax; j += kFastBlock) {
+    hmax[0][j] = 0; hmax[1][j] = 0; hmax[2][j] = 0;
+  }
+  if (threadIdx.x == 0) hhits = 0;
+  __syncthreads();
+  for (u32 j = threadIdx.x; j < nh; j += kFastBlock) {
+    const HotEntry d = hot_dir[j];
+    htag[j] = d.tag; hw0[j] = d.w0; hw1[j] = d.w1; hrec[j] = d.slot;
+    u32 hs = hot_home(d.tag);
+    while (atomicCAS(&hslot[hs], 0u, j + 1) != 0) hs = (hs + 1) & (kHotLds - 1);
+  }
+  __syncthreads();
+
+  constexpr u32 kWaves = kFastBlock / 64;
+  const u32 lane = threadIdx.x & 63;
+  const u32 nchunks = (n + 63) / 64;
+  u32 hits = 0;
+  for (u32 chunk = blockIdx.x * kWaves + threadIdx.x / 64; chunk < nchunks;
+       chunk += gridDim.x * kWaves) {
+    const u32 tid = chunk * 64 + lane;
+    const bool valid = tid < n;
+    const u32 i = valid ? tid : n - 1;
+    // round 1: name offsets and the replica fields
+    u64 off; u32 len;
+    src.template get<true>(i, off, len);
+    const u64 ra = ld<true>(ma + i), rt = ld<true>(mt + i);
+    const i64 re = ld<true>(me + i);
+    // round 2: the name
+    u64 w0, w1, w2;
+    load_words3<false>(src.blob, off, len, w0, w1, w2);
+    Name nm;
+    short_name(w0, w1, w2, off, len, nm);
+    const bool shortname = len <= kShortName;
+    const u64 tag = T.tag(nm.h);
+    const u64 ea = enc_replica_nz(ra), et = enc_replica_nz(rt), ee = (u64)re ^ kSign;
+
+    bool missed = false;
+    if (valid) {
+      int hidx = -1;
+      if (nh && shortname) {
+        for (u32 hs = hot_home(tag);; hs = (hs + 1) & (kHotLds - 1)) {
+          const u32 e = hslot[hs];
+          if (!e) break;
+          if (htag[e - 1] == tag && hw0[e - 1] == nm.w0 && hw1[e - 1] == nm.w1) {
+            hidx = (int)e - 1;
+            break;
+          }
+        }
+      }
+      if (hidx >= 0) {
+        ++hits;
+        if (ea > hmax[0][hidx]) atomicMax(&hmax[0][hidx], ea);
+        if (et > hmax[1][hidx]) atomicMax(&hmax[1][hidx], et);
+        if (ee > hmax[2][hidx]) atomicMax(&hmax[2][hidx], ee);
+        if (status) status[i] = PHIP_ST_MERGED;
+      } else {
+        // round 3: the home slot
+        u32 s = T.home(tag);
+        Rec cur = load_rec48(&T.recs[s]);
+        const bool hit = shortname && cur.tag == tag && (cur.name0 & ~0xFF00ull) == nm.w0 &&
+                         cur.name1 == nm.w1 && (rec_flags(cur) & kRecPublished);
+        int pr = kFound;
+        if (!hit) {
+          if (shortname && cur.tag == 0) {
+            pr = kMiss;
+          } else {
+            if (!shortname) load_name_wide<true>(src.blob, off, len, nm);
+            pr = probe(T, nm, src.blob, &s, &cur);
+          }
+        }
+        if (pr == kFound) {
+          Rec* r = &T.recs[s];
+          if (ea > cur.added) atomicMax(&r->added, ea);
+          if (et > cur.taken) atomicMax(&r->taken, et);
+          if (ee > ((u64)cur.elapsed ^ kSign)) atomicMax(&r->elapsed, (i64)(ee ^ kSign));
+          if (status) status[i] = PHIP_ST_MERGED;
+        } else {
+          missed = true;
+          if (pr == kFull) atomicOr(&ctr[8], 1u);
+        }
+      }
+    }
+    const u32 pos = wave_append(&ctr[2], missed);
     if (missed) miss[pos] = i;
   }
+  if (hits) atomicAdd(&hhits, hits);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (hhits) atomicAdd(&ctr[10], hhits);
+    if (blockIdx.x == 0) ctr[11] = nh;
+  }
 
-  if constexpr (kComb) {
-    if constexpr (kSkip) {
-      if (!__syncthreads_or(any_need)) return;
-    } else {
-      __syncthreads();
-    }
-    for (u32 j = threadIdx.x; j < kSlots; j += kBlock) {
-      u32 s = ckey[j];
-      if (s == kCombEmpty) continue;
+  // Directory flush: the workgroup's maxima, skipping fields already beaten.
+  for (u32 j = threadIdx.x; j < nh; j += kFastBlock) {
+    const u64 xa = hmax[0][j], xt = hmax[1][j], xe = hmax[2][j];
+    if (!(xa | xt | xe)) continue;
+    Rec* r = &T.recs[hrec[j]];
+    const u64 ca = r->added, ct = r->taken, ce = (u64)r->elapsed ^ kSign;
+    if (xa > ca) atomicMax(&r->added, xa);
+    if (xt > ct) atomicMax(&r->taken, xt);
+    if (xe > ce) atomicMax(&r->elapsed, (i64)(xe ^ kSign));
+  }
+}
+
+// The messages of a list (the fast batch's misses, after the insert
+// pipeline created their buckets): GetBucket + Merge with creator tracking
+// (the lowest-seq message of a bucket created by this batch is recorded in
+// aux[] for PHIP_ST_CREATED).
+template <class Src>
+__global__ __launch_bounds__(kBlock) void k_receive_list(
+    Src src, const uint64_t* __restrict__ ma, const uint64_t* __restrict__ mt,
+    const int64_t* __restrict__ me, u32 n, const u32* __restrict__ list, Table T,
+    u8* __restrict__ status, u32* miss, u32* ctr) {
+  const u32 tid = blockIdx.x * kBlock + threadIdx.x;
+  bool missed = false;
+  u32 i = 0;
+  if (tid < n) {
+    i = list[tid];
+    u64 off; u32 len;
+    src.get(i, off, len);
+    Name nm;
+    load_name_wide<false>(src.blob, off, len, nm);
+    u32 s;
+    Rec cur;
+    const int pr = probe(T, nm, src.blob, &s, &cur);
+    if (pr == kFound) {
+      const u64 ea = enc_replica_nz(ma[i]), et = enc_replica_nz(mt[i]), ee = (u64)me[i] ^ kSign;
       Rec* r = &T.recs[s];
-      // A field's maximum is non-zero only if some lane saw it grow.
-      const u64 sa = kSeen ? cseen[0][j] : 0, st = kSeen ? cseen[1][j] : 0;
-      const u64 se = kSeen ? cseen[2][j] : 0;
-      if (cmax[0][j] > sa) atomicMax(&r->added, cmax[0][j]);
-      if (cmax[1][j] > st) atomicMax(&r->taken, cmax[1][j]);
-      if (cmax[2][j] > se) atomicMax(&r->elapsed, (i64)(cmax[2][j] ^ kSign));
+      if (ea > cur.added) atomicMax(&r->added, ea);
+      if (et > cur.taken) atomicMax(&r->taken, et);
+      if (ee > ((u64)cur.elapsed ^ kSign)) atomicMax(&r->elapsed, (i64)(ee ^ kSign));
+      if (rec_flags(cur) & kRecNew) atomicMin(&T.aux[s], i);
+      if (status) status[i] = PHIP_ST_MERGED;
+    } else {
+      missed = true;
+      if (pr == kFull) atomicOr(&ctr[8], 1u);
     }
   }
+  const u32 pos = wave_append(&ctr[2], missed);
+  if (missed) miss[pos] = i;
 }
 
 // Status of the messages that went through the insert pipeline: the first

@@ -121,6 +121,13 @@ class GPURepo:
     def set_timing(self, on: bool):
         self.L.phip_set_timing(self.h, 1 if on else 0)
 
+    def last_stats(self):
+        """(hot-directory entries, messages folded through it, misses) of the
+        last fast-path Receive batch."""
+        out = (C.c_uint64 * 3)()
+        k = self.L.phip_last_stats(self.h, out, 3)
+        return tuple(int(out[i]) for i in range(k))
+
     def timings(self):
         names = (C.c_char_p * 256)()
         ms = (C.c_float * 256)()

@@ -148,6 +148,50 @@ def test_receive_soa_fast_path_vs_oracle(pa, seed):
     assert_same_dump(gpu_dump(g), o.dump())
 
 
+def _fast_dirty_states(rng, n):
+    """dirty_states without what routes a batch to the ordered path (-0.0
+    fields, all-zero incast states): NaN, +-Inf, negatives stay."""
+    a, t, e = _gen.dirty_states(rng, n)
+    for arr in (a, t):
+        arr[arr == np.uint64(0x8000000000000000)] = 0
+    z = (a == 0) & (t == 0) & (e == 0)
+    e[z] = 1
+    return a, t, e
+
+
+@pytest.mark.parametrize("kind", ["clean", "fastdirty"])
+def test_receive_soa_hot_directory_vs_oracle(pa, kind):
+    """Batches of >= 2^20 messages build the hot-bucket directory (the most
+    sampled buckets fold in LDS, flushed once per workgroup).  Zipf(1.1) with
+    new keys, 15-22 byte and arena-length names mixed in."""
+    rng = np.random.default_rng(11 if kind == "clean" else 12)
+    K = 30000
+    g, o = _seed_both(pa, rng, K, log2_slots=17)
+    n = 1 << 21
+    ids = _gen.zipf_ids(rng, n, K + 3000)
+    names = []
+    for i in ids:
+        i = int(i)
+        if i % 101 == 0:
+            names.append(b"a-much-longer-bucket-name-%d" % i)   # > 22 bytes: arena
+        elif i % 103 == 0:
+            names.append(b"medium-name-%d" % i)                 # 15-22 bytes
+        else:
+            names.append(b"b%d" % i)
+    a, t, e = _gen.clean_states(rng, n) if kind == "clean" else _fast_dirty_states(rng, n)
+    now = _gen.T0 + 5 * SEC
+    out = g.receive_soa(names, a, t, e, now)
+    st, _, _, _ = o.receive_soa(names, a, t, e, now)
+    assert np.array_equal(out["status"], st)
+    assert_same_dump(gpu_dump(g), o.dump())
+    # A second batch over the same keys (no inserts): only the fast kernel.
+    a2, t2, e2 = _gen.clean_states(rng, n)
+    out = g.receive_soa(names, a2, t2, e2, now + SEC)
+    st, _, _, _ = o.receive_soa(names, a2, t2, e2, now + SEC)
+    assert np.array_equal(out["status"], st)
+    assert_same_dump(gpu_dump(g), o.dump())
+
+
 @pytest.mark.parametrize("seed", [3, 4])
 def test_receive_soa_dirty_vs_oracle(pa, seed):
     """Incasts, -0.0, NaN, negatives: the ordered path, replies included."""
