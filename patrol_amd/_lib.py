@@ -10,7 +10,8 @@ import ctypes as C
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libpatrolhip.so")
+# PATROLHIP_LIB: a tuning build of the same sources (tools/build_variants.sh).
+LIB_PATH = os.environ.get("PATROLHIP_LIB") or os.path.join(HERE, "libpatrolhip.so")
 
 # Every symbol include/patrolhip.h declares (tests/test_abi.py checks both ways).
 EXPORTS = [

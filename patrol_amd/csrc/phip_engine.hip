@@ -300,7 +300,7 @@ int build_hot(phip_handle* h, Src src, u32 n, const HotHdr** hdr_out, const HotE
   const u32 nsample = (n + stride - 1) / stride;
   {
     Launch l(h, "k_hot_sample");
-    k_hot_sample<Src><<<grid_for(nsample, 256), 256, 0, h->stream>>>(src, n, stride, nsample, table(h),
+    k_hot_sample<Src><<<grid_for(nsample, kHotSamplePerBlock), 256, 0, h->stream>>>(src, n, stride, nsample, table(h),
                                                                     ckeys, ccnt);
   }
   {
@@ -320,10 +320,12 @@ inline unsigned fast_grid(phip_handle* h, u32 n) {
   return (unsigned)std::max<u64>(1, std::min<u64>(tiles, (u64)h->ncu * kFastPerCU));
 }
 
+// Counters on entry: ctr[0], ctr[1] = the batch's incast / -0.0 counts
+// (classification); every other counter 0.  *dirty is set (and nothing is
+// applied) when either count is non-zero.
 template <class Src>
 int fast_receive(phip_handle* h, Src src, const uint64_t* a, const uint64_t* t, const int64_t* e,
-                 u32 n, i64 now,
-                 u8* status) {
+                 u32 n, i64 now, u8* status, bool* dirty) {
   u32* miss;
   int rc;
   if ((rc = ensure(h, B_MISS, n, &miss))) return rc;
@@ -337,6 +339,8 @@ int fast_receive(phip_handle* h, Src src, const uint64_t* a, const uint64_t* t, 
   }
   HIPCHK(h, hipGetLastError());
   if ((rc = read_ctr(h))) return rc;
+  *dirty = h->ctr_host[0] || h->ctr_host[1];
+  if (*dirty) return PHIP_OK;
   if ((rc = check_flags(h))) return rc;
   u32 nmiss = h->ctr_host[2];
   h->stats[0] = h->ctr_host[11];
@@ -590,12 +594,12 @@ int receive_decoded(phip_handle* h, Src src, const uint64_t* a, const uint64_t* 
     k_classify<<<grid_for(n), kBlock, 0, h->stream>>>(a, t, e, n, h->ctr);
     HIPCHK(h, hipGetLastError());
   }
-  if ((rc = read_ctr(h))) return rc;
-  bool dirty = h->ctr_host[0] || h->ctr_host[1];
-  if (!dirty) {
-    if ((rc = reset_ctr(h))) return rc;
-    return fast_receive(h, src, a, t, e, n, now, ow.status);
-  }
+  // The fast path is enqueued behind the classification without a host
+  // round trip; k_receive_fast itself does nothing when the counters show an
+  // incast or a -0.0 field, and the batch then takes the ordered path.
+  bool dirty = false;
+  if ((rc = fast_receive(h, src, a, t, e, n, now, ow.status, &dirty))) return rc;
+  if (!dirty) return PHIP_OK;
   OpView ov{};
   ov.kind = nullptr; ov.kind0 = PHIP_OP_RECEIVE;
   ov.now = nullptr; ov.now0 = now;

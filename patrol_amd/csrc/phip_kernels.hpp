@@ -273,10 +273,19 @@ __device__ inline u64 enc_replica_nz(u64 b) {
 // with one atomicMax per field at the end.  Merge is an order-free max on the
 // fast path, so this is exact; the directory only decides which messages skip
 // the table read.
-constexpr u32 kHotMax = 512;          // directory entries
-constexpr u32 kHotLds = 1024;         // LDS lookup slots (power of 2, >= 2 * kHotMax)
+// (PHIP_HOT_MAX / PHIP_HOT_LDS / PHIP_FAST_BLOCK / PHIP_FAST_PER_CU override
+// the defaults for tuning builds, tools/build_variants.sh.)
+#ifndef PHIP_HOT_MAX
+#define PHIP_HOT_MAX 512
+#endif
+#ifndef PHIP_HOT_LDS
+#define PHIP_HOT_LDS 1024
+#endif
+constexpr u32 kHotMax = PHIP_HOT_MAX;     // directory entries
+constexpr u32 kHotLds = PHIP_HOT_LDS;     // LDS lookup slots (power of 2, >= 1.5 * kHotMax)
 constexpr u32 kHotCntBits = 18;       // sample count table: 2^18 (slot+1, count) pairs
 constexpr u32 kHotSampleMax = 1u << 17;   // samples per batch (half the count table)
+constexpr u32 kHotSamplePerBlock = 1024;
 constexpr u32 kHotHist = 4096;        // histogram bins of sample counts
 constexpr u32 kHotMinCount = 8;       // sample hits for a bucket to qualify
 constexpr u32 kHotMinBatch = 1u << 20;    // smaller batches skip the directory
@@ -299,29 +308,28 @@ __device__ inline u32 hot_home(u64 tag) { return (u32)(tag ^ (tag >> 29)) & (kHo
 template <class Src>
 __global__ __launch_bounds__(256) void k_hot_sample(Src src, u32 n, u32 stride, u32 nsample, Table T,
                                                     u32* __restrict__ ckeys, u32* __restrict__ ccnt) {
-  constexpr u32 kL = 512;
+  constexpr u32 kPer = kHotSamplePerBlock / 256;
+  constexpr u32 kL = 2 * kHotSamplePerBlock;
   __shared__ u32 lkey[kL], lcnt[kL];
-  lkey[threadIdx.x] = 0; lkey[threadIdx.x + 256] = 0;
-  lcnt[threadIdx.x] = 0; lcnt[threadIdx.x + 256] = 0;
+  for (u32 e = threadIdx.x; e < kL; e += 256) { lkey[e] = 0; lcnt[e] = 0; }
   __syncthreads();
-  const u32 j = blockIdx.x * blockDim.x + threadIdx.x;
-  const u32 i = j * stride;
-  if (j < nsample && i < n) {
+  for (u32 r = 0; r < kPer; ++r) {
+    const u32 j = blockIdx.x * kHotSamplePerBlock + r * 256 + threadIdx.x;
+    const u64 i = (u64)j * stride;
+    if (j >= nsample || i >= n) continue;
     u64 off; u32 len;
-    src.template get<true>(i, off, len);
-    if (len <= kShortName) {
-      Name nm;
-      load_name_wide<true>(src.blob, off, len, nm);
-      u32 s;
-      Rec r;
-      if (probe(T, nm, src.blob, &s, &r) == kFound) {
-        u32 h = (s * 2654435761u) >> (32 - 9);
-        for (;;) {   // <= 256 distinct keys in a 512-entry table: always terminates
-          const u32 old = atomicCAS(&lkey[h], 0u, s + 1);
-          if (old == 0 || old == s + 1) { atomicAdd(&lcnt[h], 1u); break; }
-          h = (h + 1) & (kL - 1);
-        }
-      }
+    src.template get<true>((u32)i, off, len);
+    if (len > kShortName) continue;
+    Name nm;
+    load_name_wide<true>(src.blob, off, len, nm);
+    u32 s;
+    Rec rec;
+    if (probe(T, nm, src.blob, &s, &rec) != kFound) continue;
+    u32 h = (s * 2654435761u) & (kL - 1);
+    for (;;) {   // at most kHotSamplePerBlock distinct keys in 2x as many entries
+      const u32 old = atomicCAS(&lkey[h], 0u, s + 1);
+      if (old == 0 || old == s + 1) { atomicAdd(&lcnt[h], 1u); break; }
+      h = (h + 1) & (kL - 1);
     }
   }
   __syncthreads();
@@ -403,8 +411,14 @@ __global__ void k_hot_build(const u32* __restrict__ ckeys, const u32* __restrict
 // grows (E-encoding, phip_device.hpp), so a stale read can only cause a
 // redundant atomic, never a lost update.  Misses are appended to `miss`; the
 // insert pipeline then creates their buckets and k_receive_list merges them.
-constexpr u32 kFastBlock = 512;
-constexpr u32 kFastPerCU = 4;         // resident workgroups per CU (LDS ~30 KB each)
+#ifndef PHIP_FAST_BLOCK
+#define PHIP_FAST_BLOCK 512
+#endif
+#ifndef PHIP_FAST_PER_CU
+#define PHIP_FAST_PER_CU 4
+#endif
+constexpr u32 kFastBlock = PHIP_FAST_BLOCK;
+constexpr u32 kFastPerCU = PHIP_FAST_PER_CU;   // resident workgroups per CU (LDS-bound)
 
 template <class Src>
 __global__ __launch_bounds__(kFastBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_receive_fast(
@@ -418,6 +432,9 @@ __global__ __launch_bounds__(kFastBlock) __attribute__((amdgpu_waves_per_eu(8, 8
   __shared__ u64 hmax[3][kHotMax];      // per-workgroup maxima (elapsed biased by 2^63)
   __shared__ u32 hhits;
 
+  // Classification gate: an incast or -0.0 in the batch (ctr[0], ctr[1])
+  // sends it to the ordered path; then nothing here may touch the table.
+  if (ctr[0] | ctr[1]) return;
   const u32 nh = hot ? min(hot->n, kHotMax) : 0u;
   for (u32 j = threadIdx.x; j < kHotLds; j += kFastBlock) hslot[j] = 0;
   for (u32 j = threadIdx.x; j < kHotMax; j += kFastBlock) {

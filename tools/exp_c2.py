@@ -38,6 +38,13 @@ def main():
         wall = (time.perf_counter() - t0) * 1e3
         ks = repo.timings()
         print("%-28s wall %.3f ms  %s  stats %s" % (label, wall, "  ".join("%s %.3f" % kv for kv in ks), repo.last_stats()))
+    quick = "--quick" in sys.argv
+    if quick:
+        run(0, "warm fresh")
+        run(1, "fresh")
+        run(1, "replay (no-op)")
+        run(2, "fresh")
+        return
     run(0, "warm fresh")
     run(1, "fresh")
     run(1, "replay (no-op)")

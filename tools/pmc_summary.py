@@ -9,10 +9,14 @@ Writes:
 
 FETCH_SIZE / WRITE_SIZE are in KiB per dispatch (rocprofv3 derived counters,
 summed over XCDs).  Per MI355X_MICROARCH.md §HBM, FETCH_SIZE counts 64 B per
-TCC_EA0_RDREQ; it under-reports wide coalesced 128-B streaming reads by 2x and
-is uncalibrated for other widths.  This kernel's HBM reads are a mix of
-streamed batch data (16-B loads) and random 48/64-B record reads, so we
-report the raw counter sum (no 2x correction) and state that beside it.
+TCC_EA0_RDREQ and so under-reports 128-B requests by 2x.  Rather than apply a
+blanket correction, the read bytes are taken from the size-bucketed request
+counters (TCC_EA0_RDREQ_32B/_64B/_128B, one pass of their own):
+  read bytes = 32*RDREQ_32B + 64*RDREQ_64B + 128*RDREQ_128B.
+On this kernel every read request is 128 B (streamed batch data and the
+random slot-record lines alike), i.e. exactly 2x FETCH_SIZE.  Writes are
+WRITE_SIZE (the fast kernel writes only through atomics; the atomic count is
+reported beside it).
 """
 import csv
 import json
@@ -46,10 +50,16 @@ def main():
         json.dump(bench, f, indent=1)
     fetch = per_dispatch(os.path.join(src, "pmc_fetch", "run_counter_collection.csv"), "FETCH_SIZE")
     write = per_dispatch(os.path.join(src, "pmc_write", "run_counter_collection.csv"), "WRITE_SIZE")
+    rd = {k: per_dispatch(os.path.join(src, "pmc_rdsize", "run_counter_collection.csv"), c)
+          for k, c in ((32, "TCC_EA0_RDREQ_32B_sum"), (64, "TCC_EA0_RDREQ_64B_sum"),
+                       (128, "TCC_EA0_RDREQ_128B_sum"))}
+    rd_bytes = sum(k * statistics.mean(v) for k, v in rd.items() if v)
+    atom = per_dispatch(os.path.join(src, "pmc_wr", "run_counter_collection.csv"), "TCC_ATOMIC_sum")
+    wrreq = per_dispatch(os.path.join(src, "pmc_wr", "run_counter_collection.csv"), "TCC_EA0_WRREQ_sum")
     hit = per_dispatch(os.path.join(src, "pmc_l2", "run_counter_collection.csv"), "TCC_HIT_sum")
     miss = per_dispatch(os.path.join(src, "pmc_l2", "run_counter_collection.csv"), "TCC_MISS_sum")
     f_kib, w_kib = statistics.mean(fetch), statistics.mean(write)
-    hbm = (f_kib + w_kib) * 1024
+    hbm = rd_bytes + w_kib * 1024
     stats = {}
     with open(os.path.join(src, "stats", "run_kernel_stats.csv")) as f:
         for r in csv.DictReader(f):
@@ -58,15 +68,19 @@ def main():
                          "min_ms": float(r["MinNs"]) / 1e6, "max_ms": float(r["MaxNs"]) / 1e6}
     pmc = {"kernel": DOMINANT, "workload": bench["config"]["workload"],
            "fetch_kib_per_launch": f_kib, "write_kib_per_launch": w_kib,
+           "read_bytes_per_launch": rd_bytes,
+           "rdreq_by_size_per_launch": {str(k): (statistics.mean(v) if v else 0.0) for k, v in rd.items()},
+           "atomics_per_launch": statistics.mean(atom) if atom else None,
+           "ea_wrreq_per_launch": statistics.mean(wrreq) if wrreq else None,
            "hbm_bytes_per_launch": hbm,
            "l2_hit_rate": statistics.mean(hit) / (statistics.mean(hit) + statistics.mean(miss)),
            "tcc_hit_per_launch": statistics.mean(hit), "tcc_miss_per_launch": statistics.mean(miss),
            "rocprof_kernel_stats": stats,
            "bench_kernel_ms": bench["roofline"]["kernel_ms"],
            "algorithmic_bytes_per_launch": bench["roofline"]["algorithmic_bytes_per_launch"],
-           "note": "FETCH_SIZE+WRITE_SIZE in KiB x 1024, summed over XCDs; no gfx950 2x "
-                   "correction applied (random 48/64-B record reads are uncalibrated, "
-                   "MI355X_MICROARCH.md §HBM)"}
+           "note": "hbm_bytes = size-bucketed EA read requests (32/64/128 B) + WRITE_SIZE; "
+                   "summed over XCDs (MI355X_MICROARCH.md §HBM: FETCH_SIZE tallies 64 B per "
+                   "request, so it reads half of the 128-B requests this kernel makes)"}
     with open(os.path.join(prof, f"{tag}_pmc.json"), "w") as f:
         json.dump(pmc, f, indent=1)
     with open(os.path.join(prof, "pmc_summary.json"), "w") as f:

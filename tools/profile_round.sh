@@ -26,5 +26,7 @@ step rocprof_stats 300 rocprofv3 --kernel-trace --stats --output-format csv -d "
 # uses 3 TCC slots, WRITE_SIZE 2; they cannot share a pass).
 step pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex k_receive_fast --output-format csv -d "$ROOT/$OUT/pmc_fetch" -o run -- python3 -u bench.py --no-cpu --steps 2 --warmup 1
 step pmc_write 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex k_receive_fast --output-format csv -d "$ROOT/$OUT/pmc_write" -o run -- python3 -u bench.py --no-cpu --steps 2 --warmup 1
+step pmc_rdsize 300 rocprofv3 --pmc TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum --kernel-include-regex k_receive_fast --output-format csv -d "$ROOT/$OUT/pmc_rdsize" -o run -- python3 -u bench.py --no-cpu --steps 2 --warmup 1
+step pmc_wr 300 rocprofv3 --pmc TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum TCC_ATOMIC_sum --kernel-include-regex k_receive_fast --output-format csv -d "$ROOT/$OUT/pmc_wr" -o run -- python3 -u bench.py --no-cpu --steps 2 --warmup 1
 step pmc_l2 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --kernel-include-regex k_receive_fast --output-format csv -d "$ROOT/$OUT/pmc_l2" -o run -- python3 -u bench.py --no-cpu --steps 2 --warmup 1
 echo done | tee -a "$OUT/steps.log"
