@@ -281,7 +281,8 @@ int clear_new(phip_handle* h, u32 n_claimed) {
 // threshold -> directory, all on the stream (no host round trip).  Returns
 // the header/directory to hand to k_receive_fast (nullptr: none).
 template <class Src>
-int build_hot(phip_handle* h, Src src, u32 n, const HotHdr** hdr_out, const HotEntry** dir_out) {
+int build_hot(phip_handle* h, Src src, u32 n, hipStream_t st, const HotHdr** hdr_out,
+              const HotEntry** dir_out) {
   *hdr_out = nullptr;
   *dir_out = nullptr;
   if (n < kHotMinBatch) return PHIP_OK;
@@ -295,19 +296,19 @@ int build_hot(phip_handle* h, Src src, u32 n, const HotHdr** hdr_out, const HotE
   u32* hist = ccnt + kCnt;
   HotHdr* hdr = (HotHdr*)(hist + kHotHist);
   HotEntry* dir = (HotEntry*)(hdr + 1);
-  HIPCHK(h, hipMemsetAsync(base, 0, zero_bytes, h->stream));
+  HIPCHK(h, hipMemsetAsync(base, 0, zero_bytes, st));
   const u32 stride = std::max<u32>(64, (n + kHotSampleMax - 1) / kHotSampleMax);
   const u32 nsample = (n + stride - 1) / stride;
   {
-    Launch l(h, "k_hot_sample");
-    k_hot_sample<Src><<<grid_for(nsample, kHotSamplePerBlock), 256, 0, h->stream>>>(src, n, stride, nsample, table(h),
-                                                                    ckeys, ccnt);
+    Launch l(h, "k_hot_sample", st);
+    k_hot_sample<Src><<<grid_for(nsample, kHotSamplePerBlock), 256, 0, st>>>(
+        src, n, stride, nsample, table(h), ckeys, ccnt);
   }
   {
-    Launch l(h, "k_hot_select");
-    k_hot_hist<<<grid_for(kCnt), kBlock, 0, h->stream>>>(ccnt, hist);
-    k_hot_select<<<1, 256, 0, h->stream>>>(hist, hdr);
-    k_hot_build<<<grid_for(kCnt), kBlock, 0, h->stream>>>(ckeys, ccnt, hdr, table(h), dir);
+    Launch l(h, "k_hot_select", st);
+    k_hot_hist<<<grid_for(kCnt), kBlock, 0, st>>>(ccnt, hist);
+    k_hot_select<<<1, 256, 0, st>>>(hist, hdr);
+    k_hot_build<<<grid_for(kCnt), kBlock, 0, st>>>(ckeys, ccnt, hdr, table(h), dir);
   }
   HIPCHK(h, hipGetLastError());
   *hdr_out = hdr;
@@ -325,13 +326,11 @@ inline unsigned fast_grid(phip_handle* h, u32 n) {
 // applied) when either count is non-zero.
 template <class Src>
 int fast_receive(phip_handle* h, Src src, const uint64_t* a, const uint64_t* t, const int64_t* e,
-                 u32 n, i64 now, u8* status, bool* dirty) {
+                 u32 n, i64 now, u8* status, const HotHdr* hot, const HotEntry* hot_dir,
+                 bool* dirty) {
   u32* miss;
   int rc;
   if ((rc = ensure(h, B_MISS, n, &miss))) return rc;
-  const HotHdr* hot;
-  const HotEntry* hot_dir;
-  if ((rc = build_hot(h, src, n, &hot, &hot_dir))) return rc;
   {
     Launch l(h, "k_receive_fast");
     k_receive_fast<Src><<<fast_grid(h, n), kFastBlock, 0, h->stream>>>(
@@ -588,17 +587,29 @@ int receive_decoded(phip_handle* h, Src src, const uint64_t* a, const uint64_t* 
                     const int64_t* e, u32 n,
                     i64 now, const OutView& ow, bool classified) {
   int rc;
+  // The hot directory (read-only on the table and the batch) is built on
+  // stream2 while the classification streams the replica fields.
+  const HotHdr* hot = nullptr;
+  const HotEntry* hot_dir = nullptr;
+  const bool with_hot = n >= kHotMinBatch;
+  if (with_hot) {
+    HIPCHK(h, hipEventRecord(h->ev_fork, h->stream));
+    HIPCHK(h, hipStreamWaitEvent(h->stream2, h->ev_fork, 0));
+    if ((rc = build_hot(h, src, n, h->stream2, &hot, &hot_dir))) return rc;
+    HIPCHK(h, hipEventRecord(h->ev_join, h->stream2));
+  }
   if (!classified) {
     if ((rc = reset_ctr(h))) return rc;
     Launch l(h, "k_classify");
     k_classify<<<grid_for(n), kBlock, 0, h->stream>>>(a, t, e, n, h->ctr);
     HIPCHK(h, hipGetLastError());
   }
+  if (with_hot) HIPCHK(h, hipStreamWaitEvent(h->stream, h->ev_join, 0));
   // The fast path is enqueued behind the classification without a host
   // round trip; k_receive_fast itself does nothing when the counters show an
   // incast or a -0.0 field, and the batch then takes the ordered path.
   bool dirty = false;
-  if ((rc = fast_receive(h, src, a, t, e, n, now, ow.status, &dirty))) return rc;
+  if ((rc = fast_receive(h, src, a, t, e, n, now, ow.status, hot, hot_dir, &dirty))) return rc;
   if (!dirty) return PHIP_OK;
   OpView ov{};
   ov.kind = nullptr; ov.kind0 = PHIP_OP_RECEIVE;

@@ -175,9 +175,10 @@ __global__ void k_classify(const uint64_t* __restrict__ a, const uint64_t* __res
   u32 i = blockIdx.x * blockDim.x + threadIdx.x;
   bool inc = false, nz = false;
   if (i < n) {
-    u64 ab = a[i], tb = t[i];
-    i64 eb = e[i];
-    inc = state_is_zero(ab, tb, eb);
+    const u64 ab = __builtin_nontemporal_load(a + i), tb = __builtin_nontemporal_load(t + i);
+    // elapsed matters only when both floats are zero: read it only then
+    // (a third of the pass's bytes on a clean batch)
+    if (is_zero_bits(ab) && is_zero_bits(tb)) inc = e[i] == 0;
     nz = !inc && (ab == kSign || tb == kSign);
   }
   u64 mi = __ballot(inc), mn = __ballot(nz);

@@ -31,6 +31,23 @@ __global__ __launch_bounds__(256) void lane_rec(const uint4* __restrict__ recs, 
   out[i] = x;
 }
 
+// one 16-B load per lane with explicit cache-policy bits
+template <int POL>
+__global__ __launch_bounds__(256) void lane_rec_pol(const uint4* __restrict__ recs, const u32* __restrict__ idx,
+                                                    u32 n, u32* __restrict__ out) {
+  u32 i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  u32 s = __builtin_nontemporal_load(idx + i);
+  const uint4* p = recs + (size_t)s * 4;
+  uint4 a;
+  if (POL == 0) asm volatile("global_load_dwordx4 %0, %1, off nt\n s_waitcnt vmcnt(0)" : "=v"(a) : "v"(p));
+  if (POL == 1) asm volatile("global_load_dwordx4 %0, %1, off sc1\n s_waitcnt vmcnt(0)" : "=v"(a) : "v"(p));
+  if (POL == 2) asm volatile("global_load_dwordx4 %0, %1, off sc0 sc1\n s_waitcnt vmcnt(0)" : "=v"(a) : "v"(p));
+  if (POL == 3) asm volatile("global_load_dwordx4 %0, %1, off sc0 sc1 nt\n s_waitcnt vmcnt(0)" : "=v"(a) : "v"(p));
+  if (POL == 4) asm volatile("global_load_dwordx4 %0, %1, off sc0\n s_waitcnt vmcnt(0)" : "=v"(a) : "v"(p));
+  out[i] = a.x ^ a.w;
+}
+
 __global__ __launch_bounds__(256) void quad_rec(const uint4* __restrict__ recs, const u32* __restrict__ idx,
                                                 u32 n, u32* __restrict__ out) {
   u32 t = blockIdx.x * 256 + threadIdx.x;
@@ -117,6 +134,11 @@ int main(int argc, char** argv) {
     snprintf(b, sizeof b, "%s lane 1x16B", sn[k]); timeit(b, [&] { lane_rec<1><<<G, 256>>>(recs, I, n, out); });
     snprintf(b, sizeof b, "%s lane 3x16B", sn[k]); timeit(b, [&] { lane_rec<3><<<G, 256>>>(recs, I, n, out); });
     snprintf(b, sizeof b, "%s lane 4x16B", sn[k]); timeit(b, [&] { lane_rec<4><<<G, 256>>>(recs, I, n, out); });
+    snprintf(b, sizeof b, "%s lane 1x16B nt", sn[k]); timeit(b, [&] { lane_rec_pol<0><<<G, 256>>>(recs, I, n, out); });
+    snprintf(b, sizeof b, "%s lane 1x16B sc1", sn[k]); timeit(b, [&] { lane_rec_pol<1><<<G, 256>>>(recs, I, n, out); });
+    snprintf(b, sizeof b, "%s lane 1x16B sc0 sc1", sn[k]); timeit(b, [&] { lane_rec_pol<2><<<G, 256>>>(recs, I, n, out); });
+    snprintf(b, sizeof b, "%s lane 1x16B sc0 sc1 nt", sn[k]); timeit(b, [&] { lane_rec_pol<3><<<G, 256>>>(recs, I, n, out); });
+    snprintf(b, sizeof b, "%s lane 1x16B sc0", sn[k]); timeit(b, [&] { lane_rec_pol<4><<<G, 256>>>(recs, I, n, out); });
     snprintf(b, sizeof b, "%s quad 4x16B", sn[k]); timeit(b, [&] { quad_rec<<<(unsigned)((4ull * n + 255) / 256), 256>>>(recs, I, n, out); });
 
     static u64 v = 1ull << 40;
