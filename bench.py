@@ -51,9 +51,13 @@ def parse():
     p.add_argument("--cpu-threads", type=int, default=0)
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--seed", type=int, default=1234)
-    p.add_argument("--workload", default="c2", choices=["c2", "c3"],
+    p.add_argument("--workload", default="c2", choices=["c2", "c3", "c4", "c5"],
                    help="c2: batched Receive merges (headline); c3: mixed Take+Merge stream")
     p.add_argument("--ops", type=int, default=50_000_000, help="c3: ops per step")
+    p.add_argument("--replicas", type=int, default=8, help="c5: simulated replicas per GPU")
+    p.add_argument("--buckets", type=int, default=1 << 24, help="c5: buckets per replica")
+    p.add_argument("--writes", type=float, default=0.01,
+                   help="c5: fraction of buckets each replica writes between rounds")
     p.add_argument("--dist-backend", default="nccl",
                    help="nccl (= RCCL on ROCm) for real runs; gloo to rehearse several ranks on one GPU")
     return p.parse_args()
@@ -186,6 +190,89 @@ def run_c3(args, torch, dev, repo, rank, K, base, gen):
     return n, step
 
 
+def run_c4(args, torch, dev, repo, rank, world, K, gen):
+    """K*world buckets hash-sharded by name over the ranks
+    (owner = top bits of FNV-1a, patrol_amd.shard.owner_of).  Every rank
+    draws its messages over ALL buckets (Zipf, as they would arrive from
+    peers), so each step packs them by owner on the GPU (phip_route_pack),
+    moves them with one all-to-all per column over RCCL and merges the
+    received ones (shard.route_messages_native, then phip_receive_soa)."""
+    from patrol_amd import shard
+    n = args.messages
+    KT = K * world
+    keys = torch.arange(KT, dtype=torch.int64, device=dev)
+    kb, ko = names_for_ids(torch, keys)
+    hk = shard.hash_names(kb, ko, repo)
+    mine = torch.nonzero(shard.owner_of(hk, world) == rank).flatten()
+    sb, _, so = shard._gather_names(kb, ko, mine)
+    st = torch.zeros((mine.numel(), 4), dtype=torch.int64, device=dev)
+    st[:, 3] = T0
+    repo.seed_device(sb, so.to(torch.int32), st, mine.numel())
+    owned = mine.numel()
+    del keys, kb, ko, hk, sb, so, st, mine
+    ids = zipf_ids(torch, gen, n, KT, args.zipf, dev)
+    blob, offs = names_for_ids(torch, ids)
+    batches = [replica_states(torch, gen, n, j, dev) for j in range(args.warmup + args.steps)]
+    torch.cuda.synchronize()
+
+    def step(j):
+        a, t, e = batches[j]
+        rb, ro, ra, rt, re = shard.route_messages_native(blob, offs, a, t, e, repo)
+        m = ro.numel() - 1
+        if m:
+            repo.receive_soa(rb, ra, rt, re, T0 + j, name_offs=ro.to(torch.int32), n=m, device=True)
+    return n, step, owned
+
+
+def run_c5(args, torch, dev, repo, rank, world, gen):
+    """R simulated replicas per GPU of B buckets each
+    (E-encoded state planes, patrol_amd.shard).  A round = fresh local writes
+    (a random fraction of each replica's buckets grows) followed by one
+    anti-entropy pass: k_ae_local_max, RCCL all-reduce(MAX) of the [3, B]
+    join over all GPUs, k_ae_apply.  One round converges (max is idempotent);
+    the loop models new writes between rounds.  A unit is one replica-bucket
+    brought to the cluster-wide join."""
+    from patrol_amd import shard
+    R, B = args.replicas, args.buckets
+    taken = torch.randint(0, 10**6, (R, B), device=dev, generator=gen).to(torch.float64)
+    added = taken + torch.rand((R, B), dtype=torch.float64, device=dev, generator=gen) * 100.0
+    reps = torch.empty((R, 3, B), dtype=torch.int64, device=dev)
+    reps[:, 0] = shard.e_encode(added.view(torch.int64))
+    reps[:, 1] = shard.e_encode(taken.view(torch.int64))
+    reps[:, 2] = torch.randint(0, 1 << 40, (R, B), device=dev, generator=gen, dtype=torch.int64)
+    del taken, added
+    nw = max(1, int(B * args.writes))
+    rounds = []
+    for j in range(args.warmup + args.steps):
+        idx = torch.randint(0, B, (R, nw), device=dev, generator=gen) + \
+            torch.arange(R, device=dev).unsqueeze(1) * (3 * B)
+        # a local Take: taken grows by a few ulps, elapsed by up to 1 ms
+        rounds.append((idx.flatten(), torch.randint(1, 8, (R * nw,), device=dev, generator=gen),
+                       torch.randint(1, 10**6, (R * nw,), device=dev, generator=gen)))
+    flat = reps.view(-1)
+    torch.cuda.synchronize()
+
+    def step(j):
+        idx, dt, de = rounds[j]
+        flat.index_add_(0, idx + B, dt)
+        flat.index_add_(0, idx + 2 * B, de)
+        tl = []
+        shard.anti_entropy_native(reps, repo, timings=tl)
+        return tl
+
+    def check():
+        ok = bool((reps == reps[0:1]).all())
+        if world > 1:
+            import torch.distributed as dist
+            s = reps[0].sum(dtype=torch.int64).view(1)
+            lo, hi = s.clone(), s.clone()
+            dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+            dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+            ok = ok and bool(lo == hi)
+        return ok
+    return R * B, step, check
+
+
 def main():
     args = parse()
     import torch
@@ -195,7 +282,12 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    if world > 1 or args.workload in ("c4", "c5"):
+        # c4/c5 exercise the collectives (all-to-all, all-reduce) even on one GPU
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(29500 + (os.getpid() % 1000)))
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
         dist.init_process_group(args.dist_backend, init_method="env://")
     import patrol_amd
 
@@ -204,7 +296,11 @@ def main():
 
     # Shard: rank r owns bucket ids [r*K, (r+1)*K) (owner-routed upstream).
     base = rank * K
+    # One stream for torch's input generation and the engine's kernels, so
+    # device-pointer calls see torch's results without extra synchronisation.
+    torch.cuda.set_stream(torch.cuda.Stream(dev))
     repo = patrol_amd.GPURepo(device=local, log2_slots=args.log2_slots, arena_bytes=1 << 20)
+    repo.use_torch_stream()
     keys = torch.arange(base, base + K, dtype=torch.int64, device=dev)
     kb, ko = names_for_ids(torch, keys)
     st = torch.zeros((K, 4), dtype=torch.int64, device=dev)
@@ -215,8 +311,16 @@ def main():
     del kb, ko, st, keys
     assert len(repo) == K
 
+    c5_check = None
+    owned = K
     if args.workload == "c3":
         n, step = run_c3(args, torch, dev, repo, rank, K, base, gen)
+        ids = None
+    elif args.workload == "c4":
+        n, step, owned = run_c4(args, torch, dev, repo, rank, world, K, gen)
+        ids = None
+    elif args.workload == "c5":
+        n, step, c5_check = run_c5(args, torch, dev, repo, rank, world, gen)
         ids = None
     else:
         ids = zipf_ids(torch, gen, n, K, args.zipf, dev)
@@ -237,8 +341,8 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for j in range(args.warmup, args.warmup + args.steps):
-        step(j)
-        for name, ms in repo.timings():
+        tl = step(j)
+        for name, ms in (tl if tl is not None else repo.timings()):
             kern.setdefault(name, []).append(ms)
     torch.cuda.synchronize()
     if world > 1:
@@ -253,7 +357,30 @@ def main():
 
     total = world * n * args.steps
     kms = {k: float(np.mean(v)) for k, v in kern.items()}
-    if args.workload == "c3":
+    extra = {}
+    if args.workload == "c5":
+        # bytes of the two local passes per round (reads R*24 + 24, writes 24;
+        # then reads 24 + R*24, writes R*24 per bucket) over their kernel time
+        R, B = args.replicas, args.buckets
+        bpo = (3 * R + 2) * 24 / R
+        dom_name = "k_ae_local_max+k_ae_apply"
+        dom_ms = kms.get("k_ae_local_max", float("nan")) + kms.get("k_ae_apply", float("nan"))
+        unit, metric = "merges/s", METRIC + " [C5: anti-entropy replica-bucket joins/sec]"
+        workload = (f"C5 anti-entropy: {R} replicas/GPU x {B} buckets, {args.writes:g} of buckets "
+                    f"written per replica per round, all-reduce(max) over {world} GPU(s)")
+        extra["converged"] = c5_check()
+        allreduce_bytes = 3 * 8 * B
+        step_s = el / args.steps
+        extra["allreduce_bytes"] = allreduce_bytes
+        extra["replicas_total"] = R * world
+    elif args.workload == "c4":
+        bpo = BYTES_PER_MERGE
+        dom_name, dom_ms = DOMINANT, float(np.mean(kern.get(DOMINANT, [float("nan")])))
+        unit, metric = "merges/s", METRIC + " [C4: owner-routed]"
+        workload = (f"C4 owner-routed merge: {n} messages/GPU over {K * world} buckets hash-sharded "
+                    f"by name across {world} GPU(s), all-to-all routing + merge, Zipf({args.zipf})")
+        extra["buckets_owned_rank0"] = owned
+    elif args.workload == "c3":
         # Take 89 B (op 24 + state read 32 + write 24 + result 9), Merge 88 B.
         bpo = 88.5
         dom_name, dom_ms = "whole step", el / args.steps * 1e3
@@ -265,6 +392,8 @@ def main():
         dom_name, dom_ms = DOMINANT, float(np.mean(kern.get(DOMINANT, [float("nan")])))
         unit, metric = "merges/s", METRIC
         workload = f"C2 merge: {n} replica messages -> {K}-bucket table (2^{args.log2_slots} slots), Zipf({args.zipf})"
+    # c4: the merged count per rank varies (owners of hot buckets receive
+    # more); the roofline uses this rank's kernel and its message share.
     achieved = bpo * n / (dom_ms / 1e3) / 1e9
     traffic = pmc_traffic(workload)
     out = {
@@ -288,6 +417,7 @@ def main():
                      "algorithmic_bytes_per_launch": bpo * n},
         "kernels_ms": kms,
     }
+    out["config"].update(extra)
     if rank == 0 and world == 1 and not args.no_cpu and args.workload == "c2":
         threads = args.cpu_threads or min(16, os.cpu_count() or 1)
         try:
@@ -299,7 +429,7 @@ def main():
     if rank == 0:
         print(json.dumps(out), flush=True)
     repo.close()
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

@@ -157,6 +157,11 @@ int phip_open(const phip_config* cfg, phip_handle** out);
 void phip_close(phip_handle* h);
 const char* phip_last_error(const phip_handle* h);
 int phip_flush(phip_handle* h);                    /* hipStreamSynchronize */
+/* Run every later call of this handle on `stream` (a hipStream_t of the
+ * handle's device, e.g. the producer's stream of PHIP_DEVICE_PTRS inputs, so
+ * that no cross-stream synchronisation is needed); NULL restores the
+ * handle's own stream.  Work queued earlier is finished first. */
+int phip_set_stream(phip_handle* h, void* stream);
 uint64_t phip_len(phip_handle* h);                 /* number of buckets */
 uint64_t phip_capacity(phip_handle* h);            /* number of slots */
 
@@ -212,6 +217,35 @@ int phip_api_take(phip_handle* h, const uint8_t* name, uint32_t len, const char*
  * NULL); with PHIP_DEVICE_PTRS the hashes are computed on h's GPU. */
 int phip_hash_names(phip_handle* h, const uint8_t* names, const uint32_t* name_offs, uint32_t n,
                     uint64_t* out, uint32_t flags);
+
+/* Owner routing, the exchange step of a sharded merge: the n
+ * decoded messages of m are stable-partitioned by owner = ((FNV-1a(name) >>
+ * 32) * world) >> 32 into owner-major send buffers (send_* have n entries,
+ * send_names holds every name byte; names are packed back to back, so
+ * send_lens carries their lengths).  counts[o] / name_bytes[o] (world
+ * entries, device memory) receive each owner's message and byte counts: the
+ * splits of the all-to-all that moves the segments to their owners.  Device
+ * pointers only; world <= 64. */
+int phip_route_pack(phip_handle* h, const phip_msgs* m, uint32_t world, uint8_t* send_names,
+                    uint32_t* send_lens, uint64_t* send_added, uint64_t* send_taken,
+                    int64_t* send_elapsed, uint64_t* counts, uint64_t* name_bytes,
+                    uint32_t flags);
+
+/* Anti-entropy over simulated replicas (BASELINE configs[4]).  `replicas`
+ * holds nrep replicas of nbuckets buckets, each as three int64 planes
+ * [r][0..2][i]: E codes (the order-preserving key of the engine, mirrored by
+ * patrol_amd.shard.e_encode) of added and taken, then elapsed ns.  Device
+ * pointers only (flags must include PHIP_DEVICE_PTRS).
+ * phip_ae_local_max writes out[3][nbuckets], the field-wise join of the local
+ * replicas in signed form (E ^ 2^63 for the float planes; a NaN replica value
+ * never wins, as Go's `<` never adopts one), ready for an RCCL all-reduce(MAX)
+ * across GPUs.  phip_ae_apply then sets every local replica to
+ * max(own, joined): Bucket.Merge (bucket.go:240-263) of every replica into
+ * every other one, a replica's own NaN sticking. */
+int phip_ae_local_max(phip_handle* h, const int64_t* replicas, uint32_t nrep, uint64_t nbuckets,
+                      int64_t* out, uint32_t flags);
+int phip_ae_apply(phip_handle* h, int64_t* replicas, uint32_t nrep, uint64_t nbuckets,
+                  const int64_t* joined, uint32_t flags);
 
 /* ---- diagnostics ---- */
 /* Per-kernel timing of the last hot-path call, measured with HIP events on

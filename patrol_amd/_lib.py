@@ -19,6 +19,7 @@ EXPORTS = [
     "phip_capacity", "phip_seed", "phip_get", "phip_dump", "phip_receive_datagrams",
     "phip_receive_soa", "phip_upsert_soa", "phip_apply_mixed", "phip_take", "phip_parse_rate",
     "phip_marshal", "phip_api_take", "phip_last_timings", "phip_set_timing", "phip_last_stats", "phip_hash_names",
+    "phip_ae_local_max", "phip_ae_apply", "phip_set_stream", "phip_route_pack",
 ]
 
 PHIP_OK = 0
@@ -101,5 +102,9 @@ def load(path: str = LIB_PATH):
     L.phip_set_timing.restype = None
     L.phip_last_stats.argtypes = [vp, C.POINTER(C.c_uint64), C.c_int]
     L.phip_last_stats.restype = C.c_int
+    L.phip_ae_local_max.argtypes = [vp, vp, u32, u64, vp, u32]
+    L.phip_ae_apply.argtypes = [vp, vp, u32, u64, vp, u32]
+    L.phip_set_stream.argtypes = [vp, vp]
+    L.phip_route_pack.argtypes = [vp, C.POINTER(phip_msgs), u32, vp, vp, vp, vp, vp, vp, vp, u32]
     _lib = L
     return L

@@ -36,7 +36,7 @@ enum BufId {
   B_MISS, B_MISS2, B_RETRY, B_CSLOT, B_CMSG,
   B_SLOT, B_IDX, B_SSLOT, B_SIDX, B_USLOT, B_SCNT, B_SSTART, B_LONG, B_HUGE, B_TEMP, B_DUMP,
   B_OPS, B_HOFF, B_HOP, B_HVAL, B_RPOS, B_RST, B_RUNN, B_SEGEX, B_WOFF, B_SUMS, B_WRUN,
-  B_STATES, B_NAME1, B_HOT, B_COUNT_
+  B_STATES, B_NAME1, B_HOT, B_ROUTE, B_COUNT_
 };
 
 struct DevBuf {
@@ -55,7 +55,8 @@ struct phip_handle {
   int device = 0;
   int ncu = 256;             // compute units (persistent grid size)
   uint64_t stats[3] = {0, 0, 0};   // last fast batch: hot entries, hot hits, misses
-  hipStream_t stream = nullptr;
+  hipStream_t stream = nullptr;      // the stream every call runs on (own_stream or the caller's)
+  hipStream_t own_stream = nullptr;  // created by phip_open
   hipStream_t stream2 = nullptr;   // second stream: the hot-bucket fold overlaps the others
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   std::mutex mu;
@@ -650,7 +651,9 @@ int phip_open(const phip_config* cfg, phip_handle** out) {
   if ((e = hipDeviceGetAttribute(&h->ncu, hipDeviceAttributeMultiprocessorCount, h->device)) !=
       hipSuccess)
     return fail(e);
-  if ((e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking)) != hipSuccess) return fail(e);
+  if ((e = hipStreamCreateWithFlags(&h->own_stream, hipStreamNonBlocking)) != hipSuccess)
+    return fail(e);
+  h->stream = h->own_stream;
   if ((e = hipStreamCreateWithFlags(&h->stream2, hipStreamNonBlocking)) != hipSuccess) return fail(e);
   if ((e = hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming)) != hipSuccess) return fail(e);
   if ((e = hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming)) != hipSuccess) return fail(e);
@@ -689,7 +692,10 @@ void phip_close(phip_handle* h) {
   if (h->ev_fork) hipEventDestroy(h->ev_fork);
   if (h->ev_join) hipEventDestroy(h->ev_join);
   if (h->stream2) hipStreamDestroy(h->stream2);
-  if (h->stream) hipStreamDestroy(h->stream);
+  if (h->own_stream) {
+    hipStreamSynchronize(h->own_stream);
+    hipStreamDestroy(h->own_stream);
+  }
   delete h;
 }
 
@@ -998,6 +1004,99 @@ int phip_hash_names(phip_handle* h, const uint8_t* names, const uint32_t* name_o
   return PHIP_OK;
 }
 
+int phip_route_pack(phip_handle* h, const phip_msgs* m, uint32_t world, uint8_t* send_names,
+                    uint32_t* send_lens, uint64_t* send_added, uint64_t* send_taken,
+                    int64_t* send_elapsed, uint64_t* counts, uint64_t* name_bytes,
+                    uint32_t flags) {
+  if (!h || !m || !(flags & PHIP_DEVICE_PTRS) || world == 0 || world > kRouteMaxWorld)
+    return PHIP_ERR_INVALID;
+  const u32 n = m->n;
+  if (n && (!m->names || !m->name_offs || !m->added || !m->taken || !m->elapsed || !send_names ||
+            !send_lens || !send_added || !send_taken || !send_elapsed || !counts || !name_bytes))
+    return PHIP_ERR_INVALID;
+  std::lock_guard<std::mutex> g(h->mu);
+  begin_call(h);
+  if (n == 0) {
+    HIPCHK(h, hipMemsetAsync(counts, 0, world * sizeof(uint64_t), h->stream));
+    HIPCHK(h, hipMemsetAsync(name_bytes, 0, world * sizeof(uint64_t), h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    return PHIP_OK;
+  }
+  const u32 nblk = grid_for(n);
+  const size_t cells = (size_t)world * nblk;
+  u8* base;
+  int rc;
+  if ((rc = ensure(h, B_ROUTE, n + 4 * cells * sizeof(u32) + 64, &base))) return rc;
+  u32* cnt = (u32*)base;
+  u32* bytes = cnt + cells;
+  u32* cbase = bytes + cells;
+  u32* bbase = cbase + cells;
+  u8* owner = (u8*)(bbase + cells);
+  NamesOffs src{m->names, m->name_offs};
+  {
+    Launch l(h, "k_route_count");
+    k_route_count<NamesOffs><<<nblk, kBlock, 0, h->stream>>>(src, n, world, owner, cnt, bytes);
+  }
+  HIPCHK(h, hipGetLastError());
+  size_t tb = 0;
+  HIPCHK(h, rocprim::exclusive_scan(nullptr, tb, cnt, cbase, 0u, cells, rocprim::plus<u32>(),
+                                    h->stream));
+  u8* temp;
+  if ((rc = ensure(h, B_TEMP, tb, &temp))) return rc;
+  {
+    Launch l(h, "route_scan");
+    HIPCHK(h, rocprim::exclusive_scan(temp, tb, cnt, cbase, 0u, cells, rocprim::plus<u32>(),
+                                      h->stream));
+    HIPCHK(h, rocprim::exclusive_scan(temp, tb, bytes, bbase, 0u, cells, rocprim::plus<u32>(),
+                                      h->stream));
+  }
+  {
+    Launch l(h, "k_route_scatter");
+    k_route_scatter<NamesOffs><<<nblk, kBlock, 0, h->stream>>>(
+        src, m->added, m->taken, m->elapsed, n, world, owner, cbase, bbase, send_names, send_lens,
+        send_added, send_taken, send_elapsed);
+  }
+  k_route_totals<<<1, kRouteMaxWorld, 0, h->stream>>>(cnt, bytes, cbase, bbase, nblk, world, counts,
+                                                     name_bytes);
+  HIPCHK(h, hipGetLastError());
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  return PHIP_OK;
+}
+
+int phip_ae_local_max(phip_handle* h, const int64_t* replicas, uint32_t nrep, uint64_t nbuckets,
+                      int64_t* out, uint32_t flags) {
+  if (!h || !(flags & PHIP_DEVICE_PTRS) || (nbuckets && (!replicas || !out)) || nrep == 0)
+    return PHIP_ERR_INVALID;
+  std::lock_guard<std::mutex> g(h->mu);
+  begin_call(h);
+  if (nbuckets == 0) return PHIP_OK;
+  {
+    Launch l(h, "k_ae_local_max");
+    k_ae_local_max<<<dim3(grid_for(nbuckets), 3), kBlock, 0, h->stream>>>(replicas, nrep, nbuckets,
+                                                                         out);
+  }
+  HIPCHK(h, hipGetLastError());
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  return PHIP_OK;
+}
+
+int phip_ae_apply(phip_handle* h, int64_t* replicas, uint32_t nrep, uint64_t nbuckets,
+                  const int64_t* joined, uint32_t flags) {
+  if (!h || !(flags & PHIP_DEVICE_PTRS) || (nbuckets && (!replicas || !joined)) || nrep == 0)
+    return PHIP_ERR_INVALID;
+  std::lock_guard<std::mutex> g(h->mu);
+  begin_call(h);
+  if (nbuckets == 0) return PHIP_OK;
+  {
+    Launch l(h, "k_ae_apply");
+    k_ae_apply<<<dim3(grid_for(nbuckets), 3), kBlock, 0, h->stream>>>(replicas, nrep, nbuckets,
+                                                                     joined);
+  }
+  HIPCHK(h, hipGetLastError());
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  return PHIP_OK;
+}
+
 int phip_last_timings(phip_handle* h, const char** names, float* ms, int max) {
   if (!h) return 0;
   std::lock_guard<std::mutex> g(h->mu);
@@ -1017,6 +1116,16 @@ int phip_last_timings(phip_handle* h, const char** names, float* ms, int max) {
 
 void phip_set_timing(phip_handle* h, int on) {
   if (h) h->timing = on != 0;
+}
+
+int phip_set_stream(phip_handle* h, void* stream) {
+  if (!h) return PHIP_ERR_INVALID;
+  std::lock_guard<std::mutex> g(h->mu);
+  hipSetDevice(h->device);
+  // work already queued on the previous stream comes first
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  h->stream = stream ? (hipStream_t)stream : h->own_stream;
+  return PHIP_OK;
 }
 
 int phip_last_stats(phip_handle* h, uint64_t* out, int max) {

@@ -1482,6 +1482,179 @@ __global__ void k_dump_gather(const u32* __restrict__ list, u32 n, const Rec* __
 }
 
 // FNV-1a 64 of every name (phip_hash_names): the probe key and the shard map.
+// Owner routing: the one exchange step of a sharded merge.
+// owner(name) = ((fnv1a64(name) >> 32) * world) >> 32 (patrol_amd.shard).
+// k_route_count histograms owners per workgroup; an exclusive scan of the
+// [owner][workgroup] counts gives every (owner, workgroup) its base in the
+// owner-major send buffer; k_route_scatter then places each message with a
+// stable rank (wave ballots per owner, wave prefix in LDS), so the send
+// buffer holds each owner's messages contiguously in their original order.
+constexpr u32 kRouteMaxWorld = 64;
+
+__device__ inline u32 owner_of_hash(u64 h, u32 world) {
+  return (u32)(((h >> 32) * (u64)world) >> 32);
+}
+
+template <class Src>
+__global__ __launch_bounds__(kBlock) void k_route_count(Src src, u32 n, u32 world,
+                                                        u8* __restrict__ owner,
+                                                        u32* __restrict__ cnt,
+                                                        u32* __restrict__ bytes) {
+  __shared__ u32 lc[kRouteMaxWorld], lb[kRouteMaxWorld];
+  if (threadIdx.x < kRouteMaxWorld) { lc[threadIdx.x] = 0; lb[threadIdx.x] = 0; }
+  __syncthreads();
+  const u32 i = blockIdx.x * kBlock + threadIdx.x;
+  if (i < n) {
+    u64 off; u32 len;
+    src.template get<true>(i, off, len);
+    Name nm;
+    load_name_wide<true>(src.blob, off, len, nm);
+    const u32 o = owner_of_hash(nm.h, world);
+    owner[i] = (u8)o;
+    atomicAdd(&lc[o], 1u);
+    atomicAdd(&lb[o], len);
+  }
+  __syncthreads();
+  if (threadIdx.x < world) {
+    cnt[(u64)threadIdx.x * gridDim.x + blockIdx.x] = lc[threadIdx.x];
+    bytes[(u64)threadIdx.x * gridDim.x + blockIdx.x] = lb[threadIdx.x];
+  }
+}
+
+// Inclusive wave scan (64 lanes).
+__device__ inline u32 wave_incl_scan(u32 v) {
+  const u32 lane = __lane_id();
+#pragma unroll
+  for (u32 d = 1; d < 64; d <<= 1) {
+    const u32 o = __shfl_up(v, d);
+    if (lane >= d) v += o;
+  }
+  return v;
+}
+
+template <class Src>
+__global__ __launch_bounds__(kBlock) void k_route_scatter(
+    Src src, const uint64_t* __restrict__ a, const uint64_t* __restrict__ t,
+    const int64_t* __restrict__ e, u32 n, u32 world, const u8* __restrict__ owner,
+    const u32* __restrict__ cbase, const u32* __restrict__ bbase, u8* __restrict__ out_names,
+    u32* __restrict__ out_lens, uint64_t* __restrict__ out_a, uint64_t* __restrict__ out_t,
+    int64_t* __restrict__ out_e) {
+  constexpr u32 kW = kBlock / 64;
+  __shared__ u32 wc[kW][kRouteMaxWorld], wb[kW][kRouteMaxWorld];
+  const u32 wave = threadIdx.x / 64, lane = __lane_id();
+  for (u32 j = threadIdx.x; j < kW * kRouteMaxWorld; j += kBlock) {
+    (&wc[0][0])[j] = 0; (&wb[0][0])[j] = 0;
+  }
+  __syncthreads();
+  const u32 i = blockIdx.x * kBlock + threadIdx.x;
+  const bool valid = i < n;
+  u64 off = 0; u32 len = 0, o = kRouteMaxWorld;
+  if (valid) {
+    src.get(i, off, len);
+    o = owner[i];
+  }
+  // stable rank and byte prefix among this wave's lanes with the same owner
+  u32 rank = 0, bpre = 0;
+  u64 rest = __ballot(valid);
+  while (rest) {
+    const u32 leader = __ffsll((long long)rest) - 1;
+    const u32 lo = __shfl(o, leader);
+    const bool mine = valid && o == lo;
+    const u64 m = __ballot(mine);
+    const u32 sc = wave_incl_scan(mine ? len : 0u);
+    if (mine) {
+      rank = __popcll(m & ((1ull << lane) - 1));
+      bpre = sc - len;
+    }
+    if (lane == 63) { wc[wave][lo] = __popcll(m); wb[wave][lo] = sc; }
+    rest &= ~m;
+  }
+  __syncthreads();
+  if (!valid) return;
+  u32 cw = 0, bw = 0;
+  for (u32 w = 0; w < wave; ++w) { cw += wc[w][o]; bw += wb[w][o]; }
+  const u64 slot = (u64)o * gridDim.x + blockIdx.x;
+  const u32 dst = cbase[slot] + cw + rank;
+  const u32 dby = bbase[slot] + bw + bpre;
+  out_lens[dst] = len;
+  out_a[dst] = a[i];
+  out_t[dst] = t[i];
+  out_e[dst] = e[i];
+  for (u32 k = 0; k < len; ++k) out_names[dby + k] = src.blob[off + k];
+}
+
+// Per-owner totals from the scanned (exclusive) bases.
+__global__ void k_route_totals(const u32* __restrict__ cnt, const u32* __restrict__ bytes,
+                               const u32* __restrict__ cbase, const u32* __restrict__ bbase,
+                               u32 nblk, u32 world, uint64_t* __restrict__ counts,
+                               uint64_t* __restrict__ nbytes) {
+  const u32 o = threadIdx.x;
+  if (o >= world) return;
+  const u64 last = (u64)world * nblk - 1;
+  const u32 c0 = cbase[(u64)o * nblk], b0 = bbase[(u64)o * nblk];
+  const u32 c1 = o + 1 < world ? cbase[(u64)(o + 1) * nblk] : cbase[last] + cnt[last];
+  const u32 b1 = o + 1 < world ? bbase[(u64)(o + 1) * nblk] : bbase[last] + bytes[last];
+  counts[o] = c1 - c0;
+  nbytes[o] = b1 - b0;
+}
+
+// ------------------------------------------------------------ shard layer --
+// Anti-entropy over simulated cluster replicas (BASELINE configs[4], SURVEY
+// §8e).  Replica r of a GPU is three planes of B int64 for the same B buckets:
+//   [r][0][i], [r][1][i]  E codes of added and taken (phip_device.hpp enc_f64)
+//   [r][2][i]             elapsed ns
+// The CvRDT join of any set of replicas is then a field-wise max, with Go's
+// `if b.x < o.x { b.x = o.x }` rule (bucket.go:250-256) for NaN: a NaN replica
+// value is never adopted (E'(NaN) = 0), a replica's own NaN sticks.  RCCL
+// reduces signed int64, so the float planes cross the wire as E ^ 2^63.
+//
+// k_ae_local_max: m[f][i] = max over the R local replicas, in the signed
+// form RCCL's all-reduce(MAX) takes; k_ae_apply: every local replica becomes
+// max(own, m) after the all-reduce (one read and one write per replica).
+__global__ __launch_bounds__(kBlock) void k_ae_local_max(const int64_t* __restrict__ rep, u32 R,
+                                                         u64 B, int64_t* __restrict__ m) {
+  const u64 i = (u64)blockIdx.x * kBlock + threadIdx.x;
+  const u32 f = blockIdx.y;
+  if (i >= B) return;
+  const int64_t* p = rep + (u64)f * B + i;
+  const u64 stride = 3 * B;
+  if (f < 2) {
+    u64 best = 0;   // E'(NaN) = 0 = E(-Inf): never wins
+    for (u32 r = 0; r < R; ++r) {
+      u64 e = (u64)__builtin_nontemporal_load(p + r * stride);
+      if (e >= kNanBase) e = 0;
+      best = e > best ? e : best;
+    }
+    m[(u64)f * B + i] = (int64_t)(best ^ kSign);
+  } else {
+    int64_t best = INT64_MIN;
+    for (u32 r = 0; r < R; ++r) {
+      const int64_t e = __builtin_nontemporal_load(p + r * stride);
+      best = e > best ? e : best;
+    }
+    m[(u64)f * B + i] = best;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_ae_apply(int64_t* __restrict__ rep, u32 R, u64 B,
+                                                     const int64_t* __restrict__ m) {
+  const u64 i = (u64)blockIdx.x * kBlock + threadIdx.x;
+  const u32 f = blockIdx.y;
+  if (i >= B) return;
+  const int64_t mv = m[(u64)f * B + i];
+  int64_t* p = rep + (u64)f * B + i;
+  const u64 stride = 3 * B;
+  for (u32 r = 0; r < R; ++r) {
+    const int64_t own = p[r * stride];
+    if (f < 2) {
+      const u64 theirs = (u64)mv ^ kSign;   // already NaN-free
+      p[r * stride] = (int64_t)((u64)own > theirs ? (u64)own : theirs);
+    } else {
+      p[r * stride] = own > mv ? own : mv;
+    }
+  }
+}
+
 __global__ void k_hash_names(NamesOffs src, u32 n, uint64_t* out) {
   u32 i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;

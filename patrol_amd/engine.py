@@ -118,6 +118,24 @@ class GPURepo:
     def flush(self):
         self._check(self.L.phip_flush(self.h))
 
+    def set_stream(self, stream=None):
+        """Run the handle's work on `stream` (a torch.cuda.Stream, a raw
+        hipStream_t int, or None for the handle's own stream).  Device-pointer
+        calls whose inputs torch produces on that stream then need no
+        synchronisation between the two."""
+        raw = getattr(stream, "cuda_stream", stream)
+        self._check(self.L.phip_set_stream(self.h, C.c_void_p(raw) if raw else None))
+
+    def use_torch_stream(self):
+        """set_stream(torch's current stream on this device).  torch's default
+        stream has the handle 0, which means "the handle's own stream" here:
+        make a dedicated torch stream current first (torch.cuda.set_stream)."""
+        import torch
+        s = torch.cuda.current_stream(self.device)
+        if not s.cuda_stream:
+            raise ValueError("torch's current stream is the default stream; set a torch.cuda.Stream first")
+        self.set_stream(s)
+
     def set_timing(self, on: bool):
         self.L.phip_set_timing(self.h, 1 if on else 0)
 

@@ -112,6 +112,54 @@ def route_messages(blob, offs, added, taken, elapsed, group=None, repo=None, h=N
     return r_blob, r_offs, r_a, r_t, r_e
 
 
+def route_messages_native(blob, offs, added, taken, elapsed, repo, group=None):
+    """route_messages with the partition on the GPU (phip_route_pack: owner
+    hash, stable owner-major pack of names, lengths and states in two
+    passes), then the all-to-all of each column over RCCL.  Same result as
+    route_messages().  repo's stream must be torch's current stream
+    (GPURepo.use_torch_stream) or the inputs complete."""
+    from .engine import phip_msgs
+    world = dist.get_world_size(group)
+    dev = blob.device
+    n = offs.numel() - 1
+    L = _lib.load()
+    offs32 = offs if offs.dtype == torch.int32 else offs.to(torch.int32)
+    s_names = torch.empty(max(blob.numel(), 1), dtype=torch.uint8, device=dev)
+    s_lens = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+    s_a = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
+    s_t = torch.empty_like(s_a)
+    s_e = torch.empty_like(s_a)
+    cnt = torch.zeros(world, dtype=torch.int64, device=dev)
+    nbytes = torch.zeros(world, dtype=torch.int64, device=dev)
+    m = phip_msgs(n, 0, blob.data_ptr(), offs32.data_ptr(), added.data_ptr(), taken.data_ptr(),
+                  elapsed.data_ptr())
+    rc = L.phip_route_pack(repo.h, C.byref(m), world, s_names.data_ptr(), s_lens.data_ptr(),
+                           s_a.data_ptr(), s_t.data_ptr(), s_e.data_ptr(), cnt.data_ptr(),
+                           nbytes.data_ptr(), _lib.DEVICE_PTRS)
+    if rc != 0:
+        raise RuntimeError(f"phip_route_pack failed: {rc}")
+    recv_cnt = torch.empty_like(cnt)
+    recv_bytes = torch.empty_like(nbytes)
+    dist.all_to_all_single(recv_cnt, cnt, group=group)
+    dist.all_to_all_single(recv_bytes, nbytes, group=group)
+    sc, rc_ = cnt.tolist(), recv_cnt.tolist()
+    sb, rb = nbytes.tolist(), recv_bytes.tolist()
+
+    def a2a(x, s_splits, r_splits, slack=0):
+        total = sum(r_splits)
+        out = torch.empty(total + slack, dtype=x.dtype, device=dev)
+        dist.all_to_all_single(out[:total], x[:sum(s_splits)], r_splits, s_splits, group=group)
+        return out if slack else out[:total]
+
+    r_lens = a2a(s_lens, sc, rc_)
+    # 8 bytes of read slack past the last name (the ABI's blob rule)
+    r_blob = a2a(s_names, sb, rb, slack=8)
+    r_a, r_t, r_e = a2a(s_a, sc, rc_), a2a(s_t, sc, rc_), a2a(s_e, sc, rc_)
+    r_offs = torch.zeros(r_lens.numel() + 1, dtype=torch.int64, device=dev)
+    r_offs[1:] = torch.cumsum(r_lens, 0)
+    return r_blob, r_offs, r_a, r_t, r_e
+
+
 # ---------------------------------------------------------- E-encoding ----
 def e_encode(bits: torch.Tensor) -> torch.Tensor:
     """float64 bit patterns (int64) -> E codes (int64 holding the u64 code).
@@ -152,6 +200,33 @@ def to_signed_order(code: torch.Tensor) -> torch.Tensor:
 def is_nan_code(code: torch.Tensor) -> torch.Tensor:
     """E codes of NaNs are the top of the unsigned order (>= NAN_BASE)."""
     return (code ^ SIGN) >= (NAN_BASE ^ SIGN)
+
+
+def anti_entropy_native(replicas: torch.Tensor, repo, group=None, timings=None) -> torch.Tensor:
+    """anti_entropy on the GPU through libpatrolhip, in place: one pass over
+    the local replicas (k_ae_local_max), one RCCL all-reduce(MAX) of the
+    [3, B] join, one pass writing every replica (k_ae_apply).  Same result
+    as anti_entropy().  With a list `timings` (and repo.set_timing(True)) the
+    two kernels' (name, ms) are appended to it."""
+    if not replicas.is_cuda or replicas.dtype != torch.int64 or not replicas.is_contiguous():
+        raise ValueError("anti_entropy_native needs a contiguous int64 CUDA tensor [R, 3, B]")
+    R, three, B = replicas.shape
+    assert three == 3
+    L = _lib.load()
+    m = torch.empty((3, B), dtype=torch.int64, device=replicas.device)
+    rc = L.phip_ae_local_max(repo.h, replicas.data_ptr(), R, B, m.data_ptr(), _lib.DEVICE_PTRS)
+    if rc != 0:
+        raise RuntimeError(f"phip_ae_local_max failed: {rc}")
+    if timings is not None:
+        timings += repo.timings()
+    if dist.is_initialized():
+        dist.all_reduce(m, op=dist.ReduceOp.MAX, group=group)
+    rc = L.phip_ae_apply(repo.h, replicas.data_ptr(), R, B, m.data_ptr(), _lib.DEVICE_PTRS)
+    if rc != 0:
+        raise RuntimeError(f"phip_ae_apply failed: {rc}")
+    if timings is not None:
+        timings += repo.timings()
+    return replicas
 
 
 def anti_entropy(replicas: torch.Tensor, group=None) -> torch.Tensor:

@@ -180,3 +180,87 @@ def test_anti_entropy_gloo_world2_equals_go_merge():
                     acc.merge(G.Bucket(added=G.b2f(a[b]), taken=G.b2f(t[b]), elapsed=e[b]))
             assert (got[0][b] & (2**64 - 1), got[1][b] & (2**64 - 1), got[2][b]) == \
                    (G.f2b(acc.added), G.f2b(acc.taken), acc.elapsed), (i, b)
+
+
+@pytest.mark.gpu
+def test_anti_entropy_native_gpu_equals_go_merge_and_torch():
+    """k_ae_local_max + k_ae_apply (libpatrolhip) on cuda:0, single rank: every
+    replica ends as the Go merge of all replicas (bucket.go:240-263), and
+    equal to the torch restatement."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import patrol_amd
+    R, B = 6, 700
+    reps = _replicas(0, 3, B) + _replicas(1, 3, B)
+    x = torch.zeros((R, 3, B), dtype=torch.int64)
+    for k, (a, t, e) in enumerate(reps):
+        x[k, 0] = shard.e_encode(torch.tensor([to_i64(v) for v in a]))
+        x[k, 1] = shard.e_encode(torch.tensor([to_i64(v) for v in t]))
+        x[k, 2] = torch.tensor(e)
+    want_t = shard.anti_entropy(x.clone())
+    repo = patrol_amd.GPURepo(device=0, log2_slots=10)
+    xd = x.cuda()
+    torch.cuda.synchronize()
+    shard.anti_entropy_native(xd, repo)
+    got = xd.cpu()
+    assert torch.equal(got, want_t)
+    for i, own in enumerate(reps):
+        for b in range(0, B, 7):
+            acc = G.Bucket(added=G.b2f(own[0][b]), taken=G.b2f(own[1][b]), elapsed=own[2][b])
+            for j, (a, t, e) in enumerate(reps):
+                if j != i:
+                    acc.merge(G.Bucket(added=G.b2f(a[b]), taken=G.b2f(t[b]), elapsed=e[b]))
+            ga = int(shard.e_decode(got[i, 0, b:b + 1])[0]) & (2**64 - 1)
+            gt = int(shard.e_decode(got[i, 1, b:b + 1])[0]) & (2**64 - 1)
+            assert (ga, gt, int(got[i, 2, b])) == (G.f2b(acc.added), G.f2b(acc.taken), acc.elapsed)
+    repo.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [1, 3, 8, 64])
+def test_route_pack_is_stable_owner_partition(world):
+    """phip_route_pack on cuda:0: owner-major, per-owner original order,
+    names/lengths/states moved intact, per-owner counts and byte totals."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import ctypes as C
+    import patrol_amd
+    from patrol_amd import _lib
+    from patrol_amd.engine import phip_msgs, names_blob
+    rng = np.random.default_rng(world)
+    n = 200_003
+    ids = rng.integers(0, 50_000, n)
+    names = [(b"b%d" % i) if i % 7 else (b"a-long-bucket-name-%d-%s" % (i, b"x" * (i % 40)))
+             for i in ids]
+    blob_np, offs_np = names_blob(names)
+    a = rng.integers(0, 1 << 62, n).astype(np.int64)
+    t = rng.integers(0, 1 << 62, n).astype(np.int64)
+    e = rng.integers(-(1 << 62), 1 << 62, n).astype(np.int64)
+    h = shard.hash_names(torch.from_numpy(blob_np), torch.from_numpy(offs_np.astype(np.int64)))
+    own = shard.owner_of(h, world).numpy()
+    order = np.argsort(own, kind="stable")
+    repo = patrol_amd.GPURepo(device=0, log2_slots=10)
+    dev = torch.device("cuda", 0)
+    blob, offs = torch.from_numpy(blob_np).to(dev), torch.from_numpy(offs_np.view(np.int32)).to(dev)
+    da, dt, de = (torch.from_numpy(x).to(dev) for x in (a, t, e))
+    s_names = torch.empty(blob.numel(), dtype=torch.uint8, device=dev)
+    s_lens = torch.empty(n, dtype=torch.int32, device=dev)
+    s_a, s_t, s_e = (torch.empty(n, dtype=torch.int64, device=dev) for _ in range(3))
+    cnt = torch.zeros(world, dtype=torch.int64, device=dev)
+    nb = torch.zeros(world, dtype=torch.int64, device=dev)
+    torch.cuda.synchronize()
+    m = phip_msgs(n, 0, blob.data_ptr(), offs.data_ptr(), da.data_ptr(), dt.data_ptr(), de.data_ptr())
+    rc = _lib.load().phip_route_pack(repo.h, C.byref(m), world, s_names.data_ptr(), s_lens.data_ptr(),
+                                     s_a.data_ptr(), s_t.data_ptr(), s_e.data_ptr(), cnt.data_ptr(),
+                                     nb.data_ptr(), _lib.DEVICE_PTRS)
+    assert rc == 0
+    lens = np.diff(offs_np.astype(np.int64))
+    assert np.array_equal(cnt.cpu().numpy(), np.bincount(own, minlength=world))
+    assert np.array_equal(nb.cpu().numpy(), np.bincount(own, weights=lens, minlength=world).astype(np.int64))
+    assert np.array_equal(s_lens.cpu().numpy(), lens[order])
+    assert np.array_equal(s_a.cpu().numpy(), a[order])
+    assert np.array_equal(s_t.cpu().numpy(), t[order])
+    assert np.array_equal(s_e.cpu().numpy(), e[order])
+    want = b"".join(names[k] for k in order)
+    assert s_names.cpu().numpy()[:len(want)].tobytes() == want
+    repo.close()

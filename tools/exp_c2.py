@@ -17,7 +17,9 @@ def main():
     dev = torch.device("cuda", 0)
     K, n = 10_000_000, 100_000_000
     gen = torch.Generator(device=dev).manual_seed(1234)
+    torch.cuda.set_stream(torch.cuda.Stream(dev))
     repo = patrol_amd.GPURepo(device=0, log2_slots=25, arena_bytes=1 << 20)
+    repo.use_torch_stream()
     keys = torch.arange(K, dtype=torch.int64, device=dev)
     kb, ko = bench.names_for_ids(torch, keys)
     st = torch.zeros((K, 4), dtype=torch.int64, device=dev)
