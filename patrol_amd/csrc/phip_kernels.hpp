@@ -1247,6 +1247,7 @@ struct FoldShared {
   u32 val[kFoldWin];
   WinSum sum[kSumChunk];
   u32 wave_min[2][kFoldThreads / 64];
+  u32 quiet_min[kFoldThreads / 64];
   u64 state[4];
   u32 cur, nrun;
 };
@@ -1368,17 +1369,43 @@ __global__ __launch_bounds__(kFoldThreads) void k_fold_block(
   u32* __restrict__ wr = win_run + woff[blockIdx.x];
   u32 round = 0;
   FoldWin A;
-  for (u32 w = 0; w < nwin; ++w) {
-    if (tid == 0) wr[w] = sh.nrun - 1;   // run in effect at the window's first op
-    if (w % kSumChunk == 0) {
+  // Quiet windows are found kSumChunk at a time: every thread tests one
+  // window's summary against the current state and a workgroup min picks
+  // the first window that may change it.  The windows before it keep the
+  // state, so a long rate-limited stretch costs one test per thread instead
+  // of one sequential test per window; only the found window is folded.
+  u32 staged = 0xFFFFFFFFu;
+  for (u32 w = 0; w < nwin;) {
+    const u32 cb = w - w % kSumChunk;
+    if (cb != staged) {
       __syncthreads();   // previous chunk's readers are done
-      if (w + tid < nwin) sh.sum[tid] = ws[w + tid];
+      if (cb + tid < nwin) sh.sum[tid] = ws[cb + tid];
+      staged = cb;
       __syncthreads();
     }
-    if (window_quiet(sh.sum[w % kSumChunk], S)) continue;   // uniform decision
-    const u32 pos = w * kFoldWin;
+    const u32 lim = min(cb + kSumChunk, nwin);
+    const u32 mine = cb + tid;
+    u32 m = (mine >= w && mine < lim && !window_quiet(sh.sum[tid], S)) ? mine : 0xFFFFFFFFu;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) m = min(m, (u32)__shfl_xor((int)m, off));
+    if ((tid & 63) == 0) sh.quiet_min[tid >> 6] = m;
+    __syncthreads();
+    u32 first = 0xFFFFFFFFu;
+#pragma unroll
+    for (u32 x = 0; x < kFoldThreads / 64; ++x) first = min(first, sh.quiet_min[x]);
+    const u32 stop = first == 0xFFFFFFFFu ? lim : first;
+    const u32 run_now = sh.nrun - 1;   // run in effect at each quiet window's first op
+    for (u32 x = w + tid; x < stop; x += kFoldThreads) wr[x] = run_now;
+    __syncthreads();   // quiet_min and nrun are rewritten below
+    if (first == 0xFFFFFFFFu) {
+      w = lim;
+      continue;
+    }
+    if (tid == 0) wr[first] = run_now;
+    const u32 pos = first * kFoldWin;
     fold_load(A, sv, so, pos, last, tid);
     fold_window<V>(A, pos, min(kFoldWin, cnt - pos), S, round, sh, rp, rs, tid);
+    w = first + 1;
   }
   if (tid == 0) {
     store_state(r, S);
