@@ -187,7 +187,34 @@ def run_c3(args, torch, dev, repo, rank, K, base, gen):
         now, a, t, e = steps[j]
         repo.apply_mixed_device(n, kind, blob, offs, now, freq, per, cnt, a, t, e,
                                 status=status, remaining=rem)
-    return n, step
+
+    def cpu():
+        """The same stream through the Go-structured restatement (oracle,
+        orc_bench_mixed) on a bounded prefix, one thread: a mixed stream
+        with per-bucket order is applied in stream order (the reference
+        serialises each bucket under its mutex; one goroutine per request)."""
+        from oracle import oracle as O
+        L = O.lib()
+        orepo = O.Repo()
+        keys = torch.arange(base, base + K, dtype=torch.int64)
+        kb, ko = names_for_ids(torch, keys)
+        z = np.zeros(K, np.uint64)
+        L.orc_repo_seed(orepo.h, kb.numpy(), ko.numpy().astype(np.uint32), K, z, z,
+                        np.zeros(K, np.int64), np.full(K, T0, np.int64))
+        del kb, ko, keys
+        m = min(args.cpu_sample // 2, n)
+        sb, so = names_for_ids(torch, ids[:m].cpu() + base)
+        now, a, t, e = steps[args.warmup]
+        cols = [x[:m].cpu().numpy() for x in (kind, now, freq, per, cnt, a, t, e)]
+        st = np.zeros(m, np.uint8)
+        rm = np.zeros(m, np.uint64)
+        secs = L.orc_bench_mixed(orepo.h, cols[0], sb.numpy(), so.numpy().astype(np.uint32), m,
+                                 cols[1], cols[2], cols[3], cols[4].view(np.uint64),
+                                 cols[5].view(np.uint64), cols[6].view(np.uint64), cols[7], st, rm)
+        return dict(value=m / secs, unit="ops/s", cores=1, kind="port",
+                    sample=f"first {m} ops of the timed stream (Zipf {args.zipf} over {K} "
+                           f"buckets) through the Go-structured restatement, 1 thread")
+    return n, step, cpu
 
 
 def run_c4(args, torch, dev, repo, rank, world, K, gen):
@@ -313,8 +340,9 @@ def main():
 
     c5_check = None
     owned = K
+    c3_cpu = None
     if args.workload == "c3":
-        n, step = run_c3(args, torch, dev, repo, rank, K, base, gen)
+        n, step, c3_cpu = run_c3(args, torch, dev, repo, rank, K, base, gen)
         ids = None
     elif args.workload == "c4":
         n, step, owned = run_c4(args, torch, dev, repo, rank, world, K, gen)
@@ -423,6 +451,11 @@ def main():
         try:
             out["cpu_baseline"] = cpu_baseline(args, K, ids.cpu(), threads)
         except Exception as ex:  # the baseline must never hide the GPU result
+            out["cpu_baseline"] = {"error": repr(ex)}
+    elif rank == 0 and world == 1 and not args.no_cpu and c3_cpu is not None:
+        try:
+            out["cpu_baseline"] = c3_cpu()
+        except Exception as ex:
             out["cpu_baseline"] = {"error": repr(ex)}
     elif rank == 0:
         out["cpu_baseline"] = None
