@@ -54,6 +54,9 @@ def parse():
     p.add_argument("--workload", default="c2", choices=["c2", "c3", "c4", "c5"],
                    help="c2: batched Receive merges (headline); c3: mixed Take+Merge stream")
     p.add_argument("--ops", type=int, default=50_000_000, help="c3: ops per step")
+    p.add_argument("--wire", action="store_true",
+                   help="c2: feed raw datagrams (bucket.go:59-64 wire format) through "
+                        "phip_receive_datagrams instead of the decoded SoA")
     p.add_argument("--replicas", type=int, default=8, help="c5: simulated replicas per GPU")
     p.add_argument("--buckets", type=int, default=1 << 24, help="c5: buckets per replica")
     p.add_argument("--writes", type=float, default=0.01,
@@ -161,6 +164,27 @@ def pmc_traffic(workload):
     except (OSError, ValueError):
         pass
     return None
+
+
+def datagrams(torch, blob, offs, a, t, e):
+    """MarshalBinary (bucket.go:51-68) of every message, back to back:
+    added, taken, elapsed as big-endian 8-byte words, one length byte, the
+    name.  Returns (bytes uint8 with 8 bytes of slack, offs int64[n+1])."""
+    dev = blob.device
+    n = offs.numel() - 1
+    lens = (offs[1:] - offs[:-1]).to(torch.int64)
+    doffs = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    doffs[1:] = torch.cumsum(lens + 25, 0)
+    out = torch.zeros(int(doffs[-1]) + 8, dtype=torch.uint8, device=dev)
+    hdr = torch.stack([a, t, e], 1).contiguous().view(torch.uint8).view(n, 3, 8).flip(2)
+    pos = doffs[:-1].unsqueeze(1) + torch.arange(24, device=dev).unsqueeze(0)
+    out[pos.flatten()] = hdr.reshape(n, 24).flatten()
+    out[doffs[:-1] + 24] = lens.to(torch.uint8)
+    seg = torch.repeat_interleave(torch.arange(n, device=dev), lens)
+    within = torch.arange(int(lens.sum()), device=dev) - offs[:-1].to(torch.int64)[seg] + \
+        offs[0].to(torch.int64)
+    out[doffs[:-1][seg] + 25 + within] = blob[offs[:-1].to(torch.int64)[seg] + within]
+    return out, doffs
 
 
 def run_c3(args, torch, dev, repo, rank, K, base, gen):
@@ -356,9 +380,20 @@ def main():
         batches = [replica_states(torch, gen, n, j, dev) for j in range(args.warmup + args.steps)]
         torch.cuda.synchronize()
 
-        def step(j):
-            a, t, e = batches[j]
-            repo.receive_soa(blob, a, t, e, T0 + j, name_offs=offs, n=n, device=True)
+        if args.wire:
+            wires = []
+            for a, t, e in batches:
+                wires.append(datagrams(torch, blob, offs, a, t, e))
+            del batches
+            torch.cuda.synchronize()
+
+            def step(j):
+                db, do = wires[j]
+                repo.receive_datagrams_device(db, do, n, T0 + j)
+        else:
+            def step(j):
+                a, t, e = batches[j]
+                repo.receive_soa(blob, a, t, e, T0 + j, name_offs=offs, n=n, device=True)
 
     for j in range(args.warmup):
         step(j)
@@ -420,6 +455,8 @@ def main():
         dom_name, dom_ms = DOMINANT, float(np.mean(kern.get(DOMINANT, [float("nan")])))
         unit, metric = "merges/s", METRIC
         workload = f"C2 merge: {n} replica messages -> {K}-bucket table (2^{args.log2_slots} slots), Zipf({args.zipf})"
+        if args.wire:
+            workload += ", raw datagrams (decode + merge)"
     # c4: the merged count per rank varies (owners of hot buckets receive
     # more); the roofline uses this rank's kernel and its message share.
     achieved = bpo * n / (dom_ms / 1e3) / 1e9

@@ -181,7 +181,10 @@ int phip_dump(phip_handle* h, uint8_t* names, uint64_t names_cap, uint64_t* name
  * bucket.go:59-64): bytes[offs[i] .. offs[i+1]).  `now` is the clock reading
  * used for buckets created by this batch.  Stops at the first malformed
  * datagram like the Go loop (repo.go:72-73): *stop_index receives its index
- * (or n) and the call returns PHIP_ERR_SHORT_BUFFER when one was found. */
+ * (or n) and the call returns PHIP_ERR_SHORT_BUFFER when one was found.
+ * With PHIP_DEVICE_PTRS, `bytes` must be 8-byte aligned and readable up to
+ * the next 8-byte boundary past offs[n] (the fast path reads the datagrams
+ * in place as aligned words). */
 int phip_receive_datagrams(phip_handle* h, const uint8_t* bytes, const uint64_t* offs, uint32_t n,
                            int64_t now, const phip_results* res, uint32_t* stop_index,
                            uint32_t flags);

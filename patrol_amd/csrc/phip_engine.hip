@@ -322,34 +322,45 @@ inline unsigned fast_grid(phip_handle* h, u32 n) {
   return (unsigned)std::max<u64>(1, std::min<u64>(tiles, (u64)h->ncu * kFastPerCU));
 }
 
-// Counters on entry: ctr[0], ctr[1] = the batch's incast / -0.0 counts
-// (classification); every other counter 0.  *dirty is set (and nothing is
-// applied) when either count is non-zero.
-template <class Src>
-int fast_receive(phip_handle* h, Src src, const uint64_t* a, const uint64_t* t, const int64_t* e,
-                 u32 n, i64 now, u8* status, const HotHdr* hot, const HotEntry* hot_dir,
-                 bool* dirty) {
+// The fast kernel over a batch input (SoaIn or WireIn).  Counters on entry:
+// ctr[0], ctr[1] = the batch's incast / -0.0 counts (classification), ctr[5]
+// = first malformed datagram (~0: none); ctr[2], 8, 10, 11 = 0.  *dirty is
+// set (and nothing applied) when either count is non-zero; otherwise *nmiss
+// messages missed the table and are listed in B_MISS.
+template <class In>
+int fast_apply(phip_handle* h, In in, u32 n, u8* status, const HotHdr* hot,
+               const HotEntry* hot_dir, bool* dirty, u32* nmiss) {
   u32* miss;
   int rc;
   if ((rc = ensure(h, B_MISS, n, &miss))) return rc;
   {
     Launch l(h, "k_receive_fast");
-    k_receive_fast<Src><<<fast_grid(h, n), kFastBlock, 0, h->stream>>>(
-        src, a, t, e, n, table(h), status, miss, h->ctr, hot, hot_dir);
+    k_receive_fast<In><<<fast_grid(h, n), kFastBlock, 0, h->stream>>>(
+        in, n, table(h), status, miss, h->ctr, hot, hot_dir);
   }
   HIPCHK(h, hipGetLastError());
   if ((rc = read_ctr(h))) return rc;
   *dirty = h->ctr_host[0] || h->ctr_host[1];
+  *nmiss = 0;
   if (*dirty) return PHIP_OK;
   if ((rc = check_flags(h))) return rc;
-  u32 nmiss = h->ctr_host[2];
+  *nmiss = h->ctr_host[2];
   h->stats[0] = h->ctr_host[11];
   h->stats[1] = h->ctr_host[10];
-  h->stats[2] = nmiss;
+  h->stats[2] = *nmiss;
+  return PHIP_OK;
+}
+
+// The messages fast_apply missed: create their buckets, merge them with
+// creator tracking (PHIP_ST_CREATED on the first message of a new bucket).
+template <class Src>
+int finish_misses(phip_handle* h, Src src, const uint64_t* a, const uint64_t* t, const int64_t* e,
+                  u32 nmiss, i64 now, u8* status) {
   if (nmiss == 0) return PHIP_OK;
+  u32* miss = (u32*)h->buf[B_MISS].p;
+  int rc;
   u32 n_claimed = 0;
   if ((rc = insert_names(h, src, miss, nmiss, nullptr, now, &n_claimed))) return rc;
-  // Merge the missed messages into their (now existing) buckets.
   HIPCHK(h, hipMemsetAsync(h->ctr + 2, 0, sizeof(u32), h->stream));
   u32* miss2;
   if ((rc = ensure(h, B_MISS2, nmiss, &miss2))) return rc;
@@ -368,6 +379,25 @@ int fast_receive(phip_handle* h, Src src, const uint64_t* a, const uint64_t* t, 
   if ((rc = read_ctr(h))) return rc;
   if (h->ctr_host[2]) return set_err(h, PHIP_ERR_INVALID, "internal: %u names missing after insert", h->ctr_host[2]);
   return clear_new(h, n_claimed);
+}
+
+// Start the hot directory of a fast batch on stream2 (joined by join_hot).
+template <class Src>
+int fork_hot(phip_handle* h, Src src, u32 n, const HotHdr** hot, const HotEntry** hot_dir) {
+  *hot = nullptr;
+  *hot_dir = nullptr;
+  if (n < kHotMinBatch) return PHIP_OK;
+  HIPCHK(h, hipEventRecord(h->ev_fork, h->stream));
+  HIPCHK(h, hipStreamWaitEvent(h->stream2, h->ev_fork, 0));
+  int rc;
+  if ((rc = build_hot(h, src, n, h->stream2, hot, hot_dir))) return rc;
+  HIPCHK(h, hipEventRecord(h->ev_join, h->stream2));
+  return PHIP_OK;
+}
+
+int join_hot(phip_handle* h, const HotHdr* hot) {
+  if (hot) HIPCHK(h, hipStreamWaitEvent(h->stream, h->ev_join, 0));
+  return PHIP_OK;
 }
 
 // ------------------------------------------------------------ ordered ----
@@ -590,28 +620,24 @@ int receive_decoded(phip_handle* h, Src src, const uint64_t* a, const uint64_t* 
   int rc;
   // The hot directory (read-only on the table and the batch) is built on
   // stream2 while the classification streams the replica fields.
-  const HotHdr* hot = nullptr;
-  const HotEntry* hot_dir = nullptr;
-  const bool with_hot = n >= kHotMinBatch;
-  if (with_hot) {
-    HIPCHK(h, hipEventRecord(h->ev_fork, h->stream));
-    HIPCHK(h, hipStreamWaitEvent(h->stream2, h->ev_fork, 0));
-    if ((rc = build_hot(h, src, n, h->stream2, &hot, &hot_dir))) return rc;
-    HIPCHK(h, hipEventRecord(h->ev_join, h->stream2));
-  }
+  const HotHdr* hot;
+  const HotEntry* hot_dir;
+  if ((rc = fork_hot(h, src, n, &hot, &hot_dir))) return rc;
   if (!classified) {
     if ((rc = reset_ctr(h))) return rc;
     Launch l(h, "k_classify");
     k_classify<<<grid_for(n), kBlock, 0, h->stream>>>(a, t, e, n, h->ctr);
     HIPCHK(h, hipGetLastError());
   }
-  if (with_hot) HIPCHK(h, hipStreamWaitEvent(h->stream, h->ev_join, 0));
+  if ((rc = join_hot(h, hot))) return rc;
   // The fast path is enqueued behind the classification without a host
   // round trip; k_receive_fast itself does nothing when the counters show an
   // incast or a -0.0 field, and the batch then takes the ordered path.
   bool dirty = false;
-  if ((rc = fast_receive(h, src, a, t, e, n, now, ow.status, hot, hot_dir, &dirty))) return rc;
-  if (!dirty) return PHIP_OK;
+  u32 nmiss = 0;
+  if ((rc = fast_apply(h, SoaIn<Src>{src, a, t, e}, n, ow.status, hot, hot_dir, &dirty, &nmiss)))
+    return rc;
+  if (!dirty) return finish_misses(h, src, a, t, e, nmiss, now, ow.status);
   OpView ov{};
   ov.kind = nullptr; ov.kind0 = PHIP_OP_RECEIVE;
   ov.now = nullptr; ov.now0 = now;
@@ -862,29 +888,54 @@ int phip_receive_datagrams(phip_handle* h, const uint8_t* bytes, const uint64_t*
   if ((rc = stage(h, B_DOFFS, offs, (size_t)n + 1, dev, &d_offs))) return rc;
   size_t nb = dev ? 0 : offs[n];
   if ((rc = stage(h, B_BYTES, bytes, nb, dev, &d_bytes))) return rc;
-  uint64_t *a, *t, *no;
-  int64_t* e;
-  u8* nl;
-  if ((rc = ensure(h, B_DA, n, &a)) || (rc = ensure(h, B_DT, n, &t)) || (rc = ensure(h, B_DE, n, &e)) ||
-      (rc = ensure(h, B_NOFF, n, &no)) || (rc = ensure(h, B_NLEN, n, &nl)))
-    return rc;
   OutView ow{};
   if ((rc = outputs(h, res, n, dev, &ow))) return rc;
+  // Fast path straight from the wire bytes: classify the headers (and find
+  // the first malformed datagram), then k_receive_fast reads every datagram
+  // in place; no decoded copy is written.  A dirty batch (incast / -0.0) or
+  // one with new buckets is decoded to the SoA form afterwards, before
+  // anything of it is applied by the paths that need it.
   if ((rc = reset_ctr(h))) return rc;
+  const HotHdr* hot;
+  const HotEntry* hot_dir;
+  if ((rc = fork_hot(h, Datagrams{d_bytes, d_offs}, n, &hot, &hot_dir))) return rc;
   {
-    Launch l(h, "k_decode");
-    k_decode<<<grid_for(n), kBlock, 0, h->stream>>>(d_bytes, d_offs, n, a, t, e, no, nl, h->ctr);
+    Launch l(h, "k_classify_wire");
+    k_classify_wire<<<grid_for(n), kBlock, 0, h->stream>>>(d_bytes, d_offs, n, h->ctr);
     HIPCHK(h, hipGetLastError());
   }
-  if ((rc = read_ctr(h))) return rc;
-  u32 stop = std::min<u32>(h->ctr_host[5], n);
+  if ((rc = join_hot(h, hot))) return rc;
+  bool dirty = false;
+  u32 nmiss = 0;
+  if ((rc = fast_apply(h, WireIn{d_bytes, d_offs}, n, ow.status, hot, hot_dir, &dirty, &nmiss)))
+    return rc;
+  const u32 stop = std::min<u32>(h->ctr_host[5], n);
   // Statuses of the short datagram and everything after it (the Go loop exits).
   if (ow.status && stop < n) {
     HIPCHK(h, hipMemsetAsync(ow.status + stop, PHIP_ST_NOT_PROCESSED, n - stop, h->stream));
     HIPCHK(h, hipMemsetAsync(ow.status + stop, PHIP_ST_SHORT, 1, h->stream));
   }
-  NamesPairs src{d_bytes, no, nl};
-  if (stop > 0 && (rc = receive_decoded(h, src, a, t, e, stop, now, ow, true))) return rc;
+  if (stop > 0 && (dirty || nmiss)) {
+    uint64_t *a, *t, *no;
+    int64_t* e;
+    u8* nl;
+    if ((rc = ensure(h, B_DA, n, &a)) || (rc = ensure(h, B_DT, n, &t)) ||
+        (rc = ensure(h, B_DE, n, &e)) || (rc = ensure(h, B_NOFF, n, &no)) ||
+        (rc = ensure(h, B_NLEN, n, &nl)))
+      return rc;
+    if ((rc = reset_ctr(h))) return rc;
+    {
+      Launch l(h, "k_decode");
+      k_decode<<<grid_for(n), kBlock, 0, h->stream>>>(d_bytes, d_offs, n, a, t, e, no, nl, h->ctr);
+      HIPCHK(h, hipGetLastError());
+    }
+    NamesPairs src{d_bytes, no, nl};
+    if (dirty) {
+      if ((rc = receive_decoded(h, src, a, t, e, stop, now, ow, true))) return rc;
+    } else {
+      if ((rc = finish_misses(h, src, a, t, e, nmiss, now, ow.status))) return rc;
+    }
+  }
   if ((rc = copy_outputs(h, res, n, dev, ow))) return rc;
   if (dev) HIPCHK(h, hipStreamSynchronize(h->stream));
   if (stop_index) *stop_index = stop;

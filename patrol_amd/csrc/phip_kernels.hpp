@@ -19,6 +19,13 @@ __device__ inline T ld(const T* p) {
   else return *p;
 }
 
+__device__ inline u64 load_be64(const u8* p) {
+  u64 v = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) v = (v << 8) | p[k];
+  return v;
+}
+
 // ---------------------------------------------------------- name sources --
 // Decoded messages: names[offs[i] .. offs[i+1]).
 struct NamesOffs {
@@ -40,6 +47,22 @@ struct NamesPairs {
   __device__ inline void get(u32 i, u64& o, u32& l) const {
     o = ld<NT>(off + i);
     l = ld<NT>(len + i);
+  }
+};
+
+// Raw datagrams (bucket.go:59-64) read in place: name at offs[i] + 25, its
+// length byte at offs[i] + 24, clamped to the datagram so that a malformed
+// one never sends a name read past its end.
+struct Datagrams {
+  const u8* blob;
+  const uint64_t* offs;
+  template <bool NT = false>
+  __device__ inline void get(u32 i, u64& o, u32& l) const {
+    const u64 a = ld<NT>(offs + i), b = ld<NT>(offs + i + 1);
+    o = a + 25;
+    const u64 room = b > o ? b - o : 0;
+    const u32 want = b >= a + 25 ? blob[a + 24] : 0;
+    l = want < room ? want : (u32)room;
   }
 };
 
@@ -421,12 +444,102 @@ __global__ void k_hot_build(const u32* __restrict__ ckeys, const u32* __restrict
 constexpr u32 kFastBlock = PHIP_FAST_BLOCK;
 constexpr u32 kFastPerCU = PHIP_FAST_PER_CU;   // resident workgroups per CU (LDS-bound)
 
+// Batch inputs of the fast kernel.  load() issues a message's loads in two
+// dependent rounds (offsets, then everything they address) and returns the
+// name's offset/length, the three words that can hold a short name, and the
+// replica fields as Go's UnmarshalBinary would hand them over.
 template <class Src>
+struct SoaIn {   // decoded messages (phip_receive_soa / decoded datagrams)
+  Src src;
+  const uint64_t* ma;
+  const uint64_t* mt;
+  const int64_t* me;
+  __device__ inline const u8* blob() const { return src.blob; }
+  __device__ inline void load(u32 i, u64& off, u32& len, u64& w0, u64& w1, u64& w2, u64& ra,
+                              u64& rt, i64& re) const {
+    src.template get<true>(i, off, len);
+    ra = ld<true>(ma + i); rt = ld<true>(mt + i); re = ld<true>(me + i);
+    load_words3<false>(src.blob, off, len, w0, w1, w2);
+  }
+};
+
+// Raw datagrams (bucket.go:59-64): bytes[offs[i] .. offs[i+1]) = added,
+// taken, elapsed (big-endian 8-byte words), one length byte, the name.  Read
+// in place: the header as four aligned words and the name as three, every
+// address clamped into the datagram, all issued in the second round (the
+// name words are placed from the datagram's end, not its length byte).  Only
+// datagrams before the first malformed one are merged (k_classify_wire).
+__device__ inline u64 funnel8(u64 lo, u64 hi, u32 sb) {   // bytes sb..sb+7 of hi:lo, sb < 8
+  return sb ? (lo >> (8 * sb)) | (hi << (64 - 8 * sb)) : lo;
+}
+struct WireIn {
+  const u8* bytes;
+  const uint64_t* offs;
+  __device__ inline const u8* blob() const { return bytes; }
+  __device__ inline void load(u32 i, u64& off, u32& len, u64& w0, u64& w1, u64& w2, u64& ra,
+                              u64& rt, i64& re) const {
+    const u64 o = ld<true>(offs + i), end = ld<true>(offs + i + 1);
+    const u64* p = reinterpret_cast<const u64*>(bytes);
+    const u64 last = (end > o ? end - 1 : o) >> 3;   // word of the datagram's last byte
+    const u64 hb = o >> 3;
+    // Plain (L1-allocating) loads: the seven words of a lane and its
+    // neighbours' share cache lines, so only the first touch of a line goes
+    // to L2.
+    u64 h[4];
+#pragma unroll
+    for (u32 k = 0; k < 4; ++k) h[k] = ld<false>(p + (hb + k < last ? hb + k : last));
+    off = o + 25;
+    const u64 nb = off >> 3;
+    const u64 nb0 = nb < last ? nb : last, nb1 = nb + 1 < last ? nb + 1 : last;
+    const u64 nb2 = nb + 2 < last ? nb + 2 : last;
+    w0 = ld<false>(p + nb0); w1 = ld<false>(p + nb1); w2 = ld<false>(p + nb2);
+    const u32 sb = (u32)(o & 7);
+    ra = __builtin_bswap64(funnel8(h[0], h[1], sb));
+    rt = __builtin_bswap64(funnel8(h[1], h[2], sb));
+    re = (i64)__builtin_bswap64(funnel8(h[2], h[3], sb));
+    len = (u32)(h[3] >> (8 * sb)) & 0xFFu;
+  }
+};
+
+// Wire classification (replaces k_decode on the fast path): first malformed
+// datagram (io.ErrShortBuffer, bucket.go:72,84) into ctr[5], incast and -0.0
+// counts into ctr[0], ctr[1] as k_classify does.  Reads the headers only.
+__global__ __launch_bounds__(kBlock) void k_classify_wire(const u8* __restrict__ bytes,
+                                                          const uint64_t* __restrict__ offs, u32 n,
+                                                          u32* ctr) {
+  const u32 i = blockIdx.x * kBlock + threadIdx.x;
+  bool inc = false, nz = false;
+  if (i < n) {
+    const u64 o = offs[i], end = offs[i + 1], sz = end - o;
+    // the header as four aligned words clamped into the datagram
+    const u64* p = reinterpret_cast<const u64*>(bytes);
+    const u64 last = (end > o ? end - 1 : o) >> 3, hb = o >> 3;
+    u64 h[4];
+#pragma unroll
+    for (u32 k = 0; k < 4; ++k) h[k] = p[hb + k < last ? hb + k : last];
+    const u32 sb = (u32)(o & 7);
+    const u32 len = (u32)(h[3] >> (8 * sb)) & 0xFFu;
+    if (sz < PHIP_BUCKET_FIXED_SIZE || sz - PHIP_BUCKET_FIXED_SIZE < len) {
+      atomicMin(&ctr[5], i);
+    } else {
+      const u64 ab = __builtin_bswap64(funnel8(h[0], h[1], sb));
+      const u64 tb = __builtin_bswap64(funnel8(h[1], h[2], sb));
+      if (is_zero_bits(ab) && is_zero_bits(tb))
+        inc = __builtin_bswap64(funnel8(h[2], h[3], sb)) == 0;
+      nz = !inc && (ab == kSign || tb == kSign);
+    }
+  }
+  const u64 mi = __ballot(inc), mn = __ballot(nz);
+  if (__lane_id() == 0) {
+    if (mi) atomicAdd(&ctr[0], (u32)__popcll(mi));
+    if (mn) atomicAdd(&ctr[1], (u32)__popcll(mn));
+  }
+}
+
+template <class In>
 __global__ __launch_bounds__(kFastBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_receive_fast(
-    Src src, const uint64_t* __restrict__ ma, const uint64_t* __restrict__ mt,
-    const int64_t* __restrict__ me, u32 n, Table T,
-    u8* __restrict__ status, u32* miss, u32* ctr, const HotHdr* __restrict__ hot,
-    const HotEntry* __restrict__ hot_dir) {
+    In in, u32 n, Table T, u8* __restrict__ status, u32* miss, u32* ctr,
+    const HotHdr* __restrict__ hot, const HotEntry* __restrict__ hot_dir) {
   __shared__ u32 hslot[kHotLds];        // directory index + 1 (0 = empty)
   __shared__ u64 htag[kHotMax], hw0[kHotMax], hw1[kHotMax];
   __shared__ u32 hrec[kHotMax];
@@ -436,6 +549,7 @@ __global__ __launch_bounds__(kFastBlock) __attribute__((amdgpu_waves_per_eu(8, 8
   // Classification gate: an incast or -0.0 in the batch (ctr[0], ctr[1])
   // sends it to the ordered path; then nothing here may touch the table.
   if (ctr[0] | ctr[1]) return;
+  n = min(n, ctr[5]);   // the first malformed datagram ends the batch (none: ~0)
   const u32 nh = hot ? min(hot->n, kHotMax) : 0u;
   for (u32 j = threadIdx.x; j < kHotLds; j += kFastBlock) hslot[j] = 0;
   for (u32 j = threadIdx.x; j < kHotMax; j += kFastBlock) {
@@ -460,14 +574,11 @@ __global__ __launch_bounds__(kFastBlock) __attribute__((amdgpu_waves_per_eu(8, 8
     const u32 tid = chunk * 64 + lane;
     const bool valid = tid < n;
     const u32 i = valid ? tid : n - 1;
-    // round 1: name offsets and the replica fields
-    u64 off; u32 len;
-    src.template get<true>(i, off, len);
-    const u64 ra = ld<true>(ma + i), rt = ld<true>(mt + i);
-    const i64 re = ld<true>(me + i);
-    // round 2: the name
-    u64 w0, w1, w2;
-    load_words3<false>(src.blob, off, len, w0, w1, w2);
+    // rounds 1-2: offsets, then the name words and replica fields
+    u64 off, w0, w1, w2, ra, rt;
+    u32 len;
+    i64 re;
+    in.load(i, off, len, w0, w1, w2, ra, rt, re);
     Name nm;
     short_name(w0, w1, w2, off, len, nm);
     const bool shortname = len <= kShortName;
@@ -504,8 +615,8 @@ __global__ __launch_bounds__(kFastBlock) __attribute__((amdgpu_waves_per_eu(8, 8
           if (shortname && cur.tag == 0) {
             pr = kMiss;
           } else {
-            if (!shortname) load_name_wide<true>(src.blob, off, len, nm);
-            pr = probe(T, nm, src.blob, &s, &cur);
+            if (!shortname) load_name_wide<true>(in.blob(), off, len, nm);
+            pr = probe(T, nm, in.blob(), &s, &cur);
           }
         }
         if (pr == kFound) {
@@ -717,12 +828,6 @@ __global__ void k_clear_new(const u32* __restrict__ claimed_slot, u32 n, Table T
 // fields, name length byte, io.ErrShortBuffer when < 25 bytes or the name is
 // truncated; trailing bytes are ignored.  The first short datagram index is
 // min-reduced into ctr[5] (the Go loop stops there, repo.go:72-73).
-__device__ inline u64 load_be64(const u8* p) {
-  u64 v = 0;
-#pragma unroll
-  for (int k = 0; k < 8; ++k) v = (v << 8) | p[k];
-  return v;
-}
 
 __global__ void k_decode(const u8* __restrict__ bytes, const uint64_t* __restrict__ offs, u32 n,
                          uint64_t* __restrict__ a, uint64_t* __restrict__ t,

@@ -224,6 +224,18 @@ class GPURepo:
                     allow=(-5,))
         return dict(status=status[:n], reply=reply[:n], stop=stop.value)
 
+    def receive_datagrams_device(self, data, offs, n: int, now: int, status=None):
+        """phip_receive_datagrams with device pointers: data (uint8 CUDA tensor
+        of back-to-back datagrams, 8 bytes of slack), offs (int64[n+1]).
+        Returns the index of the first malformed datagram (n if none)."""
+        res = phip_results(_ptr(status), None, None, None)
+        stop = C.c_uint32(0)
+        rc = self.L.phip_receive_datagrams(self.h, _ptr(data), _ptr(offs), n, int(now),
+                                           C.byref(res), C.byref(stop), DEVICE_PTRS)
+        if rc not in (0, -5):
+            self._check(rc)
+        return stop.value
+
     def receive_soa(self, names, added, taken, elapsed, now: int, name_offs=None, n=None,
                     status=None, device=False):
         """Receive over decoded states.  With device=True every array is a torch

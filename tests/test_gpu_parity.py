@@ -495,3 +495,29 @@ def test_merge_laws_at_scale(pa):
     d2 = gpu_dump(g2)
     # created differs only by the clock each batch saw; compare replicated fields
     assert {k: v[:3] for k, v in d1.items()} == {k: v[:3] for k, v in d2.items()}
+
+
+@pytest.mark.parametrize("n,short_at", [(60000, None), (60000, 41234), (1 << 21, None),
+                                        (1 << 21, 1500000)])
+def test_datagram_fast_path_vs_oracle(pa, n, short_at):
+    """Wire datagrams on the fast path (k_classify_wire + k_receive_fast
+    reading the datagrams in place; the hot directory from 2^20 messages):
+    NaN / +-Inf / negatives, new buckets, 15-22 byte and arena names, and a
+    malformed datagram that ends the batch (io.ErrShortBuffer)."""
+    import struct
+    rng = np.random.default_rng(n + (short_at or 0))
+    K = 20000
+    g, o = _seed_both(pa, rng, K, log2_slots=16)
+    ids = _gen.zipf_ids(rng, n, K + 2000)
+    names = [(b"a-much-longer-bucket-name-%d" % i) if i % 97 == 0 else
+             (b"medium-name-%d" % i) if i % 89 == 0 else (b"b%d" % i) for i in ids]
+    a, t, e = _fast_dirty_states(rng, n)
+    dgs = [struct.pack(">QQQ", int(a[i]), int(t[i]), int(e[i]) & (2**64 - 1)) +
+           bytes([len(names[i])]) + names[i] for i in range(n)]
+    if short_at is not None:
+        dgs[short_at] = dgs[short_at][:25 + len(names[short_at]) - 1]   # length byte lies
+    out = g.receive_datagrams(dgs, _gen.T0 + 3 * SEC)
+    st, _, _, _, stop = o.receive(dgs, _gen.T0 + 3 * SEC)
+    assert out["stop"] == stop == (n if short_at is None else short_at)
+    assert np.array_equal(out["status"], st)
+    assert_same_dump(gpu_dump(g), o.dump())
