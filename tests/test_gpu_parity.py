@@ -521,3 +521,30 @@ def test_datagram_fast_path_vs_oracle(pa, n, short_at):
     assert out["stop"] == stop == (n if short_at is None else short_at)
     assert np.array_equal(out["status"], st)
     assert_same_dump(gpu_dump(g), o.dump())
+
+
+@pytest.mark.parametrize("dirty", [False, True])
+def test_mixed_large_batch_vs_oracle(pa, dirty):
+    """Ordered batches at 2^21 ops over a Zipf key set, so the hottest
+    buckets take the huge-segment path (gathered runs, windowed block folds
+    with quiet-window skipping): C3 shape, plus a dirty variant with every op
+    kind (Take at several rates, Receive of dirty states with incast replies,
+    Upsert) and new buckets."""
+    rng = np.random.default_rng(2024 + dirty)
+    n, K = 1 << 21, 40000
+    ids = _gen.zipf_ids(rng, n, K + 5000)
+    names = _gen.key_names(ids)
+    now = _gen.T0 + np.arange(n, dtype=np.int64) * 20
+    if not dirty:
+        kind = (rng.random(n) < 0.5).astype(np.uint8)
+        freq = np.full(n, 100, np.int64)
+        per = np.full(n, SEC, np.int64)
+        cnt = np.ones(n, np.uint64)
+        a, t, e = _gen.clean_states(rng, n)
+    else:
+        kind = rng.choice(np.array([0, 1, 2], np.uint8), n, p=[0.5, 0.45, 0.05])
+        freq = rng.choice(np.array([1, 3, 100, 1000], np.int64), n)
+        per = rng.choice(np.array([MS, SEC, 7 * SEC], np.int64), n)
+        cnt = rng.integers(1, 4, n).astype(np.uint64)
+        a, t, e = _gen.dirty_states(rng, n, 0.02)
+    _check_mixed(pa, [kind, names, now, freq, per, cnt, a, t, e], 17, reply=dirty)
