@@ -160,7 +160,7 @@ def pmc_traffic(workload):
         with open(path) as f:
             d = json.load(f)
         if d.get("kernel") == DOMINANT and d.get("workload") == workload:
-            return d.get("hbm_bytes_per_launch")
+            return d.get("hbm_bytes_per_step")
     except (OSError, ValueError):
         pass
     return None
@@ -403,9 +403,14 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    launches = {}
     for j in range(args.warmup, args.warmup + args.steps):
         tl = step(j)
+        per = {}   # a kernel launched several times in a step (chunks): summed
         for name, ms in (tl if tl is not None else repo.timings()):
+            per[name] = per.get(name, 0.0) + ms
+            launches[name] = launches.get(name, 0) + 1
+        for name, ms in per.items():
             kern.setdefault(name, []).append(ms)
     torch.cuda.synchronize()
     if world > 1:
@@ -478,8 +483,9 @@ def main():
                    "slots_per_gpu": 1 << args.log2_slots, "parallelism": f"shard{world}"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": dom_name, "kernel_ms": dom_ms,
-                     "algorithmic_bytes_per_launch": bpo * n},
+                     "kernel": dom_name, "kernel_ms_per_step": dom_ms,
+                     "launches_per_step": launches.get(dom_name, args.steps) / args.steps,
+                     "algorithmic_bytes_per_step": bpo * n},
         "kernels_ms": kms,
     }
     out["config"].update(extra)

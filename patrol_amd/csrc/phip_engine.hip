@@ -165,8 +165,10 @@ int read_ctr(phip_handle* h) {
 
 int reset_ctr(phip_handle* h) {
   HIPCHK(h, hipMemsetAsync(h->ctr, 0, 16 * sizeof(u32), h->stream));
-  // ctr[5] = first short datagram index: start at "none".
+  // ctr[5] = first short datagram, ctr[kCtrDirty] = first dirty message
+  // (phip_kernels.hpp): both start at "none".
   HIPCHK(h, hipMemsetAsync(h->ctr + 5, 0xFF, sizeof(u32), h->stream));
+  HIPCHK(h, hipMemsetAsync(h->ctr + kCtrDirty, 0xFF, sizeof(u32), h->stream));
   return PHIP_OK;
 }
 
@@ -322,17 +324,27 @@ inline unsigned fast_grid(phip_handle* h, u32 n) {
   return (unsigned)std::max<u64>(1, std::min<u64>(tiles, (u64)h->ncu * kFastPerCU));
 }
 
-// The fast kernel over a batch input (SoaIn or WireIn).  Counters on entry:
-// ctr[0], ctr[1] = the batch's incast / -0.0 counts (classification), ctr[5]
-// = first malformed datagram (~0: none); ctr[2], 8, 10, 11 = 0.  *dirty is
-// set (and nothing applied) when either count is non-zero; otherwise *nmiss
-// messages missed the table and are listed in B_MISS.
+int join_hot(phip_handle* h, const HotHdr* hot);
+
+// The fast path over a batch input (SoaIn or WireIn), with the counters reset
+// (reset_ctr) and the hot directory forked (fork_hot).  Applies the batch's
+// clean prefix: the messages before the first dirty one (*first_dirty; n if
+// none) and before the first malformed datagram (ctr[5]).  The prefix's
+// misses (*nmiss of them) are listed in B_MISS.
 template <class In>
 int fast_apply(phip_handle* h, In in, u32 n, u8* status, const HotHdr* hot,
-               const HotEntry* hot_dir, bool* dirty, u32* nmiss) {
+               const HotEntry* hot_dir, u32* first_dirty, u32* nmiss) {
   u32* miss;
   int rc;
   if ((rc = ensure(h, B_MISS, n, &miss))) return rc;
+  {
+    Launch l(h, "k_classify");
+    k_classify<In><<<grid_for(n), kBlock, 0, h->stream>>>(in, n, h->ctr);
+  }
+  HIPCHK(h, hipGetLastError());
+  // The fast kernel is enqueued behind the classification without a host
+  // round trip; it reads the counters itself.
+  if ((rc = join_hot(h, hot))) return rc;
   {
     Launch l(h, "k_receive_fast");
     k_receive_fast<In><<<fast_grid(h, n), kFastBlock, 0, h->stream>>>(
@@ -340,10 +352,8 @@ int fast_apply(phip_handle* h, In in, u32 n, u8* status, const HotHdr* hot,
   }
   HIPCHK(h, hipGetLastError());
   if ((rc = read_ctr(h))) return rc;
-  *dirty = h->ctr_host[0] || h->ctr_host[1];
-  *nmiss = 0;
-  if (*dirty) return PHIP_OK;
   if ((rc = check_flags(h))) return rc;
+  *first_dirty = std::min<u32>(h->ctr_host[kCtrDirty], n);
   *nmiss = h->ctr_host[2];
   h->stats[0] = h->ctr_host[11];
   h->stats[1] = h->ctr_host[10];
@@ -612,37 +622,58 @@ int copy_outputs(phip_handle* h, const phip_results* res, u32 n, bool dev, const
   return PHIP_OK;
 }
 
-// Receive-mode batch (decoded): fast path unless it holds an incast or -0.0.
+// A batch from message k on.
+inline NamesOffs shifted(NamesOffs s, u32 k) {
+  s.offs += k;
+  return s;
+}
+inline NamesPairs shifted(NamesPairs s, u32 k) {
+  s.off += k;
+  s.len += k;
+  return s;
+}
+inline OutView shifted(OutView o, u32 k) {
+  if (o.status) o.status += k;
+  if (o.remaining) o.remaining += k;
+  if (o.have) o.have += k;
+  if (o.reply) o.reply += k;
+  return o;
+}
+
+// After the fast path: the clean prefix's new buckets (finish_misses), then
+// the ordered path over messages [first_dirty, stop), which starts from the
+// state the prefix left (the Go loop's state at that message).
 template <class Src>
-int receive_decoded(phip_handle* h, Src src, const uint64_t* a, const uint64_t* t,
-                    const int64_t* e, u32 n,
-                    i64 now, const OutView& ow, bool classified) {
+int finish_receive(phip_handle* h, Src src, const uint64_t* a, const uint64_t* t,
+                   const int64_t* e, u32 stop, u32 first_dirty, u32 nmiss, i64 now,
+                   const OutView& ow) {
   int rc;
-  // The hot directory (read-only on the table and the batch) is built on
-  // stream2 while the classification streams the replica fields.
-  const HotHdr* hot;
-  const HotEntry* hot_dir;
-  if ((rc = fork_hot(h, src, n, &hot, &hot_dir))) return rc;
-  if (!classified) {
-    if ((rc = reset_ctr(h))) return rc;
-    Launch l(h, "k_classify");
-    k_classify<<<grid_for(n), kBlock, 0, h->stream>>>(a, t, e, n, h->ctr);
-    HIPCHK(h, hipGetLastError());
-  }
-  if ((rc = join_hot(h, hot))) return rc;
-  // The fast path is enqueued behind the classification without a host
-  // round trip; k_receive_fast itself does nothing when the counters show an
-  // incast or a -0.0 field, and the batch then takes the ordered path.
-  bool dirty = false;
-  u32 nmiss = 0;
-  if ((rc = fast_apply(h, SoaIn<Src>{src, a, t, e}, n, ow.status, hot, hot_dir, &dirty, &nmiss)))
-    return rc;
-  if (!dirty) return finish_misses(h, src, a, t, e, nmiss, now, ow.status);
+  if ((rc = finish_misses(h, src, a, t, e, nmiss, now, ow.status))) return rc;
+  if (first_dirty >= stop) return PHIP_OK;
+  const u32 k = first_dirty;
   OpView ov{};
   ov.kind = nullptr; ov.kind0 = PHIP_OP_RECEIVE;
   ov.now = nullptr; ov.now0 = now;
-  ov.a = a; ov.t = t; ov.e = e;
-  return ordered(h, src, n, ov, ow);
+  ov.a = a + k; ov.t = t + k; ov.e = e + k;
+  return ordered(h, shifted(src, k), stop - k, ov, shifted(ow, k));
+}
+
+// Receive-mode batch (decoded): the fast path over its clean prefix, the
+// ordered path from its first incast or -0.0 on.
+template <class Src>
+int receive_decoded(phip_handle* h, Src src, const uint64_t* a, const uint64_t* t,
+                    const int64_t* e, u32 n, i64 now, const OutView& ow) {
+  int rc;
+  if ((rc = reset_ctr(h))) return rc;
+  // The hot directory (read-only on the table and the batch) is built on
+  // stream2 while the batch is classified.
+  const HotHdr* hot;
+  const HotEntry* hot_dir;
+  if ((rc = fork_hot(h, src, n, &hot, &hot_dir))) return rc;
+  u32 fd = n, nmiss = 0;
+  if ((rc = fast_apply(h, SoaIn<Src>{src, a, t, e}, n, ow.status, hot, hot_dir, &fd, &nmiss)))
+    return rc;
+  return finish_receive(h, src, a, t, e, n, fd, nmiss, now, ow);
 }
 
 }  // namespace
@@ -869,7 +900,7 @@ int phip_receive_soa(phip_handle* h, const phip_msgs* m, int64_t now, const phip
       (rc = stage(h, B_A, m->added, n, dev, &a)) || (rc = stage(h, B_T, m->taken, n, dev, &t)) ||
       (rc = stage(h, B_E, m->elapsed, n, dev, &e)) || (rc = outputs(h, res, n, dev, &ow)))
     return rc;
-  if ((rc = receive_decoded(h, src, a, t, e, n, now, ow, false))) return rc;
+  if ((rc = receive_decoded(h, src, a, t, e, n, now, ow))) return rc;
   return copy_outputs(h, res, n, dev, ow);
 }
 
@@ -890,24 +921,17 @@ int phip_receive_datagrams(phip_handle* h, const uint8_t* bytes, const uint64_t*
   if ((rc = stage(h, B_BYTES, bytes, nb, dev, &d_bytes))) return rc;
   OutView ow{};
   if ((rc = outputs(h, res, n, dev, &ow))) return rc;
-  // Fast path straight from the wire bytes: classify the headers (and find
-  // the first malformed datagram), then k_receive_fast reads every datagram
-  // in place; no decoded copy is written.  A dirty batch (incast / -0.0) or
-  // one with new buckets is decoded to the SoA form afterwards, before
-  // anything of it is applied by the paths that need it.
+  // Fast path straight from the wire bytes: k_classify reads the headers
+  // (and finds the first malformed datagram), k_receive_fast reads every
+  // datagram in place; no decoded copy is written.
+  // Only a clean prefix with new buckets, or an incast / -0.0, has the
+  // datagrams decoded to the SoA form, for the paths that need it.
   if ((rc = reset_ctr(h))) return rc;
   const HotHdr* hot;
   const HotEntry* hot_dir;
   if ((rc = fork_hot(h, Datagrams{d_bytes, d_offs}, n, &hot, &hot_dir))) return rc;
-  {
-    Launch l(h, "k_classify_wire");
-    k_classify_wire<<<grid_for(n), kBlock, 0, h->stream>>>(d_bytes, d_offs, n, h->ctr);
-    HIPCHK(h, hipGetLastError());
-  }
-  if ((rc = join_hot(h, hot))) return rc;
-  bool dirty = false;
-  u32 nmiss = 0;
-  if ((rc = fast_apply(h, WireIn{d_bytes, d_offs}, n, ow.status, hot, hot_dir, &dirty, &nmiss)))
+  u32 fd = n, nmiss = 0;
+  if ((rc = fast_apply(h, WireIn{d_bytes, d_offs}, n, ow.status, hot, hot_dir, &fd, &nmiss)))
     return rc;
   const u32 stop = std::min<u32>(h->ctr_host[5], n);
   // Statuses of the short datagram and everything after it (the Go loop exits).
@@ -915,7 +939,7 @@ int phip_receive_datagrams(phip_handle* h, const uint8_t* bytes, const uint64_t*
     HIPCHK(h, hipMemsetAsync(ow.status + stop, PHIP_ST_NOT_PROCESSED, n - stop, h->stream));
     HIPCHK(h, hipMemsetAsync(ow.status + stop, PHIP_ST_SHORT, 1, h->stream));
   }
-  if (stop > 0 && (dirty || nmiss)) {
+  if (fd < stop || nmiss) {
     uint64_t *a, *t, *no;
     int64_t* e;
     u8* nl;
@@ -923,18 +947,14 @@ int phip_receive_datagrams(phip_handle* h, const uint8_t* bytes, const uint64_t*
         (rc = ensure(h, B_DE, n, &e)) || (rc = ensure(h, B_NOFF, n, &no)) ||
         (rc = ensure(h, B_NLEN, n, &nl)))
       return rc;
-    if ((rc = reset_ctr(h))) return rc;
     {
       Launch l(h, "k_decode");
-      k_decode<<<grid_for(n), kBlock, 0, h->stream>>>(d_bytes, d_offs, n, a, t, e, no, nl, h->ctr);
+      k_decode<<<grid_for(stop), kBlock, 0, h->stream>>>(d_bytes, d_offs, stop, a, t, e, no, nl,
+                                                          h->ctr);
       HIPCHK(h, hipGetLastError());
     }
-    NamesPairs src{d_bytes, no, nl};
-    if (dirty) {
-      if ((rc = receive_decoded(h, src, a, t, e, stop, now, ow, true))) return rc;
-    } else {
-      if ((rc = finish_misses(h, src, a, t, e, nmiss, now, ow.status))) return rc;
-    }
+    if ((rc = finish_receive(h, NamesPairs{d_bytes, no, nl}, a, t, e, stop, fd, nmiss, now, ow)))
+      return rc;
   }
   if ((rc = copy_outputs(h, res, n, dev, ow))) return rc;
   if (dev) HIPCHK(h, hipStreamSynchronize(h->stream));

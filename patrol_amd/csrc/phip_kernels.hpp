@@ -191,24 +191,23 @@ __device__ inline int probe(const Table& T, const Name& nm, const u8* src, u32* 
 }
 
 // ----------------------------------------------------------- classify ----
-// Batch routing: any incast (IsZero remote, repo.go:78) or -0.0 replica
-// field sends the batch to the ordered path.
-__global__ void k_classify(const uint64_t* __restrict__ a, const uint64_t* __restrict__ t,
-                           const int64_t* __restrict__ e, u32 n, u32* ctr) {
-  u32 i = blockIdx.x * blockDim.x + threadIdx.x;
-  bool inc = false, nz = false;
-  if (i < n) {
-    const u64 ab = __builtin_nontemporal_load(a + i), tb = __builtin_nontemporal_load(t + i);
-    // elapsed matters only when both floats are zero: read it only then
-    // (a third of the pass's bytes on a clean batch)
-    if (is_zero_bits(ab) && is_zero_bits(tb)) inc = e[i] == 0;
-    nz = !inc && (ab == kSign || tb == kSign);
-  }
-  u64 mi = __ballot(inc), mn = __ballot(nz);
-  if (__lane_id() == 0) {
-    if (mi) atomicAdd(&ctr[0], (u32)__popcll(mi));
-    if (mn) atomicAdd(&ctr[1], (u32)__popcll(mn));
-  }
+// Counter slot of the first dirty message of a Receive batch: an incast
+// (an all-zero state asks for a reply, repo.go:78,86-90) or a -0.0 field (Go's
+// `>` and the E order disagree on +-0), the two things only the ordered path
+// handles.  The fast path applies the clean prefix before it (merges commute),
+// the ordered path the rest.
+constexpr u32 kCtrDirty = 12;
+
+// Min-reduce the index of a wave's first dirty lane (lanes hold increasing
+// indices, so the lowest set lane has the lowest index).
+__device__ inline void note_dirty(bool d, u32 i, u32* ctr) {
+  const u64 m = __ballot(d);
+  if (m && __lane_id() == (u32)(__ffsll((long long)m) - 1)) atomicMin(&ctr[kCtrDirty], i);
+}
+
+__device__ inline bool replica_dirty(u64 ab, u64 tb, i64 e) {
+  const bool inc = is_zero_bits(ab) && is_zero_bits(tb) && e == 0;
+  return inc || ab == kSign || tb == kSign;
 }
 
 // ------------------------------------------------------- fast receive ----
@@ -461,6 +460,13 @@ struct SoaIn {   // decoded messages (phip_receive_soa / decoded datagrams)
     ra = ld<true>(ma + i); rt = ld<true>(mt + i); re = ld<true>(me + i);
     load_words3<false>(src.blob, off, len, w0, w1, w2);
   }
+  // Classification (elapsed matters only when both floats are zero, so it is
+  // read only then: a third of the pass's bytes on a clean batch).
+  __device__ inline bool dirty(u32 i, u32* ctr) const {
+    const u64 ab = __builtin_nontemporal_load(ma + i), tb = __builtin_nontemporal_load(mt + i);
+    if (is_zero_bits(ab) && is_zero_bits(tb)) return me[i] == 0 || ab == kSign || tb == kSign;
+    return ab == kSign || tb == kSign;
+  }
 };
 
 // Raw datagrams (bucket.go:59-64): bytes[offs[i] .. offs[i+1]) = added,
@@ -499,19 +505,11 @@ struct WireIn {
     re = (i64)__builtin_bswap64(funnel8(h[2], h[3], sb));
     len = (u32)(h[3] >> (8 * sb)) & 0xFFu;
   }
-};
-
-// Wire classification (replaces k_decode on the fast path): first malformed
-// datagram (io.ErrShortBuffer, bucket.go:72,84) into ctr[5], incast and -0.0
-// counts into ctr[0], ctr[1] as k_classify does.  Reads the headers only.
-__global__ __launch_bounds__(kBlock) void k_classify_wire(const u8* __restrict__ bytes,
-                                                          const uint64_t* __restrict__ offs, u32 n,
-                                                          u32* ctr) {
-  const u32 i = blockIdx.x * kBlock + threadIdx.x;
-  bool inc = false, nz = false;
-  if (i < n) {
+  // Classification from the header words: a malformed datagram
+  // (io.ErrShortBuffer, bucket.go:72,84) min-reduces its index into ctr[5]
+  // (the Go loop stops there); otherwise incast / -0.0 as SoaIn::dirty.
+  __device__ inline bool dirty(u32 i, u32* ctr) const {
     const u64 o = offs[i], end = offs[i + 1], sz = end - o;
-    // the header as four aligned words clamped into the datagram
     const u64* p = reinterpret_cast<const u64*>(bytes);
     const u64 last = (end > o ? end - 1 : o) >> 3, hb = o >> 3;
     u64 h[4];
@@ -521,19 +519,21 @@ __global__ __launch_bounds__(kBlock) void k_classify_wire(const u8* __restrict__
     const u32 len = (u32)(h[3] >> (8 * sb)) & 0xFFu;
     if (sz < PHIP_BUCKET_FIXED_SIZE || sz - PHIP_BUCKET_FIXED_SIZE < len) {
       atomicMin(&ctr[5], i);
-    } else {
-      const u64 ab = __builtin_bswap64(funnel8(h[0], h[1], sb));
-      const u64 tb = __builtin_bswap64(funnel8(h[1], h[2], sb));
-      if (is_zero_bits(ab) && is_zero_bits(tb))
-        inc = __builtin_bswap64(funnel8(h[2], h[3], sb)) == 0;
-      nz = !inc && (ab == kSign || tb == kSign);
+      return false;
     }
+    return replica_dirty(__builtin_bswap64(funnel8(h[0], h[1], sb)),
+                         __builtin_bswap64(funnel8(h[1], h[2], sb)),
+                         (i64)__builtin_bswap64(funnel8(h[2], h[3], sb)));
   }
-  const u64 mi = __ballot(inc), mn = __ballot(nz);
-  if (__lane_id() == 0) {
-    if (mi) atomicAdd(&ctr[0], (u32)__popcll(mi));
-    if (mn) atomicAdd(&ctr[1], (u32)__popcll(mn));
-  }
+};
+
+// Classification of a fast batch: the first dirty message into
+// ctr[kCtrDirty], the first malformed datagram into ctr[5].  One atomic per
+// wave that finds one, none on a clean batch.
+template <class In>
+__global__ __launch_bounds__(kBlock) void k_classify(In in, u32 n, u32* ctr) {
+  const u32 i = blockIdx.x * kBlock + threadIdx.x;
+  note_dirty(i < n && in.dirty(i, ctr), i, ctr);
 }
 
 template <class In>
@@ -546,10 +546,11 @@ __global__ __launch_bounds__(kFastBlock) __attribute__((amdgpu_waves_per_eu(8, 8
   __shared__ u64 hmax[3][kHotMax];      // per-workgroup maxima (elapsed biased by 2^63)
   __shared__ u32 hhits;
 
-  // Classification gate: an incast or -0.0 in the batch (ctr[0], ctr[1])
-  // sends it to the ordered path; then nothing here may touch the table.
-  if (ctr[0] | ctr[1]) return;
-  n = min(n, ctr[5]);   // the first malformed datagram ends the batch (none: ~0)
+  // Gate (k_classify ran before): only the clean prefix is applied, the
+  // messages before the first dirty one (ctr[kCtrDirty]) and before the first
+  // malformed datagram (ctr[5]); none: ~0.
+  n = min(n, min(ctr[5], ctr[kCtrDirty]));
+  if (n == 0) return;
   const u32 nh = hot ? min(hot->n, kHotMax) : 0u;
   for (u32 j = threadIdx.x; j < kHotLds; j += kFastBlock) hslot[j] = 0;
   for (u32 j = threadIdx.x; j < kHotMax; j += kFastBlock) {
@@ -834,7 +835,6 @@ __global__ void k_decode(const u8* __restrict__ bytes, const uint64_t* __restric
                          int64_t* __restrict__ e, uint64_t* __restrict__ noff,
                          u8* __restrict__ nlen, u32* ctr) {
   u32 i = blockIdx.x * blockDim.x + threadIdx.x;
-  bool inc = false, nz = false;
   if (i < n) {
     u64 o = offs[i], sz = offs[i + 1] - o;
     bool bad = sz < 25;
@@ -847,18 +847,11 @@ __global__ void k_decode(const u8* __restrict__ bytes, const uint64_t* __restric
       a[i] = ab; t[i] = tb; e[i] = eb;
       noff[i] = o + 25;
       nlen[i] = (u8)l;
-      inc = !bad && state_is_zero(ab, tb, eb);
-      nz = !bad && !inc && (ab == kSign || tb == kSign);
     }
     if (bad) {
       nlen[i] = 0; noff[i] = o;
       atomicMin(&ctr[5], i);
     }
-  }
-  u64 mi = __ballot(inc), mn = __ballot(nz);
-  if (__lane_id() == 0) {
-    if (mi) atomicAdd(&ctr[0], (u32)__popcll(mi));
-    if (mn) atomicAdd(&ctr[1], (u32)__popcll(mn));
   }
 }
 

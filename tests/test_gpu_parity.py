@@ -548,3 +548,47 @@ def test_mixed_large_batch_vs_oracle(pa, dirty):
         cnt = rng.integers(1, 4, n).astype(np.uint64)
         a, t, e = _gen.dirty_states(rng, n, 0.02)
     _check_mixed(pa, [kind, names, now, freq, per, cnt, a, t, e], 17, reply=dirty)
+
+
+@pytest.mark.parametrize("wire", [False, True])
+@pytest.mark.parametrize("first", [0, 131000, 131072 + 5, 1500001])
+def test_receive_clean_prefix_then_ordered_vs_oracle(pa, wire, first):
+    """A 2^21-message batch (hot directory on) whose first incast or -0.0
+    sits at `first`: the clean prefix is merged on the fast path, everything
+    from `first` on by the ordered path from the state the prefix left,
+    replies included.  Wire variant: a malformed datagram after the dirty
+    ones ends the batch."""
+    import struct
+    rng = np.random.default_rng(first + 3 * wire)
+    K = 20000
+    g, o = _seed_both(pa, rng, K, log2_slots=16)
+    n = 1 << 21
+    ids = _gen.zipf_ids(rng, n, K + 2000)
+    names = _gen.key_names(ids)
+    a, t, e = _fast_dirty_states(rng, n)
+    later = np.sort(rng.integers(first + 1, n - 100, 40))
+    if first % 2:
+        a[first] = np.uint64(0x8000000000000000)           # -0.0 first
+    else:
+        a[first], t[first], e[first] = 0, 0, 0               # incast first
+    a[later[:20]], t[later[:20]], e[later[:20]] = 0, 0, 0    # incasts (replies)
+    t[later[20:]] = np.uint64(0x8000000000000000)            # -0.0
+    now = _gen.T0 + 4 * SEC
+    if wire:
+        dgs = [struct.pack(">QQQ", int(a[i]), int(t[i]), int(e[i]) & (2**64 - 1)) +
+               bytes([len(names[i])]) + names[i] for i in range(n)]
+        short = n - 50
+        dgs[short] = dgs[short][:20]
+        out = g.receive_datagrams(dgs, now)
+        st, ra, rt, re, stop = o.receive(dgs, now)
+        assert out["stop"] == stop == short
+    else:
+        out = g.receive_soa(names, a, t, e, now)
+        st, ra, rt, re = o.receive_soa(names, a, t, e, now)
+    assert np.array_equal(out["status"], st)
+    rep = (st & 0x7F) == 2
+    assert rep.sum() > 0
+    assert np.array_equal(out["reply"]["a"][rep], ra[rep])
+    assert np.array_equal(out["reply"]["t"][rep], rt[rep])
+    assert np.array_equal(out["reply"]["e"][rep], re[rep])
+    assert_same_dump(gpu_dump(g), o.dump())

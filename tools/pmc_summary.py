@@ -17,6 +17,10 @@ On this kernel every read request is 128 B (streamed batch data and the
 random slot-record lines alike), i.e. exactly 2x FETCH_SIZE.  Writes are
 WRITE_SIZE (the fast kernel writes only through atomics; the atomic count is
 reported beside it).
+
+The fast path launches the dominant kernel once per chunk of a batch
+(bench.json: roofline.launches_per_step), so every figure is per step: the
+sum over all dispatches divided by the number of steps they make up.
 """
 import csv
 import json
@@ -38,6 +42,11 @@ def per_dispatch(path, counter):
     return list(vals.values())
 
 
+def per_step(vals, lps):
+    """Sum of the dispatches of one step (the list holds whole steps only)."""
+    return statistics.mean(vals) * lps if vals else None
+
+
 def main():
     src, tag = sys.argv[1], sys.argv[2]
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -53,12 +62,13 @@ def main():
     rd = {k: per_dispatch(os.path.join(src, "pmc_rdsize", "run_counter_collection.csv"), c)
           for k, c in ((32, "TCC_EA0_RDREQ_32B_sum"), (64, "TCC_EA0_RDREQ_64B_sum"),
                        (128, "TCC_EA0_RDREQ_128B_sum"))}
-    rd_bytes = sum(k * statistics.mean(v) for k, v in rd.items() if v)
+    lps = bench["roofline"].get("launches_per_step", 1)
+    rd_bytes = sum(k * per_step(v, lps) for k, v in rd.items() if v)
     atom = per_dispatch(os.path.join(src, "pmc_wr", "run_counter_collection.csv"), "TCC_ATOMIC_sum")
     wrreq = per_dispatch(os.path.join(src, "pmc_wr", "run_counter_collection.csv"), "TCC_EA0_WRREQ_sum")
     hit = per_dispatch(os.path.join(src, "pmc_l2", "run_counter_collection.csv"), "TCC_HIT_sum")
     miss = per_dispatch(os.path.join(src, "pmc_l2", "run_counter_collection.csv"), "TCC_MISS_sum")
-    f_kib, w_kib = statistics.mean(fetch), statistics.mean(write)
+    f_kib, w_kib = per_step(fetch, lps), per_step(write, lps)
     hbm = rd_bytes + w_kib * 1024
     stats = {}
     with open(os.path.join(src, "stats", "run_kernel_stats.csv")) as f:
@@ -66,21 +76,25 @@ def main():
             if DOMINANT in r["Name"]:
                 stats = {"calls": int(r["Calls"]), "avg_ms": float(r["AverageNs"]) / 1e6,
                          "min_ms": float(r["MinNs"]) / 1e6, "max_ms": float(r["MaxNs"]) / 1e6}
+    h_s, m_s = per_step(hit, lps), per_step(miss, lps)
     pmc = {"kernel": DOMINANT, "workload": bench["config"]["workload"],
-           "fetch_kib_per_launch": f_kib, "write_kib_per_launch": w_kib,
-           "read_bytes_per_launch": rd_bytes,
-           "rdreq_by_size_per_launch": {str(k): (statistics.mean(v) if v else 0.0) for k, v in rd.items()},
-           "atomics_per_launch": statistics.mean(atom) if atom else None,
-           "ea_wrreq_per_launch": statistics.mean(wrreq) if wrreq else None,
-           "hbm_bytes_per_launch": hbm,
-           "l2_hit_rate": statistics.mean(hit) / (statistics.mean(hit) + statistics.mean(miss)),
-           "tcc_hit_per_launch": statistics.mean(hit), "tcc_miss_per_launch": statistics.mean(miss),
+           "launches_per_step": lps,
+           "fetch_kib_per_step": f_kib, "write_kib_per_step": w_kib,
+           "read_bytes_per_step": rd_bytes,
+           "rdreq_by_size_per_step": {str(k): (per_step(v, lps) or 0.0) for k, v in rd.items()},
+           "atomics_per_step": per_step(atom, lps),
+           "ea_wrreq_per_step": per_step(wrreq, lps),
+           "hbm_bytes_per_step": hbm,
+           "l2_hit_rate": h_s / (h_s + m_s),
+           "tcc_hit_per_step": h_s, "tcc_miss_per_step": m_s,
            "rocprof_kernel_stats": stats,
-           "bench_kernel_ms": bench["roofline"]["kernel_ms"],
-           "algorithmic_bytes_per_launch": bench["roofline"]["algorithmic_bytes_per_launch"],
-           "note": "hbm_bytes = size-bucketed EA read requests (32/64/128 B) + WRITE_SIZE; "
-                   "summed over XCDs (MI355X_MICROARCH.md §HBM: FETCH_SIZE tallies 64 B per "
-                   "request, so it reads half of the 128-B requests this kernel makes)"}
+           "rocprof_kernel_ms_per_step": stats.get("avg_ms", float("nan")) * lps,
+           "bench_kernel_ms_per_step": bench["roofline"]["kernel_ms_per_step"],
+           "algorithmic_bytes_per_step": bench["roofline"]["algorithmic_bytes_per_step"],
+           "note": "per step = sum over the step's launches of the kernel; hbm_bytes = "
+                   "size-bucketed EA read requests (32/64/128 B) + WRITE_SIZE; summed over XCDs "
+                   "(MI355X_MICROARCH.md §HBM: FETCH_SIZE tallies 64 B per request, so it reads "
+                   "half of the 128-B requests this kernel makes)"}
     with open(os.path.join(prof, f"{tag}_pmc.json"), "w") as f:
         json.dump(pmc, f, indent=1)
     with open(os.path.join(prof, "pmc_summary.json"), "w") as f:
