@@ -271,7 +271,7 @@ def run_c4(args, torch, dev, repo, rank, world, K, gen):
         rb, ro, ra, rt, re = shard.route_messages_native(blob, offs, a, t, e, repo)
         m = ro.numel() - 1
         if m:
-            repo.receive_soa(rb, ra, rt, re, T0 + j, name_offs=ro.to(torch.int32), n=m, device=True)
+            repo.receive_soa(rb, ra, rt, re, T0 + j, name_offs=ro, n=m, device=True)
     return n, step, owned
 
 

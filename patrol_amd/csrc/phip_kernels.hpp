@@ -1629,15 +1629,33 @@ __global__ __launch_bounds__(kBlock) void k_route_count(Src src, u32 n, u32 worl
   if (threadIdx.x < kRouteMaxWorld) { lc[threadIdx.x] = 0; lb[threadIdx.x] = 0; }
   __syncthreads();
   const u32 i = blockIdx.x * kBlock + threadIdx.x;
-  if (i < n) {
-    u64 off; u32 len;
+  const bool valid = i < n;
+  u32 o = 0, len = 0;
+  if (valid) {
+    u64 off;
     src.template get<true>(i, off, len);
     Name nm;
     load_name_wide<true>(src.blob, off, len, nm);
-    const u32 o = owner_of_hash(nm.h, world);
+    o = owner_of_hash(nm.h, world);
     owner[i] = (u8)o;
-    atomicAdd(&lc[o], 1u);
-    atomicAdd(&lb[o], len);
+  }
+  // One LDS atomic per (wave, owner), not per message: with few owners every
+  // lane would hit the same LDS word.
+  const u32 lane = __lane_id();
+  u64 rest = __ballot(valid);
+  while (rest) {
+    const u32 leader = __ffsll((long long)rest) - 1;
+    const u32 b = __shfl(o, leader);
+    const bool mine = valid && o == b;
+    const u64 m = __ballot(mine);
+    u32 v = mine ? len : 0;
+#pragma unroll
+    for (u32 d = 32; d; d >>= 1) v += __shfl_xor(v, d);
+    if (lane == leader) {
+      atomicAdd(&lc[b], (u32)__popcll(m));
+      atomicAdd(&lb[b], v);
+    }
+    rest &= ~m;
   }
   __syncthreads();
   if (threadIdx.x < world) {

@@ -107,8 +107,10 @@ def route_messages(blob, offs, added, taken, elapsed, group=None, repo=None, h=N
     r_a = a2a(added[order], sc, rc)
     r_t = a2a(taken[order], sc, rc)
     r_e = a2a(elapsed[order], sc, rc)
-    r_offs = torch.zeros(r_lens.numel() + 1, dtype=torch.int64, device=dev)
-    r_offs[1:] = torch.cumsum(r_lens, 0)
+    # name offsets in the received blob: one int32 scan of the lengths
+    r_offs = torch.empty(r_lens.numel() + 1, dtype=torch.int32, device=dev)
+    r_offs[0] = 0
+    torch.cumsum(r_lens, 0, dtype=torch.int32, out=r_offs[1:])
     return r_blob, r_offs, r_a, r_t, r_e
 
 
@@ -138,12 +140,11 @@ def route_messages_native(blob, offs, added, taken, elapsed, repo, group=None):
                            nbytes.data_ptr(), _lib.DEVICE_PTRS)
     if rc != 0:
         raise RuntimeError(f"phip_route_pack failed: {rc}")
-    recv_cnt = torch.empty_like(cnt)
-    recv_bytes = torch.empty_like(nbytes)
-    dist.all_to_all_single(recv_cnt, cnt, group=group)
-    dist.all_to_all_single(recv_bytes, nbytes, group=group)
-    sc, rc_ = cnt.tolist(), recv_cnt.tolist()
-    sb, rb = nbytes.tolist(), recv_bytes.tolist()
+    # one exchange of the (messages, name bytes) split sizes, one host sync
+    sizes = torch.stack([cnt, nbytes], 1)                  # [world, 2]
+    recv_sizes = torch.empty_like(sizes)
+    dist.all_to_all_single(recv_sizes, sizes, group=group)
+    (sc, sb), (rc_, rb) = torch.cat([sizes, recv_sizes], 1).t().reshape(2, 2, world).tolist()
 
     def a2a(x, s_splits, r_splits, slack=0):
         total = sum(r_splits)
@@ -155,8 +156,10 @@ def route_messages_native(blob, offs, added, taken, elapsed, repo, group=None):
     # 8 bytes of read slack past the last name (the ABI's blob rule)
     r_blob = a2a(s_names, sb, rb, slack=8)
     r_a, r_t, r_e = a2a(s_a, sc, rc_), a2a(s_t, sc, rc_), a2a(s_e, sc, rc_)
-    r_offs = torch.zeros(r_lens.numel() + 1, dtype=torch.int64, device=dev)
-    r_offs[1:] = torch.cumsum(r_lens, 0)
+    # name offsets in the received blob: one int32 scan of the lengths
+    r_offs = torch.empty(r_lens.numel() + 1, dtype=torch.int32, device=dev)
+    r_offs[0] = 0
+    torch.cumsum(r_lens, 0, dtype=torch.int32, out=r_offs[1:])
     return r_blob, r_offs, r_a, r_t, r_e
 
 
