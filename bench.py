@@ -51,6 +51,8 @@ def parse():
     p.add_argument("--cpu-threads", type=int, default=0)
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--seed", type=int, default=1234)
+    p.add_argument("--no-combine", action="store_true",
+                   help="c4: no sender-side combine of hot names (PHIP_ROUTE_COMBINE)")
     p.add_argument("--workload", default="c2", choices=["c2", "c3", "c4", "c5"],
                    help="c2: batched Receive merges (headline); c3: mixed Take+Merge stream")
     p.add_argument("--ops", type=int, default=50_000_000, help="c3: ops per step")
@@ -268,7 +270,8 @@ def run_c4(args, torch, dev, repo, rank, world, K, gen):
 
     def step(j):
         a, t, e = batches[j]
-        rb, ro, ra, rt, re = shard.route_messages_native(blob, offs, a, t, e, repo)
+        rb, ro, ra, rt, re = shard.route_messages_native(blob, offs, a, t, e, repo,
+                                                         combine=not args.no_combine)
         m = ro.numel() - 1
         if m:
             repo.receive_soa(rb, ra, rt, re, T0 + j, name_offs=ro, n=m, device=True)
@@ -448,6 +451,7 @@ def main():
         workload = (f"C4 owner-routed merge: {n} messages/GPU over {K * world} buckets hash-sharded "
                     f"by name across {world} GPU(s), all-to-all routing + merge, Zipf({args.zipf})")
         extra["buckets_owned_rank0"] = owned
+        extra["sender_combine"] = not args.no_combine
     elif args.workload == "c3":
         # Take 89 B (op 24 + state read 32 + write 24 + result 9), Merge 88 B.
         bpo = 88.5

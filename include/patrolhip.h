@@ -94,6 +94,7 @@ enum {
 
 /* Call flags. */
 #define PHIP_DEVICE_PTRS 0x1u   /* all pointers of the call are device memory */
+#define PHIP_ROUTE_COMBINE 0x2u /* phip_route_pack: combine hot names at the sender */
 
 typedef struct phip_config {
   int32_t device;        /* HIP device ordinal                                          */
@@ -228,7 +229,19 @@ int phip_hash_names(phip_handle* h, const uint8_t* names, const uint32_t* name_o
  * send_lens carries their lengths).  counts[o] / name_bytes[o] (world
  * entries, device memory) receive each owner's message and byte counts: the
  * splits of the all-to-all that moves the segments to their owners.  Device
- * pointers only; world <= 64. */
+ * pointers only; world <= 64.
+ *
+ * With PHIP_ROUTE_COMBINE (SURVEY §8e "sender-side combine"), a batch of
+ * >= 2^20 messages with no incast and no -0.0 field has the messages of its
+ * hottest names (a sampled directory of <= 512 short names) max-combined
+ * per workgroup: each workgroup sends one message per hot name it saw,
+ * carrying the field-wise maxima (NaN for a float field no message of the
+ * group raised), after its other messages.  Merging that message equals
+ * merging the ones it replaces (merges commute in that domain); messages
+ * whose three fields are all <= 0 or NaN are never combined, so a combined
+ * message is never an incast.  counts / name_bytes then describe the
+ * combined buffers (never more than without the flag).  A dirty or smaller
+ * batch is packed exactly as without the flag. */
 int phip_route_pack(phip_handle* h, const phip_msgs* m, uint32_t world, uint8_t* send_names,
                     uint32_t* send_lens, uint64_t* send_added, uint64_t* send_taken,
                     int64_t* send_elapsed, uint64_t* counts, uint64_t* name_bytes,

@@ -29,6 +29,7 @@ ST_MERGED, ST_INCAST_REPLY, ST_INCAST_NOREPLY, ST_SHORT, ST_NOT_PROCESSED = 1, 2
 ST_TAKE_OK, ST_TAKE_DENIED, ST_UPSERT_INSERTED, ST_CREATED = 6, 7, 8, 0x80
 OP_TAKE, OP_RECEIVE, OP_UPSERT = 0, 1, 2
 DEVICE_PTRS = 0x1
+ROUTE_COMBINE = 0x2
 
 
 class phip_config(C.Structure):

@@ -22,6 +22,7 @@ typedef unsigned long long u64;
 typedef long long i64;
 typedef unsigned int u32;
 typedef unsigned char u8;
+typedef unsigned short u16;
 
 constexpr u64 kSign = 0x8000000000000000ull;
 constexpr u64 kInfBits = 0x7FF0000000000000ull;      // +Inf

@@ -1093,20 +1093,64 @@ int phip_route_pack(phip_handle* h, const phip_msgs* m, uint32_t world, uint8_t*
     HIPCHK(h, hipStreamSynchronize(h->stream));
     return PHIP_OK;
   }
-  const u32 nblk = grid_for(n);
-  const size_t cells = (size_t)world * nblk;
+  // One wave per tile of `span` messages, eight per workgroup, four
+  // workgroups per CU.
+  const u32 nblk = (u32)std::max<u64>(1, std::min<u64>((n + kRouteBlock - 1) / kRouteBlock,
+                                                       (u64)h->ncu * 4));
+  const u32 ntile = nblk * kRouteWaves;
+  const u32 span = (u32)(((u64)n + ntile - 1) / ntile + 63) & ~63u;
+  const size_t cells = (size_t)world * ntile;
   u8* base;
   int rc;
-  if ((rc = ensure(h, B_ROUTE, n + 4 * cells * sizeof(u32) + 64, &base))) return rc;
+  if ((rc = ensure(h, B_ROUTE, 2 * (size_t)n + 4 * cells * sizeof(u32) + 64, &base))) return rc;
   u32* cnt = (u32*)base;
   u32* bytes = cnt + cells;
   u32* cbase = bytes + cells;
   u32* bbase = cbase + cells;
-  u8* owner = (u8*)(bbase + cells);
+  u16* code = (u16*)(bbase + cells);
   NamesOffs src{m->names, m->name_offs};
+  // Sender-side combine: classify (clean domain only), then the hot names of
+  // a strided sample, counted by name hash.
+  const HotHdr* hot = nullptr;
+  const RouteHot* dir = nullptr;
+  if ((flags & PHIP_ROUTE_COMBINE) && n >= kHotMinBatch) {
+    if ((rc = reset_ctr(h))) return rc;
+    {
+      Launch l(h, "k_route_classify");
+      k_route_classify<<<grid_for(n), kBlock, 0, h->stream>>>(m->added, m->taken, m->elapsed, n,
+                                                              h->ctr);
+    }
+    constexpr size_t kCnt = size_t(1) << kHotCntBits;
+    const size_t zero_bytes = 3 * kCnt * sizeof(u32) + kHotHist * sizeof(u32) + sizeof(HotHdr);
+    u8* hb;
+    if ((rc = ensure(h, B_HOT, zero_bytes + kHotMax * sizeof(RouteHot), &hb))) return rc;
+    u32* ckeys = (u32*)hb;
+    u32* ccnt = ckeys + kCnt;
+    u32* cidx = ccnt + kCnt;
+    u32* hist = cidx + kCnt;
+    HotHdr* hdr = (HotHdr*)(hist + kHotHist);
+    RouteHot* d = (RouteHot*)(hdr + 1);
+    HIPCHK(h, hipMemsetAsync(hb, 0, zero_bytes, h->stream));
+    const u32 stride = std::max<u32>(64, (n + kHotSampleMax - 1) / kHotSampleMax);
+    const u32 nsample = (n + stride - 1) / stride;
+    {
+      Launch l(h, "k_route_sample");
+      k_route_sample<NamesOffs><<<grid_for(nsample, kHotSamplePerBlock), 256, 0, h->stream>>>(
+          src, n, stride, nsample, ckeys, ccnt, cidx);
+      k_hot_hist<<<grid_for(kCnt), kBlock, 0, h->stream>>>(ccnt, hist);
+      k_hot_select<<<1, 256, 0, h->stream>>>(hist, hdr);
+      k_route_dir_build<NamesOffs><<<grid_for(kCnt), kBlock, 0, h->stream>>>(ckeys, ccnt, cidx, hdr,
+                                                                             src, world, d);
+    }
+    HIPCHK(h, hipGetLastError());
+    hot = hdr;
+    dir = d;
+  }
   {
     Launch l(h, "k_route_count");
-    k_route_count<NamesOffs><<<nblk, kBlock, 0, h->stream>>>(src, n, world, owner, cnt, bytes);
+    k_route_count<NamesOffs><<<nblk, kRouteBlock, 0, h->stream>>>(
+        src, m->added, m->taken, m->elapsed, n, span, world, ntile, hot, dir, h->ctr, code, cnt,
+        bytes);
   }
   HIPCHK(h, hipGetLastError());
   size_t tb = 0;
@@ -1123,11 +1167,11 @@ int phip_route_pack(phip_handle* h, const phip_msgs* m, uint32_t world, uint8_t*
   }
   {
     Launch l(h, "k_route_scatter");
-    k_route_scatter<NamesOffs><<<nblk, kBlock, 0, h->stream>>>(
-        src, m->added, m->taken, m->elapsed, n, world, owner, cbase, bbase, send_names, send_lens,
-        send_added, send_taken, send_elapsed);
+    k_route_scatter<NamesOffs><<<nblk, kRouteBlock, 0, h->stream>>>(
+        src, m->added, m->taken, m->elapsed, n, span, world, ntile, hot, dir, h->ctr, code, cbase,
+        bbase, send_names, send_lens, send_added, send_taken, send_elapsed);
   }
-  k_route_totals<<<1, kRouteMaxWorld, 0, h->stream>>>(cnt, bytes, cbase, bbase, nblk, world, counts,
+  k_route_totals<<<1, kRouteMaxWorld, 0, h->stream>>>(cnt, bytes, cbase, bbase, ntile, world, counts,
                                                      name_bytes);
   HIPCHK(h, hipGetLastError());
   HIPCHK(h, hipStreamSynchronize(h->stream));

@@ -1609,58 +1609,246 @@ __global__ void k_dump_gather(const u32* __restrict__ list, u32 n, const Rec* __
 // FNV-1a 64 of every name (phip_hash_names): the probe key and the shard map.
 // Owner routing: the one exchange step of a sharded merge.
 // owner(name) = ((fnv1a64(name) >> 32) * world) >> 32 (patrol_amd.shard).
-// k_route_count histograms owners per workgroup; an exclusive scan of the
-// [owner][workgroup] counts gives every (owner, workgroup) its base in the
-// owner-major send buffer; k_route_scatter then places each message with a
-// stable rank (wave ballots per owner, wave prefix in LDS), so the send
-// buffer holds each owner's messages contiguously in their original order.
+//
+// Layout: every wave owns a contiguous tile of `span` messages.  The count
+// pass fills cells [owner][tile] with message and name-byte counts; their
+// exclusive scans are each (owner, tile)'s base in the owner-major send
+// buffers, so an owner's segment holds its messages tile after tile, each
+// tile's in their original order (a stable partition).  No barrier inside
+// the loops: a wave ranks its lanes per owner with ballots and keeps its own
+// running place per owner in LDS.
+//
+// Sender-side combine (flag PHIP_ROUTE_COMBINE): a Zipf batch
+// puts most messages on a few names, and in the clean domain (no incast, no
+// -0.0: k_classify) merges commute, so a workgroup's messages for one hot
+// name can leave as ONE message carrying the field-wise maxima (E order).
+// The hot names are the most sampled names of a strided sample, counted by
+// name hash (the buckets live on other ranks: there is no slot to count).
+// A message whose three fields are all <= 0 (or NaN) is never combined: the
+// maxima of such messages alone could be the all-zero state, which its owner
+// would read as an incast request; every combined message thus has a field
+// > 0.  A workgroup's combined messages follow its last wave's tile.
 constexpr u32 kRouteMaxWorld = 64;
+constexpr u32 kRouteBlock = 512;
+constexpr u32 kRouteWaves = kRouteBlock / 64;
+constexpr u16 kRouteHot = 0x8000;   // route code: combined into hot entry (low bits)
+#ifndef PHIP_ROUTE_UNROLL
+#define PHIP_ROUTE_UNROLL 2
+#endif
+constexpr u32 kRU = PHIP_ROUTE_UNROLL;   // chunks of 64 messages per wave step
 
 __device__ inline u32 owner_of_hash(u64 h, u32 world) {
   return (u32)(((h >> 32) * (u64)world) >> 32);
 }
 
+struct RouteHot {   // a hot name: FNV-1a, canonical words (short names only), owner
+  u64 h, w0, w1;
+  u32 owner, pad;
+};
+
+// Strided sample of the batch, counted by name hash (k_hot_sample's shape:
+// LDS aggregation per workgroup, then the global count table).  cidx keeps
+// one sampled message of each key, the name the directory takes.
 template <class Src>
-__global__ __launch_bounds__(kBlock) void k_route_count(Src src, u32 n, u32 world,
-                                                        u8* __restrict__ owner,
-                                                        u32* __restrict__ cnt,
-                                                        u32* __restrict__ bytes) {
-  __shared__ u32 lc[kRouteMaxWorld], lb[kRouteMaxWorld];
-  if (threadIdx.x < kRouteMaxWorld) { lc[threadIdx.x] = 0; lb[threadIdx.x] = 0; }
+__global__ __launch_bounds__(256) void k_route_sample(Src src, u32 n, u32 stride, u32 nsample,
+                                                     u32* __restrict__ ckeys, u32* __restrict__ ccnt,
+                                                     u32* __restrict__ cidx) {
+  constexpr u32 kPer = kHotSamplePerBlock / 256;
+  constexpr u32 kL = 2 * kHotSamplePerBlock;
+  __shared__ u32 lkey[kL], lcnt[kL], lidx[kL];
+  for (u32 e = threadIdx.x; e < kL; e += 256) { lkey[e] = 0; lcnt[e] = 0; }
   __syncthreads();
-  const u32 i = blockIdx.x * kBlock + threadIdx.x;
-  const bool valid = i < n;
-  u32 o = 0, len = 0;
-  if (valid) {
-    u64 off;
-    src.template get<true>(i, off, len);
+  for (u32 r = 0; r < kPer; ++r) {
+    const u32 j = blockIdx.x * kHotSamplePerBlock + r * 256 + threadIdx.x;
+    const u64 i = (u64)j * stride;
+    if (j >= nsample || i >= n) continue;
+    u64 off; u32 len;
+    src.template get<true>((u32)i, off, len);
+    if (len > kShortName) continue;
     Name nm;
     load_name_wide<true>(src.blob, off, len, nm);
-    o = owner_of_hash(nm.h, world);
-    owner[i] = (u8)o;
-  }
-  // One LDS atomic per (wave, owner), not per message: with few owners every
-  // lane would hit the same LDS word.
-  const u32 lane = __lane_id();
-  u64 rest = __ballot(valid);
-  while (rest) {
-    const u32 leader = __ffsll((long long)rest) - 1;
-    const u32 b = __shfl(o, leader);
-    const bool mine = valid && o == b;
-    const u64 m = __ballot(mine);
-    u32 v = mine ? len : 0;
-#pragma unroll
-    for (u32 d = 32; d; d >>= 1) v += __shfl_xor(v, d);
-    if (lane == leader) {
-      atomicAdd(&lc[b], (u32)__popcll(m));
-      atomicAdd(&lb[b], v);
+    const u32 key = (u32)(nm.h ^ (nm.h >> 32)) | 1u;
+    u32 hs = (key * 2654435761u) & (kL - 1);
+    for (;;) {   // at most kHotSamplePerBlock distinct keys in 2x as many entries
+      const u32 old = atomicCAS(&lkey[hs], 0u, key);
+      if (old == 0) lidx[hs] = (u32)i;
+      if (old == 0 || old == key) { atomicAdd(&lcnt[hs], 1u); break; }
+      hs = (hs + 1) & (kL - 1);
     }
-    rest &= ~m;
   }
   __syncthreads();
-  if (threadIdx.x < world) {
-    cnt[(u64)threadIdx.x * gridDim.x + blockIdx.x] = lc[threadIdx.x];
-    bytes[(u64)threadIdx.x * gridDim.x + blockIdx.x] = lb[threadIdx.x];
+  constexpr u32 mask = (1u << kHotCntBits) - 1;
+  for (u32 e = threadIdx.x; e < kL; e += 256) {
+    const u32 key = lkey[e];
+    if (!key) continue;
+    u32 hs = (key * 2654435761u) >> (32 - kHotCntBits);
+    for (u32 k = 0; k <= mask; ++k) {
+      const u32 old = atomicCAS(&ckeys[hs], 0u, key);
+      if (old == 0) cidx[hs] = lidx[e];
+      if (old == 0 || old == key) { atomicAdd(&ccnt[hs], lcnt[e]); break; }
+      hs = (hs + 1) & mask;
+    }
+  }
+}
+
+// The sampled keys at or above k_hot_select's threshold, named by their
+// sampled message.
+template <class Src>
+__global__ void k_route_dir_build(const u32* __restrict__ ckeys, const u32* __restrict__ ccnt,
+                                  const u32* __restrict__ cidx, HotHdr* hdr, Src src, u32 world,
+                                  RouteHot* __restrict__ dir) {
+  const u32 e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (1u << kHotCntBits)) return;
+  const u32 c = ccnt[e];
+  if (!ckeys[e] || c < kHotMinCount || c < hdr->thresh) return;
+  const u32 idx = atomicAdd(&hdr->n, 1u);
+  if (idx >= kHotMax) return;   // cannot happen: the threshold bounds the count
+  u64 off; u32 len;
+  src.get(cidx[e], off, len);
+  Name nm;
+  load_name_wide<false>(src.blob, off, len, nm);
+  dir[idx] = RouteHot{nm.h, nm.w0, nm.w1, owner_of_hash(nm.h, world), 0};
+}
+
+struct RouteLds {   // the hot directory in LDS, open-addressed by name hash
+  u32 slot[kHotLds];   // entry + 1 (0 = empty)
+  u64 h[kHotMax], w0[kHotMax], w1[kHotMax];
+  u32 owner[kHotMax];
+};
+
+// Entries used by this launch: none without a directory or on a dirty batch.
+__device__ inline u32 route_hot_n(const HotHdr* hot, const u32* ctr) {
+  return (hot && ctr[kCtrDirty] == ~0u) ? min(hot->n, kHotMax) : 0u;
+}
+
+__device__ inline void route_lds_load(RouteLds& L, const RouteHot* dir, u32 nh) {
+  for (u32 j = threadIdx.x; j < kHotLds; j += kRouteBlock) L.slot[j] = 0;
+  __syncthreads();
+  for (u32 j = threadIdx.x; j < nh; j += kRouteBlock) {
+    const RouteHot d = dir[j];
+    L.h[j] = d.h; L.w0[j] = d.w0; L.w1[j] = d.w1; L.owner[j] = d.owner;
+    u32 hs = hot_home(d.h);
+    while (atomicCAS(&L.slot[hs], 0u, j + 1) != 0) hs = (hs + 1) & (kHotLds - 1);
+  }
+}
+
+__device__ inline int route_hot_find(const RouteLds& L, const Name& nm) {
+  for (u32 hs = hot_home(nm.h);; hs = (hs + 1) & (kHotLds - 1)) {
+    const u32 e = L.slot[hs];
+    if (!e) return -1;
+    if (L.h[e - 1] == nm.h && L.w0[e - 1] == nm.w0 && L.w1[e - 1] == nm.w1) return (int)e - 1;
+  }
+}
+
+// A message that may be combined: some field > 0 (module comment).
+__device__ inline bool route_combinable(u64 ab, u64 tb, i64 e) {
+  return as_f64(ab) > 0.0 || as_f64(tb) > 0.0 || e > 0;
+}
+
+// Classification for the combine: the first dirty message (as k_classify)
+// and, in ctr[kCtrNonPos], whether any message is not combinable, so that
+// k_route_count reads the replica fields only when some is.
+constexpr u32 kCtrNonPos = 13;
+__global__ __launch_bounds__(kBlock) void k_route_classify(const uint64_t* __restrict__ a,
+                                                           const uint64_t* __restrict__ t,
+                                                           const int64_t* __restrict__ e, u32 n,
+                                                           u32* ctr) {
+  const u32 i = blockIdx.x * kBlock + threadIdx.x;
+  bool dirty = false, nonpos = false;
+  if (i < n) {
+    const u64 ab = __builtin_nontemporal_load(a + i), tb = __builtin_nontemporal_load(t + i);
+    const bool ap = as_f64(ab) > 0.0, tp = as_f64(tb) > 0.0;
+    if (!ap && !tp) {   // elapsed matters only then
+      const i64 ev = e[i];
+      dirty = replica_dirty(ab, tb, ev);
+      nonpos = ev <= 0;
+    } else {
+      dirty = ab == kSign || tb == kSign;
+    }
+  }
+  note_dirty(dirty, i, ctr);
+  if (__ballot(nonpos) && __lane_id() == 0) ctr[kCtrNonPos] = 1;
+}
+
+template <class Src>
+__global__ __launch_bounds__(kRouteBlock) void k_route_count(
+    Src src, const uint64_t* __restrict__ a, const uint64_t* __restrict__ t,
+    const int64_t* __restrict__ e, u32 n, u32 span, u32 world, u32 ntile,
+    const HotHdr* __restrict__ hot, const RouteHot* __restrict__ dir, const u32* __restrict__ ctr,
+    u16* __restrict__ code, u32* __restrict__ cnt, u32* __restrict__ bytes) {
+  __shared__ RouteLds L;
+  __shared__ u32 wc[kRouteWaves][kRouteMaxWorld], wb[kRouteWaves][kRouteMaxWorld];
+  __shared__ u32 hit[kHotMax];
+  const u32 nh = route_hot_n(hot, ctr);
+  const bool nonpos = nh && ctr[kCtrNonPos];
+  for (u32 j = threadIdx.x; j < kRouteWaves * kRouteMaxWorld; j += kRouteBlock) {
+    (&wc[0][0])[j] = 0; (&wb[0][0])[j] = 0;
+  }
+  for (u32 j = threadIdx.x; j < kHotMax; j += kRouteBlock) hit[j] = 0;
+  route_lds_load(L, dir, nh);
+  __syncthreads();
+  const u32 wave = threadIdx.x / 64, lane = threadIdx.x & 63;
+  const u32 tile = blockIdx.x * kRouteWaves + wave;
+  const u64 t0 = (u64)tile * span, t1 = min((u64)n, t0 + span);
+  // kRU chunks of 64 per step, their loads issued together (the loads of one
+  // message depend on each other; those of different chunks do not)
+  for (u64 b0 = t0; b0 < t1; b0 += 64 * kRU) {
+    u32 o[kRU], len[kRU];
+    int hidx[kRU];
+    bool valid[kRU];
+    u64 off[kRU], w0[kRU], w1[kRU], w2[kRU];
+#pragma unroll
+    for (u32 u = 0; u < kRU; ++u) {
+      const u64 i = b0 + u * 64 + lane;
+      valid[u] = i < t1;
+      src.template get<true>((u32)(valid[u] ? i : t0), off[u], len[u]);
+    }
+#pragma unroll
+    for (u32 u = 0; u < kRU; ++u) load_words3<true>(src.blob, off[u], len[u], w0[u], w1[u], w2[u]);
+#pragma unroll
+    for (u32 u = 0; u < kRU; ++u) {
+      const u64 i = b0 + u * 64 + lane;
+      Name nm;
+      if (len[u] <= kShortName) short_name(w0[u], w1[u], w2[u], off[u], len[u], nm);
+      else load_name_wide<true>(src.blob, off[u], len[u], nm);
+      o[u] = owner_of_hash(nm.h, world);
+      hidx[u] = -1;
+      if (valid[u] && nh && len[u] <= kShortName) {
+        hidx[u] = route_hot_find(L, nm);
+        if (hidx[u] >= 0 && nonpos && !route_combinable(a[i], t[i], e[i])) hidx[u] = -1;
+      }
+      if (valid[u]) code[i] = hidx[u] >= 0 ? (u16)(kRouteHot | (u32)hidx[u]) : (u16)o[u];
+      if (hidx[u] >= 0) hit[hidx[u]] = 1;
+    }
+#pragma unroll
+    for (u32 u = 0; u < kRU; ++u) {   // one LDS update per (wave, owner), not per message
+      const bool plain = valid[u] && hidx[u] < 0;
+      u64 rest = __ballot(plain);
+      while (rest) {
+        const u32 leader = __ffsll((long long)rest) - 1;
+        const u32 ob = __shfl(o[u], leader);
+        const bool mine = plain && o[u] == ob;
+        const u64 m = __ballot(mine);
+        u32 v = mine ? len[u] : 0;
+#pragma unroll
+        for (u32 d = 32; d; d >>= 1) v += __shfl_xor(v, d);
+        if (lane == leader) { wc[wave][ob] += (u32)__popcll(m); wb[wave][ob] += v; }
+        rest &= ~m;
+      }
+    }
+  }
+  __syncthreads();
+  if (wave == kRouteWaves - 1) {   // the workgroup's combined messages
+    for (u32 j = lane; j < nh; j += 64) {
+      if (!hit[j]) continue;
+      atomicAdd(&wc[wave][L.owner[j]], 1u);
+      atomicAdd(&wb[wave][L.owner[j]], (u32)(L.w0[j] & 0xFFu));
+    }
+  }
+  __syncthreads();
+  for (u32 o = lane; o < world; o += 64) {
+    cnt[(u64)o * ntile + tile] = wc[wave][o];
+    bytes[(u64)o * ntile + tile] = wb[wave][o];
   }
 }
 
@@ -1675,55 +1863,113 @@ __device__ inline u32 wave_incl_scan(u32 v) {
   return v;
 }
 
-template <class Src>
-__global__ __launch_bounds__(kBlock) void k_route_scatter(
-    Src src, const uint64_t* __restrict__ a, const uint64_t* __restrict__ t,
-    const int64_t* __restrict__ e, u32 n, u32 world, const u8* __restrict__ owner,
-    const u32* __restrict__ cbase, const u32* __restrict__ bbase, u8* __restrict__ out_names,
-    u32* __restrict__ out_lens, uint64_t* __restrict__ out_a, uint64_t* __restrict__ out_t,
-    int64_t* __restrict__ out_e) {
-  constexpr u32 kW = kBlock / 64;
-  __shared__ u32 wc[kW][kRouteMaxWorld], wb[kW][kRouteMaxWorld];
-  const u32 wave = threadIdx.x / 64, lane = __lane_id();
-  for (u32 j = threadIdx.x; j < kW * kRouteMaxWorld; j += kBlock) {
-    (&wc[0][0])[j] = 0; (&wb[0][0])[j] = 0;
-  }
-  __syncthreads();
-  const u32 i = blockIdx.x * kBlock + threadIdx.x;
-  const bool valid = i < n;
-  u64 off = 0; u32 len = 0, o = kRouteMaxWorld;
-  if (valid) {
-    src.get(i, off, len);
-    o = owner[i];
-  }
-  // stable rank and byte prefix among this wave's lanes with the same owner
-  u32 rank = 0, bpre = 0;
-  u64 rest = __ballot(valid);
+// Place the lanes of `take` by owner `o`, in lane order, after each owner's
+// running place run[o] / runb[o] (messages / name bytes), which advance.
+__device__ inline void route_place(bool take, u32 o, u32 len, u32* run, u32* runb, u32& dst,
+                                   u32& dby) {
+  const u32 lane = __lane_id();
+  u64 rest = __ballot(take);
   while (rest) {
     const u32 leader = __ffsll((long long)rest) - 1;
-    const u32 lo = __shfl(o, leader);
-    const bool mine = valid && o == lo;
+    const u32 ob = __shfl(o, leader);
+    const bool mine = take && o == ob;
     const u64 m = __ballot(mine);
     const u32 sc = wave_incl_scan(mine ? len : 0u);
+    const u32 base = run[ob], bbase = runb[ob];
     if (mine) {
-      rank = __popcll(m & ((1ull << lane) - 1));
-      bpre = sc - len;
+      dst = base + __popcll(m & ((1ull << lane) - 1));
+      dby = bbase + sc - len;
     }
-    if (lane == 63) { wc[wave][lo] = __popcll(m); wb[wave][lo] = sc; }
+    const u32 tot = __shfl(sc, 63);
+    if (lane == leader) { run[ob] = base + __popcll(m); runb[ob] = bbase + tot; }
     rest &= ~m;
   }
+}
+
+template <class Src>
+__global__ __launch_bounds__(kRouteBlock) void k_route_scatter(
+    Src src, const uint64_t* __restrict__ a, const uint64_t* __restrict__ t,
+    const int64_t* __restrict__ e, u32 n, u32 span, u32 world, u32 ntile,
+    const HotHdr* __restrict__ hot, const RouteHot* __restrict__ dir, const u32* __restrict__ ctr,
+    const u16* __restrict__ code, const u32* __restrict__ cbase, const u32* __restrict__ bbase,
+    u8* __restrict__ out_names, u32* __restrict__ out_lens, uint64_t* __restrict__ out_a,
+    uint64_t* __restrict__ out_t, int64_t* __restrict__ out_e) {
+  __shared__ RouteLds L;
+  __shared__ u32 run[kRouteWaves][kRouteMaxWorld], runb[kRouteWaves][kRouteMaxWorld];
+  __shared__ u64 hmax[3][kHotMax];
+  __shared__ u32 hit[kHotMax];
+  const u32 nh = route_hot_n(hot, ctr);
+  const u32 wave = threadIdx.x / 64, lane = threadIdx.x & 63;
+  const u32 tile = blockIdx.x * kRouteWaves + wave;
+  for (u32 j = threadIdx.x; j < kHotMax; j += kRouteBlock) {
+    hit[j] = 0; hmax[0][j] = 0; hmax[1][j] = 0; hmax[2][j] = 0;
+  }
+  for (u32 o = lane; o < world; o += 64) {
+    run[wave][o] = cbase[(u64)o * ntile + tile];
+    runb[wave][o] = bbase[(u64)o * ntile + tile];
+  }
+  route_lds_load(L, dir, nh);
   __syncthreads();
-  if (!valid) return;
-  u32 cw = 0, bw = 0;
-  for (u32 w = 0; w < wave; ++w) { cw += wc[w][o]; bw += wb[w][o]; }
-  const u64 slot = (u64)o * gridDim.x + blockIdx.x;
-  const u32 dst = cbase[slot] + cw + rank;
-  const u32 dby = bbase[slot] + bw + bpre;
-  out_lens[dst] = len;
-  out_a[dst] = a[i];
-  out_t[dst] = t[i];
-  out_e[dst] = e[i];
-  for (u32 k = 0; k < len; ++k) out_names[dby + k] = src.blob[off + k];
+  const u64 t0 = (u64)tile * span, t1 = min((u64)n, t0 + span);
+  for (u64 b0 = t0; b0 < t1; b0 += 64 * kRU) {
+    u32 c[kRU], len[kRU];
+    u64 off[kRU], va[kRU], vt[kRU];
+    i64 ve[kRU];
+    bool valid[kRU];
+#pragma unroll
+    for (u32 u = 0; u < kRU; ++u) {   // every load unconditional (index clamped into the tile)
+      const u64 i = b0 + u * 64 + lane;
+      valid[u] = i < t1;
+      const u32 ic = (u32)(valid[u] ? i : t0);
+      c[u] = code[ic];
+      src.get(ic, off[u], len[u]);
+      va[u] = a[ic]; vt[u] = t[ic]; ve[u] = e[ic];
+    }
+#pragma unroll
+    for (u32 u = 0; u < kRU; ++u) {
+      const bool comb = valid[u] && (c[u] & kRouteHot);
+      const bool plain = valid[u] && !(c[u] & kRouteHot);
+      if (comb) {   // clean domain: replica fields hold no -0.0
+        const u32 j = c[u] & (kRouteHot - 1);
+        const u64 ea = enc_replica_nz(va[u]), et = enc_replica_nz(vt[u]);
+        const u64 ee = (u64)ve[u] ^ kSign;
+        if (ea > hmax[0][j]) atomicMax(&hmax[0][j], ea);
+        if (et > hmax[1][j]) atomicMax(&hmax[1][j], et);
+        if (ee > hmax[2][j]) atomicMax(&hmax[2][j], ee);
+        hit[j] = 1;
+      }
+      u32 dst = 0, dby = 0;
+      route_place(plain, c[u], plain ? len[u] : 0u, run[wave], runb[wave], dst, dby);
+      if (!plain) continue;
+      out_lens[dst] = len[u];
+      out_a[dst] = va[u];
+      out_t[dst] = vt[u];
+      out_e[dst] = ve[u];
+      for (u32 k = 0; k < len[u]; ++k) out_names[dby + k] = src.blob[off[u] + k];
+    }
+  }
+  __syncthreads();
+  if (wave != kRouteWaves - 1 || !nh) return;
+  // The workgroup's combined messages, in directory order, after this tile.
+  constexpr u64 kNaN = 0x7FF8000000000000ull;   // "no value": a merge never adopts NaN
+  for (u32 j0 = 0; j0 < nh; j0 += 64) {
+    const u32 j = j0 + lane;
+    const bool on = j < nh && hit[j];
+    const u32 o = on ? L.owner[j] : 0u;
+    const u32 len = on ? (u32)(L.w0[j] & 0xFFu) : 0u;
+    u32 dst = 0, dby = 0;
+    route_place(on, o, len, run[wave], runb[wave], dst, dby);
+    if (!on) continue;
+    const u64 ma = hmax[0][j], mt = hmax[1][j];
+    out_lens[dst] = len;
+    out_a[dst] = ma ? dec_f64(ma) : kNaN;
+    out_t[dst] = mt ? dec_f64(mt) : kNaN;
+    out_e[dst] = (i64)(hmax[2][j] ^ kSign);
+    for (u32 k = 0; k < len; ++k) {   // name byte k is canonical byte k + 2
+      const u32 cb = k + 2;
+      out_names[dby + k] = (u8)((cb < 8 ? L.w0[j] >> (8 * cb) : L.w1[j] >> (8 * (cb - 8))) & 0xFFu);
+    }
+  }
 }
 
 // Per-owner totals from the scanned (exclusive) bases.

@@ -114,12 +114,15 @@ def route_messages(blob, offs, added, taken, elapsed, group=None, repo=None, h=N
     return r_blob, r_offs, r_a, r_t, r_e
 
 
-def route_messages_native(blob, offs, added, taken, elapsed, repo, group=None):
+def route_messages_native(blob, offs, added, taken, elapsed, repo, group=None, combine=False):
     """route_messages with the partition on the GPU (phip_route_pack: owner
     hash, stable owner-major pack of names, lengths and states in two
     passes), then the all-to-all of each column over RCCL.  Same result as
-    route_messages().  repo's stream must be torch's current stream
-    (GPURepo.use_torch_stream) or the inputs complete."""
+    route_messages(); with combine=True a clean batch's hot names are
+    max-combined at the sender (PHIP_ROUTE_COMBINE), which leaves every
+    owner's merged state the same with fewer messages moved.  repo's stream
+    must be torch's current stream (GPURepo.use_torch_stream) or the inputs
+    complete."""
     from .engine import phip_msgs
     world = dist.get_world_size(group)
     dev = blob.device
@@ -137,7 +140,8 @@ def route_messages_native(blob, offs, added, taken, elapsed, repo, group=None):
                   elapsed.data_ptr())
     rc = L.phip_route_pack(repo.h, C.byref(m), world, s_names.data_ptr(), s_lens.data_ptr(),
                            s_a.data_ptr(), s_t.data_ptr(), s_e.data_ptr(), cnt.data_ptr(),
-                           nbytes.data_ptr(), _lib.DEVICE_PTRS)
+                           nbytes.data_ptr(),
+                           _lib.DEVICE_PTRS | (_lib.ROUTE_COMBINE if combine else 0))
     if rc != 0:
         raise RuntimeError(f"phip_route_pack failed: {rc}")
     # one exchange of the (messages, name bytes) split sizes, one host sync

@@ -264,3 +264,104 @@ def test_route_pack_is_stable_owner_partition(world):
     want = b"".join(names[k] for k in order)
     assert s_names.cpu().numpy()[:len(want)].tobytes() == want
     repo.close()
+
+
+def _route_pack(repo, blob, offs, da, dt, de, world, flags):
+    import ctypes as C
+    from patrol_amd import _lib
+    from patrol_amd.engine import phip_msgs
+    dev = blob.device
+    n = offs.numel() - 1
+    s_names = torch.zeros(blob.numel() + 64, dtype=torch.uint8, device=dev)
+    s_lens = torch.zeros(n, dtype=torch.int32, device=dev)
+    s_a, s_t, s_e = (torch.zeros(n, dtype=torch.int64, device=dev) for _ in range(3))
+    cnt = torch.zeros(world, dtype=torch.int64, device=dev)
+    nb = torch.zeros(world, dtype=torch.int64, device=dev)
+    torch.cuda.synchronize()
+    m = phip_msgs(n, 0, blob.data_ptr(), offs.data_ptr(), da.data_ptr(), dt.data_ptr(), de.data_ptr())
+    rc = _lib.load().phip_route_pack(repo.h, C.byref(m), world, s_names.data_ptr(), s_lens.data_ptr(),
+                                     s_a.data_ptr(), s_t.data_ptr(), s_e.data_ptr(), cnt.data_ptr(),
+                                     nb.data_ptr(), _lib.DEVICE_PTRS | flags)
+    assert rc == 0
+    return s_names, s_lens, s_a, s_t, s_e, cnt.cpu().tolist(), nb.cpu().tolist()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [1, 3])
+def test_route_pack_combine_owner_states_equal_oracle(world):
+    """PHIP_ROUTE_COMBINE on a 2^21-message clean Zipf batch (long and
+    medium names, NaN fields, all-non-positive messages that must not be
+    combined): every owner's segment received into its own table gives,
+    together, exactly the oracle's table for the whole batch, with far fewer
+    messages sent.  A dirty batch (one incast) packs exactly as without the
+    flag."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import patrol_amd
+    from oracle import oracle as O
+    from patrol_amd import _lib
+    from patrol_amd.engine import names_blob
+    from tests import _gen
+    rng = np.random.default_rng(77 + world)
+    n, K = 1 << 21, 30000
+    ids = _gen.zipf_ids(rng, n, K)
+    names = [(b"a-much-longer-bucket-name-%d" % i) if i % 97 == 0 else
+             (b"medium-name-%d" % i) if i % 89 == 0 else (b"b%d" % i) for i in ids]
+    a, t, e = _gen.clean_states(rng, n)
+    nanb = np.uint64(0x7FF8000000000000)
+    sel = rng.random(n) < 0.02
+    a[sel] = nanb
+    sel = rng.random(n) < 0.02
+    t[sel] = nanb
+    neg = rng.random(n) < 0.01      # all fields <= 0: never combined
+    a[neg] = np.float64(-3.0).view(np.uint64)
+    t[neg] = np.float64(-1.0).view(np.uint64)
+    e[neg] = -7
+    now = _gen.T0 + 2 * _gen.SEC
+    dev = torch.device("cuda", 0)
+    blob_np, offs_np = names_blob(names)
+    blob = torch.from_numpy(blob_np).to(dev)
+    offs = torch.from_numpy(offs_np.view(np.int32)).to(dev)
+    da, dt, de = (torch.from_numpy(x.view(np.int64)).to(dev) for x in (a, t, e))
+    router = patrol_amd.GPURepo(device=0, log2_slots=10)
+    s_names, s_lens, s_a, s_t, s_e, cnt, nb = _route_pack(router, blob, offs, da, dt, de, world,
+                                                          _lib.ROUTE_COMBINE)
+    assert sum(cnt) < 3 * n // 4      # the Zipf head went out combined
+    o = O.Repo()
+    o.receive_soa(names, a, t, e, now)
+    want = o.dump()
+    got = {}
+    c0 = b0 = 0
+    for r in range(world):
+        m = cnt[r]
+        g = patrol_amd.GPURepo(device=0, log2_slots=16)
+        if m:
+            lens = s_lens[c0:c0 + m]
+            ro = torch.zeros(m + 1, dtype=torch.int32, device=dev)
+            torch.cumsum(lens, 0, dtype=torch.int32, out=ro[1:])
+            g.receive_soa(s_names[b0:], s_a[c0:c0 + m], s_t[c0:c0 + m], s_e[c0:c0 + m], now,
+                          name_offs=ro, n=m, device=True)
+            torch.cuda.synchronize()
+        d = {k: (v.added, v.taken, v.elapsed, v.created) for k, v in g.dump().items()}
+        assert not (set(d) & set(got))
+        got.update(d)
+        c0 += m
+        b0 += nb[r]
+        g.close()
+    assert len(got) == len(want)
+    bad = [k for k in want if got.get(k) != want[k]]
+    assert not bad, [(k, got.get(k), want[k]) for k in bad[:5]]
+    # a dirty batch: exactly the plain stable partition
+    a2 = a.copy()
+    a2[n // 3] = 0
+    t2 = t.copy()
+    t2[n // 3] = 0
+    e2 = e.copy()
+    e2[n // 3] = 0
+    da2, dt2, de2 = (torch.from_numpy(x.view(np.int64)).to(dev) for x in (a2, t2, e2))
+    x = _route_pack(router, blob, offs, da2, dt2, de2, world, _lib.ROUTE_COMBINE)
+    y = _route_pack(router, blob, offs, da2, dt2, de2, world, 0)
+    assert x[5] == y[5] and x[6] == y[6] and sum(x[5]) == n
+    for u, v in zip(x[:5], y[:5]):
+        assert torch.equal(u, v)
+    router.close()
