@@ -174,6 +174,29 @@ int phip_seed(phip_handle* h, const uint8_t* names, const uint32_t* name_offs, u
 int phip_get(phip_handle* h, const uint8_t* name, uint32_t len, phip_state* out);
 /* Dump every bucket (unordered).  Call with names==NULL to size: *n_out and
  * *names_bytes_out are filled.  name_offs has n+1 entries. */
+/* Snapshot / restore (the reference has none and recovers a
+ * restarted node through incast, repo.go:96-106).  phip_snapshot writes
+ * phip_snapshot_bytes(h) bytes into a host buffer: a 64-byte header (magic
+ * "PHIPSNP1", ABI version, log2_slots, bucket count, arena bytes), the 2^L
+ * slot records as they lie in HBM (64 B each), then the used long-name arena.
+ * phip_restore loads such an image into a handle opened with the same
+ * log2_slots (and an arena at least as large): the table is reproduced
+ * exactly, with no rehash.  phip_dump + phip_seed is the portable route
+ * between different table sizes. */
+uint64_t phip_snapshot_bytes(phip_handle* h);
+int phip_snapshot(phip_handle* h, uint8_t* out, uint64_t cap);
+int phip_restore(phip_handle* h, const uint8_t* in, uint64_t len);
+
+/* Egress batching (replaces the per-peer, per-take marshal of
+ * repo.go:129-158 broadcast and :160-169 unicast): the current state of each
+ * named bucket as its byte-identical MarshalBinary datagram (bucket.go:51-68).
+ * Datagram i is out[25*i + (name_offs[i] - name_offs[0])], 25 + len_i bytes
+ * long, so `out` holds 25*n + name bytes and the datagrams are back to back
+ * in the order given (ready for one sendmmsg).  found[i] = 1 when the bucket
+ * exists; an absent bucket's datagram bytes are zero.  Host or device
+ * pointers (PHIP_DEVICE_PTRS). */
+int phip_export_datagrams(phip_handle* h, const uint8_t* names, const uint32_t* name_offs,
+                          uint32_t n, uint8_t* out, uint8_t* found, uint32_t flags);
 int phip_dump(phip_handle* h, uint8_t* names, uint64_t names_cap, uint64_t* name_offs,
               phip_state* states, uint64_t max_n, uint64_t* n_out, uint64_t* names_bytes_out);
 

@@ -20,6 +20,7 @@ EXPORTS = [
     "phip_receive_soa", "phip_upsert_soa", "phip_apply_mixed", "phip_take", "phip_parse_rate",
     "phip_marshal", "phip_api_take", "phip_last_timings", "phip_set_timing", "phip_last_stats", "phip_hash_names",
     "phip_ae_local_max", "phip_ae_apply", "phip_set_stream", "phip_route_pack",
+    "phip_export_datagrams", "phip_snapshot_bytes", "phip_snapshot", "phip_restore",
 ]
 
 PHIP_OK = 0
@@ -87,6 +88,11 @@ def load(path: str = LIB_PATH):
     L.phip_seed.argtypes = [vp, vp, vp, u32, vp, u32]
     L.phip_get.argtypes = [vp, C.c_char_p, u32, C.POINTER(phip_state)]
     L.phip_dump.argtypes = [vp, vp, u64, vp, vp, u64, C.POINTER(u64), C.POINTER(u64)]
+    L.phip_export_datagrams.argtypes = [vp, vp, vp, u32, vp, vp, u32]
+    L.phip_snapshot_bytes.argtypes = [vp]
+    L.phip_snapshot_bytes.restype = u64
+    L.phip_snapshot.argtypes = [vp, vp, u64]
+    L.phip_restore.argtypes = [vp, vp, u64]
     L.phip_receive_datagrams.argtypes = [vp, vp, vp, u32, i64, C.POINTER(phip_results),
                                          C.POINTER(u32), u32]
     L.phip_receive_soa.argtypes = [vp, C.POINTER(phip_msgs), i64, C.POINTER(phip_results), u32]

@@ -36,7 +36,7 @@ enum BufId {
   B_MISS, B_MISS2, B_RETRY, B_CSLOT, B_CMSG,
   B_SLOT, B_IDX, B_SSLOT, B_SIDX, B_USLOT, B_SCNT, B_SSTART, B_LONG, B_HUGE, B_TEMP, B_DUMP,
   B_OPS, B_HOFF, B_HOP, B_HVAL, B_RPOS, B_RST, B_RUNN, B_SEGEX, B_WOFF, B_SUMS, B_WRUN,
-  B_STATES, B_NAME1, B_HOT, B_ROUTE, B_COUNT_
+  B_STATES, B_NAME1, B_HOT, B_ROUTE, B_EXPORT, B_COUNT_
 };
 
 struct DevBuf {
@@ -821,6 +821,111 @@ int phip_get(phip_handle* h, const uint8_t* name, uint32_t len, phip_state* out)
   out->elapsed = r.elapsed;
   out->created = r.created;
   return 1;
+}
+
+// Snapshot image: header, the 2^L slot records as they lie in HBM, then the
+// used part of the long-name arena.  Restoring it into a handle of the same
+// table size reproduces the table exactly (slots, probe chains, arena
+// offsets), with no rehash.
+struct SnapHeader {
+  char magic[8];
+  u32 abi, log2_slots;
+  u64 n_buckets, arena_used, rec_bytes, reserved[3];
+};
+static_assert(sizeof(SnapHeader) == 64, "snapshot header");
+constexpr char kSnapMagic[8] = {'P', 'H', 'I', 'P', 'S', 'N', 'P', '1'};
+
+static u64 arena_used(phip_handle* h) {
+  u64 used = 0;
+  if (hipMemcpyAsync(&used, h->arena_cursor, sizeof(u64), hipMemcpyDeviceToHost, h->stream) !=
+          hipSuccess ||
+      hipStreamSynchronize(h->stream) != hipSuccess)
+    return ~0ull;
+  return std::min<u64>(used, h->arena_cap);
+}
+
+uint64_t phip_snapshot_bytes(phip_handle* h) {
+  if (!h) return 0;
+  std::lock_guard<std::mutex> g(h->mu);
+  begin_call(h);
+  const u64 used = arena_used(h);
+  if (used == ~0ull) return 0;
+  return sizeof(SnapHeader) + h->cap * sizeof(Rec) + used;
+}
+
+int phip_snapshot(phip_handle* h, uint8_t* out, uint64_t cap) {
+  if (!h || !out) return PHIP_ERR_INVALID;
+  std::lock_guard<std::mutex> g(h->mu);
+  begin_call(h);
+  const u64 used = arena_used(h);
+  if (used == ~0ull) return set_err(h, PHIP_ERR_HIP, "snapshot: arena cursor read failed");
+  const u64 need = sizeof(SnapHeader) + h->cap * sizeof(Rec) + used;
+  if (cap < need) return set_err(h, PHIP_ERR_INVALID, "snapshot needs %llu bytes", (unsigned long long)need);
+  SnapHeader hd{};
+  std::memcpy(hd.magic, kSnapMagic, 8);
+  hd.abi = PHIP_ABI_VERSION;
+  hd.log2_slots = h->L;
+  hd.n_buckets = h->n_buckets;
+  hd.arena_used = used;
+  hd.rec_bytes = sizeof(Rec);
+  std::memcpy(out, &hd, sizeof hd);
+  u8* p = out + sizeof hd;
+  HIPCHK(h, hipMemcpyAsync(p, h->recs, h->cap * sizeof(Rec), hipMemcpyDeviceToHost, h->stream));
+  if (used) HIPCHK(h, hipMemcpyAsync(p + h->cap * sizeof(Rec), h->arena, used, hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  return PHIP_OK;
+}
+
+int phip_restore(phip_handle* h, const uint8_t* in, uint64_t len) {
+  if (!h || !in || len < sizeof(SnapHeader)) return PHIP_ERR_INVALID;
+  std::lock_guard<std::mutex> g(h->mu);
+  begin_call(h);
+  SnapHeader hd;
+  std::memcpy(&hd, in, sizeof hd);
+  if (std::memcmp(hd.magic, kSnapMagic, 8) || hd.abi != PHIP_ABI_VERSION || hd.rec_bytes != sizeof(Rec))
+    return set_err(h, PHIP_ERR_INVALID, "not a snapshot of this ABI");
+  if (hd.log2_slots != h->L)
+    return set_err(h, PHIP_ERR_INVALID, "snapshot of 2^%u slots, handle has 2^%u", hd.log2_slots, h->L);
+  if (hd.arena_used > h->arena_cap) return set_err(h, PHIP_ERR_ARENA, "snapshot arena larger than the handle's");
+  if (hd.n_buckets > h->max_load) return set_err(h, PHIP_ERR_FULL, "snapshot above the handle's load limit");
+  if (len != sizeof hd + h->cap * sizeof(Rec) + hd.arena_used)
+    return set_err(h, PHIP_ERR_INVALID, "snapshot truncated");
+  const u8* p = in + sizeof hd;
+  HIPCHK(h, hipMemcpyAsync(h->recs, p, h->cap * sizeof(Rec), hipMemcpyHostToDevice, h->stream));
+  if (hd.arena_used)
+    HIPCHK(h, hipMemcpyAsync(h->arena, p + h->cap * sizeof(Rec), hd.arena_used, hipMemcpyHostToDevice, h->stream));
+  HIPCHK(h, hipMemsetAsync(h->aux, 0, h->cap * sizeof(u32), h->stream));
+  HIPCHK(h, hipMemcpyAsync(h->arena_cursor, &hd.arena_used, sizeof(u64), hipMemcpyHostToDevice, h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  h->n_buckets = hd.n_buckets;
+  return PHIP_OK;
+}
+
+int phip_export_datagrams(phip_handle* h, const uint8_t* names, const uint32_t* name_offs,
+                          uint32_t n, uint8_t* out, uint8_t* found, uint32_t flags) {
+  if (!h || (n && (!names || !name_offs || !out || !found))) return PHIP_ERR_INVALID;
+  std::lock_guard<std::mutex> g(h->mu);
+  begin_call(h);
+  if (n == 0) return PHIP_OK;
+  const bool dev = flags & PHIP_DEVICE_PTRS;
+  if (!dev && !names_ok(name_offs, n)) return set_err(h, PHIP_ERR_NAME_TOO_LARGE, "name > 231 bytes");
+  int rc;
+  NamesOffs src;
+  if ((rc = stage_names(h, names, name_offs, n, dev, &src))) return rc;
+  const size_t nbytes = dev ? 0 : (size_t)PHIP_BUCKET_FIXED_SIZE * n + (name_offs[n] - name_offs[0]);
+  u8 *d_out, *d_found;
+  if ((rc = out_buf(h, B_EXPORT, out, nbytes, dev, &d_out)) ||
+      (rc = out_buf(h, B_STATUS, found, n, dev, &d_found)))
+    return rc;
+  {
+    Launch l(h, "k_export");
+    k_export<<<grid_for(n), kBlock, 0, h->stream>>>(src, n, table(h), d_out, d_found);
+  }
+  HIPCHK(h, hipGetLastError());
+  if ((rc = copy_back(h, out, d_out, nbytes, dev)) || (rc = copy_back(h, found, d_found, n, dev)))
+    return rc;
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  return PHIP_OK;
 }
 
 int phip_dump(phip_handle* h, uint8_t* names, uint64_t names_cap, uint64_t* name_offs,

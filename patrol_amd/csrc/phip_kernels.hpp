@@ -2054,6 +2054,36 @@ __global__ void k_hash_names(NamesOffs src, u32 n, uint64_t* out) {
   out[i] = nm.h;
 }
 
+// Egress batching (phip_export_datagrams; SURVEY §8f, repo.go:129-169): the
+// current state of bucket names[i] as its MarshalBinary datagram
+// (bucket.go:51-68: added, taken, elapsed big-endian, one length byte, the
+// name) at out[25 * i + name_offs[i] - name_offs[0]].  An absent bucket
+// gets zero bytes and found[i] = 0.
+__global__ void k_export(NamesOffs src, u32 n, Table T, u8* __restrict__ out,
+                         u8* __restrict__ found) {
+  const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  u64 off; u32 len;
+  src.get(i, off, len);
+  Name nm;
+  load_name(src.blob, off, len, nm);
+  u32 s;
+  Rec r;
+  const bool hit = probe(T, nm, src.blob, &s, &r) == kFound;
+  u64 w[3] = {0, 0, 0};
+  if (hit) {
+    r = load_rec(&T.recs[s]);   // probe's copy may be the 48-byte view
+    w[0] = dec_f64(r.added);
+    w[1] = dec_f64(r.taken);
+    w[2] = (u64)r.elapsed;
+  }
+  u8* d = out + (u64)PHIP_BUCKET_FIXED_SIZE * i + (off - src.offs[0]);
+  for (u32 k = 0; k < 24; ++k) d[k] = hit ? (u8)(w[k >> 3] >> (56 - 8 * (k & 7))) : 0;
+  d[24] = hit ? (u8)len : 0;
+  for (u32 k = 0; k < len; ++k) d[PHIP_BUCKET_FIXED_SIZE + k] = hit ? src.blob[off + k] : 0;
+  found[i] = hit;
+}
+
 // Single lookup (phip_get).
 __global__ void k_get_one(const u8* name, u32 len, Table T, Rec* out, int* found) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;

@@ -15,6 +15,7 @@ call then passes PHIP_DEVICE_PTRS).
 from __future__ import annotations
 
 import ctypes as C
+import os
 from dataclasses import dataclass
 from typing import Iterable, Sequence
 
@@ -177,6 +178,40 @@ class GPURepo:
         if rc == 0:
             return None
         return BucketState(s.added, s.taken, s.elapsed, s.created)
+
+    def export_datagrams(self, names: Sequence[bytes]):
+        """Egress batch: each named bucket's current state as its MarshalBinary
+        datagram (bucket.go:51-68).  -> (list of datagrams, found uint8[n]);
+        an absent bucket's datagram is zero bytes."""
+        n = len(names)
+        blob, offs = names_blob(names)
+        out = np.zeros(25 * n + int(offs[-1]) + 1, np.uint8)
+        found = np.zeros(max(n, 1), np.uint8)
+        self._check(self.L.phip_export_datagrams(self.h, blob.ctypes.data, offs.ctypes.data, n,
+                                                 out.ctypes.data, found.ctypes.data, 0))
+        raw = out.tobytes()
+        dgs = [raw[25 * i + int(offs[i]):25 * (i + 1) + int(offs[i + 1])] for i in range(n)]
+        return dgs, found[:n]
+
+    def snapshot(self, path=None):
+        """The table as a raw image (phip_snapshot); written to `path` if given,
+        else returned as a uint8 array."""
+        nb = int(self.L.phip_snapshot_bytes(self.h))
+        if nb == 0:
+            raise PatrolHipError(-1, "phip_snapshot_bytes failed")
+        buf = np.empty(nb, np.uint8)
+        self._check(self.L.phip_snapshot(self.h, buf.ctypes.data, nb))
+        if path is None:
+            return buf
+        buf.tofile(path)
+        return None
+
+    def restore(self, src):
+        """Load a snapshot (a path or a uint8 array) into this handle, which must
+        have the snapshot's log2_slots (phip_restore)."""
+        buf = np.fromfile(src, np.uint8) if isinstance(src, (str, bytes, os.PathLike)) else \
+            np.ascontiguousarray(src, np.uint8)
+        self._check(self.L.phip_restore(self.h, buf.ctypes.data, buf.size))
 
     def dump(self):
         """{name: BucketState} of every bucket."""

@@ -592,3 +592,72 @@ def test_receive_clean_prefix_then_ordered_vs_oracle(pa, wire, first):
     assert np.array_equal(out["reply"]["t"][rep], rt[rep])
     assert np.array_equal(out["reply"]["e"][rep], re[rep])
     assert_same_dump(gpu_dump(g), o.dump())
+
+
+def test_export_datagrams_are_marshal_binary(pa):
+    """Egress batch (phip_export_datagrams): every named bucket's state as the
+    byte-identical MarshalBinary datagram (bucket.go:51-68) of the oracle's
+    state after the same batches; absent names give found = 0.  Short,
+    15-22 byte and arena names, NaN / -0.0 / negative states."""
+    import struct
+    rng = np.random.default_rng(91)
+    K = 5000
+    g, o = _seed_both(pa, rng, K, log2_slots=14)
+    n = 40000
+    ids = _gen.zipf_ids(rng, n, K + 800)
+    names = [(b"an-arena-length-bucket-name-%d" % i) if i % 13 == 0 else
+             (b"medium-name-%d" % i) if i % 11 == 0 else (b"b%d" % i) for i in ids]
+    a, t, e = _gen.dirty_states(rng, n, 0.05)
+    g.receive_soa(names, a, t, e, _gen.T0 + SEC)
+    o.receive_soa(names, a, t, e, _gen.T0 + SEC)
+    ask = sorted(set(names))[:3000] + [b"absent-%d" % i for i in range(50)] + [b"b0", b"b0"]
+    rng.shuffle(ask)
+    dgs, found = g.export_datagrams(ask)
+    for nm, d, f in zip(ask, dgs, found):
+        st = o.get(nm)
+        assert bool(f) == (st is not None), nm
+        if st is None:
+            assert d == bytes(25 + len(nm))
+            continue
+        want = struct.pack(">QQQ", st[0], st[1], st[2] & (2**64 - 1)) + bytes([len(nm)]) + nm
+        assert d == want, (nm, d.hex(), want.hex())
+
+
+def test_snapshot_restore_round_trip(pa, tmp_path):
+    """phip_snapshot / phip_restore: a restored handle has the same buckets
+    (arena names included) and keeps behaving exactly like the original:
+    the same later batch (inserts, incasts, -0.0, Takes) gives the same
+    outputs and the same table, which also equals the oracle's.  A handle of
+    another table size refuses the image."""
+    rng = np.random.default_rng(93)
+    K = 4000
+    g, o = _seed_both(pa, rng, K, log2_slots=14)
+    n = 30000
+    ids = _gen.zipf_ids(rng, n, K + 600)
+    names = [(b"an-arena-length-bucket-name-%d" % i) if i % 7 == 0 else (b"b%d" % i) for i in ids]
+    a, t, e = _gen.dirty_states(rng, n, 0.05)
+    g.receive_soa(names, a, t, e, _gen.T0 + SEC)
+    o.receive_soa(names, a, t, e, _gen.T0 + SEC)
+    path = str(tmp_path / "table.snap")
+    g.snapshot(path)
+    r = pa.GPURepo(log2_slots=14)
+    r.restore(path)
+    assert len(r) == len(g)
+    assert gpu_dump(r) == gpu_dump(g)
+    ids2 = _gen.zipf_ids(rng, n, K + 1200)
+    names2 = [(b"an-arena-length-bucket-name-%d" % i) if i % 7 == 0 else (b"b%d" % i) for i in ids2]
+    kind = rng.choice(np.array([0, 1, 2], np.uint8), n, p=[0.5, 0.45, 0.05])
+    now = _gen.T0 + 2 * SEC + np.arange(n, dtype=np.int64) * 1000
+    freq = rng.choice(np.array([1, 100, 1000], np.int64), n)
+    per = np.full(n, SEC, np.int64)
+    cnt = rng.integers(1, 3, n).astype(np.uint64)
+    a2, t2, e2 = _gen.dirty_states(rng, n, 0.02)
+    outs = [x.apply_mixed(kind, names2, now, freq, per, cnt, a2, t2, e2) for x in (g, r)]
+    for k in ("status", "remaining", "have"):
+        assert np.array_equal(outs[0][k], outs[1][k]), k
+    o.apply_mixed(kind, names2, now, freq, per, cnt, a2, t2, e2)
+    assert gpu_dump(r) == gpu_dump(g)
+    assert_same_dump(gpu_dump(r), o.dump())
+    other = pa.GPURepo(log2_slots=15)
+    with pytest.raises(pa.PatrolHipError):
+        other.restore(path)
