@@ -69,7 +69,9 @@ typedef enum phip_err {
   PHIP_ERR_ARENA = -4,          /* long-name arena exhausted */
   PHIP_ERR_SHORT_BUFFER = -5,   /* io.ErrShortBuffer from a datagram (bucket.go:72,84) */
   PHIP_ERR_NAME_TOO_LARGE = -6, /* ErrNameTooLarge (bucket.go:48) */
-  PHIP_ERR_NO_DEVICE = -7
+  PHIP_ERR_NO_DEVICE = -7,
+  PHIP_ERR_IO = -8,             /* socket error (phip_udp_*; errno holds the cause) */
+  PHIP_ERR_BUSY = -9            /* ring slot not available (phip_ring_*) */
 } phip_err;
 
 /* Per-op status codes (one uint8 per op). */
@@ -237,6 +239,67 @@ int phip_marshal(const uint8_t* name, uint32_t len, const phip_state* s, uint8_t
 int phip_api_take(phip_handle* h, const uint8_t* name, uint32_t len, const char* rate,
                   uint32_t rate_len, const char* count, uint32_t count_len, int64_t now,
                   char* body, uint32_t* body_len);
+
+/* ---- batched UDP ingest (command.go's replicator) ----
+ * The reference's Receive goroutine reads ONE datagram per iteration into a
+ * 256-byte buffer under a 3 s deadline (repo.go:54-73,108-120) and answers
+ * each incast with its own WriteTo (repo.go:86-90,160-169).  The batched
+ * pipeline is:
+ *
+ *   phip_ring_acquire      a free pinned host slot (bytes + offs arrays)
+ *   phip_udp_recv_batch    recvmmsg straight into that slot
+ *   phip_ring_submit       hipMemcpyAsync of the slot on the ring's copy
+ *                          stream (returns at once; the next slot can be
+ *                          filled while this one is copied and merged)
+ *   phip_ring_receive      the handle's stream waits for the copy, then
+ *                          phip_receive_datagrams over the device copy;
+ *                          results land in host buffers; the slot is freed
+ *   phip_incast_replies +  MarshalBinary of the batch's INCAST_REPLY states
+ *   phip_udp_send_batch    and one sendmmsg back to their peers
+ *
+ * Peers are sockaddr_storage records (PHIP_PEER_BYTES each). */
+#define PHIP_PEER_BYTES 128
+
+typedef struct phip_ring phip_ring;
+/* nslots pinned slots of max_msgs datagrams / max_bytes bytes each (max_bytes
+ * >= 256 * max_msgs lets phip_udp_recv_batch fill a slot to max_msgs). */
+int phip_ring_open(phip_handle* h, uint32_t nslots, uint32_t max_msgs, uint64_t max_bytes,
+                   phip_ring** out);
+void phip_ring_close(phip_ring* r);
+/* The next slot in ring order, if it is free (PHIP_ERR_BUSY: that slot is
+ * still submitted and not yet received).  *bytes / *offs are pinned host
+ * arrays of max_bytes and max_msgs + 1 entries; the caller writes datagram i
+ * to bytes[offs[i] .. offs[i+1]) with offs[0] = 0. */
+int phip_ring_acquire(phip_ring* r, uint32_t* slot, uint8_t** bytes, uint64_t** offs);
+/* Start the host->device copy of the slot's first n datagrams. */
+int phip_ring_submit(phip_ring* r, uint32_t slot, uint32_t n);
+/* ReplicatedRepo.Receive over a submitted slot (phip_receive_datagrams
+ * semantics; res holds host pointers) and release the slot.  Slots must be
+ * received in the order they were submitted. */
+int phip_ring_receive(phip_ring* r, uint32_t slot, int64_t now, const phip_results* res,
+                      uint32_t* stop_index);
+
+/* recvmmsg up to max_msgs datagrams from fd: waits up to timeout_ms for the
+ * first (a timeout returns PHIP_OK with *n_out = 0, as the Go loop continues
+ * on a Timeout error), then takes what is queued without waiting.  Each
+ * datagram is cut at PHIP_BUCKET_PACKET_SIZE bytes (Go's read buffer) and
+ * packed back to back: datagram i is bytes[offs[i] .. offs[i+1]), offs[0] = 0.
+ * peers (optional) receives each sender's address. */
+int phip_udp_recv_batch(int fd, uint8_t* bytes, uint64_t cap, uint64_t* offs, uint32_t max_msgs,
+                        uint8_t* peers, int timeout_ms, uint32_t* n_out);
+/* MarshalBinary (bucket.go:51-68) of reply[i] under datagram i's name for
+ * every message whose status is PHIP_ST_INCAST_REPLY, in batch order, packed
+ * into out / out_offs (as phip_udp_recv_batch packs); out_peers (optional)
+ * receives the matching peers[i]. */
+int phip_incast_replies(const uint8_t* bytes, const uint64_t* offs, uint32_t n,
+                        const uint8_t* status, const phip_state* reply, const uint8_t* peers,
+                        uint8_t* out, uint64_t cap, uint64_t* out_offs, uint8_t* out_peers,
+                        uint32_t* n_out);
+/* sendmmsg datagrams bytes[offs[i] .. offs[i+1]) for i < n, datagram i to
+ * peers + i * peer_stride (stride 0: every datagram to one peer, e.g. an
+ * egress batch from phip_export_datagrams; peers NULL: a connected socket). */
+int phip_udp_send_batch(int fd, const uint8_t* bytes, const uint64_t* offs, uint32_t n,
+                        const uint8_t* peers, uint32_t peer_stride, uint32_t* sent_out);
 
 /* ---- shard layer ---- */
 /* FNV-1a 64 of each name (the table's probe key; also the shard map:

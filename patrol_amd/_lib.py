@@ -21,11 +21,14 @@ EXPORTS = [
     "phip_marshal", "phip_api_take", "phip_last_timings", "phip_set_timing", "phip_last_stats", "phip_hash_names",
     "phip_ae_local_max", "phip_ae_apply", "phip_set_stream", "phip_route_pack",
     "phip_export_datagrams", "phip_snapshot_bytes", "phip_snapshot", "phip_restore",
+    "phip_ring_open", "phip_ring_close", "phip_ring_acquire", "phip_ring_submit",
+    "phip_ring_receive", "phip_udp_recv_batch", "phip_incast_replies", "phip_udp_send_batch",
 ]
 
 PHIP_OK = 0
 PHIP_ERR = {-1: "INVALID", -2: "HIP", -3: "FULL", -4: "ARENA", -5: "SHORT_BUFFER",
-            -6: "NAME_TOO_LARGE", -7: "NO_DEVICE"}
+            -6: "NAME_TOO_LARGE", -7: "NO_DEVICE", -8: "IO", -9: "BUSY"}
+PEER_BYTES = 128   # PHIP_PEER_BYTES = sizeof(struct sockaddr_storage)
 ST_MERGED, ST_INCAST_REPLY, ST_INCAST_NOREPLY, ST_SHORT, ST_NOT_PROCESSED = 1, 2, 3, 4, 5
 ST_TAKE_OK, ST_TAKE_DENIED, ST_UPSERT_INSERTED, ST_CREATED = 6, 7, 8, 0x80
 OP_TAKE, OP_RECEIVE, OP_UPSERT = 0, 1, 2
@@ -72,6 +75,14 @@ def load(path: str = LIB_PATH):
     if not os.path.exists(path):
         raise OSError(f"libpatrolhip.so not built at {path}: run `make -C patrol_amd` "
                       "or __graft_entry__.build()")
+    # One HIP runtime per process: torch ships its own libamdhip64.so.7 (same
+    # soname as /opt/rocm's), and whichever is loaded first serves both.  The
+    # engine shares streams and device memory with torch, so torch's runtime
+    # must be the one: load it before this library when torch is present.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = C.CDLL(path)
     vp, u32, u64, i64 = C.c_void_p, C.c_uint32, C.c_uint64, C.c_int64
     L.phip_abi_version.restype = C.c_int
@@ -113,5 +124,14 @@ def load(path: str = LIB_PATH):
     L.phip_ae_apply.argtypes = [vp, vp, u32, u64, vp, u32]
     L.phip_set_stream.argtypes = [vp, vp]
     L.phip_route_pack.argtypes = [vp, C.POINTER(phip_msgs), u32, vp, vp, vp, vp, vp, vp, vp, u32]
+    L.phip_ring_open.argtypes = [vp, u32, u32, u64, C.POINTER(vp)]
+    L.phip_ring_close.argtypes = [vp]
+    L.phip_ring_close.restype = None
+    L.phip_ring_acquire.argtypes = [vp, C.POINTER(u32), C.POINTER(vp), C.POINTER(vp)]
+    L.phip_ring_submit.argtypes = [vp, u32, u32]
+    L.phip_ring_receive.argtypes = [vp, u32, i64, C.POINTER(phip_results), C.POINTER(u32)]
+    L.phip_udp_recv_batch.argtypes = [C.c_int, vp, u64, vp, u32, vp, C.c_int, C.POINTER(u32)]
+    L.phip_incast_replies.argtypes = [vp, vp, u32, vp, vp, vp, vp, u64, vp, vp, C.POINTER(u32)]
+    L.phip_udp_send_batch.argtypes = [C.c_int, vp, vp, u32, vp, u32, C.POINTER(u32)]
     _lib = L
     return L

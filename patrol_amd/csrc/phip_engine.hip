@@ -1009,21 +1009,15 @@ int phip_receive_soa(phip_handle* h, const phip_msgs* m, int64_t now, const phip
   return copy_outputs(h, res, n, dev, ow);
 }
 
-int phip_receive_datagrams(phip_handle* h, const uint8_t* bytes, const uint64_t* offs, uint32_t n,
-                           int64_t now, const phip_results* res, uint32_t* stop_index,
-                           uint32_t flags) {
-  if (!h || (n && (!bytes || !offs))) return PHIP_ERR_INVALID;
-  std::lock_guard<std::mutex> g(h->mu);
-  begin_call(h);
-  if (stop_index) *stop_index = n;
-  if (n == 0) return PHIP_OK;
-  bool dev = flags & PHIP_DEVICE_PTRS;
+}  // extern "C"
+
+namespace {
+// ReplicatedRepo.Receive over datagrams already in device memory (the
+// caller's, the staging buffers, or a ring slot's copy); results go to
+// device (dev) or host buffers.  Called with the handle's mutex held.
+int receive_datagrams_dev(phip_handle* h, const u8* d_bytes, const uint64_t* d_offs, u32 n,
+                          int64_t now, const phip_results* res, uint32_t* stop_index, bool dev) {
   int rc;
-  const uint64_t* d_offs;
-  const u8* d_bytes;
-  if ((rc = stage(h, B_DOFFS, offs, (size_t)n + 1, dev, &d_offs))) return rc;
-  size_t nb = dev ? 0 : offs[n];
-  if ((rc = stage(h, B_BYTES, bytes, nb, dev, &d_bytes))) return rc;
   OutView ow{};
   if ((rc = outputs(h, res, n, dev, &ow))) return rc;
   // Fast path straight from the wire bytes: k_classify reads the headers
@@ -1066,6 +1060,169 @@ int phip_receive_datagrams(phip_handle* h, const uint8_t* bytes, const uint64_t*
   if (stop_index) *stop_index = stop;
   if (stop < n) return set_err(h, PHIP_ERR_SHORT_BUFFER, "short buffer at datagram %u", stop);
   return PHIP_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int phip_receive_datagrams(phip_handle* h, const uint8_t* bytes, const uint64_t* offs, uint32_t n,
+                           int64_t now, const phip_results* res, uint32_t* stop_index,
+                           uint32_t flags) {
+  if (!h || (n && (!bytes || !offs))) return PHIP_ERR_INVALID;
+  std::lock_guard<std::mutex> g(h->mu);
+  begin_call(h);
+  if (stop_index) *stop_index = n;
+  if (n == 0) return PHIP_OK;
+  bool dev = flags & PHIP_DEVICE_PTRS;
+  int rc;
+  const uint64_t* d_offs;
+  const u8* d_bytes;
+  if ((rc = stage(h, B_DOFFS, offs, (size_t)n + 1, dev, &d_offs))) return rc;
+  size_t nb = dev ? 0 : offs[n];
+  if ((rc = stage(h, B_BYTES, bytes, nb, dev, &d_bytes))) return rc;
+  return receive_datagrams_dev(h, d_bytes, d_offs, n, now, res, stop_index, dev);
+}
+
+// ------------------------------------------------------------ ingest ring --
+// Pinned host slots, each with its own device copy; the copies run on the
+// ring's stream, so filling and copying slot k+1 overlaps merging slot k.
+struct phip_ring {
+  phip_handle* h = nullptr;
+  hipStream_t copy = nullptr;
+  std::mutex mu;
+  u32 max_msgs = 0;
+  u64 max_bytes = 0;
+  enum State { kFree, kAcquired, kSubmitted };
+  struct Slot {
+    u8* hbytes = nullptr;
+    uint64_t* hoffs = nullptr;
+    u8* dbytes = nullptr;
+    uint64_t* doffs = nullptr;
+    hipEvent_t copied = nullptr;
+    u32 n = 0;
+    State state = kFree;
+  };
+  std::vector<Slot> slots;
+  u32 next_acquire = 0, next_receive = 0;
+  std::string err;
+};
+
+void phip_ring_close(phip_ring* r) {
+  if (!r) return;
+  hipSetDevice(r->h->device);
+  if (r->copy) hipStreamSynchronize(r->copy);
+  for (auto& s : r->slots) {
+    if (s.hbytes) hipHostFree(s.hbytes);
+    if (s.hoffs) hipHostFree(s.hoffs);
+    if (s.dbytes) hipFree(s.dbytes);
+    if (s.doffs) hipFree(s.doffs);
+    if (s.copied) hipEventDestroy(s.copied);
+  }
+  if (r->copy) hipStreamDestroy(r->copy);
+  delete r;
+}
+
+int phip_ring_open(phip_handle* h, uint32_t nslots, uint32_t max_msgs, uint64_t max_bytes,
+                   phip_ring** out) {
+  if (!out) return PHIP_ERR_INVALID;
+  *out = nullptr;
+  if (!h || nslots < 1 || nslots > 64 || max_msgs < 1 || max_bytes < 1) return PHIP_ERR_INVALID;
+  std::lock_guard<std::mutex> g(h->mu);
+  begin_call(h);
+  phip_ring* r = new phip_ring;
+  r->h = h;
+  r->max_msgs = max_msgs;
+  r->max_bytes = max_bytes;
+  r->slots.resize(nslots);
+  auto fail = [&](hipError_t e, const char* what) {
+    set_err(h, PHIP_ERR_HIP, "phip_ring_open: %s failed: %s", what, hipGetErrorString(e));
+    phip_ring_close(r);
+    return PHIP_ERR_HIP;
+  };
+  hipError_t e;
+  if ((e = hipStreamCreateWithFlags(&r->copy, hipStreamNonBlocking)) != hipSuccess)
+    return fail(e, "hipStreamCreate");
+  // +64: the fast path's 8-byte over-read slack past the last datagram.
+  const size_t nbytes = max_bytes + 64, noffs = ((size_t)max_msgs + 1) * sizeof(uint64_t);
+  for (auto& s : r->slots) {
+    if ((e = hipHostMalloc(&s.hbytes, nbytes, 0)) != hipSuccess) return fail(e, "hipHostMalloc");
+    if ((e = hipHostMalloc(&s.hoffs, noffs, 0)) != hipSuccess) return fail(e, "hipHostMalloc");
+    if ((e = hipMalloc(&s.dbytes, nbytes)) != hipSuccess) return fail(e, "hipMalloc");
+    if ((e = hipMalloc(&s.doffs, noffs)) != hipSuccess) return fail(e, "hipMalloc");
+    if ((e = hipEventCreateWithFlags(&s.copied, hipEventDisableTiming)) != hipSuccess)
+      return fail(e, "hipEventCreate");
+    s.hoffs[0] = 0;
+  }
+  *out = r;
+  return PHIP_OK;
+}
+
+int phip_ring_acquire(phip_ring* r, uint32_t* slot, uint8_t** bytes, uint64_t** offs) {
+  if (!r || !slot || !bytes || !offs) return PHIP_ERR_INVALID;
+  std::lock_guard<std::mutex> g(r->mu);
+  phip_ring::Slot& s = r->slots[r->next_acquire];
+  if (s.state != phip_ring::kFree) return PHIP_ERR_BUSY;
+  s.state = phip_ring::kAcquired;
+  *slot = r->next_acquire;
+  *bytes = s.hbytes;
+  *offs = s.hoffs;
+  s.hoffs[0] = 0;
+  r->next_acquire = (r->next_acquire + 1) % (u32)r->slots.size();
+  return PHIP_OK;
+}
+
+int phip_ring_submit(phip_ring* r, uint32_t slot, uint32_t n) {
+  if (!r || slot >= r->slots.size() || n > r->max_msgs) return PHIP_ERR_INVALID;
+  std::lock_guard<std::mutex> g(r->mu);
+  phip_ring::Slot& s = r->slots[slot];
+  if (s.state != phip_ring::kAcquired) return PHIP_ERR_BUSY;
+  const u64 nb = s.hoffs[n];
+  if (s.hoffs[0] != 0 || nb > r->max_bytes) return PHIP_ERR_INVALID;
+  hipSetDevice(r->h->device);
+  hipError_t e;
+  if ((e = hipMemcpyAsync(s.doffs, s.hoffs, ((size_t)n + 1) * sizeof(uint64_t),
+                          hipMemcpyHostToDevice, r->copy)) != hipSuccess ||
+      (nb && (e = hipMemcpyAsync(s.dbytes, s.hbytes, nb, hipMemcpyHostToDevice, r->copy)) !=
+                 hipSuccess) ||
+      (e = hipEventRecord(s.copied, r->copy)) != hipSuccess) {
+    r->err = hipGetErrorString(e);
+    return PHIP_ERR_HIP;
+  }
+  s.n = n;
+  s.state = phip_ring::kSubmitted;
+  return PHIP_OK;
+}
+
+int phip_ring_receive(phip_ring* r, uint32_t slot, int64_t now, const phip_results* res,
+                      uint32_t* stop_index) {
+  if (!r || slot >= r->slots.size()) return PHIP_ERR_INVALID;
+  phip_ring::Slot* s;
+  {
+    std::lock_guard<std::mutex> g(r->mu);
+    s = &r->slots[slot];
+    if (s->state != phip_ring::kSubmitted || slot != r->next_receive) return PHIP_ERR_BUSY;
+  }
+  phip_handle* h = r->h;
+  int rc;
+  {
+    std::lock_guard<std::mutex> g(h->mu);
+    begin_call(h);
+    if (stop_index) *stop_index = s->n;
+    hipError_t e = hipStreamWaitEvent(h->stream, s->copied, 0);
+    if (e != hipSuccess)
+      rc = set_err(h, PHIP_ERR_HIP, "hipStreamWaitEvent: %s", hipGetErrorString(e));
+    else if (s->n == 0)
+      rc = PHIP_OK;
+    else
+      rc = receive_datagrams_dev(h, s->dbytes, s->doffs, s->n, now, res, stop_index, false);
+    // On success the stream has drained (results copied back), so the slot's
+    // host and device buffers are free; after an error wait for them first.
+    if (rc) hipStreamSynchronize(h->stream);
+  }
+  std::lock_guard<std::mutex> g(r->mu);
+  s->state = phip_ring::kFree;
+  r->next_receive = (r->next_receive + 1) % (u32)r->slots.size();
+  return rc;
 }
 
 int phip_upsert_soa(phip_handle* h, const phip_msgs* m, int64_t now, const phip_results* res,

@@ -440,6 +440,9 @@ __global__ void k_hot_build(const u32* __restrict__ ckeys, const u32* __restrict
 #ifndef PHIP_FAST_PER_CU
 #define PHIP_FAST_PER_CU 4
 #endif
+#ifndef PHIP_FAST_PIPE
+#define PHIP_FAST_PIPE 1
+#endif
 constexpr u32 kFastBlock = PHIP_FAST_BLOCK;
 constexpr u32 kFastPerCU = PHIP_FAST_PER_CU;   // resident workgroups per CU (LDS-bound)
 
@@ -454,9 +457,18 @@ struct SoaIn {   // decoded messages (phip_receive_soa / decoded datagrams)
   const uint64_t* mt;
   const int64_t* me;
   __device__ inline const u8* blob() const { return src.blob; }
-  __device__ inline void load(u32 i, u64& off, u32& len, u64& w0, u64& w1, u64& w2, u64& ra,
-                              u64& rt, i64& re) const {
-    src.template get<true>(i, off, len);
+  // Round 1 of a message on its own (the name's offset and length), so the
+  // fast kernel can issue it one chunk ahead.
+  // (Src = NamesOffs: the two u32 offsets as loaded.)
+  struct Pre { u32 a, b; };
+  __device__ inline Pre pre(u32 i) const {
+    static_assert(std::is_same<Src, NamesOffs>::value, "fast path input: names + u32 offsets");
+    return Pre{ld<true>(src.offs + i), ld<true>(src.offs + i + 1)};
+  }
+  // Round 2 given round 1: the name words and the replica fields.
+  __device__ inline void load(u32 i, const Pre& p, u64& off, u32& len, u64& w0, u64& w1, u64& w2,
+                              u64& ra, u64& rt, i64& re) const {
+    off = p.a; len = p.b - p.a;
     ra = ld<true>(ma + i); rt = ld<true>(mt + i); re = ld<true>(me + i);
     load_words3<false>(src.blob, off, len, w0, w1, w2);
   }
@@ -482,9 +494,14 @@ struct WireIn {
   const u8* bytes;
   const uint64_t* offs;
   __device__ inline const u8* blob() const { return bytes; }
-  __device__ inline void load(u32 i, u64& off, u32& len, u64& w0, u64& w1, u64& w2, u64& ra,
-                              u64& rt, i64& re) const {
+  struct Pre { u64 o; u32 sz; };   // round 1: the datagram's start and size
+  __device__ inline Pre pre(u32 i) const {
     const u64 o = ld<true>(offs + i), end = ld<true>(offs + i + 1);
+    return Pre{o, (u32)min(end - o, (u64)0xFFFFFFFFu)};
+  }
+  __device__ inline void load(u32 i, const Pre& pr, u64& off, u32& len, u64& w0, u64& w1, u64& w2,
+                              u64& ra, u64& rt, i64& re) const {
+    const u64 o = pr.o, end = pr.o + pr.sz;
     const u64* p = reinterpret_cast<const u64*>(bytes);
     const u64 last = (end > o ? end - 1 : o) >> 3;   // word of the datagram's last byte
     const u64 hb = o >> 3;
@@ -569,17 +586,28 @@ __global__ __launch_bounds__(kFastBlock) __attribute__((amdgpu_waves_per_eu(8, 8
   constexpr u32 kWaves = kFastBlock / 64;
   const u32 lane = threadIdx.x & 63;
   const u32 nchunks = (n + 63) / 64;
+  const u32 cstride = gridDim.x * kWaves;
   u32 hits = 0;
-  for (u32 chunk = blockIdx.x * kWaves + threadIdx.x / 64; chunk < nchunks;
-       chunk += gridDim.x * kWaves) {
+  // Round 1 (the name offsets) runs one chunk ahead: a chunk's dependent
+  // chain is then name words -> home slot, and the next chunk's offsets
+  // arrive meanwhile.
+  u32 chunk = blockIdx.x * kWaves + threadIdx.x / 64;
+  typename In::Pre pre{};
+  if (chunk < nchunks) pre = in.pre(min(chunk * 64 + lane, n - 1));
+  for (; chunk < nchunks; chunk += cstride) {
     const u32 tid = chunk * 64 + lane;
     const bool valid = tid < n;
     const u32 i = valid ? tid : n - 1;
-    // rounds 1-2: offsets, then the name words and replica fields
+    // round 2: the name words and replica fields
     u64 off, w0, w1, w2, ra, rt;
     u32 len;
     i64 re;
-    in.load(i, off, len, w0, w1, w2, ra, rt, re);
+#if PHIP_FAST_PIPE
+    in.load(i, pre, off, len, w0, w1, w2, ra, rt, re);
+    if (chunk + cstride < nchunks) pre = in.pre(min((chunk + cstride) * 64 + lane, n - 1));
+#else
+    in.load(i, in.pre(i), off, len, w0, w1, w2, ra, rt, re);
+#endif
     Name nm;
     short_name(w0, w1, w2, off, len, nm);
     const bool shortname = len <= kShortName;

@@ -348,6 +348,138 @@ class GPURepo:
         return code, body.raw[:bl.value].decode()
 
 
+class Ring:
+    """Pinned ingest ring over a GPURepo (phip_ring_*, include/patrolhip.h):
+    the batched form of the Receive goroutine (repo.go:54-92).  Slots are
+    filled in host memory (fill(), or recv() from a UDP socket), submitted
+    (an async host->device copy on the ring's own stream) and received in
+    order; submitting slot k+1 before receiving slot k overlaps its copy with
+    slot k's merge."""
+
+    def __init__(self, repo: "GPURepo", nslots: int = 3, max_msgs: int = 1 << 16,
+                 max_bytes: int | None = None):
+        self.repo, self.L = repo, repo.L
+        self.max_msgs = max_msgs
+        self.max_bytes = max_bytes if max_bytes is not None else 256 * max_msgs
+        r = C.c_void_p()
+        repo._check(self.L.phip_ring_open(repo.h, nslots, max_msgs, self.max_bytes, C.byref(r)))
+        self.r = r
+        self._views = {}
+
+    def close(self):
+        if getattr(self, "r", None):
+            self.L.phip_ring_close(self.r)
+            self.r = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def acquire(self):
+        """-> (slot, bytes view uint8[max_bytes], offs view uint64[max_msgs+1])."""
+        slot, b, o = C.c_uint32(), C.c_void_p(), C.c_void_p()
+        self.repo._check(self.L.phip_ring_acquire(self.r, C.byref(slot), C.byref(b), C.byref(o)))
+        bv = np.ctypeslib.as_array(C.cast(b, C.POINTER(C.c_uint8)), (self.max_bytes,))
+        ov = np.ctypeslib.as_array(C.cast(o, C.POINTER(C.c_uint64)), (self.max_msgs + 1,))
+        return slot.value, bv, ov
+
+    def fill(self, datagrams: Sequence[bytes]):
+        """Acquire a slot and pack `datagrams` into it -> (slot, n)."""
+        slot, bv, ov = self.acquire()
+        n = len(datagrams)
+        if n > self.max_msgs:
+            raise ValueError("batch larger than the ring's slots")
+        ov[0] = 0
+        if n:
+            ov[1:n + 1] = np.cumsum([len(d) for d in datagrams])
+            bv[:int(ov[n])] = np.frombuffer(b"".join(datagrams), np.uint8)
+        return slot, n
+
+    def recv(self, sock, timeout_ms: int = 3000, peers: bool = True):
+        """Acquire a slot and fill it from a UDP socket (phip_udp_recv_batch)
+        -> (slot, n, peers uint8[n, PEER_BYTES] or None)."""
+        slot, bv, ov = self.acquire()
+        pbuf = np.zeros((self.max_msgs, _lib.PEER_BYTES), np.uint8) if peers else None
+        n = C.c_uint32()
+        self.repo._check(self.L.phip_udp_recv_batch(sock.fileno(), bv.ctypes.data, self.max_bytes,
+                                                    ov.ctypes.data, self.max_msgs, _ptr(pbuf),
+                                                    int(timeout_ms), C.byref(n)))
+        return slot, n.value, (pbuf[:n.value] if peers else None)
+
+    def submit(self, slot: int, n: int):
+        self.repo._check(self.L.phip_ring_submit(self.r, slot, n))
+
+    def receive(self, slot: int, n: int, now: int, want_reply: bool = True,
+                want_status: bool = True, status=None):
+        """-> dict(status, reply, stop) as GPURepo.receive_datagrams.
+        `status`: a caller uint8[>= n] array to fill instead of a new one."""
+        if status is not None:
+            res, reply = phip_results(status.ctypes.data, None, None, None), None
+        elif want_status or want_reply:
+            res, status, _, _, reply = GPURepo._results(n, want_reply=want_reply)
+        else:
+            res, reply = None, None
+        stop = C.c_uint32()
+        self.repo._check(self.L.phip_ring_receive(self.r, slot, int(now),
+                                                  C.byref(res) if res is not None else None,
+                                                  C.byref(stop)), allow=(-5,))
+        return dict(status=status[:n] if status is not None else None,
+                    reply=reply[:n] if reply is not None else None, stop=stop.value)
+
+
+def udp_send_batch(sock, data: bytes | np.ndarray, offs: np.ndarray, peers=None,
+                   peer_stride: int = 0) -> int:
+    """sendmmsg of datagrams data[offs[i]:offs[i+1]] (phip_udp_send_batch)."""
+    L = _lib.load()
+    buf = np.frombuffer(data, np.uint8) if isinstance(data, (bytes, bytearray)) else data
+    offs = np.ascontiguousarray(offs, np.uint64)
+    sent = C.c_uint32()
+    rc = L.phip_udp_send_batch(sock.fileno(), buf.ctypes.data if buf.size else None,
+                               offs.ctypes.data, len(offs) - 1, _ptr(peers), peer_stride,
+                               C.byref(sent))
+    if rc != 0:
+        raise PatrolHipError(rc, "sendmmsg failed")
+    return sent.value
+
+
+def udp_recv_batch(sock, max_msgs: int, timeout_ms: int = 3000, cap: int | None = None):
+    """recvmmsg into plain host arrays (phip_udp_recv_batch) ->
+    (list of datagrams, peers uint8[n, PEER_BYTES])."""
+    L = _lib.load()
+    cap = cap if cap is not None else 256 * max_msgs
+    buf = np.zeros(cap + 8, np.uint8)
+    offs = np.zeros(max_msgs + 1, np.uint64)
+    peers = np.zeros((max(max_msgs, 1), _lib.PEER_BYTES), np.uint8)
+    n = C.c_uint32()
+    rc = L.phip_udp_recv_batch(sock.fileno(), buf.ctypes.data, cap, offs.ctypes.data, max_msgs,
+                               peers.ctypes.data, int(timeout_ms), C.byref(n))
+    if rc != 0:
+        raise PatrolHipError(rc, "recvmmsg failed")
+    k = n.value
+    return [bytes(buf[int(offs[i]):int(offs[i + 1])]) for i in range(k)], peers[:k]
+
+
+def incast_replies(data: np.ndarray, offs: np.ndarray, status, reply, peers=None):
+    """phip_incast_replies -> (packed replies uint8, offs uint64[m+1], peers or None)."""
+    L = _lib.load()
+    n = len(offs) - 1
+    status = np.ascontiguousarray(status, np.uint8)
+    cap = 256 * max(n, 1)
+    out = np.zeros(cap, np.uint8)
+    oo = np.zeros(n + 1, np.uint64)
+    op = np.zeros((max(n, 1), _lib.PEER_BYTES), np.uint8) if peers is not None else None
+    m = C.c_uint32()
+    rc = L.phip_incast_replies(data.ctypes.data, offs.ctypes.data, n, status.ctypes.data,
+                               reply.ctypes.data, _ptr(peers), out.ctypes.data, cap,
+                               oo.ctypes.data, _ptr(op), C.byref(m))
+    if rc != 0:
+        raise PatrolHipError(rc, "incast replies")
+    k = m.value
+    return out[:int(oo[k])], oo[:k + 1], (op[:k] if op is not None else None)
+
+
 def parse_rate(s: bytes):
     """ParseRate (bucket.go:102-123): (freq, per_ns, ok) with Go's error values."""
     L = _lib.load()
