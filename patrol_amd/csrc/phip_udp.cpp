@@ -115,7 +115,7 @@ int phip_incast_replies(const uint8_t* bytes, const uint64_t* offs, uint32_t n,
     const int sz = phip_marshal(d + PHIP_BUCKET_FIXED_SIZE, len, &reply[i], out + pos);
     if (sz < 0) return sz;
     if (peers && out_peers)
-      std::memcpy(out_peers + (uint64_t)m * PHIP_PEER_BYTES, peers + (uint64_t)i * PHIP_PEER_BYTES,
+      std::memmove(out_peers + (uint64_t)m * PHIP_PEER_BYTES, peers + (uint64_t)i * PHIP_PEER_BYTES,
                   PHIP_PEER_BYTES);
     pos += (uint64_t)sz;
     out_offs[++m] = pos;
