@@ -310,7 +310,7 @@ int build_hot(phip_handle* h, Src src, u32 n, hipStream_t st, const HotHdr** hdr
   {
     Launch l(h, "k_hot_select", st);
     k_hot_hist<<<grid_for(kCnt), kBlock, 0, st>>>(ccnt, hist);
-    k_hot_select<<<1, 256, 0, st>>>(hist, hdr);
+    k_hot_select<<<1, 256, 0, st>>>(hist, hdr, kHotMax);
     k_hot_build<<<grid_for(kCnt), kBlock, 0, st>>>(ckeys, ccnt, hdr, table(h), dir);
   }
   HIPCHK(h, hipGetLastError());
@@ -1385,7 +1385,7 @@ int phip_route_pack(phip_handle* h, const phip_msgs* m, uint32_t world, uint8_t*
     constexpr size_t kCnt = size_t(1) << kHotCntBits;
     const size_t zero_bytes = 3 * kCnt * sizeof(u32) + kHotHist * sizeof(u32) + sizeof(HotHdr);
     u8* hb;
-    if ((rc = ensure(h, B_HOT, zero_bytes + kHotMax * sizeof(RouteHot), &hb))) return rc;
+    if ((rc = ensure(h, B_HOT, zero_bytes + kRouteHotMax * sizeof(RouteHot), &hb))) return rc;
     u32* ckeys = (u32*)hb;
     u32* ccnt = ckeys + kCnt;
     u32* cidx = ccnt + kCnt;
@@ -1400,7 +1400,7 @@ int phip_route_pack(phip_handle* h, const phip_msgs* m, uint32_t world, uint8_t*
       k_route_sample<NamesOffs><<<grid_for(nsample, kHotSamplePerBlock), 256, 0, h->stream>>>(
           src, n, stride, nsample, ckeys, ccnt, cidx);
       k_hot_hist<<<grid_for(kCnt), kBlock, 0, h->stream>>>(ccnt, hist);
-      k_hot_select<<<1, 256, 0, h->stream>>>(hist, hdr);
+      k_hot_select<<<1, 256, 0, h->stream>>>(hist, hdr, kRouteHotMax);
       k_route_dir_build<NamesOffs><<<grid_for(kCnt), kBlock, 0, h->stream>>>(ckeys, ccnt, cidx, hdr,
                                                                              src, world, d);
     }

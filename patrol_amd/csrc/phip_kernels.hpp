@@ -287,8 +287,8 @@ __device__ inline u64 enc_replica_nz(u64 b) {
 }
 
 // ------------------------------------------------- hot-bucket directory --
-// Zipf-skewed batches put most messages on a few buckets (C2: the top 512 of
-// 10M buckets carry 61% of the messages).  Before the fast kernel runs, a
+// Zipf-skewed batches put most messages on a few buckets (C2: the top 384 of
+// 10M buckets carry 59% of the messages).  Before the fast kernel runs, a
 // strided sample of the batch is resolved and counted; the (at most kHotMax)
 // buckets sampled most often form the batch's hot directory.  Every fast
 // workgroup keeps the directory in LDS and folds the messages of those
@@ -299,13 +299,17 @@ __device__ inline u64 enc_replica_nz(u64 b) {
 // (PHIP_HOT_MAX / PHIP_HOT_LDS / PHIP_FAST_BLOCK / PHIP_FAST_PER_CU override
 // the defaults for tuning builds, tools/build_variants.sh.)
 #ifndef PHIP_HOT_MAX
-#define PHIP_HOT_MAX 512
+#define PHIP_HOT_MAX 384
 #endif
 #ifndef PHIP_HOT_LDS
 #define PHIP_HOT_LDS 1024
 #endif
 constexpr u32 kHotMax = PHIP_HOT_MAX;     // directory entries
 constexpr u32 kHotLds = PHIP_HOT_LDS;     // LDS lookup slots (power of 2, >= 1.5 * kHotMax)
+// The sender-side combine's directory (phip_route_pack): its own size, as its
+// kernels hold less per entry in LDS than k_receive_fast.
+constexpr u32 kRouteHotMax = 512;
+static_assert(kHotLds * 2 >= kRouteHotMax * 3 && kHotLds * 2 >= kHotMax * 3, "LDS lookup load");
 constexpr u32 kHotCntBits = 18;       // sample count table: 2^18 (slot+1, count) pairs
 constexpr u32 kHotSampleMax = 1u << 17;   // samples per batch (half the count table)
 constexpr u32 kHotSamplePerBlock = 1024;
@@ -377,8 +381,9 @@ __global__ void k_hot_hist(const u32* __restrict__ ccnt, u32* __restrict__ hist)
 }
 
 // One workgroup of 256: the lowest threshold t >= kHotMinCount with at most
-// kHotMax sampled slots counted t or more times.
-__global__ __launch_bounds__(256) void k_hot_select(const u32* __restrict__ hist, HotHdr* hdr) {
+// maxn sampled slots counted t or more times (maxn: the directory's size).
+__global__ __launch_bounds__(256) void k_hot_select(const u32* __restrict__ hist, HotHdr* hdr,
+                                                    u32 maxn) {
   constexpr u32 kPer = kHotHist / 256;
   __shared__ u32 part[256];
   __shared__ u32 best;
@@ -393,7 +398,7 @@ __global__ __launch_bounds__(256) void k_hot_select(const u32* __restrict__ hist
   u32 lo = kHotHist;
   for (int b = (int)kPer - 1; b >= 0; --b) {
     run += hist[t * kPer + b];
-    if (run <= kHotMax) lo = t * kPer + b;
+    if (run <= maxn) lo = t * kPer + b;
   }
   atomicMin(&best, lo);
   __syncthreads();
@@ -671,6 +676,9 @@ __global__ __launch_bounds__(kFastBlock) __attribute__((amdgpu_waves_per_eu(8, 8
   }
 
   // Directory flush: the workgroup's maxima, skipping fields already beaten.
+#ifdef PHIP_FAST_NOFLUSH   // timing experiments only (drops the hot buckets' merges)
+  return;
+#endif
   for (u32 j = threadIdx.x; j < nh; j += kFastBlock) {
     const u64 xa = hmax[0][j], xt = hmax[1][j], xe = hmax[2][j];
     if (!(xa | xt | xe)) continue;
@@ -1730,7 +1738,7 @@ __global__ void k_route_dir_build(const u32* __restrict__ ckeys, const u32* __re
   const u32 c = ccnt[e];
   if (!ckeys[e] || c < kHotMinCount || c < hdr->thresh) return;
   const u32 idx = atomicAdd(&hdr->n, 1u);
-  if (idx >= kHotMax) return;   // cannot happen: the threshold bounds the count
+  if (idx >= kRouteHotMax) return;   // cannot happen: the threshold bounds the count
   u64 off; u32 len;
   src.get(cidx[e], off, len);
   Name nm;
@@ -1740,13 +1748,13 @@ __global__ void k_route_dir_build(const u32* __restrict__ ckeys, const u32* __re
 
 struct RouteLds {   // the hot directory in LDS, open-addressed by name hash
   u32 slot[kHotLds];   // entry + 1 (0 = empty)
-  u64 h[kHotMax], w0[kHotMax], w1[kHotMax];
-  u32 owner[kHotMax];
+  u64 h[kRouteHotMax], w0[kRouteHotMax], w1[kRouteHotMax];
+  u32 owner[kRouteHotMax];
 };
 
 // Entries used by this launch: none without a directory or on a dirty batch.
 __device__ inline u32 route_hot_n(const HotHdr* hot, const u32* ctr) {
-  return (hot && ctr[kCtrDirty] == ~0u) ? min(hot->n, kHotMax) : 0u;
+  return (hot && ctr[kCtrDirty] == ~0u) ? min(hot->n, kRouteHotMax) : 0u;
 }
 
 __device__ inline void route_lds_load(RouteLds& L, const RouteHot* dir, u32 nh) {
@@ -1806,13 +1814,13 @@ __global__ __launch_bounds__(kRouteBlock) void k_route_count(
     u16* __restrict__ code, u32* __restrict__ cnt, u32* __restrict__ bytes) {
   __shared__ RouteLds L;
   __shared__ u32 wc[kRouteWaves][kRouteMaxWorld], wb[kRouteWaves][kRouteMaxWorld];
-  __shared__ u32 hit[kHotMax];
+  __shared__ u32 hit[kRouteHotMax];
   const u32 nh = route_hot_n(hot, ctr);
   const bool nonpos = nh && ctr[kCtrNonPos];
   for (u32 j = threadIdx.x; j < kRouteWaves * kRouteMaxWorld; j += kRouteBlock) {
     (&wc[0][0])[j] = 0; (&wb[0][0])[j] = 0;
   }
-  for (u32 j = threadIdx.x; j < kHotMax; j += kRouteBlock) hit[j] = 0;
+  for (u32 j = threadIdx.x; j < kRouteHotMax; j += kRouteBlock) hit[j] = 0;
   route_lds_load(L, dir, nh);
   __syncthreads();
   const u32 wave = threadIdx.x / 64, lane = threadIdx.x & 63;
@@ -1924,12 +1932,12 @@ __global__ __launch_bounds__(kRouteBlock) void k_route_scatter(
     uint64_t* __restrict__ out_t, int64_t* __restrict__ out_e) {
   __shared__ RouteLds L;
   __shared__ u32 run[kRouteWaves][kRouteMaxWorld], runb[kRouteWaves][kRouteMaxWorld];
-  __shared__ u64 hmax[3][kHotMax];
-  __shared__ u32 hit[kHotMax];
+  __shared__ u64 hmax[3][kRouteHotMax];
+  __shared__ u32 hit[kRouteHotMax];
   const u32 nh = route_hot_n(hot, ctr);
   const u32 wave = threadIdx.x / 64, lane = threadIdx.x & 63;
   const u32 tile = blockIdx.x * kRouteWaves + wave;
-  for (u32 j = threadIdx.x; j < kHotMax; j += kRouteBlock) {
+  for (u32 j = threadIdx.x; j < kRouteHotMax; j += kRouteBlock) {
     hit[j] = 0; hmax[0][j] = 0; hmax[1][j] = 0; hmax[2][j] = 0;
   }
   for (u32 o = lane; o < world; o += 64) {
