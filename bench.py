@@ -53,8 +53,10 @@ def parse():
     p.add_argument("--seed", type=int, default=1234)
     p.add_argument("--no-combine", action="store_true",
                    help="c4: no sender-side combine of hot names (PHIP_ROUTE_COMBINE)")
-    p.add_argument("--workload", default="c2", choices=["c2", "c3", "c4", "c5"],
-                   help="c2: batched Receive merges (headline); c3: mixed Take+Merge stream")
+    p.add_argument("--workload", default="c2", choices=["c1", "c2", "c3", "c4", "c5"],
+                   help="c2: batched Receive merges (headline); c1: the reference's CPU case "
+                        "(1M messages into 100k buckets, the whole of it timed on the CPU "
+                        "restatement beside the GPU); c3: mixed Take+Merge stream")
     p.add_argument("--ops", type=int, default=50_000_000, help="c3: ops per step")
     p.add_argument("--wire", action="store_true",
                    help="c2: feed raw datagrams (bucket.go:59-64 wire format) through "
@@ -332,6 +334,13 @@ def run_c5(args, torch, dev, repo, rank, world, gen):
 
 def main():
     args = parse()
+    c1 = args.workload == "c1"
+    if c1:
+        # BASELINE configs[0]: 1M replica states into a 100k-bucket
+        # repo; the C2 code path at that size, the CPU restatement on all of it.
+        args.workload = "c2"
+        args.keys, args.messages, args.log2_slots = 100_000, 1_000_000, 18
+        args.cpu_sample = args.messages
     import torch
     import torch.distributed as dist
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -501,6 +510,8 @@ def main():
         dom_name, dom_ms = DOMINANT, float(np.mean(kern.get(DOMINANT, [float("nan")])))
         unit, metric = "merges/s", METRIC
         workload = f"C2 merge: {n} replica messages -> {K}-bucket table (2^{args.log2_slots} slots), Zipf({args.zipf})"
+        if c1:
+            workload = "C1 (the reference's CPU case) " + workload[3:]
         if args.wire:
             workload += ", raw datagrams (decode + merge)"
         if args.ring:

@@ -1375,7 +1375,7 @@ int phip_route_pack(phip_handle* h, const phip_msgs* m, uint32_t world, uint8_t*
   // a strided sample, counted by name hash.
   const HotHdr* hot = nullptr;
   const RouteHot* dir = nullptr;
-  if ((flags & PHIP_ROUTE_COMBINE) && n >= kHotMinBatch) {
+  if ((flags & PHIP_ROUTE_COMBINE) && n >= kRouteMinBatch) {
     if ((rc = reset_ctr(h))) return rc;
     {
       Launch l(h, "k_route_classify");

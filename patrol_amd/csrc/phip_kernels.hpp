@@ -315,7 +315,12 @@ constexpr u32 kHotSampleMax = 1u << 17;   // samples per batch (half the count t
 constexpr u32 kHotSamplePerBlock = 1024;
 constexpr u32 kHotHist = 4096;        // histogram bins of sample counts
 constexpr u32 kHotMinCount = 8;       // sample hits for a bucket to qualify
-constexpr u32 kHotMinBatch = 1u << 20;    // smaller batches skip the directory
+// Smaller batches skip the directory.  2^16, not larger: a skewed batch of a
+// few 100k messages (C1: 1M into 100k buckets, 13% of them on one bucket)
+// otherwise sends every message of its hottest bucket to one record as a
+// device-scope atomicMax, and those serialise at the memory side.
+constexpr u32 kHotMinBatch = 1u << 16;
+constexpr u32 kRouteMinBatch = 1u << 20;   // the route combine's (phip_route_pack)
 
 struct HotEntry {
   u64 tag, w0, w1;   // table tag and canonical name words 0-1 (flags byte cleared)

@@ -161,7 +161,7 @@ def _fast_dirty_states(rng, n):
 
 @pytest.mark.parametrize("kind", ["clean", "fastdirty"])
 def test_receive_soa_hot_directory_vs_oracle(pa, kind):
-    """Batches of >= 2^20 messages build the hot-bucket directory (the most
+    """Batches of >= 2^16 messages build the hot-bucket directory (the most
     sampled buckets fold in LDS, flushed once per workgroup).  Zipf(1.1) with
     new keys, 15-22 byte and arena-length names mixed in."""
     rng = np.random.default_rng(11 if kind == "clean" else 12)
@@ -501,7 +501,7 @@ def test_merge_laws_at_scale(pa):
                                         (1 << 21, 1500000)])
 def test_datagram_fast_path_vs_oracle(pa, n, short_at):
     """Wire datagrams on the fast path (k_classify_wire + k_receive_fast
-    reading the datagrams in place; the hot directory from 2^20 messages):
+    reading the datagrams in place; the hot directory from 2^16 messages):
     NaN / +-Inf / negatives, new buckets, 15-22 byte and arena names, and a
     malformed datagram that ends the batch (io.ErrShortBuffer)."""
     import struct
@@ -661,3 +661,42 @@ def test_snapshot_restore_round_trip(pa, tmp_path):
     other = pa.GPURepo(log2_slots=15)
     with pytest.raises(pa.PatrolHipError):
         other.restore(path)
+
+
+# ------------------------------------------------ C1 (BASELINE configs[0]) --
+@pytest.mark.parametrize("dist", ["zipf", "uniform"])
+def test_c1_receive_vs_oracle(pa, dist):
+    """SURVEY C1, the reference's CPU case: 1M replica states merged into a
+    pre-populated 100k-bucket repo (Receive path: GetBucket + Merge,
+    repo.go:78-79), Zipf(1.1) and uniform, every status and the final state
+    of every bucket bit-exact."""
+    rng = np.random.default_rng(101 if dist == "zipf" else 102)
+    K, n = 100_000, 1_000_000
+    g, o = _seed_both(pa, rng, K, log2_slots=18)
+    ids = _gen.zipf_ids(rng, n, K) if dist == "zipf" else rng.integers(0, K, n)
+    names = _gen.key_names(ids)
+    a, t, e = _gen.clean_states(rng, n)
+    now = _gen.T0 + 7 * SEC
+    out = g.receive_soa(names, a, t, e, now)
+    st, _, _, _ = o.receive_soa(names, a, t, e, now)
+    assert np.array_equal(out["status"], st)
+    assert (st == 1).all()
+    assert_same_dump(gpu_dump(g), o.dump())
+
+
+def test_c1_upsert_vs_oracle(pa):
+    """SURVEY C1's Upsert path: 1M distinct states through
+    LocalRepo.UpsertBucket (repo.go:215-235: insert as-is on a miss, Merge
+    under the write lock on a hit) into the 100k-bucket repo, 5% new names."""
+    rng = np.random.default_rng(103)
+    K, n = 100_000, 1_000_000
+    g, o = _seed_both(pa, rng, K, log2_slots=18)
+    ids = _gen.zipf_ids(rng, n, K + 5000)
+    names = _gen.key_names(ids)
+    a, t, e = _gen.dirty_states(rng, n)
+    now = _gen.T0 + 9 * SEC
+    st = g.upsert_soa(names, a, t, e, now)["status"]
+    merged = o.upsert_soa(names, a, t, e, now).astype(bool)
+    assert np.array_equal(st, np.where(merged, 1, 8 | 0x80).astype(np.uint8))
+    assert (~merged).sum() > 1000
+    assert_same_dump(gpu_dump(g), o.dump())
