@@ -61,6 +61,8 @@ def parse():
     p.add_argument("--wire", action="store_true",
                    help="c2: feed raw datagrams (bucket.go:59-64 wire format) through "
                         "phip_receive_datagrams instead of the decoded SoA")
+    p.add_argument("--insert", action="store_true",
+                   help="c2: insert-on-miss variant (fresh key range every step; 2^27 slots)")
     p.add_argument("--ring", action="store_true",
                    help="c2: datagrams from pinned host ring slots (phip_ring_*), PCIe-inclusive; "
                         "not the headline (inputs are not resident in HBM)")
@@ -358,6 +360,8 @@ def main():
     import patrol_amd
 
     K, n = args.keys, args.messages
+    if args.insert:
+        args.log2_slots = max(args.log2_slots, 27)
     gen = torch.Generator(device=dev).manual_seed(args.seed + 7919 * rank)
 
     # Shard: rank r owns bucket ids [r*K, (r+1)*K) (owner-routed upstream).
@@ -393,6 +397,13 @@ def main():
         ids = zipf_ids(torch, gen, n, K, args.zipf, dev)
         blob, offs = names_for_ids(torch, ids + base)
         batches = [replica_states(torch, gen, n, j, dev) for j in range(args.warmup + args.steps)]
+        if args.insert:
+            # SURVEY C2's insert-on-miss variant: every step names a fresh
+            # key range (same Zipf shape), so each step creates the buckets it
+            # touches (GetBucket's miss branch, repo.go:195-210).
+            fresh = [names_for_ids(torch, ids + base + (j + 1) * world * K)
+                     for j in range(args.warmup + args.steps)]
+            n_new = []
         torch.cuda.synchronize()
 
         if args.ring:
@@ -439,6 +450,13 @@ def main():
             def step(j):
                 db, do = wires[j]
                 repo.receive_datagrams_device(db, do, n, T0 + j)
+        elif args.insert:
+            def step(j):
+                a, t, e = batches[j]
+                fb, fo = fresh[j]
+                before = len(repo)
+                repo.receive_soa(fb, a, t, e, T0 + j, name_offs=fo, n=n, device=True)
+                n_new.append(len(repo) - before)
         else:
             def step(j):
                 a, t, e = batches[j]
@@ -514,6 +532,9 @@ def main():
             workload = "C1 (the reference's CPU case) " + workload[3:]
         if args.wire:
             workload += ", raw datagrams (decode + merge)"
+        if args.insert:
+            workload += ", insert-on-miss (every step names a fresh key range)"
+            extra["buckets_created_per_step"] = float(np.mean(n_new[args.warmup:]))
         if args.ring:
             workload = (f"C2 ingest ring (PCIe-inclusive): {n} datagrams per batch from pinned host "
                         f"slots -> {K}-bucket table, copy of batch j+1 overlapping merge of batch "

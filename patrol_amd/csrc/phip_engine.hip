@@ -36,7 +36,7 @@ enum BufId {
   B_MISS, B_MISS2, B_RETRY, B_CSLOT, B_CMSG,
   B_SLOT, B_IDX, B_SSLOT, B_SIDX, B_USLOT, B_SCNT, B_SSTART, B_LONG, B_HUGE, B_TEMP, B_DUMP,
   B_OPS, B_HOFF, B_HOP, B_HVAL, B_RPOS, B_RST, B_RUNN, B_SEGEX, B_WOFF, B_SUMS, B_WRUN,
-  B_STATES, B_NAME1, B_HOT, B_ROUTE, B_EXPORT, B_COUNT_
+  B_STATES, B_NAME1, B_HOT, B_ROUTE, B_EXPORT, B_MSHARD, B_MSCNT, B_DEDUP, B_DSET, B_COUNT_
 };
 
 struct DevBuf {
@@ -331,12 +331,45 @@ int join_hot(phip_handle* h, const HotHdr* hot);
 // clean prefix: the messages before the first dirty one (*first_dirty; n if
 // none) and before the first malformed datagram (ctr[5]).  The prefix's
 // misses (*nmiss of them) are listed in B_MISS.
+// A sharded append list over `units` units of up to `per_unit` entries
+// (counters zeroed on the stream).
+int sharded(phip_handle* h, BufId base_id, u32 units, u32 per_unit, Sharded* out) {
+  int rc;
+  out->cap = shard_cap(units, per_unit);
+  if ((rc = ensure(h, base_id, (size_t)kShards * out->cap, &out->base)) ||
+      (rc = ensure(h, B_MSCNT, 2 * kShards, &out->cnt)))
+    return rc;
+  HIPCHK(h, hipMemsetAsync(out->cnt, 0, kShards * sizeof(u32), h->stream));
+  return PHIP_OK;
+}
+
+// Pack a sharded list into `out`: the total lands in ctr[total_slot] and is
+// returned in *total (one counter read-back).
+int pack_sharded(phip_handle* h, const Sharded& sh, u32 total_slot, u32* out, u32* total) {
+  HIPCHK(h, hipMemsetAsync(h->ctr + 13, 0, sizeof(u32), h->stream));
+  k_shard_scan<<<1, kShards, 0, h->stream>>>(sh.cnt, h->ctr + total_slot, h->ctr + 13);
+  HIPCHK(h, hipGetLastError());
+  int rc;
+  if ((rc = read_ctr(h))) return rc;
+  *total = h->ctr_host[total_slot];
+  if (*total) {
+    Launch l(h, "k_shard_compact");
+    dim3 grid(grid_for(h->ctr_host[13]), kShards);
+    k_shard_compact<<<grid, 256, 0, h->stream>>>(sh.base, sh.cap, sh.cnt, out);
+    HIPCHK(h, hipGetLastError());
+  }
+  return PHIP_OK;
+}
+
 template <class In>
 int fast_apply(phip_handle* h, In in, u32 n, u8* status, const HotHdr* hot,
                const HotEntry* hot_dir, u32* first_dirty, u32* nmiss) {
   u32* miss;
   int rc;
-  if ((rc = ensure(h, B_MISS, n, &miss))) return rc;
+  Sharded msh;
+  if ((rc = ensure(h, B_MISS, n, &miss)) ||
+      (rc = sharded(h, B_MSHARD, (n + 63) / 64, 64, &msh)))
+    return rc;
   {
     Launch l(h, "k_classify");
     k_classify<In><<<grid_for(n), kBlock, 0, h->stream>>>(in, n, h->ctr);
@@ -348,27 +381,95 @@ int fast_apply(phip_handle* h, In in, u32 n, u8* status, const HotHdr* hot,
   {
     Launch l(h, "k_receive_fast");
     k_receive_fast<In><<<fast_grid(h, n), kFastBlock, 0, h->stream>>>(
-        in, n, table(h), status, miss, h->ctr, hot, hot_dir);
+        in, n, table(h), status, msh, h->ctr, hot, hot_dir);
   }
   HIPCHK(h, hipGetLastError());
-  if ((rc = read_ctr(h))) return rc;
+  if ((rc = pack_sharded(h, msh, 2, miss, nmiss))) return rc;
   if ((rc = check_flags(h))) return rc;
   *first_dirty = std::min<u32>(h->ctr_host[kCtrDirty], n);
-  *nmiss = h->ctr_host[2];
   h->stats[0] = h->ctr_host[11];
   h->stats[1] = h->ctr_host[10];
   h->stats[2] = *nmiss;
   return PHIP_OK;
 }
 
+template <class Src>
+int fork_hot(phip_handle* h, Src src, u32 n, const HotHdr** hot, const HotEntry** hot_dir);
+
+// Many misses (an insert-heavy batch: a node starting empty, a fresh key
+// range): create each distinct missing name once (k_dedupe, then the insert
+// pipeline over one message per name), then merge by running the fast pass
+// again over the whole clean prefix [0, prefix).  In that prefix every merge
+// is an order-free max, so the messages the first pass already merged are
+// merged again to no effect, and the hot directory now covers the new hot
+// buckets: their messages fold in LDS instead of each sending a
+// device-scope atomic to one record (134 ms per 100M-message batch through
+// k_receive_list).  Returns the misses of the second pass
+// (names dropped by k_dedupe for a shared tag) in *nmiss2, listed in B_MISS.
+template <class Src>
+int finish_many_misses(phip_handle* h, Src src, const uint64_t* a, const uint64_t* t,
+                       const int64_t* e, u32 nmiss, u32 prefix, i64 now, u8* status, u32* nmiss2) {
+  u32* miss = (u32*)h->buf[B_MISS].p;
+  int rc;
+  // 1. distinct names
+  u32 setbits = 1;
+  while ((1ull << setbits) < 2ull * nmiss) ++setbits;
+  u64* set;
+  u32* dedup;
+  Sharded dsh;
+  if ((rc = ensure(h, B_DSET, size_t(1) << setbits, &set)) ||
+      (rc = ensure(h, B_DEDUP, nmiss, &dedup)) ||
+      (rc = sharded(h, B_MSHARD, grid_for(nmiss), kBlock, &dsh)))
+    return rc;
+  HIPCHK(h, hipMemsetAsync(set, 0, (size_t(1) << setbits) * sizeof(u64), h->stream));
+  {
+    Launch l(h, "k_dedupe");
+    k_dedupe<Src><<<grid_for(nmiss), kBlock, 0, h->stream>>>(src, nmiss, miss, table(h), set,
+                                                             setbits, dsh);
+    HIPCHK(h, hipGetLastError());
+  }
+  u32 nd = 0;
+  if ((rc = pack_sharded(h, dsh, 14, dedup, &nd))) return rc;
+  // 2. create them (aux = ~0 and the NEW flag on every claimed slot)
+  u32 n_claimed = 0;
+  if ((rc = insert_names(h, src, dedup, nd, nullptr, now, &n_claimed))) return rc;
+  // 3. creator tracking over the first pass's misses (every message of a new
+  //    bucket is among them), before the second pass reuses B_MISS
+  if (status) {
+    Launch l(h, "k_first_seen");
+    k_first_seen<Src><<<grid_for(nmiss), kBlock, 0, h->stream>>>(src, nmiss, miss, table(h));
+    HIPCHK(h, hipGetLastError());
+  }
+  // 4. the fast pass again
+  if ((rc = reset_ctr(h))) return rc;
+  const HotHdr* hot;
+  const HotEntry* hot_dir;
+  if ((rc = fork_hot(h, src, prefix, &hot, &hot_dir))) return rc;
+  u32 fd = prefix;
+  if ((rc = fast_apply(h, SoaIn<Src>{src, a, t, e}, prefix, status, hot, hot_dir, &fd, nmiss2)))
+    return rc;
+  // 5. PHIP_ST_CREATED after the second pass wrote its statuses
+  if (status && n_claimed) {
+    Launch l(h, "k_mark_created");
+    k_mark_created_slots<<<grid_for(n_claimed), kBlock, 0, h->stream>>>(
+        (const u32*)h->buf[B_CSLOT].p, n_claimed, table(h), status);
+    HIPCHK(h, hipGetLastError());
+  }
+  return clear_new(h, n_claimed);
+}
+
 // The messages fast_apply missed: create their buckets, merge them with
 // creator tracking (PHIP_ST_CREATED on the first message of a new bucket).
 template <class Src>
 int finish_misses(phip_handle* h, Src src, const uint64_t* a, const uint64_t* t, const int64_t* e,
-                  u32 nmiss, i64 now, u8* status) {
+                  u32 nmiss, u32 prefix, i64 now, u8* status) {
+  if (nmiss == 0) return PHIP_OK;
+  int rc;
+  if (nmiss >= kManyMisses &&
+      (rc = finish_many_misses(h, src, a, t, e, nmiss, prefix, now, status, &nmiss)))
+    return rc;
   if (nmiss == 0) return PHIP_OK;
   u32* miss = (u32*)h->buf[B_MISS].p;
-  int rc;
   u32 n_claimed = 0;
   if ((rc = insert_names(h, src, miss, nmiss, nullptr, now, &n_claimed))) return rc;
   HIPCHK(h, hipMemsetAsync(h->ctr + 2, 0, sizeof(u32), h->stream));
@@ -648,7 +749,8 @@ int finish_receive(phip_handle* h, Src src, const uint64_t* a, const uint64_t* t
                    const int64_t* e, u32 stop, u32 first_dirty, u32 nmiss, i64 now,
                    const OutView& ow) {
   int rc;
-  if ((rc = finish_misses(h, src, a, t, e, nmiss, now, ow.status))) return rc;
+  if ((rc = finish_misses(h, src, a, t, e, nmiss, std::min(stop, first_dirty), now, ow.status)))
+    return rc;
   if (first_dirty >= stop) return PHIP_OK;
   const u32 k = first_dirty;
   OpView ov{};

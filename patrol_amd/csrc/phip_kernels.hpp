@@ -5,6 +5,8 @@
 // Home slot = top L bits of tag * 2^64/phi (Fibonacci hashing), linear
 // probing; a lookup touches one 64-byte record per probe step.
 #pragma once
+#include <type_traits>
+
 #include "phip_device.hpp"
 
 namespace phip {
@@ -105,6 +107,54 @@ __device__ inline u32 wave_append(u32* counter, bool pred) {
   if (lane == leader) base = atomicAdd(counter, (u32)__popcll(mask));
   base = __shfl(base, leader);
   return base + rank;
+}
+
+// Sharded append list.  A list that every wave of a large grid appends to
+// through ONE counter serialises on that word once most waves have an entry
+// (an insert-heavy batch: 1.5M appends per 100M messages, ~11 ns each).
+// Instead, unit u (a wave's chunk, or a block) appends to shard u % kShards,
+// whose region holds the entries of at most ceil(units / kShards) units;
+// k_shard_scan + k_shard_compact then pack the shards into one list.
+constexpr u32 kShards = 256;
+__host__ __device__ inline u32 shard_cap(u32 units, u32 per_unit) {
+  return per_unit * ((units + kShards - 1) / kShards);
+}
+struct Sharded {
+  u32* base;   // kShards regions of `cap` entries
+  u32* cnt;    // kShards counters (zeroed before the kernel)
+  u32 cap;
+  __device__ inline void append(u32 unit, bool pred, u32 v) const {
+    const u32 sh = unit & (kShards - 1);
+    const u32 pos = wave_append(&cnt[sh], pred);
+    if (pred) base[(size_t)sh * cap + pos] = v;
+  }
+};
+
+// One workgroup of kShards lanes: exclusive offsets of the shards (into
+// cnt[kShards + s]), the total into *total and the largest shard into *maxc.
+__global__ __launch_bounds__(kShards) void k_shard_scan(u32* cnt, u32* total, u32* maxc) {
+  __shared__ u32 v[kShards];
+  const u32 t = threadIdx.x, c = cnt[t];
+  v[t] = c;
+  __syncthreads();
+  for (u32 off = 1; off < kShards; off <<= 1) {
+    const u32 x = t >= off ? v[t - off] : 0u;
+    __syncthreads();
+    v[t] += x;
+    __syncthreads();
+  }
+  cnt[kShards + t] = v[t] - c;
+  if (t == kShards - 1) *total = v[t];
+  if (c) atomicMax(maxc, c);
+}
+
+// grid (ceil(max shard count / 256), kShards): shard s's entries, in order,
+// to out[offset(s) ...].
+__global__ __launch_bounds__(256) void k_shard_compact(const u32* __restrict__ base, u32 cap,
+                                                       const u32* __restrict__ cnt,
+                                                       u32* __restrict__ out) {
+  const u32 s = blockIdx.y, j = blockIdx.x * 256 + threadIdx.x;
+  if (j < cnt[s]) out[cnt[kShards + s] + j] = base[(size_t)s * cap + j];
 }
 
 // Full-name equality for a candidate record (names > 22 bytes live in the arena).
@@ -321,6 +371,13 @@ constexpr u32 kHotMinCount = 8;       // sample hits for a bucket to qualify
 // device-scope atomicMax, and those serialise at the memory side.
 constexpr u32 kHotMinBatch = 1u << 16;
 constexpr u32 kRouteMinBatch = 1u << 20;   // the route combine's (phip_route_pack)
+// A fast batch with this many misses creates its buckets from one message per
+// name and merges by a second fast pass (finish_many_misses); fewer go
+// through k_receive_list.
+#ifndef PHIP_MANY_MISSES
+#define PHIP_MANY_MISSES (1u << 16)
+#endif
+constexpr u32 kManyMisses = PHIP_MANY_MISSES;
 
 struct HotEntry {
   u64 tag, w0, w1;   // table tag and canonical name words 0-1 (flags byte cleared)
@@ -469,16 +526,27 @@ struct SoaIn {   // decoded messages (phip_receive_soa / decoded datagrams)
   __device__ inline const u8* blob() const { return src.blob; }
   // Round 1 of a message on its own (the name's offset and length), so the
   // fast kernel can issue it one chunk ahead.
-  // (Src = NamesOffs: the two u32 offsets as loaded.)
-  struct Pre { u32 a, b; };
+  // (NamesOffs: the two u32 offsets as loaded, two registers; other name
+  // sources: offset and length.)
+  struct PreOffs { u32 a, b; };
+  struct PreGen { u64 off; u32 len; };
+  static constexpr bool kOffs = std::is_same<Src, NamesOffs>::value;
+  using Pre = typename std::conditional<kOffs, PreOffs, PreGen>::type;
   __device__ inline Pre pre(u32 i) const {
-    static_assert(std::is_same<Src, NamesOffs>::value, "fast path input: names + u32 offsets");
-    return Pre{ld<true>(src.offs + i), ld<true>(src.offs + i + 1)};
+    Pre p;
+    if constexpr (kOffs) {
+      p.a = ld<true>(src.offs + i);
+      p.b = ld<true>(src.offs + i + 1);
+    } else {
+      src.template get<true>(i, p.off, p.len);
+    }
+    return p;
   }
   // Round 2 given round 1: the name words and the replica fields.
   __device__ inline void load(u32 i, const Pre& p, u64& off, u32& len, u64& w0, u64& w1, u64& w2,
                               u64& ra, u64& rt, i64& re) const {
-    off = p.a; len = p.b - p.a;
+    if constexpr (kOffs) { off = p.a; len = p.b - p.a; }
+    else { off = p.off; len = p.len; }
     ra = ld<true>(ma + i); rt = ld<true>(mt + i); re = ld<true>(me + i);
     load_words3<false>(src.blob, off, len, w0, w1, w2);
   }
@@ -565,7 +633,7 @@ __global__ __launch_bounds__(kBlock) void k_classify(In in, u32 n, u32* ctr) {
 
 template <class In>
 __global__ __launch_bounds__(kFastBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_receive_fast(
-    In in, u32 n, Table T, u8* __restrict__ status, u32* miss, u32* ctr,
+    In in, u32 n, Table T, u8* __restrict__ status, Sharded miss, u32* ctr,
     const HotHdr* __restrict__ hot, const HotEntry* __restrict__ hot_dir) {
   __shared__ u32 hslot[kHotLds];        // directory index + 1 (0 = empty)
   __shared__ u64 htag[kHotMax], hw0[kHotMax], hw1[kHotMax];
@@ -601,7 +669,8 @@ __global__ __launch_bounds__(kFastBlock) __attribute__((amdgpu_waves_per_eu(8, 8
   // Round 1 (the name offsets) runs one chunk ahead: a chunk's dependent
   // chain is then name words -> home slot, and the next chunk's offsets
   // arrive meanwhile.
-  u32 chunk = blockIdx.x * kWaves + threadIdx.x / 64;
+  // wave-uniform (in SGPRs): the chunk index, its shard of the miss list
+  u32 chunk = blockIdx.x * kWaves + __builtin_amdgcn_readfirstlane(threadIdx.x / 64);
   typename In::Pre pre{};
   if (chunk < nchunks) pre = in.pre(min(chunk * 64 + lane, n - 1));
   for (; chunk < nchunks; chunk += cstride) {
@@ -670,8 +739,7 @@ __global__ __launch_bounds__(kFastBlock) __attribute__((amdgpu_waves_per_eu(8, 8
         }
       }
     }
-    const u32 pos = wave_append(&ctr[2], missed);
-    if (missed) miss[pos] = i;
+    miss.append(chunk, missed, i);
   }
   if (hits) atomicAdd(&hhits, hits);
   __syncthreads();
@@ -722,7 +790,12 @@ __global__ __launch_bounds__(kBlock) void k_receive_list(
       if (ea > cur.added) atomicMax(&r->added, ea);
       if (et > cur.taken) atomicMax(&r->taken, et);
       if (ee > ((u64)cur.elapsed ^ kSign)) atomicMax(&r->elapsed, (i64)(ee ^ kSign));
-      if (rec_flags(cur) & kRecNew) atomicMin(&T.aux[s], i);
+      // Creator tracking: the lowest index wins.  aux only falls, so a stale
+      // read costs at most a redundant atomic; reading first keeps the
+      // messages of a hot new bucket from serialising on one word.
+      if ((rec_flags(cur) & kRecNew) && i < __hip_atomic_load(&T.aux[s], __ATOMIC_RELAXED,
+                                                               __HIP_MEMORY_SCOPE_AGENT))
+        atomicMin(&T.aux[s], i);
       if (status) status[i] = PHIP_ST_MERGED;
     } else {
       missed = true;
@@ -731,6 +804,67 @@ __global__ __launch_bounds__(kBlock) void k_receive_list(
   }
   const u32 pos = wave_append(&ctr[2], missed);
   if (missed) miss[pos] = i;
+}
+
+// Distinct names of a (large) miss list, for the insert pipeline: one
+// message per name hash goes on (a set of 64-bit table tags in `set`, probed
+// linearly; the load before the CAS keeps a hot name's messages from
+// serialising on its word).  Two names that share a tag keep only one
+// message: the other name then misses the fast pass that follows and takes
+// the general insert path (finish_misses), so dropping it is safe.
+template <class Src>
+__global__ __launch_bounds__(kBlock) void k_dedupe(Src src, u32 n, const u32* __restrict__ list,
+                                                   Table T, u64* set, u32 setbits, Sharded out) {
+  const u32 tid = blockIdx.x * kBlock + threadIdx.x;
+  bool keep = false;
+  u32 i = 0;
+  if (tid < n) {
+    i = list[tid];
+    u64 off; u32 len;
+    src.get(i, off, len);
+    Name nm;
+    load_name_wide<false>(src.blob, off, len, nm);
+    const u64 tag = T.tag(nm.h);
+    const u64 mask = (1ull << setbits) - 1;
+    u64 h = (tag * 0x9E3779B97F4A7C15ull) >> (64 - setbits);
+    keep = true;   // no free entry found (cannot happen at <= 50% load): keep it
+    for (u64 k = 0; k <= mask; ++k, h = (h + 1) & mask) {
+      u64 v = __hip_atomic_load(&set[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (v == 0) v = atomicCAS(&set[h], 0ull, tag);
+      if (v == 0) break;                      // first of its name: keep
+      if (v == tag) { keep = false; break; }  // a message of this name went on
+    }
+  }
+  out.append(blockIdx.x, keep, i);
+}
+
+// Creator tracking without merging (the large-miss path merges by a second
+// fast pass): aux[s] = the lowest index among the list's messages of every
+// bucket this batch created.
+template <class Src>
+__global__ __launch_bounds__(kBlock) void k_first_seen(Src src, u32 n, const u32* __restrict__ list,
+                                                       Table T) {
+  const u32 tid = blockIdx.x * kBlock + threadIdx.x;
+  if (tid >= n) return;
+  const u32 i = list[tid];
+  u64 off; u32 len;
+  src.get(i, off, len);
+  Name nm;
+  load_name_wide<false>(src.blob, off, len, nm);
+  u32 s;
+  Rec cur;
+  if (probe(T, nm, src.blob, &s, &cur) != kFound) return;
+  if ((rec_flags(cur) & kRecNew) &&
+      i < __hip_atomic_load(&T.aux[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+    atomicMin(&T.aux[s], i);
+}
+
+// PHIP_ST_CREATED from the claimed slots: status[aux[s]] of each.
+__global__ void k_mark_created_slots(const u32* __restrict__ cslot, u32 n, Table T, u8* status) {
+  const u32 j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  const u32 i = T.aux[cslot[j]];
+  if (i != 0xFFFFFFFFu) status[i] |= 0x80;
 }
 
 // Status of the messages that went through the insert pipeline: the first

@@ -700,3 +700,44 @@ def test_c1_upsert_vs_oracle(pa):
     assert np.array_equal(st, np.where(merged, 1, 8 | 0x80).astype(np.uint8))
     assert (~merged).sum() > 1000
     assert_same_dump(gpu_dump(g), o.dump())
+
+
+# ----------------------------------------- insert-heavy (many misses) ----
+@pytest.mark.parametrize("wire,tag_bits", [(False, 0), (True, 0), (False, 14)])
+def test_insert_heavy_batch_vs_oracle(pa, wire, tag_bits):
+    """A batch whose names are mostly new (a node starting nearly empty; the
+    C2 insert-on-miss variant): >= 2^16 misses take finish_many_misses
+    (one message per distinct name into the insert pipeline, then a second
+    fast pass over the prefix).  Statuses (PHIP_ST_CREATED on the lowest-seq
+    message of each new bucket), replies and the final table equal the
+    oracle's.  tag_bits=14 forces shared tags, so k_dedupe drops names that
+    the general insert path must then create."""
+    import struct
+    rng = np.random.default_rng(77 + tag_bits + wire)
+    K = 1000
+    names0 = _gen.key_names(np.arange(K))
+    a0, t0, e0 = _gen.clean_states(rng, K)
+    created = _gen.T0 - rng.integers(0, SEC, K)
+    g = pa.GPURepo(log2_slots=18, debug_tag_bits=tag_bits)
+    g.seed(names0, a0, t0, e0, created)
+    o = O.Repo()
+    o.seed(names0, a0, t0, e0, created)
+    n = 300_000
+    ids = _gen.zipf_ids(rng, n, 60_000)
+    names = [(b"a-long-replicated-bucket-name-%d" % i) if i % 71 == 0 else b"b%d" % i
+             for i in ids]
+    a, t, e = _fast_dirty_states(rng, n)
+    now = _gen.T0 + 11 * SEC
+    if wire:
+        dgs = [struct.pack(">QQQ", int(a[i]), int(t[i]), int(e[i]) & (2**64 - 1)) +
+               bytes([len(names[i])]) + names[i] for i in range(n)]
+        out = g.receive_datagrams(dgs, now)
+        st, _, _, _, stop = o.receive(dgs, now)
+        assert out["stop"] == stop == n
+    else:
+        out = g.receive_soa(names, a, t, e, now)
+        st, _, _, _ = o.receive_soa(names, a, t, e, now)
+    assert np.array_equal(out["status"], st)
+    assert int(((st & 0x80) != 0).sum()) > 10_000
+    assert_same_dump(gpu_dump(g), o.dump())
+    g.close()
