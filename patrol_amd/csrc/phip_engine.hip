@@ -396,6 +396,27 @@ int fast_apply(phip_handle* h, In in, u32 n, u8* status, const HotHdr* hot,
 template <class Src>
 int fork_hot(phip_handle* h, Src src, u32 n, const HotHdr** hot, const HotEntry** hot_dir);
 
+// One message per distinct name of list[0..n) (k_dedupe) into B_DEDUP.
+template <class Src>
+int dedupe_names(phip_handle* h, Src src, const u32* list, u32 n, u32** out, u32* nout) {
+  int rc;
+  u32 setbits = 1;
+  while ((1ull << setbits) < 2ull * n) ++setbits;
+  u64* set;
+  Sharded dsh;
+  if ((rc = ensure(h, B_DSET, size_t(1) << setbits, &set)) ||
+      (rc = ensure(h, B_DEDUP, n, out)) ||
+      (rc = sharded(h, B_MSHARD, grid_for(n), kBlock, &dsh)))
+    return rc;
+  HIPCHK(h, hipMemsetAsync(set, 0, (size_t(1) << setbits) * sizeof(u64), h->stream));
+  {
+    Launch l(h, "k_dedupe");
+    k_dedupe<Src><<<grid_for(n), kBlock, 0, h->stream>>>(src, n, list, table(h), set, setbits, dsh);
+    HIPCHK(h, hipGetLastError());
+  }
+  return pack_sharded(h, dsh, 14, *out, nout);
+}
+
 // Many misses (an insert-heavy batch: a node starting empty, a fresh key
 // range): create each distinct missing name once (k_dedupe, then the insert
 // pipeline over one message per name), then merge by running the fast pass
@@ -412,24 +433,8 @@ int finish_many_misses(phip_handle* h, Src src, const uint64_t* a, const uint64_
   u32* miss = (u32*)h->buf[B_MISS].p;
   int rc;
   // 1. distinct names
-  u32 setbits = 1;
-  while ((1ull << setbits) < 2ull * nmiss) ++setbits;
-  u64* set;
-  u32* dedup;
-  Sharded dsh;
-  if ((rc = ensure(h, B_DSET, size_t(1) << setbits, &set)) ||
-      (rc = ensure(h, B_DEDUP, nmiss, &dedup)) ||
-      (rc = sharded(h, B_MSHARD, grid_for(nmiss), kBlock, &dsh)))
-    return rc;
-  HIPCHK(h, hipMemsetAsync(set, 0, (size_t(1) << setbits) * sizeof(u64), h->stream));
-  {
-    Launch l(h, "k_dedupe");
-    k_dedupe<Src><<<grid_for(nmiss), kBlock, 0, h->stream>>>(src, nmiss, miss, table(h), set,
-                                                             setbits, dsh);
-    HIPCHK(h, hipGetLastError());
-  }
-  u32 nd = 0;
-  if ((rc = pack_sharded(h, dsh, 14, dedup, &nd))) return rc;
+  u32 *dedup, nd = 0;
+  if ((rc = dedupe_names(h, src, miss, nmiss, &dedup, &nd))) return rc;
   // 2. create them (aux = ~0 and the NEW flag on every claimed slot)
   u32 n_claimed = 0;
   if ((rc = insert_names(h, src, dedup, nd, nullptr, now, &n_claimed))) return rc;
@@ -518,24 +523,46 @@ int resolve_all(phip_handle* h, Src src, u32 n, const int64_t* now_arr, i64 now0
                 u32* n_claimed) {
   u32 *slot, *miss;
   int rc;
-  if ((rc = ensure(h, B_SLOT, n, &slot)) || (rc = ensure(h, B_MISS, n, &miss))) return rc;
+  Sharded rsh;
+  if ((rc = ensure(h, B_SLOT, n, &slot)) || (rc = ensure(h, B_MISS, n, &miss)) ||
+      (rc = sharded(h, B_MSHARD, grid_for(n), kBlock, &rsh)))
+    return rc;
   if ((rc = reset_ctr(h))) return rc;
   {
     Launch l(h, "k_resolve");
-    k_resolve<Src><<<grid_for(n), kBlock, 0, h->stream>>>(src, n, nullptr, table(h), slot, miss,
+    k_resolve<Src><<<grid_for(n), kBlock, 0, h->stream>>>(src, n, nullptr, table(h), slot, rsh,
                                                            h->ctr);
   }
   HIPCHK(h, hipGetLastError());
-  if ((rc = read_ctr(h))) return rc;
+  u32 nmiss = 0;
+  if ((rc = pack_sharded(h, rsh, 2, miss, &nmiss))) return rc;
   if ((rc = check_flags(h))) return rc;
-  u32 nmiss = h->ctr_host[2];
   *n_claimed = 0;
+  if (nmiss >= kManyMisses) {
+    // Many new names (an ordered batch on a fresh key range, a large seed):
+    // create each once, then resolve the misses again; names k_dedupe
+    // dropped for a shared tag miss again and take the general rounds below.
+    u32 *dedup, nd = 0;
+    if ((rc = dedupe_names(h, src, miss, nmiss, &dedup, &nd)) ||
+        (rc = insert_names(h, src, dedup, nd, now_arr, now0, n_claimed)))
+      return rc;
+    Sharded r2;
+    if ((rc = sharded(h, B_MSHARD, grid_for(nmiss), kBlock, &r2))) return rc;
+    {
+      Launch l(h, "k_resolve_miss");
+      k_resolve<Src><<<grid_for(nmiss), kBlock, 0, h->stream>>>(src, nmiss, miss, table(h), slot,
+                                                                 r2, h->ctr);
+    }
+    HIPCHK(h, hipGetLastError());
+    if ((rc = pack_sharded(h, r2, 2, miss, &nmiss))) return rc;
+  }
   if (nmiss) {
-    if ((rc = insert_names(h, src, miss, nmiss, now_arr, now0, n_claimed))) return rc;
-    HIPCHK(h, hipMemsetAsync(h->ctr + 2, 0, sizeof(u32), h->stream));
+    u32 more = 0;
+    if ((rc = insert_names(h, src, miss, nmiss, now_arr, now0, &more))) return rc;
+    *n_claimed += more;
     Launch l(h, "k_resolve_miss");
     k_resolve<Src><<<grid_for(nmiss), kBlock, 0, h->stream>>>(src, nmiss, miss, table(h), slot,
-                                                               nullptr, h->ctr);
+                                                               Sharded{}, h->ctr);
     HIPCHK(h, hipGetLastError());
   }
   *slot_out = slot;

@@ -120,9 +120,9 @@ __host__ __device__ inline u32 shard_cap(u32 units, u32 per_unit) {
   return per_unit * ((units + kShards - 1) / kShards);
 }
 struct Sharded {
-  u32* base;   // kShards regions of `cap` entries
-  u32* cnt;    // kShards counters (zeroed before the kernel)
-  u32 cap;
+  u32* base = nullptr;   // kShards regions of `cap` entries (nullptr: no list)
+  u32* cnt = nullptr;    // kShards counters (zeroed before the kernel)
+  u32 cap = 0;
   __device__ inline void append(u32 unit, bool pred, u32 v) const {
     const u32 sh = unit & (kShards - 1);
     const u32 pos = wave_append(&cnt[sh], pred);
@@ -889,7 +889,7 @@ __global__ void k_mark_created(Src src, u32 n, const u32* __restrict__ list, Tab
 // Name -> slot for every op (ordered path, seed, get).  Misses appended.
 template <class Src>
 __global__ __launch_bounds__(kBlock) void k_resolve(Src src, u32 n, const u32* __restrict__ list,
-                                                    Table T, u32* __restrict__ slot_out, u32* miss,
+                                                    Table T, u32* __restrict__ slot_out, Sharded miss,
                                                     u32* ctr) {
   u32 tid = blockIdx.x * blockDim.x + threadIdx.x;
   bool missed = false;
@@ -909,10 +909,7 @@ __global__ __launch_bounds__(kBlock) void k_resolve(Src src, u32 n, const u32* _
       if (pr == kFull) atomicOr(&ctr[8], 1u);
     }
   }
-  if (miss) {
-    u32 pos = wave_append(&ctr[2], missed);
-    if (missed) miss[pos] = i;
-  }
+  if (miss.base) miss.append(blockIdx.x, missed, i);
 }
 
 // ------------------------------------------------------------- inserts ---

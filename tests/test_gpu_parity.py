@@ -741,3 +741,41 @@ def test_insert_heavy_batch_vs_oracle(pa, wire, tag_bits):
     assert int(((st & 0x80) != 0).sum()) > 10_000
     assert_same_dump(gpu_dump(g), o.dump())
     g.close()
+
+
+@pytest.mark.parametrize("tag_bits", [0, 14])
+def test_mixed_stream_many_new_buckets_vs_oracle(pa, tag_bits):
+    """An ordered Take/Merge stream on an empty table with >= 2^16 distinct
+    names: resolve_all creates one message per name (k_dedupe) and resolves
+    the rest; `created` is still the first op's clock for every bucket and
+    shared tags (tag_bits=14) still resolve exactly."""
+    rng = np.random.default_rng(91 + tag_bits)
+    n, K = 400_000, 150_000
+    args = _mixed_stream(rng, n, K)
+    g = pa.GPURepo(log2_slots=19, debug_tag_bits=tag_bits)
+    o = O.Repo()
+    out = g.apply_mixed(*args)
+    ref = o.apply_mixed(*args)
+    assert np.array_equal(out["status"], ref["status"])
+    assert np.array_equal(out["remaining"], ref["remaining"])
+    assert int(((ref["status"] & 0x80) != 0).sum()) > 40_000   # all 400k ops miss first
+    assert_same_dump(gpu_dump(g), o.dump())
+    g.close()
+
+
+def test_seed_many_names_with_duplicates(pa):
+    """phip_seed of >= 2^16 names (the large-miss resolve path), some named
+    twice: the last entry of a name wins, as NewLocalRepo's map build does."""
+    rng = np.random.default_rng(5)
+    K = 120_000
+    ids = np.concatenate([np.arange(K), rng.integers(0, K, 5000)])
+    names = _gen.key_names(ids)
+    a, t, e = _gen.clean_states(rng, len(ids))
+    created = _gen.T0 + rng.integers(0, SEC, len(ids))
+    g = pa.GPURepo(log2_slots=18)
+    g.seed(names, a, t, e, created)
+    o = O.Repo()
+    o.seed(names, a, t, e, created)
+    assert len(g) == K
+    assert_same_dump(gpu_dump(g), o.dump())
+    g.close()
