@@ -464,25 +464,31 @@ def main():
 
     for j in range(args.warmup):
         step(j)
-    repo.set_timing(True)
+    # HIP events around every kernel of the timed steps, kept by the library
+    # and read once after the timed region (reading them synchronises).
+    # (c5's step reads its own per-call timings from the shard layer.)
+    repo.set_timing(True, accumulate=args.workload != "c5")
     kern = {}
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     launches = {}
+    step_tl = []
     for j in range(args.warmup, args.warmup + args.steps):
         tl = step(j)
-        per = {}   # a kernel launched several times in a step (chunks): summed
-        for name, ms in (tl if tl is not None else repo.timings()):
-            per[name] = per.get(name, 0.0) + ms
-            launches[name] = launches.get(name, 0) + 1
-        for name, ms in per.items():
-            kern.setdefault(name, []).append(ms)
+        if tl is not None:
+            step_tl.append(tl)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
+    # per step: a kernel launched several times in a step (chunks) is summed
+    for tl in (step_tl or [repo.timings()]):
+        for name, ms in tl:
+            kern[name] = kern.get(name, 0.0) + ms / (1 if step_tl else args.steps)
+            launches[name] = launches.get(name, 0) + 1
+    kern = {k: [v / (args.steps if step_tl else 1)] for k, v in kern.items()}
     repo.set_timing(False)
     if world > 1:
         tt = torch.tensor([el], dtype=torch.float64,

@@ -350,11 +350,14 @@ int phip_ae_apply(phip_handle* h, int64_t* replicas, uint32_t nrep, uint64_t nbu
                   const int64_t* joined, uint32_t flags);
 
 /* ---- diagnostics ---- */
-/* Per-kernel timing of the last hot-path call, measured with HIP events on
- * the handle's stream: writes up to max entries of (name, ms) and returns the
+/* Per-kernel timing of the last hot-path call (every call since
+ * phip_set_timing(h, 2) in that mode), measured with HIP events on the
+ * handle's stream: writes up to max entries of (name, ms) and returns the
  * count. */
 int phip_last_timings(phip_handle* h, const char** names, float* ms, int max);
-/* Enable (1) or disable (0) event timing (off by default). */
+/* Enable (1) or disable (0) event timing (off by default); 2 keeps the
+ * timings of every later call until the next phip_set_timing, so a timed
+ * loop can read them once, after it ends (the reads synchronise). */
 void phip_set_timing(phip_handle* h, int on);
 /* Counters of the last fast-path Receive batch: out[0] hot-directory
  * entries, out[1] messages folded through the directory, out[2] messages

@@ -75,6 +75,7 @@ struct phip_handle {
   u64 tag_mask = ~0ull;
   DevBuf buf[B_COUNT_];
   bool timing = false;
+  bool timing_accumulate = false;   // phip_set_timing(h, 2): keep every call's timings
   std::vector<Timing> timings;
   std::vector<Timing> event_pool;
   size_t pool_used = 0;
@@ -181,7 +182,7 @@ int check_flags(phip_handle* h) {
 void begin_call(phip_handle* h) {
   h->err.clear();
   hipSetDevice(h->device);
-  if (h->timing) {
+  if (h->timing && !h->timing_accumulate) {
     h->timings.clear();
     h->pool_used = 0;
   }
@@ -1621,7 +1622,19 @@ int phip_last_timings(phip_handle* h, const char** names, float* ms, int max) {
 }
 
 void phip_set_timing(phip_handle* h, int on) {
-  if (h) h->timing = on != 0;
+  if (!h) return;
+  std::lock_guard<std::mutex> g(h->mu);
+  h->timing = on != 0;
+  h->timing_accumulate = on == 2;
+  h->timings.clear();
+  h->pool_used = 0;
+  // events for a timed loop made up front, not inside it
+  while (on == 2 && h->event_pool.size() < 1024) {
+    Timing tm{"", nullptr, nullptr};
+    hipEventCreate(&tm.a);
+    hipEventCreate(&tm.b);
+    h->event_pool.push_back(tm);
+  }
 }
 
 int phip_set_stream(phip_handle* h, void* stream) {

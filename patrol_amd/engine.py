@@ -137,8 +137,10 @@ class GPURepo:
             raise ValueError("torch's current stream is the default stream; set a torch.cuda.Stream first")
         self.set_stream(s)
 
-    def set_timing(self, on: bool):
-        self.L.phip_set_timing(self.h, 1 if on else 0)
+    def set_timing(self, on, accumulate: bool = False):
+        """Event timing per kernel; accumulate=True keeps every call's
+        timings until timings() is read (for a timed loop)."""
+        self.L.phip_set_timing(self.h, (2 if accumulate else 1) if on else 0)
 
     def last_stats(self):
         """(hot-directory entries, messages folded through it, misses) of the
@@ -147,10 +149,10 @@ class GPURepo:
         k = self.L.phip_last_stats(self.h, out, 3)
         return tuple(int(out[i]) for i in range(k))
 
-    def timings(self):
-        names = (C.c_char_p * 256)()
-        ms = (C.c_float * 256)()
-        k = self.L.phip_last_timings(self.h, names, ms, 256)
+    def timings(self, max_entries: int = 1 << 14):
+        names = (C.c_char_p * max_entries)()
+        ms = (C.c_float * max_entries)()
+        k = self.L.phip_last_timings(self.h, names, ms, max_entries)
         return [(names[i].decode(), float(ms[i])) for i in range(k)]
 
     # -------------------------------------------------------------- repo --
