@@ -228,6 +228,10 @@ int insert_names(phip_handle* h, Src src, u32* list, u32 nlist, const int64_t* n
       (rc = ensure(h, B_RETRY, nlist, &retry)))
     return rc;
   u32 total = 0, ncur = nlist;
+  // ctr[3] counts this call's claims (B_CSLOT/B_CMSG positions): a batch can
+  // run the pipeline twice (finish_many_misses, resolve_all), so it starts
+  // from zero here, not at the batch's reset_ctr.
+  HIPCHK(h, hipMemsetAsync(h->ctr + 3, 0, sizeof(u32), h->stream));
   // Swap buffers between rounds: round k reads `cur`, writes retries to `nxt`.
   u32* nxt = retry;
   u32* spare = nullptr;
@@ -714,6 +718,14 @@ int stage_names(phip_handle* h, const uint8_t* names, const uint32_t* offs, u32 
   src->blob = d_names;
   src->offs = d_offs;
   return PHIP_OK;
+}
+
+// Datagram offsets from the host: non-decreasing, so every datagram the
+// kernels read lies inside the bytes[offs[0] .. offs[n]) that were copied.
+bool datagrams_ok(const uint64_t* offs, u32 n) {
+  for (u32 i = 0; i < n; ++i)
+    if (offs[i + 1] < offs[i]) return false;
+  return true;
 }
 
 bool names_ok(const uint32_t* offs, u32 n) {
@@ -1207,6 +1219,8 @@ int phip_receive_datagrams(phip_handle* h, const uint8_t* bytes, const uint64_t*
   int rc;
   const uint64_t* d_offs;
   const u8* d_bytes;
+  if (!dev && !datagrams_ok(offs, n))
+    return set_err(h, PHIP_ERR_INVALID, "datagram offsets decrease");
   if ((rc = stage(h, B_DOFFS, offs, (size_t)n + 1, dev, &d_offs))) return rc;
   size_t nb = dev ? 0 : offs[n];
   if ((rc = stage(h, B_BYTES, bytes, nb, dev, &d_bytes))) return rc;
@@ -1307,7 +1321,7 @@ int phip_ring_submit(phip_ring* r, uint32_t slot, uint32_t n) {
   phip_ring::Slot& s = r->slots[slot];
   if (s.state != phip_ring::kAcquired) return PHIP_ERR_BUSY;
   const u64 nb = s.hoffs[n];
-  if (s.hoffs[0] != 0 || nb > r->max_bytes) return PHIP_ERR_INVALID;
+  if (s.hoffs[0] != 0 || nb > r->max_bytes || !datagrams_ok(s.hoffs, n)) return PHIP_ERR_INVALID;
   hipSetDevice(r->h->device);
   hipError_t e;
   if ((e = hipMemcpyAsync(s.doffs, s.hoffs, ((size_t)n + 1) * sizeof(uint64_t),

@@ -39,11 +39,14 @@ def pa():
 
 
 def gpu_dump(repo):
-    return {k: (v.added, v.taken, v.elapsed, v.created) for k, v in repo.dump().items()}
+    d = {k: (v.added, v.taken, v.elapsed, v.created) for k, v in repo.dump().items()}
+    # one record per name: the bucket count equals the distinct names dumped
+    assert len(repo) == len(d), (len(repo), len(d))
+    return d
 
 
 def assert_same_dump(g, o):
-    assert len(g) == len(o)
+    assert len(g) == len(o)   # distinct names (the dump is keyed by name)
     bad = [k for k in o if g.get(k) != o[k]]
     assert not bad, [(k, g.get(k), o[k]) for k in bad[:5]]
 

@@ -337,3 +337,34 @@ def test_udp_round_trip_through_ring(lib):
         rx.close()
         tx.close()
         g.close()
+
+
+@pytest.mark.gpu
+def test_bad_offsets_are_refused_before_any_device_read(lib):
+    """Decreasing datagram offsets from the host would send the kernels
+    outside the copied bytes: phip_ring_submit and phip_receive_datagrams
+    refuse them (PHIP_ERR_INVALID), and the slot stays usable."""
+    import ctypes as C
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    g = lib.GPURepo(log2_slots=10)
+    ring = lib.Ring(g, nslots=2, max_msgs=8)
+    slot, bv, ov = ring.acquire()
+    d = [_datagram(b"b%d" % i, i + 1, 0, 0) for i in range(3)]
+    blob = b"".join(d)
+    bv[:len(blob)] = np.frombuffer(blob, np.uint8)
+    ov[:4] = [0, len(d[0]), 5, len(blob)]                 # offs[2] < offs[1]
+    with pytest.raises(lib.PatrolHipError) as ex:
+        ring.submit(slot, 3)
+    assert ex.value.code == -1
+    ov[:4] = np.cumsum([0] + [len(x) for x in d])
+    ring.submit(slot, 3)
+    assert list(ring.receive(slot, 3, _gen.T0)["status"]) == [1 | 0x80] * 3
+    offs = np.array([0, 40, 20, 60], np.uint64)
+    data = np.zeros(72, np.uint8)
+    rc = g.L.phip_receive_datagrams(g.h, data.ctypes.data, offs.ctypes.data, 3, _gen.T0, None,
+                                    None, 0)
+    assert rc == -1
+    ring.close()
+    g.close()
