@@ -165,11 +165,11 @@ int read_ctr(phip_handle* h) {
 }
 
 int reset_ctr(phip_handle* h) {
-  HIPCHK(h, hipMemsetAsync(h->ctr, 0, 16 * sizeof(u32), h->stream));
   // ctr[5] = first short datagram, ctr[kCtrDirty] = first dirty message
-  // (phip_kernels.hpp): both start at "none".
-  HIPCHK(h, hipMemsetAsync(h->ctr + 5, 0xFF, sizeof(u32), h->stream));
-  HIPCHK(h, hipMemsetAsync(h->ctr + kCtrDirty, 0xFF, sizeof(u32), h->stream));
+  // (phip_kernels.hpp): both start at "none", the rest at zero.
+  static_assert(kCtrDirty == 12, "k_batch_reset");
+  k_batch_reset<<<1, kShards, 0, h->stream>>>(h->ctr, nullptr);
+  HIPCHK(h, hipGetLastError());
   return PHIP_OK;
 }
 
@@ -331,20 +331,22 @@ inline unsigned fast_grid(phip_handle* h, u32 n) {
 
 int join_hot(phip_handle* h, const HotHdr* hot);
 
-// The fast path over a batch input (SoaIn or WireIn), with the counters reset
-// (reset_ctr) and the hot directory forked (fork_hot).  Applies the batch's
-// clean prefix: the messages before the first dirty one (*first_dirty; n if
-// none) and before the first malformed datagram (ctr[5]).  The prefix's
-// misses (*nmiss of them) are listed in B_MISS.
+// The fast path over a batch input (SoaIn or WireIn; hsrc: its names for the
+// hot-directory sample).  Resets the batch's counters, classifies, builds the
+// hot directory on stream2 and applies the batch's clean prefix: the messages
+// before the first dirty one (*first_dirty; n if none) and before the first
+// malformed datagram (ctr[5]).  The prefix's misses (*nmiss of them) are
+// listed in B_MISS.
 // A sharded append list over `units` units of up to `per_unit` entries
 // (counters zeroed on the stream).
-int sharded(phip_handle* h, BufId base_id, u32 units, u32 per_unit, Sharded* out) {
+int sharded(phip_handle* h, BufId base_id, u32 units, u32 per_unit, Sharded* out,
+            bool zero = true) {
   int rc;
   out->cap = shard_cap(units, per_unit);
   if ((rc = ensure(h, base_id, (size_t)kShards * out->cap, &out->base)) ||
       (rc = ensure(h, B_MSCNT, 2 * kShards, &out->cnt)))
     return rc;
-  HIPCHK(h, hipMemsetAsync(out->cnt, 0, kShards * sizeof(u32), h->stream));
+  if (zero) HIPCHK(h, hipMemsetAsync(out->cnt, 0, kShards * sizeof(u32), h->stream));
   return PHIP_OK;
 }
 
@@ -366,20 +368,38 @@ int pack_sharded(phip_handle* h, const Sharded& sh, u32 total_slot, u32* out, u3
   return PHIP_OK;
 }
 
-template <class In>
-int fast_apply(phip_handle* h, In in, u32 n, u8* status, const HotHdr* hot,
-               const HotEntry* hot_dir, u32* first_dirty, u32* nmiss) {
+template <class Src>
+int fork_hot(phip_handle* h, Src src, u32 n, const HotHdr** hot, const HotEntry** hot_dir);
+
+// Enqueue order matters at this size (2 ms per 100M messages): the counter
+// reset and the classification go first, so the GPU starts reading the batch
+// while the host still enqueues the hot-directory chain on stream2 (about
+// 0.1 ms of API calls that used to sit in front of k_classify).
+template <class In, class HotSrc>
+int fast_apply(phip_handle* h, In in, HotSrc hsrc, u32 n, u8* status, u32* first_dirty,
+               u32* nmiss) {
   u32* miss;
   int rc;
   Sharded msh;
   if ((rc = ensure(h, B_MISS, n, &miss)) ||
-      (rc = sharded(h, B_MSHARD, (n + 63) / 64, 64, &msh)))
+      (rc = sharded(h, B_MSHARD, (n + 63) / 64, 64, &msh, false)))
     return rc;
+  k_batch_reset<<<1, kShards, 0, h->stream>>>(h->ctr, msh.cnt);
+  HIPCHK(h, hipGetLastError());
+  const bool with_hot = n >= kHotMinBatch;
+  // A small batch classifies in a few µs, less than the directory chain
+  // takes: that chain goes first then.
+  const bool hot_first = n < (1u << 23);
+  const HotHdr* hot = nullptr;
+  const HotEntry* hot_dir = nullptr;
+  if (with_hot) HIPCHK(h, hipEventRecord(h->ev_fork, h->stream));
+  if (with_hot && hot_first && (rc = fork_hot(h, hsrc, n, &hot, &hot_dir))) return rc;
   {
     Launch l(h, "k_classify");
     k_classify<In><<<grid_for(n), kBlock, 0, h->stream>>>(in, n, h->ctr);
   }
   HIPCHK(h, hipGetLastError());
+  if (with_hot && !hot_first && (rc = fork_hot(h, hsrc, n, &hot, &hot_dir))) return rc;
   // The fast kernel is enqueued behind the classification without a host
   // round trip; it reads the counters itself.
   if ((rc = join_hot(h, hot))) return rc;
@@ -451,13 +471,8 @@ int finish_many_misses(phip_handle* h, Src src, const uint64_t* a, const uint64_
     HIPCHK(h, hipGetLastError());
   }
   // 4. the fast pass again
-  if ((rc = reset_ctr(h))) return rc;
-  const HotHdr* hot;
-  const HotEntry* hot_dir;
-  if ((rc = fork_hot(h, src, prefix, &hot, &hot_dir))) return rc;
   u32 fd = prefix;
-  if ((rc = fast_apply(h, SoaIn<Src>{src, a, t, e}, prefix, status, hot, hot_dir, &fd, nmiss2)))
-    return rc;
+  if ((rc = fast_apply(h, SoaIn<Src>{src, a, t, e}, src, prefix, status, &fd, nmiss2))) return rc;
   // 5. PHIP_ST_CREATED after the second pass wrote its statuses
   if (status && n_claimed) {
     Launch l(h, "k_mark_created");
@@ -508,7 +523,8 @@ int fork_hot(phip_handle* h, Src src, u32 n, const HotHdr** hot, const HotEntry*
   *hot = nullptr;
   *hot_dir = nullptr;
   if (n < kHotMinBatch) return PHIP_OK;
-  HIPCHK(h, hipEventRecord(h->ev_fork, h->stream));
+  // ev_fork: recorded by fast_apply before the classification (stream2 waits
+  // only for the batch's producers, not for k_classify)
   HIPCHK(h, hipStreamWaitEvent(h->stream2, h->ev_fork, 0));
   int rc;
   if ((rc = build_hot(h, src, n, h->stream2, hot, hot_dir))) return rc;
@@ -806,15 +822,10 @@ template <class Src>
 int receive_decoded(phip_handle* h, Src src, const uint64_t* a, const uint64_t* t,
                     const int64_t* e, u32 n, i64 now, const OutView& ow) {
   int rc;
-  if ((rc = reset_ctr(h))) return rc;
   // The hot directory (read-only on the table and the batch) is built on
   // stream2 while the batch is classified.
-  const HotHdr* hot;
-  const HotEntry* hot_dir;
-  if ((rc = fork_hot(h, src, n, &hot, &hot_dir))) return rc;
   u32 fd = n, nmiss = 0;
-  if ((rc = fast_apply(h, SoaIn<Src>{src, a, t, e}, n, ow.status, hot, hot_dir, &fd, &nmiss)))
-    return rc;
+  if ((rc = fast_apply(h, SoaIn<Src>{src, a, t, e}, src, n, ow.status, &fd, &nmiss))) return rc;
   return finish_receive(h, src, a, t, e, n, fd, nmiss, now, ow);
 }
 
@@ -1167,12 +1178,9 @@ int receive_datagrams_dev(phip_handle* h, const u8* d_bytes, const uint64_t* d_o
   // datagram in place; no decoded copy is written.
   // Only a clean prefix with new buckets, or an incast / -0.0, has the
   // datagrams decoded to the SoA form, for the paths that need it.
-  if ((rc = reset_ctr(h))) return rc;
-  const HotHdr* hot;
-  const HotEntry* hot_dir;
-  if ((rc = fork_hot(h, Datagrams{d_bytes, d_offs}, n, &hot, &hot_dir))) return rc;
   u32 fd = n, nmiss = 0;
-  if ((rc = fast_apply(h, WireIn{d_bytes, d_offs}, n, ow.status, hot, hot_dir, &fd, &nmiss)))
+  if ((rc = fast_apply(h, WireIn{d_bytes, d_offs}, Datagrams{d_bytes, d_offs}, n, ow.status, &fd,
+                       &nmiss)))
     return rc;
   const u32 stop = std::min<u32>(h->ctr_host[5], n);
   // Statuses of the short datagram and everything after it (the Go loop exits).

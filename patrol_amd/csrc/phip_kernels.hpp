@@ -130,6 +130,15 @@ struct Sharded {
   }
 };
 
+// A batch's counters in one launch: ctr[16] zero except ctr[5] (first
+// malformed datagram) and ctr[kCtrDirty] (first dirty message), which start
+// at "none"; and, when given, a sharded list's kShards counters.
+__global__ __launch_bounds__(kShards) void k_batch_reset(u32* ctr, u32* shard_cnt) {
+  const u32 t = threadIdx.x;
+  if (t < 16) ctr[t] = (t == 5 || t == 12) ? ~0u : 0u;
+  if (shard_cnt) shard_cnt[t] = 0;
+}
+
 // One workgroup of kShards lanes: exclusive offsets of the shards (into
 // cnt[kShards + s]), the total into *total and the largest shard into *maxc.
 __global__ __launch_bounds__(kShards) void k_shard_scan(u32* cnt, u32* total, u32* maxc) {

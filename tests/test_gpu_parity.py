@@ -782,3 +782,26 @@ def test_seed_many_names_with_duplicates(pa):
     assert len(g) == K
     assert_same_dump(gpu_dump(g), o.dump())
     g.close()
+
+
+def test_empty_batches_are_no_ops(pa):
+    """n = 0 on every batched entry point: PHIP_OK, nothing created, nothing
+    read (the Go loops simply do not iterate)."""
+    g = pa.GPURepo(log2_slots=10)
+    g.seed([b"b1"], [0x3FF0000000000000], [0], [5], [_gen.T0])
+    before = gpu_dump(g)
+    out = g.receive_datagrams([], _gen.T0)
+    assert out["stop"] == 0 and len(out["status"]) == 0
+    assert len(g.receive_soa([], [], [], [], _gen.T0)["status"]) == 0
+    assert len(g.upsert_soa([], [], [], [], _gen.T0)["status"]) == 0
+    e = np.zeros(0, np.int64)
+    res = g.apply_mixed(np.zeros(0, np.uint8), [], e, e, e, np.zeros(0, np.uint64),
+                        np.zeros(0, np.uint64), np.zeros(0, np.uint64), e)
+    assert len(res["status"]) == 0
+    ring = pa.Ring(g, nslots=2, max_msgs=4)
+    slot, n = ring.fill([])
+    ring.submit(slot, n)
+    assert len(ring.receive(slot, n, _gen.T0)["status"]) == 0
+    ring.close()
+    assert gpu_dump(g) == before
+    g.close()
