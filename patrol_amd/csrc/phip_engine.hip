@@ -396,7 +396,15 @@ int fast_apply(phip_handle* h, In in, HotSrc hsrc, u32 n, u8* status, u32* first
   if (with_hot && hot_first && (rc = fork_hot(h, hsrc, n, &hot, &hot_dir))) return rc;
   {
     Launch l(h, "k_classify");
-    k_classify<In><<<grid_for(n), kBlock, 0, h->stream>>>(in, n, h->ctr);
+    bool done = false;
+    if constexpr (In::kSoa) {
+      if ((((uintptr_t)in.ma | (uintptr_t)in.mt) & 15) == 0) {
+        k_classify_soa2<<<grid_for((n + 1) / 2), kBlock, 0, h->stream>>>(in.ma, in.mt, in.me, n,
+                                                                          h->ctr);
+        done = true;
+      }
+    }
+    if (!done) k_classify<In><<<grid_for(n), kBlock, 0, h->stream>>>(in, n, h->ctr);
   }
   HIPCHK(h, hipGetLastError());
   if (with_hot && !hot_first && (rc = fork_hot(h, hsrc, n, &hot, &hot_dir))) return rc;

@@ -532,6 +532,7 @@ struct SoaIn {   // decoded messages (phip_receive_soa / decoded datagrams)
   const uint64_t* ma;
   const uint64_t* mt;
   const int64_t* me;
+  static constexpr bool kSoa = true;
   __device__ inline const u8* blob() const { return src.blob; }
   // Round 1 of a message on its own (the name's offset and length), so the
   // fast kernel can issue it one chunk ahead.
@@ -580,6 +581,7 @@ __device__ inline u64 funnel8(u64 lo, u64 hi, u32 sb) {   // bytes sb..sb+7 of h
 struct WireIn {
   const u8* bytes;
   const uint64_t* offs;
+  static constexpr bool kSoa = false;
   __device__ inline const u8* blob() const { return bytes; }
   struct Pre { u64 o; u32 sz; };   // round 1: the datagram's start and size
   __device__ inline Pre pre(u32 i) const {
@@ -638,6 +640,35 @@ template <class In>
 __global__ __launch_bounds__(kBlock) void k_classify(In in, u32 n, u32* ctr) {
   const u32 i = blockIdx.x * kBlock + threadIdx.x;
   note_dirty(i < n && in.dirty(i, ctr), i, ctr);
+}
+
+// The same for decoded messages with 16-byte aligned replica columns: two
+// messages per lane, one 16-byte load per column (the pass is a pure stream
+// of 16 bytes per message; elapsed is read only when both floats are zero).
+// Lane l holds messages 2l, 2l+1 of its wave's 128, so the lowest dirty lane
+// still holds the lowest dirty index.
+typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+__global__ __launch_bounds__(kBlock) void k_classify_soa2(const uint64_t* __restrict__ ma,
+                                                          const uint64_t* __restrict__ mt,
+                                                          const int64_t* __restrict__ me, u32 n,
+                                                          u32* ctr) {
+  const u32 i0 = 2 * (blockIdx.x * kBlock + threadIdx.x);
+  bool d = false;
+  u32 at = i0;
+  if (i0 + 1 < n) {
+    const u64x2 a = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(ma + i0));
+    const u64x2 t = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(mt + i0));
+    const bool z0 = is_zero_bits(a.x) && is_zero_bits(t.x);
+    const bool z1 = is_zero_bits(a.y) && is_zero_bits(t.y);
+    const bool d0 = (z0 && me[i0] == 0) || a.x == kSign || t.x == kSign;
+    const bool d1 = (z1 && me[i0 + 1] == 0) || a.y == kSign || t.y == kSign;
+    d = d0 || d1;
+    at = d0 ? i0 : i0 + 1;
+  } else if (i0 < n) {
+    const u64 a = ma[i0], t = mt[i0];
+    d = (is_zero_bits(a) && is_zero_bits(t) && me[i0] == 0) || a == kSign || t == kSign;
+  }
+  note_dirty(d, at, ctr);
 }
 
 template <class In>
