@@ -29,6 +29,25 @@ using namespace phip;
 
 namespace {
 
+// The ordered path's (slot, seq) sort: slots have L <= 31 bits (25 for the
+// C2/C3 tables), so 8-bit places spend a whole fourth pass on one bit; wider
+// places (PHIP_SORT_BITS) cover 25 bits in three.
+#ifndef PHIP_SORT_BITS
+#define PHIP_SORT_BITS 9
+#endif
+#ifndef PHIP_SORT_BLOCK
+#define PHIP_SORT_BLOCK 1024
+#endif
+#ifndef PHIP_SORT_ITEMS
+#define PHIP_SORT_ITEMS 8
+#endif
+using SlotSortConfig = rocprim::radix_sort_config<
+    rocprim::default_config, rocprim::default_config,
+    rocprim::radix_sort_onesweep_config<
+        rocprim::kernel_config<PHIP_SORT_BLOCK, PHIP_SORT_ITEMS>,
+        rocprim::kernel_config<PHIP_SORT_BLOCK, PHIP_SORT_ITEMS>, PHIP_SORT_BITS,
+        rocprim::block_radix_rank_algorithm::match>>;
+
 enum BufId {
   B_NAMES, B_OFFS, B_A, B_T, B_E, B_KIND, B_NOW, B_FREQ, B_PER, B_COUNT,
   B_STATUS, B_REM, B_HAVE, B_REPLY,
@@ -623,7 +642,8 @@ int ordered(phip_handle* h, Src src, u32 n, const OpView& ov, const OutView& ow)
   }
   // Stable radix sort of (slot, seq) pairs: per-bucket arrival order kept.
   size_t tb = 0;
-  HIPCHK(h, rocprim::radix_sort_pairs(nullptr, tb, slot, sslot, idx, sidx, n, 0u, h->L, h->stream));
+  HIPCHK(h, rocprim::radix_sort_pairs<SlotSortConfig>(nullptr, tb, slot, sslot, idx, sidx, n, 0u, h->L,
+                                                       h->stream));
   size_t tb2 = 0;
   HIPCHK(h, rocprim::run_length_encode(nullptr, tb2, sslot, n, uslot, scnt, h->ctr + 6, h->stream));
   size_t tb3 = 0;
@@ -633,7 +653,8 @@ int ordered(phip_handle* h, Src src, u32 n, const OpView& ov, const OutView& ow)
   if ((rc = ensure(h, B_TEMP, std::max(tb, std::max(tb2, tb3)), &temp))) return rc;
   {
     Launch l(h, "radix_sort_pairs");
-    HIPCHK(h, rocprim::radix_sort_pairs(temp, tb, slot, sslot, idx, sidx, n, 0u, h->L, h->stream));
+    HIPCHK(h, rocprim::radix_sort_pairs<SlotSortConfig>(temp, tb, slot, sslot, idx, sidx, n, 0u,
+                                                         h->L, h->stream));
   }
   {
     Launch l(h, "run_length_encode");
