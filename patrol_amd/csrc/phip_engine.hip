@@ -161,18 +161,20 @@ struct Launch {
     if (!h->timing) return;
     if (h->pool_used == h->event_pool.size()) {
       Timing tm{n, nullptr, nullptr};
-      hipEventCreate(&tm.a);
-      hipEventCreate(&tm.b);
+      if (hipEventCreate(&tm.a) != hipSuccess) return;
+      if (hipEventCreate(&tm.b) != hipSuccess) {
+        (void)hipEventDestroy(tm.a);
+        return;
+      }
       h->event_pool.push_back(tm);
     }
     t = &h->event_pool[h->pool_used++];
     t->name = n;
-    hipEventRecord(t->a, s);
+    if (hipEventRecord(t->a, s) != hipSuccess) t = nullptr;
   }
   ~Launch() {
     if (t) {
-      hipEventRecord(t->b, s);
-      h->timings.push_back(*t);
+      if (hipEventRecord(t->b, s) == hipSuccess) h->timings.push_back(*t);
     }
   }
 };
@@ -198,13 +200,16 @@ int check_flags(phip_handle* h) {
   return PHIP_OK;
 }
 
-void begin_call(phip_handle* h) {
+// Every entry point binds the handle's device first: Go goroutines migrate
+// across OS threads, and the HIP current device is per thread.
+int begin_call(phip_handle* h) {
   h->err.clear();
-  hipSetDevice(h->device);
   if (h->timing && !h->timing_accumulate) {
     h->timings.clear();
     h->pool_used = 0;
   }
+  HIPCHK(h, hipSetDevice(h->device));
+  return PHIP_OK;
 }
 
 // Copy a host array into a device staging buffer (or pass device pointers).
@@ -258,7 +263,7 @@ int insert_names(phip_handle* h, Src src, u32* list, u32 nlist, const int64_t* n
   // Every round claims at least one slot while names are pending (a pending
   // name met a slot claimed in that same round), so this terminates; with a
   // 64-bit tag a second round is already rare.
-  for (int round = 0; ncur > 0; ++round) {
+  while (ncur > 0) {
     if (h->n_buckets >= h->max_load)
       return set_err(h, PHIP_ERR_FULL, "table load limit reached: %llu buckets of %llu allowed",
                      (unsigned long long)h->n_buckets, (unsigned long long)h->max_load);
@@ -912,28 +917,30 @@ int phip_open(const phip_config* cfg, phip_handle** out) {
 }
 
 void phip_close(phip_handle* h) {
+  // Teardown is best effort: every resource is released whatever the
+  // earlier calls return.
   if (!h) return;
-  hipSetDevice(h->device);
-  if (h->stream) hipStreamSynchronize(h->stream);
-  if (h->stream2) hipStreamSynchronize(h->stream2);
+  (void)hipSetDevice(h->device);
+  if (h->stream) (void)hipStreamSynchronize(h->stream);
+  if (h->stream2) (void)hipStreamSynchronize(h->stream2);
   for (auto& b : h->buf)
-    if (b.p) hipFree(b.p);
+    if (b.p) (void)hipFree(b.p);
   for (auto& t : h->event_pool) {
-    hipEventDestroy(t.a);
-    hipEventDestroy(t.b);
+    (void)hipEventDestroy(t.a);
+    (void)hipEventDestroy(t.b);
   }
-  if (h->recs) hipFree(h->recs);
-  if (h->aux) hipFree(h->aux);
-  if (h->arena) hipFree(h->arena);
-  if (h->arena_cursor) hipFree(h->arena_cursor);
-  if (h->ctr) hipFree(h->ctr);
-  if (h->ctr_host) hipHostFree(h->ctr_host);
-  if (h->ev_fork) hipEventDestroy(h->ev_fork);
-  if (h->ev_join) hipEventDestroy(h->ev_join);
-  if (h->stream2) hipStreamDestroy(h->stream2);
+  if (h->recs) (void)hipFree(h->recs);
+  if (h->aux) (void)hipFree(h->aux);
+  if (h->arena) (void)hipFree(h->arena);
+  if (h->arena_cursor) (void)hipFree(h->arena_cursor);
+  if (h->ctr) (void)hipFree(h->ctr);
+  if (h->ctr_host) (void)hipHostFree(h->ctr_host);
+  if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
+  if (h->ev_join) (void)hipEventDestroy(h->ev_join);
+  if (h->stream2) (void)hipStreamDestroy(h->stream2);
   if (h->own_stream) {
-    hipStreamSynchronize(h->own_stream);
-    hipStreamDestroy(h->own_stream);
+    (void)hipStreamSynchronize(h->own_stream);
+    (void)hipStreamDestroy(h->own_stream);
   }
   delete h;
 }
@@ -943,7 +950,7 @@ const char* phip_last_error(const phip_handle* h) { return h ? h->err.c_str() : 
 int phip_flush(phip_handle* h) {
   if (!h) return PHIP_ERR_INVALID;
   std::lock_guard<std::mutex> g(h->mu);
-  hipSetDevice(h->device);
+  HIPCHK(h, hipSetDevice(h->device));
   HIPCHK(h, hipStreamSynchronize(h->stream));
   return PHIP_OK;
 }
@@ -955,7 +962,7 @@ int phip_seed(phip_handle* h, const uint8_t* names, const uint32_t* name_offs, u
               const phip_state* states, uint32_t flags) {
   if (!h || (n && (!names || !name_offs || !states))) return PHIP_ERR_INVALID;
   std::lock_guard<std::mutex> g(h->mu);
-  begin_call(h);
+  if (int rc0 = begin_call(h)) return rc0;
   if (n == 0) return PHIP_OK;
   bool dev = flags & PHIP_DEVICE_PTRS;
   if (!dev && !names_ok(name_offs, n)) return set_err(h, PHIP_ERR_NAME_TOO_LARGE, "name > 231 bytes");
@@ -982,7 +989,7 @@ int phip_get(phip_handle* h, const uint8_t* name, uint32_t len, phip_state* out)
   if (!h || (!name && len) || !out) return PHIP_ERR_INVALID;
   if (len > PHIP_MAX_NAME_LEN) return 0;
   std::lock_guard<std::mutex> g(h->mu);
-  begin_call(h);
+  if (int rc0 = begin_call(h)) return rc0;
   u8* d_name;
   Rec* d_rec;
   int rc;
@@ -1029,7 +1036,7 @@ static u64 arena_used(phip_handle* h) {
 uint64_t phip_snapshot_bytes(phip_handle* h) {
   if (!h) return 0;
   std::lock_guard<std::mutex> g(h->mu);
-  begin_call(h);
+  if (begin_call(h)) return 0;
   const u64 used = arena_used(h);
   if (used == ~0ull) return 0;
   return sizeof(SnapHeader) + h->cap * sizeof(Rec) + used;
@@ -1038,7 +1045,7 @@ uint64_t phip_snapshot_bytes(phip_handle* h) {
 int phip_snapshot(phip_handle* h, uint8_t* out, uint64_t cap) {
   if (!h || !out) return PHIP_ERR_INVALID;
   std::lock_guard<std::mutex> g(h->mu);
-  begin_call(h);
+  if (int rc0 = begin_call(h)) return rc0;
   const u64 used = arena_used(h);
   if (used == ~0ull) return set_err(h, PHIP_ERR_HIP, "snapshot: arena cursor read failed");
   const u64 need = sizeof(SnapHeader) + h->cap * sizeof(Rec) + used;
@@ -1061,7 +1068,7 @@ int phip_snapshot(phip_handle* h, uint8_t* out, uint64_t cap) {
 int phip_restore(phip_handle* h, const uint8_t* in, uint64_t len) {
   if (!h || !in || len < sizeof(SnapHeader)) return PHIP_ERR_INVALID;
   std::lock_guard<std::mutex> g(h->mu);
-  begin_call(h);
+  if (int rc0 = begin_call(h)) return rc0;
   SnapHeader hd;
   std::memcpy(&hd, in, sizeof hd);
   if (std::memcmp(hd.magic, kSnapMagic, 8) || hd.abi != PHIP_ABI_VERSION || hd.rec_bytes != sizeof(Rec))
@@ -1087,7 +1094,7 @@ int phip_export_datagrams(phip_handle* h, const uint8_t* names, const uint32_t* 
                           uint32_t n, uint8_t* out, uint8_t* found, uint32_t flags) {
   if (!h || (n && (!names || !name_offs || !out || !found))) return PHIP_ERR_INVALID;
   std::lock_guard<std::mutex> g(h->mu);
-  begin_call(h);
+  if (int rc0 = begin_call(h)) return rc0;
   if (n == 0) return PHIP_OK;
   const bool dev = flags & PHIP_DEVICE_PTRS;
   if (!dev && !names_ok(name_offs, n)) return set_err(h, PHIP_ERR_NAME_TOO_LARGE, "name > 231 bytes");
@@ -1114,7 +1121,7 @@ int phip_dump(phip_handle* h, uint8_t* names, uint64_t names_cap, uint64_t* name
               phip_state* states, uint64_t max_n, uint64_t* n_out, uint64_t* names_bytes_out) {
   if (!h) return PHIP_ERR_INVALID;
   std::lock_guard<std::mutex> g(h->mu);
-  begin_call(h);
+  if (int rc0 = begin_call(h)) return rc0;
   int rc;
   u32* list;
   if ((rc = ensure(h, B_DUMP, h->n_buckets + 1, &list))) return rc;
@@ -1172,7 +1179,7 @@ int phip_receive_soa(phip_handle* h, const phip_msgs* m, int64_t now, const phip
                      uint32_t flags) {
   if (!h || !m) return PHIP_ERR_INVALID;
   std::lock_guard<std::mutex> g(h->mu);
-  begin_call(h);
+  if (int rc0 = begin_call(h)) return rc0;
   u32 n = m->n;
   if (n == 0) return PHIP_OK;
   if (!m->names || !m->name_offs || !m->added || !m->taken || !m->elapsed) return PHIP_ERR_INVALID;
@@ -1249,7 +1256,7 @@ int phip_receive_datagrams(phip_handle* h, const uint8_t* bytes, const uint64_t*
                            uint32_t flags) {
   if (!h || (n && (!bytes || !offs))) return PHIP_ERR_INVALID;
   std::lock_guard<std::mutex> g(h->mu);
-  begin_call(h);
+  if (int rc0 = begin_call(h)) return rc0;
   if (stop_index) *stop_index = n;
   if (n == 0) return PHIP_OK;
   bool dev = flags & PHIP_DEVICE_PTRS;
@@ -1290,16 +1297,16 @@ struct phip_ring {
 
 void phip_ring_close(phip_ring* r) {
   if (!r) return;
-  hipSetDevice(r->h->device);
-  if (r->copy) hipStreamSynchronize(r->copy);
+  (void)hipSetDevice(r->h->device);
+  if (r->copy) (void)hipStreamSynchronize(r->copy);
   for (auto& s : r->slots) {
-    if (s.hbytes) hipHostFree(s.hbytes);
-    if (s.hoffs) hipHostFree(s.hoffs);
-    if (s.dbytes) hipFree(s.dbytes);
-    if (s.doffs) hipFree(s.doffs);
-    if (s.copied) hipEventDestroy(s.copied);
+    if (s.hbytes) (void)hipHostFree(s.hbytes);
+    if (s.hoffs) (void)hipHostFree(s.hoffs);
+    if (s.dbytes) (void)hipFree(s.dbytes);
+    if (s.doffs) (void)hipFree(s.doffs);
+    if (s.copied) (void)hipEventDestroy(s.copied);
   }
-  if (r->copy) hipStreamDestroy(r->copy);
+  if (r->copy) (void)hipStreamDestroy(r->copy);
   delete r;
 }
 
@@ -1309,7 +1316,7 @@ int phip_ring_open(phip_handle* h, uint32_t nslots, uint32_t max_msgs, uint64_t 
   *out = nullptr;
   if (!h || nslots < 1 || nslots > 64 || max_msgs < 1 || max_bytes < 1) return PHIP_ERR_INVALID;
   std::lock_guard<std::mutex> g(h->mu);
-  begin_call(h);
+  if (int rc0 = begin_call(h)) return rc0;
   phip_ring* r = new phip_ring;
   r->h = h;
   r->max_msgs = max_msgs;
@@ -1359,8 +1366,11 @@ int phip_ring_submit(phip_ring* r, uint32_t slot, uint32_t n) {
   if (s.state != phip_ring::kAcquired) return PHIP_ERR_BUSY;
   const u64 nb = s.hoffs[n];
   if (s.hoffs[0] != 0 || nb > r->max_bytes || !datagrams_ok(s.hoffs, n)) return PHIP_ERR_INVALID;
-  hipSetDevice(r->h->device);
-  hipError_t e;
+  hipError_t e = hipSetDevice(r->h->device);
+  if (e != hipSuccess) {
+    r->err = hipGetErrorString(e);
+    return PHIP_ERR_HIP;
+  }
   if ((e = hipMemcpyAsync(s.doffs, s.hoffs, ((size_t)n + 1) * sizeof(uint64_t),
                           hipMemcpyHostToDevice, r->copy)) != hipSuccess ||
       (nb && (e = hipMemcpyAsync(s.dbytes, s.hbytes, nb, hipMemcpyHostToDevice, r->copy)) !=
@@ -1387,7 +1397,7 @@ int phip_ring_receive(phip_ring* r, uint32_t slot, int64_t now, const phip_resul
   int rc;
   {
     std::lock_guard<std::mutex> g(h->mu);
-    begin_call(h);
+    if ((rc = begin_call(h))) return rc;
     if (stop_index) *stop_index = s->n;
     hipError_t e = hipStreamWaitEvent(h->stream, s->copied, 0);
     if (e != hipSuccess)
@@ -1398,7 +1408,7 @@ int phip_ring_receive(phip_ring* r, uint32_t slot, int64_t now, const phip_resul
       rc = receive_datagrams_dev(h, s->dbytes, s->doffs, s->n, now, res, stop_index, false);
     // On success the stream has drained (results copied back), so the slot's
     // host and device buffers are free; after an error wait for them first.
-    if (rc) hipStreamSynchronize(h->stream);
+    if (rc) (void)hipStreamSynchronize(h->stream);  // drain; rc already set
   }
   std::lock_guard<std::mutex> g(r->mu);
   s->state = phip_ring::kFree;
@@ -1410,7 +1420,7 @@ int phip_upsert_soa(phip_handle* h, const phip_msgs* m, int64_t now, const phip_
                     uint32_t flags) {
   if (!h || !m) return PHIP_ERR_INVALID;
   std::lock_guard<std::mutex> g(h->mu);
-  begin_call(h);
+  if (int rc0 = begin_call(h)) return rc0;
   u32 n = m->n;
   if (n == 0) return PHIP_OK;
   if (!m->names || !m->name_offs || !m->added || !m->taken || !m->elapsed) return PHIP_ERR_INVALID;
@@ -1436,7 +1446,7 @@ int phip_upsert_soa(phip_handle* h, const phip_msgs* m, int64_t now, const phip_
 int phip_apply_mixed(phip_handle* h, const phip_ops* ops, const phip_results* res, uint32_t flags) {
   if (!h || !ops) return PHIP_ERR_INVALID;
   std::lock_guard<std::mutex> g(h->mu);
-  begin_call(h);
+  if (int rc0 = begin_call(h)) return rc0;
   u32 n = ops->n;
   if (n == 0) return PHIP_OK;
   if (!ops->kind || !ops->names || !ops->name_offs || !ops->now) return PHIP_ERR_INVALID;
@@ -1510,7 +1520,7 @@ int phip_hash_names(phip_handle* h, const uint8_t* names, const uint32_t* name_o
   }
   if (!h) return PHIP_ERR_INVALID;
   std::lock_guard<std::mutex> g(h->mu);
-  begin_call(h);
+  if (int rc0 = begin_call(h)) return rc0;
   if (n == 0) return PHIP_OK;
   k_hash_names<<<grid_for(n), kBlock, 0, h->stream>>>(NamesOffs{names, name_offs}, n, out);
   HIPCHK(h, hipGetLastError());
@@ -1529,7 +1539,7 @@ int phip_route_pack(phip_handle* h, const phip_msgs* m, uint32_t world, uint8_t*
             !send_lens || !send_added || !send_taken || !send_elapsed || !counts || !name_bytes))
     return PHIP_ERR_INVALID;
   std::lock_guard<std::mutex> g(h->mu);
-  begin_call(h);
+  if (int rc0 = begin_call(h)) return rc0;
   if (n == 0) {
     HIPCHK(h, hipMemsetAsync(counts, 0, world * sizeof(uint64_t), h->stream));
     HIPCHK(h, hipMemsetAsync(name_bytes, 0, world * sizeof(uint64_t), h->stream));
@@ -1626,7 +1636,7 @@ int phip_ae_local_max(phip_handle* h, const int64_t* replicas, uint32_t nrep, ui
   if (!h || !(flags & PHIP_DEVICE_PTRS) || (nbuckets && (!replicas || !out)) || nrep == 0)
     return PHIP_ERR_INVALID;
   std::lock_guard<std::mutex> g(h->mu);
-  begin_call(h);
+  if (int rc0 = begin_call(h)) return rc0;
   if (nbuckets == 0) return PHIP_OK;
   {
     Launch l(h, "k_ae_local_max");
@@ -1643,7 +1653,7 @@ int phip_ae_apply(phip_handle* h, int64_t* replicas, uint32_t nrep, uint64_t nbu
   if (!h || !(flags & PHIP_DEVICE_PTRS) || (nbuckets && (!replicas || !joined)) || nrep == 0)
     return PHIP_ERR_INVALID;
   std::lock_guard<std::mutex> g(h->mu);
-  begin_call(h);
+  if (int rc0 = begin_call(h)) return rc0;
   if (nbuckets == 0) return PHIP_OK;
   {
     Launch l(h, "k_ae_apply");
@@ -1658,13 +1668,12 @@ int phip_ae_apply(phip_handle* h, int64_t* replicas, uint32_t nrep, uint64_t nbu
 int phip_last_timings(phip_handle* h, const char** names, float* ms, int max) {
   if (!h) return 0;
   std::lock_guard<std::mutex> g(h->mu);
-  hipSetDevice(h->device);
-  hipStreamSynchronize(h->stream);
+  if (hipSetDevice(h->device) != hipSuccess || hipStreamSynchronize(h->stream) != hipSuccess) return 0;
   int k = 0;
   for (auto& t : h->timings) {
     if (k >= max) break;
     float v = 0;
-    hipEventElapsedTime(&v, t.a, t.b);
+    if (hipEventElapsedTime(&v, t.a, t.b) != hipSuccess) v = -1.0f;
     if (names) names[k] = t.name;
     if (ms) ms[k] = v;
     ++k;
@@ -1682,8 +1691,11 @@ void phip_set_timing(phip_handle* h, int on) {
   // events for a timed loop made up front, not inside it
   while (on == 2 && h->event_pool.size() < 1024) {
     Timing tm{"", nullptr, nullptr};
-    hipEventCreate(&tm.a);
-    hipEventCreate(&tm.b);
+    if (hipEventCreate(&tm.a) != hipSuccess) break;
+    if (hipEventCreate(&tm.b) != hipSuccess) {
+      (void)hipEventDestroy(tm.a);
+      break;
+    }
     h->event_pool.push_back(tm);
   }
 }
@@ -1691,7 +1703,7 @@ void phip_set_timing(phip_handle* h, int on) {
 int phip_set_stream(phip_handle* h, void* stream) {
   if (!h) return PHIP_ERR_INVALID;
   std::lock_guard<std::mutex> g(h->mu);
-  hipSetDevice(h->device);
+  HIPCHK(h, hipSetDevice(h->device));
   // work already queued on the previous stream comes first
   HIPCHK(h, hipStreamSynchronize(h->stream));
   h->stream = stream ? (hipStream_t)stream : h->own_stream;
