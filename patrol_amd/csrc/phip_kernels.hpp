@@ -15,10 +15,15 @@ constexpr int kBlock = 256;
 
 // Streaming loads, optionally non-temporal (read-once batch data should not
 // push hot slot records out of the XCD's L2).
+// (PHIP_PLAIN_STREAM: every streaming load plain, for A/B timing only.)
 template <bool NT, class T>
 __device__ inline T ld(const T* p) {
+#ifndef PHIP_PLAIN_STREAM
   if constexpr (NT) return __builtin_nontemporal_load(p);
   else return *p;
+#else
+  return *p;
+#endif
 }
 
 __device__ inline u64 load_be64(const u8* p) {
@@ -558,7 +563,11 @@ struct SoaIn {   // decoded messages (phip_receive_soa / decoded datagrams)
     if constexpr (kOffs) { off = p.a; len = p.b - p.a; }
     else { off = p.off; len = p.len; }
     ra = ld<true>(ma + i); rt = ld<true>(mt + i); re = ld<true>(me + i);
+#ifndef PHIP_NT_NAMES
     load_words3<false>(src.blob, off, len, w0, w1, w2);
+#else   // A/B timing only
+    load_words3<true>(src.blob, off, len, w0, w1, w2);
+#endif
   }
   // Classification (elapsed matters only when both floats are zero, so it is
   // read only then: a third of the pass's bytes on a clean batch).
