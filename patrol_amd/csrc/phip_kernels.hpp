@@ -220,7 +220,18 @@ __device__ inline Rec load_rec(const Rec* p) {
 // are left 0.  Enough to find and merge a name of <= kShortName bytes.
 __device__ inline Rec load_rec48(const Rec* p) {
   const uint4* q = reinterpret_cast<const uint4*>(p);
+#ifndef PHIP_NT_REC   // (A/B timing only: non-temporal record loads)
   uint4 a = q[0], b = q[1], c = q[2];
+#else
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  const u32x4* v = reinterpret_cast<const u32x4*>(p);
+  const u32x4 va = __builtin_nontemporal_load(v), vb = __builtin_nontemporal_load(v + 1),
+              vc = __builtin_nontemporal_load(v + 2);
+  uint4 a, b, c;
+  a.x = va.x; a.y = va.y; a.z = va.z; a.w = va.w;
+  b.x = vb.x; b.y = vb.y; b.z = vb.z; b.w = vb.w;
+  c.x = vc.x; c.y = vc.y; c.z = vc.z; c.w = vc.w;
+#endif
   Rec r;
   r.tag = ((u64)a.y << 32) | a.x;
   r.added = ((u64)a.w << 32) | a.z;
