@@ -676,8 +676,13 @@ __global__ __launch_bounds__(kBlock) void k_classify_soa2(const uint64_t* __rest
   bool d = false;
   u32 at = i0;
   if (i0 + 1 < n) {
+#ifndef PHIP_PLAIN_CLASSIFY   // (A/B timing only: plain loads)
     const u64x2 a = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(ma + i0));
     const u64x2 t = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(mt + i0));
+#else
+    const u64x2 a = *reinterpret_cast<const u64x2*>(ma + i0);
+    const u64x2 t = *reinterpret_cast<const u64x2*>(mt + i0);
+#endif
     const bool z0 = is_zero_bits(a.x) && is_zero_bits(t.x);
     const bool z1 = is_zero_bits(a.y) && is_zero_bits(t.y);
     const bool d0 = (z0 && me[i0] == 0) || a.x == kSign || t.x == kSign;
