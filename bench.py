@@ -2,7 +2,7 @@
 """Headline benchmark: batched replica-state merges into a device bucket table.
 
 Workload (BASELINE.json configs[1], SURVEY.md §8d "C2"): a table pre-populated
-with K = 10M buckets (2^24 slots), and per step one batch of n = 100M decoded
+with K = 10M buckets (2^25 slots), and per step one batch of n = 100M decoded
 replica messages (name + added/taken/elapsed), Zipf(1.1) over the keys, run
 through the Receive loop semantics (repo.go:54-92: GetBucket by full name,
 then Bucket.Merge) by phip_receive_soa with inputs resident in HBM.  Every
@@ -11,10 +11,17 @@ step uses a fresh batch whose states are later than the previous step's
 of its messages to the table; the batches are generated before the timed
 region.
 
-Multi-GPU (torch.distributed, one process per GPU): buckets are sharded by
-owner; each rank holds its own K-bucket shard and merges its own pre-routed
-n-message stream (weak scaling, no data-path collective).  value = all
-merges of all ranks / max-over-ranks time.
+Multi-GPU (one process per GPU; `--gpus N` without WORLD_SIZE in the
+environment starts the N ranks itself through torch.distributed.run):
+buckets are sharded by owner; each rank holds its own K-bucket shard and
+merges its own pre-routed n-message stream (weak scaling, no data-path
+collective).  value = all merges of all ranks / max-over-ranks time.
+
+Beside it, the same JSON line carries `owner_routed`: C2's fixed total
+(K buckets, n messages per step) hash-sharded by name over the N GPUs, every
+rank drawing n/N messages over ALL buckets as they arrive from peers, packed
+by owner on the GPU (phip_route_pack, sender-side combine), moved by RCCL
+all-to-alls and merged by their owners (strong scaling).
 
 Prints ONE JSON line (rank 0).  See DESIGN.md §4 for the roofline accounting.
 """
@@ -23,6 +30,8 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -72,12 +81,44 @@ def parse():
                    help="c5: fraction of buckets each replica writes between rounds")
     p.add_argument("--dist-backend", default="nccl",
                    help="nccl (= RCCL on ROCm) for real runs; gloo to rehearse several ranks on one GPU")
+    p.add_argument("--c3-clock", default="below", choices=["below", "ahead"],
+                   help="c3: replica elapsed drawn below the local clock (U[0, now - created): "
+                        "Takes refill, succeed and deny) or ahead of it (round 1's input: every "
+                        "Take clamps last to now, dt = 0)")
+    p.add_argument("--name-len", type=int, default=0,
+                   help="c2: pad every bucket name to this many bytes (e.g. 32: the arena path)")
+    p.add_argument("--no-routed", action="store_true",
+                   help="c2: skip the owner_routed (strong-scaling) object")
     return p.parse_args()
 
 
+def launch_ranks(args):
+    """--gpus N is authoritative.  Without WORLD_SIZE in the environment and
+    N > 1, start the N ranks (torch.distributed.run, one process per GPU)
+    before anything touches a GPU and exit with their status; under a
+    launcher, its WORLD_SIZE must equal N."""
+    ws = os.environ.get("WORLD_SIZE")
+    if ws is None:
+        if args.gpus > 1:
+            s = socket.socket()
+            s.bind(("127.0.0.1", 0))
+            port = s.getsockname()[1]
+            s.close()
+            cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                   f"--nproc-per-node={args.gpus}", "--master-addr", "127.0.0.1",
+                   f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+            sys.exit(subprocess.call(cmd))
+        return
+    if int(ws) != args.gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={ws} but --gpus {args.gpus}")
+
+
 # ------------------------------------------------------------ synthetic ----
-def names_for_ids(torch, ids):
-    """ids (int64 tensor) -> (blob uint8, offs int32[n+1]) with name = b"b%d"."""
+def names_for_ids(torch, ids, pad_to=0):
+    """ids (int64 tensor) -> (blob uint8, offs int32[n+1]) with name = b"b%d"
+    (pad_to > 0: b"b" + "x" * k + "%d", k making the name pad_to bytes)."""
+    if pad_to:
+        return padded_names(torch, ids, pad_to)
     dev = ids.device
     nd = torch.ones_like(ids)
     p = torch.full_like(ids, 10)
@@ -100,6 +141,23 @@ def names_for_ids(torch, ids):
         digit = (ids[m] // pw) % 10
         blob[start[m] + 1 + d] = (48 + digit).to(torch.uint8)
     assert total < 2**32
+    return blob, offs.to(torch.int32)
+
+
+def padded_names(torch, ids, width):
+    """Names of exactly `width` bytes: "b", then "x" padding, then the decimal id."""
+    dev = ids.device
+    n = ids.numel()
+    assert width >= 12
+    offs = torch.arange(n + 1, dtype=torch.int64, device=dev) * width
+    blob = torch.full((n * width + 8,), ord("x"), dtype=torch.uint8, device=dev)
+    blob[offs[:-1]] = ord("b")
+    v = ids.clone()
+    for d in range(11):   # ids < 10^11, right-aligned digits
+        blob[offs[:-1] + width - 1 - d] = (48 + v % 10).to(torch.uint8)
+        v //= 10
+    blob[n * width:] = 0
+    assert n * width < 2**32
     return blob, offs.to(torch.int32)
 
 
@@ -134,14 +192,14 @@ def cpu_baseline(args, K, ids_host, threads):
     L = O.lib()
     repo = O.Repo()
     keys = torch.arange(K, dtype=torch.int64)
-    kb, ko = names_for_ids(torch, keys)
+    kb, ko = names_for_ids(torch, keys, args.name_len)
     z = np.zeros(K, np.uint64)
     L.orc_repo_seed(repo.h, kb.numpy(), ko.numpy().astype(np.uint32), K, z, z,
                     np.zeros(K, np.int64), np.full(K, T0, np.int64))
     del kb, ko, keys
     n = min(args.cpu_sample, ids_host.numel())
     ids = ids_host[:n]
-    blob, offs = names_for_ids(torch, ids)
+    blob, offs = names_for_ids(torch, ids, args.name_len)
     g = torch.Generator().manual_seed(args.seed + 99)
     a, t, e = replica_states(torch, g, n, 0, "cpu")
     blob_np, offs_np = blob.numpy(), offs.numpy().astype(np.uint32)
@@ -150,27 +208,48 @@ def cpu_baseline(args, K, ids_host, threads):
     n1 = min(n, 2_000_000)
     # single goroutine, as the reference's Receive loop runs (repo.go:54)
     repo1 = O.Repo()
-    kb, ko = names_for_ids(torch, torch.arange(K, dtype=torch.int64))
+    kb, ko = names_for_ids(torch, torch.arange(K, dtype=torch.int64), args.name_len)
     L.orc_repo_seed(repo1.h, kb.numpy(), ko.numpy().astype(np.uint32), K, z, z,
                     np.zeros(K, np.int64), np.full(K, T0, np.int64))
     secs1 = L.orc_bench_receive(repo1.h, blob_np, offs_np, n1, a_np, t_np, e_np, T0, 1)
-    return dict(value=n / secs, unit="merges/s", cores=threads, kind="port",
+    return dict(value=n / secs, unit="merges/s", cores=threads, kind="port", **host_cpu(),
                 sample=f"{n} of the step-0 messages (Zipf {args.zipf} over {K} buckets) into a "
                        f"{K}-bucket Go-structured map, {threads} threads",
                 single_thread=dict(value=n1 / secs1, sample=f"{n1} messages, 1 thread (the "
                                    "reference's single Receive goroutine)"))
 
 
-def pmc_traffic(workload):
+def host_cpu():
+    """Provenance of the CPU baseline: the host's logical CPUs and model."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = None
+    return {"host_nproc": os.cpu_count(), "host_affinity_cpus": affinity, "host_cpu_model": model}
+
+
+def pmc_traffic(key, workload):
     """HBM bytes per launch of the dominant kernel from the committed PMC
-    summary (profiles/pmc_summary.json, produced by tools/pmc_summary.py)."""
+    summary (profiles/pmc_summary.json, produced by tools/pmc_summary.py):
+    one entry per workload key (c1..c5), used when it was measured on the
+    same workload description."""
     path = os.path.join(ROOT, "profiles", "pmc_summary.json")
     try:
         with open(path) as f:
             d = json.load(f)
-        if d.get("kernel") == DOMINANT and d.get("workload") == workload:
+        d = d.get(key, d) if "kernel" not in d else d
+        if d.get("workload") == workload:
             return d.get("hbm_bytes_per_step")
-    except (OSError, ValueError):
+    except (OSError, ValueError, AttributeError):
         pass
     return None
 
@@ -196,10 +275,11 @@ def datagrams(torch, blob, offs, a, t, e):
     return out, doffs
 
 
-def run_c3(args, torch, dev, repo, rank, K, base, gen):
+def c3_inputs(args, torch, dev, K, base, gen):
     """n ops, 50% Take(rate=100:1s, count=1) / 50% received
     replica states, interleaved by seq, Zipf over the K buckets; now = t0 +
-    seq*20ns (+1 s per step).  Per-bucket order is the op order."""
+    seq*20ns (+1 s per step).  Per-bucket order is the op order.  One op
+    stream (names, kinds, rates); per step its clock and replica states."""
     n = args.ops
     ids = zipf_ids(torch, gen, n, K, args.zipf, dev)
     blob, offs = names_for_ids(torch, ids + base)
@@ -211,7 +291,23 @@ def run_c3(args, torch, dev, repo, rank, K, base, gen):
     steps = []
     for j in range(args.warmup + args.steps):
         a, t, e = replica_states(torch, gen, n, j, dev)
-        steps.append((T0 + j * 10**9 + seq_now, a, t, e))
+        now = T0 + j * 10**9 + seq_now
+        if args.c3_clock == "below":
+            # replica elapsed below the local clock: created + elapsed < now,
+            # so Takes refill (dt > 0, bucket.go:198-212), succeed and deny
+            e = (torch.rand(n, dtype=torch.float64, device=dev, generator=gen) *
+                 (now - T0).to(torch.float64)).to(torch.int64)
+        steps.append((now, a, t, e))
+    return dict(n=n, ids=ids, blob=blob, offs=offs, kind=kind, freq=freq, per=per, cnt=cnt,
+                steps=steps)
+
+
+def run_c3(args, torch, dev, repo, rank, K, base, gen):
+    """The C3 bench step over c3_inputs(): phip_apply_mixed with statuses and
+    `remaining` written, every array resident in HBM."""
+    c = c3_inputs(args, torch, dev, K, base, gen)
+    n, ids, blob, offs, steps = c["n"], c["ids"], c["blob"], c["offs"], c["steps"]
+    kind, freq, per, cnt = c["kind"], c["freq"], c["per"], c["cnt"]
     status = torch.empty(n, dtype=torch.uint8, device=dev)
     rem = torch.empty(n, dtype=torch.int64, device=dev)
     torch.cuda.synchronize()
@@ -244,7 +340,7 @@ def run_c3(args, torch, dev, repo, rank, K, base, gen):
         secs = L.orc_bench_mixed(orepo.h, cols[0], sb.numpy(), so.numpy().astype(np.uint32), m,
                                  cols[1], cols[2], cols[3], cols[4].view(np.uint64),
                                  cols[5].view(np.uint64), cols[6].view(np.uint64), cols[7], st, rm)
-        return dict(value=m / secs, unit="ops/s", cores=1, kind="port",
+        return dict(value=m / secs, unit="ops/s", cores=1, kind="port", **host_cpu(),
                     sample=f"first {m} ops of the timed stream (Zipf {args.zipf} over {K} "
                            f"buckets) through the Go-structured restatement, 1 thread")
     return n, step, cpu
@@ -275,14 +371,93 @@ def run_c4(args, torch, dev, repo, rank, world, K, gen):
     batches = [replica_states(torch, gen, n, j, dev) for j in range(args.warmup + args.steps)]
     torch.cuda.synchronize()
 
+    merged = []
+
     def step(j):
         a, t, e = batches[j]
         rb, ro, ra, rt, re = shard.route_messages_native(blob, offs, a, t, e, repo,
                                                          combine=not args.no_combine)
         m = ro.numel() - 1
+        if j >= args.warmup:
+            merged.append(m)
         if m:
             repo.receive_soa(rb, ra, rt, re, T0 + j, name_offs=ro, n=m, device=True)
-    return n, step, owned
+    return n, step, owned, merged
+
+
+def run_routed(args, torch, dist, dev, local, rank, world):
+    """The owner_routed object (SURVEY §8d/§8e strong scaling): C2's fixed
+    total of K buckets and n messages per step, the buckets hash-sharded by
+    name over the `world` GPUs.  Each rank draws n/world messages Zipf over
+    ALL K buckets (as they arrive from peers), and a step is the sharded
+    merge: phip_route_pack (owner partition + sender-side combine), one RCCL
+    all-to-all per column, phip_receive_soa of the owned messages.  Timed
+    with barriers, max over ranks; value = n * steps / time."""
+    import patrol_amd
+    from patrol_amd import shard
+    K, n = args.keys, args.messages
+    m = n // world
+    gen = torch.Generator(device=dev).manual_seed(args.seed + 31 + 7919 * rank)
+    # shard table sized like C2's at 1/world of the buckets (load ~0.3)
+    L = max(16, args.log2_slots - (world - 1).bit_length())
+    repo = patrol_amd.GPURepo(device=local, log2_slots=L, arena_bytes=1 << 20)
+    repo.use_torch_stream()
+    keys = torch.arange(K, dtype=torch.int64, device=dev)
+    kb, ko = names_for_ids(torch, keys, args.name_len)
+    hk = shard.hash_names(kb, ko, repo)
+    mine = torch.nonzero(shard.owner_of(hk, world) == rank).flatten()
+    sb, _, so = shard._gather_names(kb, ko, mine)
+    st = torch.zeros((mine.numel(), 4), dtype=torch.int64, device=dev)
+    st[:, 3] = T0
+    torch.cuda.synchronize()
+    repo.seed_device(sb, so.to(torch.int32), st, mine.numel())
+    owned = mine.numel()
+    del keys, kb, ko, hk, sb, so, st, mine
+    ids = zipf_ids(torch, gen, m, K, args.zipf, dev)
+    blob, offs = names_for_ids(torch, ids, args.name_len)
+    del ids
+    batches = [replica_states(torch, gen, m, j, dev) for j in range(args.warmup + args.steps)]
+    torch.cuda.synchronize()
+    merged = []
+
+    def step(j):
+        a, t, e = batches[j]
+        rb, ro, ra, rt, re = shard.route_messages_native(blob, offs, a, t, e, repo, combine=True)
+        k = ro.numel() - 1
+        if j >= args.warmup:
+            merged.append(k)
+        if k:
+            repo.receive_soa(rb, ra, rt, re, T0 + j, name_offs=ro, n=k, device=True)
+
+    for j in range(args.warmup):
+        step(j)
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for j in range(args.warmup, args.warmup + args.steps):
+        step(j)
+    torch.cuda.synchronize()
+    dist.barrier()
+    el = time.perf_counter() - t0
+    tt = torch.tensor([el, float(np.mean(merged)), float(owned)], dtype=torch.float64,
+                      device=dev if args.dist_backend == "nccl" else "cpu")
+    mx = tt.clone()
+    dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+    sm = tt.clone()
+    dist.all_reduce(sm, op=dist.ReduceOp.SUM)
+    repo.close()
+    del batches, blob, offs
+    el = float(mx[0])
+    return {
+        "metric": "bucket-state merges/sec, owner-routed (C2's fixed total sharded by name)",
+        "value": n * args.steps / el, "unit": "merges/s", "scaling": "strong",
+        "n_gpus": world, "ms_per_step": el / args.steps * 1e3,
+        "messages_per_step_total": n, "messages_per_step_per_gpu": m, "buckets_total": K,
+        "merged_per_step_total": float(sm[1]), "merged_per_step_max_gpu": float(mx[1]),
+        "buckets_max_gpu": int(mx[2]), "slots_per_gpu": 1 << L, "sender_combine": True,
+        "step": "phip_route_pack (owner partition + sender-side combine) -> RCCL all-to-all per "
+                "column -> phip_receive_soa on the owner",
+    }
 
 
 def run_c5(args, torch, dev, repo, rank, world, gen):
@@ -336,6 +511,13 @@ def run_c5(args, torch, dev, repo, rank, world, gen):
 
 def main():
     args = parse()
+    launch_ranks(args)
+    # The one JSON line goes to the real stdout; everything the libraries
+    # print to fd 1 (RCCL's version banner at its first communicator) goes
+    # to stderr instead.
+    json_out = os.fdopen(os.dup(1), "w")
+    sys.stdout.flush()
+    os.dup2(2, 1)
     c1 = args.workload == "c1"
     if c1:
         # BASELINE configs[0]: 1M replica states into a 100k-bucket
@@ -350,8 +532,11 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1 or args.workload in ("c4", "c5"):
-        # c4/c5 exercise the collectives (all-to-all, all-reduce) even on one GPU
+    routed = (args.workload == "c2" and not (c1 or args.no_routed or args.wire or args.insert or
+                                             args.ring))
+    if world > 1 or args.workload in ("c4", "c5") or routed:
+        # c4/c5 and the owner-routed line exercise the collectives
+        # (all-to-all, all-reduce) even on one GPU
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", str(29500 + (os.getpid() % 1000)))
         os.environ.setdefault("RANK", "0")
@@ -372,7 +557,7 @@ def main():
     repo = patrol_amd.GPURepo(device=local, log2_slots=args.log2_slots, arena_bytes=1 << 20)
     repo.use_torch_stream()
     keys = torch.arange(base, base + K, dtype=torch.int64, device=dev)
-    kb, ko = names_for_ids(torch, keys)
+    kb, ko = names_for_ids(torch, keys, args.name_len if args.workload == "c2" else 0)
     st = torch.zeros((K, 4), dtype=torch.int64, device=dev)
     # added = taken = +0.0 bits, elapsed 0: the zero state GetBucket creates (repo.go:208)
     st[:, 3] = T0
@@ -388,15 +573,17 @@ def main():
         n, step, c3_cpu = run_c3(args, torch, dev, repo, rank, K, base, gen)
         ids = None
     elif args.workload == "c4":
-        n, step, owned = run_c4(args, torch, dev, repo, rank, world, K, gen)
+        n, step, owned, c4_merged = run_c4(args, torch, dev, repo, rank, world, K, gen)
         ids = None
     elif args.workload == "c5":
         n, step, c5_check = run_c5(args, torch, dev, repo, rank, world, gen)
         ids = None
     else:
         ids = zipf_ids(torch, gen, n, K, args.zipf, dev)
-        blob, offs = names_for_ids(torch, ids + base)
+        blob, offs = names_for_ids(torch, ids + base, args.name_len)
         batches = [replica_states(torch, gen, n, j, dev) for j in range(args.warmup + args.steps)]
+        # the per-message status column a Receive caller reads (merge vs incast)
+        c2_status = torch.empty(n, dtype=torch.uint8, device=dev)
         if args.insert:
             # SURVEY C2's insert-on-miss variant: every step names a fresh
             # key range (same Zipf shape), so each step creates the buckets it
@@ -460,7 +647,8 @@ def main():
         else:
             def step(j):
                 a, t, e = batches[j]
-                repo.receive_soa(blob, a, t, e, T0 + j, name_offs=offs, n=n, device=True)
+                repo.receive_soa(blob, a, t, e, T0 + j, name_offs=offs, n=n, status=c2_status,
+                                 device=True)
 
     for j in range(args.warmup):
         step(j)
@@ -522,13 +710,19 @@ def main():
                     f"by name across {world} GPU(s), all-to-all routing + merge, Zipf({args.zipf})")
         extra["buckets_owned_rank0"] = owned
         extra["sender_combine"] = not args.no_combine
+        # the fast kernel merges what this rank received after routing and
+        # the sender-side combine, not the n messages it sent
+        extra["messages_sent_per_step_rank0"] = n
+        extra["messages_merged_per_step_rank0"] = float(np.mean(c4_merged))
     elif args.workload == "c3":
         # Take 89 B (op 24 + state read 32 + write 24 + result 9), Merge 88 B.
         bpo = 88.5
         dom_name, dom_ms = "whole step", el / args.steps * 1e3
         unit, metric = "ops/s", METRIC + " [C3: mixed Take+Merge ops/sec]"
         workload = (f"C3 mixed: {n} ops (50% Take 100:1s n=1, 50% Merge), Zipf({args.zipf}) over "
-                    f"{K} buckets (2^{args.log2_slots} slots), per-bucket order kept")
+                    f"{K} buckets (2^{args.log2_slots} slots), per-bucket order kept, replica "
+                    f"elapsed {args.c3_clock} the local clock")
+        extra["c3_clock"] = args.c3_clock
     else:
         bpo = BYTES_PER_MERGE
         dom_name, dom_ms = DOMINANT, float(np.mean(kern.get(DOMINANT, [float("nan")])))
@@ -547,10 +741,11 @@ def main():
                         f"j, statuses back to host, Zipf({args.zipf}); slots cycle 3 batches")
             extra["h2d_bytes_per_step"] = ring_bytes
             extra["h2d_GBps"] = ring_bytes * args.steps / el / 1e9
-    # c4: the merged count per rank varies (owners of hot buckets receive
-    # more); the roofline uses this rank's kernel and its message share.
-    achieved = bpo * n / (dom_ms / 1e3) / 1e9
-    traffic = pmc_traffic(workload)
+    # c4: the dominant kernel merges this rank's received (routed, combined)
+    # messages, so its algorithmic bytes count those
+    n_roof = float(np.mean(c4_merged)) if args.workload == "c4" else n
+    achieved = bpo * n_roof / (dom_ms / 1e3) / 1e9
+    traffic = pmc_traffic(args.workload if not c1 else "c1", workload)
     out = {
         "metric": metric,
         "value": total / el,
@@ -565,12 +760,15 @@ def main():
         "dtype": "f64",
         "data": "synthetic (seeded Zipf keys, SURVEY §8d replica states; batches resident in HBM)",
         "config": {"workload": workload, "keys_per_gpu": K, "messages_per_step_per_gpu": n,
-                   "slots_per_gpu": 1 << args.log2_slots, "parallelism": f"shard{world}"},
+                   "slots_per_gpu": 1 << args.log2_slots, "parallelism": f"shard{world}",
+                   "name_bytes": args.name_len or "2-8 (b<id>)",
+                   "world_size": world,
+                   "dist_backend": args.dist_backend if dist.is_initialized() else None},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": dom_name, "kernel_ms_per_step": dom_ms,
                      "launches_per_step": launches.get(dom_name, args.steps) / args.steps,
-                     "algorithmic_bytes_per_step": bpo * n},
+                     "algorithmic_bytes_per_step": bpo * n_roof},
         "kernels_ms": kms,
     }
     out["config"].update(extra)
@@ -587,11 +785,19 @@ def main():
             out["cpu_baseline"] = {"error": repr(ex)}
     elif rank == 0:
         out["cpu_baseline"] = None
-    if rank == 0:
-        print(json.dumps(out), flush=True)
     if args.ring and args.workload == "c2":
         ring.close()
     repo.close()
+    if routed:
+        # the C2 batches are freed first: the owner-routed line has its own
+        del step
+        if args.workload == "c2":
+            del batches, blob, offs, ids
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+        out["owner_routed"] = run_routed(args, torch, dist, dev, local, rank, world)
+    if rank == 0:
+        print(json.dumps(out), file=json_out, flush=True)
     if dist.is_initialized():
         dist.destroy_process_group()
 

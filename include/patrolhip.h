@@ -52,7 +52,7 @@
 extern "C" {
 #endif
 
-#define PHIP_ABI_VERSION 1
+#define PHIP_ABI_VERSION 2
 
 /* bucket.go:36-44 */
 #define PHIP_BUCKET_FIXED_SIZE 25
@@ -98,14 +98,33 @@ enum {
 #define PHIP_DEVICE_PTRS 0x1u   /* all pointers of the call are device memory */
 #define PHIP_ROUTE_COMBINE 0x2u /* phip_route_pack: combine hot names at the sender */
 
+/* phip_config.flags */
+#define PHIP_CFG_NO_GROW 0x1u   /* refuse (PHIP_ERR_FULL / PHIP_ERR_ARENA) instead of growing */
+
 typedef struct phip_config {
   int32_t device;        /* HIP device ordinal                                          */
-  uint32_t log2_slots;   /* table capacity = 2^log2_slots slots (10..31)                */
-  uint64_t arena_bytes;  /* device arena for names longer than 23 bytes                 */
-  uint32_t max_load_pct; /* refuse inserts beyond this load factor (default 90)         */
+  uint32_t log2_slots;   /* initial table capacity = 2^log2_slots slots (4..31)         */
+  uint64_t arena_bytes;  /* initial device arena for names longer than 22 bytes         */
+  uint32_t max_load_pct; /* load factor that triggers growth (default 90, at most 95)  */
   uint32_t debug_tag_bits; /* 0 in production; 1..63 truncates the name hash so tests can
                               force tag collisions (names are always compared)          */
+  uint32_t flags;        /* PHIP_CFG_*                                                   */
+  uint32_t reserved;
 } phip_config;
+/*
+ * Capacity.  Go's map never refuses a bucket (repo.go:204-207,225-227), so by
+ * default the table and the long-name arena grow: before a batch creates
+ * buckets, the engine reserves room for all of them (an upper bound: the
+ * batch's distinct missing names) and rehashes into a table of 2x the slots
+ * (k_rehash) or a larger arena whenever the reservation would pass
+ * max_load_pct or the arena's end.  PHIP_ERR_FULL / PHIP_ERR_ARENA are then
+ * only returned when growth is impossible (2^31 slots, device memory) or
+ * disabled (PHIP_CFG_NO_GROW).  Such a refusal comes before any bucket of
+ * the insert step is claimed: no bucket of the refused names is created, and
+ * the table holds exactly what it held plus the merges the call's per-op
+ * statuses report as applied (merges into existing buckets commute, so
+ * re-submitting the other ops later is exact).
+ */
 
 /* Bucket state as Patrol holds it (bucket.go:20-32, name excluded). */
 typedef struct phip_state {
@@ -240,6 +259,40 @@ int phip_api_take(phip_handle* h, const uint8_t* name, uint32_t len, const char*
                   uint32_t rate_len, const char* count, uint32_t count_len, int64_t now,
                   char* body, uint32_t* body_len);
 
+/* ---- request-coalescing Take batcher ----
+ * Replaces the per-request GetBucket -> Take -> UpsertBucket of the HTTP
+ * handler (api.go:67-74; Bucket.Take bucket.go:186-225) for callers that
+ * serve one request per thread (a Go goroutine per HTTP request calling
+ * through cgo).  Each call enqueues one Take and blocks until its batch ran:
+ * a dispatcher thread closes a batch window_us after the batch's first
+ * request arrived, or at max_batch requests, and runs it with
+ * phip_apply_mixed (arrival order = op order, so each bucket sees its Takes
+ * in the order they were enqueued).  Requests arriving while a batch runs
+ * form the next one.  Thread-safe; the handle must not be closed before the
+ * batcher. */
+typedef struct phip_batcher phip_batcher;
+typedef struct phip_batcher_config {
+  uint32_t window_us;   /* batch window after its first request (0: dispatch at once)  */
+  uint32_t max_batch;   /* requests per batch at most (0: 65536)                       */
+} phip_batcher_config;
+int phip_batcher_open(phip_handle* h, const phip_batcher_config* cfg, phip_batcher** out);
+/* Runs the requests already queued, then stops the dispatcher. */
+void phip_batcher_close(phip_batcher* b);
+/* GetBucket + Take(now, Rate{freq, per}, count): *remaining and *ok as Go's
+ * Take returns them (ok = 1 means HTTP 200, 0 means 429). */
+int phip_batcher_take(phip_batcher* b, const uint8_t* name, uint32_t len, int64_t now,
+                      int64_t freq, int64_t per, uint64_t count, uint64_t* remaining,
+                      uint8_t* ok);
+/* API.takeBucket (api.go:51-86) through the batcher: phip_api_take's
+ * contract (HTTP status 200/429/400, body <= 64 bytes). */
+int phip_batcher_api_take(phip_batcher* b, const uint8_t* name, uint32_t len, const char* rate,
+                          uint32_t rate_len, const char* count, uint32_t count_len, int64_t now,
+                          char* body, uint32_t* body_len);
+/* out[0] batches run, out[1] requests served, out[2] largest batch,
+ * out[3] ns spent in phip_apply_mixed, out[4] batches that failed.
+ * Returns the number written (<= 5). */
+int phip_batcher_stats(phip_batcher* b, uint64_t* out, int max);
+
 /* ---- batched UDP ingest (command.go's replicator) ----
  * The reference's Receive goroutine reads ONE datagram per iteration into a
  * 256-byte buffer under a 3 s deadline (repo.go:54-73,108-120) and answers
@@ -361,7 +414,8 @@ int phip_last_timings(phip_handle* h, const char** names, float* ms, int max);
 void phip_set_timing(phip_handle* h, int on);
 /* Counters of the last fast-path Receive batch: out[0] hot-directory
  * entries, out[1] messages folded through the directory, out[2] messages
- * that missed the table (inserted).  Returns the number written (<= 3). */
+ * that missed the table (inserted); out[3] table growths (rehashes) since
+ * phip_open.  Returns the number written (<= 4). */
 int phip_last_stats(phip_handle* h, uint64_t* out, int max);
 
 #ifdef __cplusplus

@@ -87,6 +87,9 @@ def lib():
     L.orc_bench_mixed.argtypes = [vp, u8p, u8p, u32p, C.c_uint32, i64p, i64p, i64p, u64p, u64p,
                                   u64p, i64p, u8p, u64p]
     L.orc_bench_mixed.restype = C.c_double
+    L.orc_check_dump.argtypes = [vp, u8p, u64p, C.c_uint64, u64p, u64p, i64p, i64p,
+                                 C.POINTER(C.c_uint64)]
+    L.orc_check_dump.restype = C.c_uint64
     L.orc_fnv1a64.argtypes = [C.c_char_p, C.c_uint32]
     L.orc_fnv1a64.restype = C.c_uint64
     _lib = L
@@ -207,6 +210,18 @@ class Repo:
         nb = names.tobytes()
         return {nb[int(offs[i]):int(offs[i + 1])]: (int(a[i]), int(t[i]), int(e[i]), int(c[i]))
                 for i in range(n)}
+
+    def check_dump(self, names, offs, added, taken, elapsed, created):
+        """Differences between a table dump given as arrays (GPURepo.dump_arrays)
+        and this repo -> (count, index of the first differing entry)."""
+        fb = C.c_uint64()
+        bad = self.L.orc_check_dump(self.h, np.ascontiguousarray(names, np.uint8),
+                                    np.ascontiguousarray(offs, np.uint64), len(offs) - 1,
+                                    np.ascontiguousarray(added, np.uint64),
+                                    np.ascontiguousarray(taken, np.uint64),
+                                    np.ascontiguousarray(elapsed, np.int64),
+                                    np.ascontiguousarray(created, np.int64), C.byref(fb))
+        return int(bad), int(fb.value)
 
     def api_take(self, name: bytes, rate: bytes, count: bytes, now: int):
         body = C.create_string_buffer(64)

@@ -572,6 +572,37 @@ int64_t orc_dump(void* r, uint8_t* names, uint64_t cap, uint64_t* offs, uint64_t
   return (int64_t)v.size();
 }
 
+// Compare a table dump (any order; names blob + u64 offsets[n+1], float64
+// bits, elapsed, created) with this repo, for full-size parity checks where
+// a per-bucket Python comparison would be too slow.  Returns the number of
+// differences: an entry whose name is absent here or whose state differs,
+// a name listed twice, and (once) a bucket count that differs.  *first_bad
+// receives the index of the first differing entry (n if none).
+uint64_t orc_check_dump(void* r, const uint8_t* names, const uint64_t* offs, uint64_t n,
+                        const uint64_t* added, const uint64_t* taken, const int64_t* elapsed,
+                        const int64_t* created, uint64_t* first_bad) {
+  LocalRepo* repo = (LocalRepo*)r;
+  std::unordered_map<const Bucket*, uint64_t> seen;
+  seen.reserve(n);
+  uint64_t bad = 0;
+  *first_bad = n;
+  for (uint64_t i = 0; i < n; ++i) {
+    auto it = repo->buckets.find(std::string_view((const char*)names + offs[i], offs[i + 1] - offs[i]));
+    bool ok = it != repo->buckets.end();
+    if (ok) {
+      const Bucket* b = it->second;
+      ok = f2b(b->added) == added[i] && f2b(b->taken) == taken[i] && b->elapsed == elapsed[i] &&
+           b->created == created[i] && seen.emplace(b, i).second;
+    }
+    if (!ok) {
+      if (*first_bad == n) *first_bad = i;
+      ++bad;
+    }
+  }
+  if (n != repo->buckets.size()) ++bad;
+  return bad;
+}
+
 // ------------------------------------------------------- scalar helpers ----
 int orc_parse_rate(const char* s, uint32_t len, int64_t* freq, int64_t* per) {
   Rate r;

@@ -23,6 +23,8 @@ EXPORTS = [
     "phip_export_datagrams", "phip_snapshot_bytes", "phip_snapshot", "phip_restore",
     "phip_ring_open", "phip_ring_close", "phip_ring_acquire", "phip_ring_submit",
     "phip_ring_receive", "phip_udp_recv_batch", "phip_incast_replies", "phip_udp_send_batch",
+    "phip_batcher_open", "phip_batcher_close", "phip_batcher_take", "phip_batcher_api_take",
+    "phip_batcher_stats",
 ]
 
 PHIP_OK = 0
@@ -33,12 +35,14 @@ ST_MERGED, ST_INCAST_REPLY, ST_INCAST_NOREPLY, ST_SHORT, ST_NOT_PROCESSED = 1, 2
 ST_TAKE_OK, ST_TAKE_DENIED, ST_UPSERT_INSERTED, ST_CREATED = 6, 7, 8, 0x80
 OP_TAKE, OP_RECEIVE, OP_UPSERT = 0, 1, 2
 DEVICE_PTRS = 0x1
+CFG_NO_GROW = 0x1
 ROUTE_COMBINE = 0x2
 
 
 class phip_config(C.Structure):
     _fields_ = [("device", C.c_int32), ("log2_slots", C.c_uint32), ("arena_bytes", C.c_uint64),
-                ("max_load_pct", C.c_uint32), ("debug_tag_bits", C.c_uint32)]
+                ("max_load_pct", C.c_uint32), ("debug_tag_bits", C.c_uint32),
+                ("flags", C.c_uint32), ("reserved", C.c_uint32)]
 
 
 class phip_state(C.Structure):
@@ -57,6 +61,10 @@ class phip_ops(C.Structure):
                 ("names", C.c_void_p), ("name_offs", C.c_void_p), ("now", C.c_void_p),
                 ("freq", C.c_void_p), ("per", C.c_void_p), ("count", C.c_void_p),
                 ("added", C.c_void_p), ("taken", C.c_void_p), ("elapsed", C.c_void_p)]
+
+
+class phip_batcher_config(C.Structure):
+    _fields_ = [("window_us", C.c_uint32), ("max_batch", C.c_uint32)]
 
 
 class phip_results(C.Structure):
@@ -133,5 +141,13 @@ def load(path: str = LIB_PATH):
     L.phip_udp_recv_batch.argtypes = [C.c_int, vp, u64, vp, u32, vp, C.c_int, C.POINTER(u32)]
     L.phip_incast_replies.argtypes = [vp, vp, u32, vp, vp, vp, vp, u64, vp, vp, C.POINTER(u32)]
     L.phip_udp_send_batch.argtypes = [C.c_int, vp, vp, u32, vp, u32, C.POINTER(u32)]
+    L.phip_batcher_open.argtypes = [vp, C.POINTER(phip_batcher_config), C.POINTER(vp)]
+    L.phip_batcher_close.argtypes = [vp]
+    L.phip_batcher_close.restype = None
+    L.phip_batcher_take.argtypes = [vp, C.c_char_p, u32, i64, i64, i64, u64, C.POINTER(u64),
+                                    C.POINTER(C.c_uint8)]
+    L.phip_batcher_api_take.argtypes = [vp, C.c_char_p, u32, C.c_char_p, u32, C.c_char_p, u32,
+                                        i64, C.c_char_p, C.POINTER(u32)]
+    L.phip_batcher_stats.argtypes = [vp, C.POINTER(u64), C.c_int]
     _lib = L
     return L

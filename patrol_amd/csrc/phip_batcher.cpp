@@ -1,0 +1,230 @@
+// Request-coalescing Take batcher: the drop-in form of
+// Patrol's POST /take handler over the batched engine.
+//
+// The reference answers every HTTP request on its own goroutine with
+// GetBucket -> Bucket.Take -> UpsertBucket under the bucket's mutex
+// (api.go:67-74, bucket.go:186-225).  A device-resident table wants batches,
+// so concurrent requests are coalesced here: each caller thread enqueues its
+// Take (arrival order is the batch order, which per-bucket order follows, as
+// the bucket mutex serialises the reference's goroutines in lock order) and
+// blocks; one dispatcher thread closes a batch `window_us` after its first
+// request arrived (or at max_batch requests), runs it through
+// phip_apply_mixed (GetBucket + Take per op, exact Go semantics in index
+// order) and wakes the callers with their (remaining, ok).  Requests that
+// arrive while a batch is on the GPU form the next batch, so under load the
+// batches grow by themselves.
+//
+// Host code only: every device call goes through the public C ABI.
+#include <algorithm>
+#include <chrono>
+#include <condition_variable>
+#include <cstdint>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "patrolhip.h"
+#include "phip_host.hpp"
+
+namespace {
+
+using Clock = std::chrono::steady_clock;
+
+struct Req {
+  const uint8_t* name;
+  uint32_t len;
+  int64_t now, freq, per;
+  uint64_t count;
+  uint64_t remaining = 0;
+  uint8_t status = 0;
+  int rc = 0;
+  bool done = false;
+};
+
+}  // namespace
+
+struct phip_batcher {
+  phip_handle* h = nullptr;
+  uint32_t window_us = 20;
+  uint32_t max_batch = 1u << 16;
+  std::mutex mu;
+  std::condition_variable cv_submit;   // the dispatcher waits for requests
+  std::condition_variable cv_done;     // callers wait for their batch
+  std::vector<Req*> pending;
+  Clock::time_point first_arrival;
+  bool stop = false;
+  std::thread th;
+  // stats
+  uint64_t batches = 0, requests = 0, max_seen = 0, gpu_ns = 0, errors = 0;
+  // dispatcher scratch (host arrays of one batch)
+  std::vector<uint8_t> kind, names, status;
+  std::vector<uint32_t> offs;
+  std::vector<int64_t> now, freq, per;
+  std::vector<uint64_t> count, remaining;
+
+  void run();
+  void dispatch(std::vector<Req*>& batch);
+};
+
+void phip_batcher::dispatch(std::vector<Req*>& batch) {
+  const uint32_t n = (uint32_t)batch.size();
+  kind.assign(n, PHIP_OP_TAKE);
+  offs.resize(n + 1);
+  now.resize(n); freq.resize(n); per.resize(n); count.resize(n);
+  status.assign(n, 0); remaining.assign(n, 0);
+  size_t nb = 0;
+  for (uint32_t i = 0; i < n; ++i) nb += batch[i]->len;
+  names.resize(nb + 8);
+  size_t o = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    const Req* r = batch[i];
+    offs[i] = (uint32_t)o;
+    if (r->len) std::memcpy(names.data() + o, r->name, r->len);
+    o += r->len;
+    now[i] = r->now; freq[i] = r->freq; per[i] = r->per; count[i] = r->count;
+  }
+  offs[n] = (uint32_t)o;
+  phip_ops ops{};
+  ops.n = n;
+  ops.kind = kind.data();
+  ops.names = names.data();
+  ops.name_offs = offs.data();
+  ops.now = now.data();
+  ops.freq = freq.data();
+  ops.per = per.data();
+  ops.count = count.data();
+  phip_results res{};
+  res.status = status.data();
+  res.remaining = remaining.data();
+  const auto t0 = Clock::now();
+  const int rc = phip_apply_mixed(h, &ops, &res, 0);
+  gpu_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now() - t0).count();
+  for (uint32_t i = 0; i < n; ++i) {
+    batch[i]->rc = rc;
+    batch[i]->status = status[i];
+    batch[i]->remaining = remaining[i];
+  }
+  if (rc) ++errors;
+}
+
+void phip_batcher::run() {
+  std::vector<Req*> batch;
+  std::unique_lock<std::mutex> l(mu);
+  for (;;) {
+    cv_submit.wait(l, [&] { return stop || !pending.empty(); });
+    if (pending.empty()) break;   // stop, nothing left
+    const auto deadline = first_arrival + std::chrono::microseconds(window_us);
+    while (!stop && pending.size() < max_batch && Clock::now() < deadline)
+      cv_submit.wait_until(l, deadline);
+    const size_t take = std::min<size_t>(pending.size(), max_batch);
+    batch.assign(pending.begin(), pending.begin() + take);
+    pending.erase(pending.begin(), pending.begin() + take);
+    if (!pending.empty()) first_arrival = Clock::now();
+    l.unlock();
+    dispatch(batch);
+    l.lock();
+    for (Req* r : batch) r->done = true;
+    ++batches;
+    requests += batch.size();
+    max_seen = std::max<uint64_t>(max_seen, batch.size());
+    cv_done.notify_all();
+  }
+}
+
+namespace {
+
+int submit_and_wait(phip_batcher* b, Req* r) {
+  std::unique_lock<std::mutex> l(b->mu);
+  if (b->stop) return PHIP_ERR_INVALID;
+  if (b->pending.empty()) b->first_arrival = Clock::now();
+  b->pending.push_back(r);
+  if (b->pending.size() == 1 || b->pending.size() >= b->max_batch) b->cv_submit.notify_one();
+  b->cv_done.wait(l, [&] { return r->done; });
+  return r->rc;
+}
+
+}  // namespace
+
+extern "C" {
+
+int phip_batcher_open(phip_handle* h, const phip_batcher_config* cfg, phip_batcher** out) {
+  if (!h || !out) return PHIP_ERR_INVALID;
+  *out = nullptr;
+  phip_batcher* b = new phip_batcher;
+  b->h = h;
+  if (cfg) {
+    b->window_us = cfg->window_us;
+    if (cfg->max_batch) b->max_batch = cfg->max_batch;
+  }
+  try {
+    b->th = std::thread([b] { b->run(); });
+  } catch (...) {
+    delete b;
+    return PHIP_ERR_INVALID;
+  }
+  *out = b;
+  return PHIP_OK;
+}
+
+void phip_batcher_close(phip_batcher* b) {
+  if (!b) return;
+  {
+    std::lock_guard<std::mutex> l(b->mu);
+    b->stop = true;
+  }
+  b->cv_submit.notify_all();
+  if (b->th.joinable()) b->th.join();
+  delete b;
+}
+
+int phip_batcher_take(phip_batcher* b, const uint8_t* name, uint32_t len, int64_t now,
+                      int64_t freq, int64_t per, uint64_t count, uint64_t* remaining,
+                      uint8_t* ok) {
+  if (!b || (!name && len)) return PHIP_ERR_INVALID;
+  if (len > PHIP_MAX_NAME_LEN) return PHIP_ERR_NAME_TOO_LARGE;
+  Req r;
+  r.name = name;
+  r.len = len;
+  r.now = now;
+  r.freq = freq;
+  r.per = per;
+  r.count = count;
+  const int rc = submit_and_wait(b, &r);
+  if (rc) return rc;
+  if (remaining) *remaining = r.remaining;
+  if (ok) *ok = (r.status & 0x7F) == PHIP_ST_TAKE_OK;
+  return PHIP_OK;
+}
+
+int phip_batcher_api_take(phip_batcher* b, const uint8_t* name, uint32_t len, const char* rate,
+                          uint32_t rate_len, const char* count, uint32_t count_len, int64_t now,
+                          char* body, uint32_t* body_len) {
+  if (!b || !body || !body_len) return PHIP_ERR_INVALID;
+  int64_t freq, per;
+  uint64_t n;
+  const int pre = phip_host::api_prepare(name, len, rate, rate_len, count, count_len, &freq,
+                                         &per, &n, body, body_len);
+  if (pre) return pre;                                    // 400: name too large
+  uint64_t rem = 0;
+  uint8_t ok = 0;
+  const int rc = phip_batcher_take(b, len ? name : (const uint8_t*)"", len, now, freq, per, n,
+                                   &rem, &ok);
+  if (rc < 0) return rc;
+  const std::string s = std::to_string(rem);              // api.go:84-85
+  std::memcpy(body, s.data(), s.size());
+  *body_len = (uint32_t)s.size();
+  return ok ? 200 : 429;
+}
+
+int phip_batcher_stats(phip_batcher* b, uint64_t* out, int max) {
+  if (!b || !out) return 0;
+  std::lock_guard<std::mutex> l(b->mu);
+  const uint64_t v[5] = {b->batches, b->requests, b->max_seen, b->gpu_ns, b->errors};
+  int k = 0;
+  for (; k < max && k < 5; ++k) out[k] = v[k];
+  return k;
+}
+
+}  // extern "C"

@@ -83,6 +83,10 @@ struct phip_handle {
   u32 L = 0;
   u64 cap = 0;
   u64 max_load = 0;
+  u32 load_pct = 90;
+  bool grow = true;          // !PHIP_CFG_NO_GROW
+  u64 grows = 0;             // table rehashes so far
+  u64 long_need = 0;         // arena bytes the last reserve() counted
   Rec* recs = nullptr;
   u32* aux = nullptr;
   u8* arena = nullptr;
@@ -179,8 +183,14 @@ struct Launch {
   }
 };
 
+// Device counters: ctr[0..15] u32 per batch (k_batch_reset), ctr[16..17] one
+// u64 scratch sum (k_list_long_bytes).
+constexpr u32 kCtrWords = 32;
+constexpr u32 kCtrLongBytes = 16;
+
 int read_ctr(phip_handle* h) {
-  HIPCHK(h, hipMemcpyAsync(h->ctr_host, h->ctr, 16 * sizeof(u32), hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(h, hipMemcpyAsync(h->ctr_host, h->ctr, kCtrWords * sizeof(u32), hipMemcpyDeviceToHost,
+                           h->stream));
   HIPCHK(h, hipStreamSynchronize(h->stream));
   return PHIP_OK;
 }
@@ -240,14 +250,117 @@ int copy_back(phip_handle* h, T* user, const T* dev_buf, size_t count, bool dev)
 }
 
 // ----------------------------------------------------------- inserts -----
-// Insert every name of `list` (all known to be absent) into the table.
-// Claimed slots are accumulated in B_CSLOT/B_CMSG; *n_claimed returns their
-// count (callers clear the NEW flag once done).
+inline u64 load_limit(u64 cap, u32 pct) { return cap * pct / 100; }
+
+// Rehash the table into 2^newL slots (k_rehash).  Both tables are resident
+// while records move; the old one is freed after.
+int grow_table(phip_handle* h, u32 newL) {
+  const u64 ncap = 1ull << newL;
+  Rec* nrecs = nullptr;
+  u32* naux = nullptr;
+  if (hipMalloc(&nrecs, ncap * sizeof(Rec)) != hipSuccess) {
+    (void)hipGetLastError();
+    return set_err(h, PHIP_ERR_FULL, "table growth to 2^%u slots: device memory", newL);
+  }
+  if (hipMalloc(&naux, ncap * sizeof(u32)) != hipSuccess) {
+    (void)hipGetLastError();
+    (void)hipFree(nrecs);
+    return set_err(h, PHIP_ERR_FULL, "table growth to 2^%u slots: device memory", newL);
+  }
+  HIPCHK(h, hipMemsetAsync(nrecs, 0, ncap * sizeof(Rec), h->stream));
+  HIPCHK(h, hipMemsetAsync(naux, 0, ncap * sizeof(u32), h->stream));
+  HIPCHK(h, hipMemsetAsync(h->ctr + 8, 0, sizeof(u32), h->stream));
+  Table nt = table(h);
+  nt.recs = nrecs;
+  nt.aux = naux;
+  nt.L = newL;
+  {
+    Launch l(h, "k_rehash");
+    k_rehash<<<grid_for(h->cap), kBlock, 0, h->stream>>>(h->recs, h->aux, h->cap, nt, h->ctr);
+  }
+  HIPCHK(h, hipGetLastError());
+  int rc;
+  if ((rc = read_ctr(h))) return rc;   // synchronises: the old table is no longer read
+  if (h->ctr_host[8]) return set_err(h, PHIP_ERR_INVALID, "internal: rehash probe wrapped");
+  HIPCHK(h, hipFree(h->recs));
+  HIPCHK(h, hipFree(h->aux));
+  h->recs = nrecs;
+  h->aux = naux;
+  h->L = newL;
+  h->cap = ncap;
+  h->max_load = load_limit(ncap, h->load_pct);
+  ++h->grows;
+  return PHIP_OK;
+}
+
+int grow_arena(phip_handle* h, u64 used, u64 want) {
+  u64 ncap = std::max<u64>(h->arena_cap * 2, want);
+  u8* na = nullptr;
+  if (hipMalloc(&na, ncap + 64) != hipSuccess) {
+    (void)hipGetLastError();
+    return set_err(h, PHIP_ERR_ARENA, "arena growth to %llu bytes: device memory",
+                   (unsigned long long)ncap);
+  }
+  if (used) HIPCHK(h, hipMemcpyAsync(na, h->arena, used, hipMemcpyDeviceToDevice, h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  HIPCHK(h, hipFree(h->arena));
+  h->arena = na;
+  h->arena_cap = ncap;
+  return PHIP_OK;
+}
+
+// Room for `bound` more buckets and the long names of list[0..nlist), before
+// any of them is claimed: grow the table / arena, or refuse with nothing
+// claimed.  *grew is set when the table was rehashed (slot numbers changed).
+template <class Src>
+int reserve(phip_handle* h, Src src, const u32* list, u32 nlist, u64 bound, bool* grew) {
+  u64* lb = (u64*)(h->ctr + kCtrLongBytes);
+  HIPCHK(h, hipMemsetAsync(lb, 0, sizeof(u64), h->stream));
+  k_list_long_bytes<Src><<<grid_for(nlist), kBlock, 0, h->stream>>>(src, nlist, list, lb);
+  HIPCHK(h, hipGetLastError());
+  u64 used = 0;
+  HIPCHK(h, hipMemcpyAsync(&used, h->arena_cursor, sizeof(u64), hipMemcpyDeviceToHost, h->stream));
+  int rc;
+  if ((rc = read_ctr(h))) return rc;
+  u64 need;
+  std::memcpy(&need, h->ctr_host + kCtrLongBytes, sizeof need);
+  h->long_need = need;
+  if (used + need > h->arena_cap) {
+    if (!h->grow)
+      return set_err(h, PHIP_ERR_ARENA, "long-name arena: %llu of %llu bytes used, %llu more needed",
+                     (unsigned long long)used, (unsigned long long)h->arena_cap,
+                     (unsigned long long)need);
+    if ((rc = grow_arena(h, used, used + need))) return rc;
+  }
+  if (h->n_buckets + bound > h->max_load) {
+    u32 L = h->L;
+    while (L < 31 && h->n_buckets + bound > load_limit(1ull << L, h->load_pct)) ++L;
+    if (!h->grow || h->n_buckets + bound > load_limit(1ull << L, h->load_pct))
+      return set_err(h, PHIP_ERR_FULL,
+                     "table load limit: %llu buckets + up to %llu new > %llu allowed in 2^%u slots",
+                     (unsigned long long)h->n_buckets, (unsigned long long)bound,
+                     (unsigned long long)(h->grow ? load_limit(1ull << L, h->load_pct) : h->max_load),
+                     h->grow ? L : h->L);
+    if ((rc = grow_table(h, L))) return rc;
+    *grew = true;
+  }
+  return PHIP_OK;
+}
+
+// Insert every name of `list` (all known to be absent) into the table, after
+// reserve() made room for all of them.  Claimed slots are accumulated in
+// B_CSLOT/B_CMSG; *n_claimed returns their count (callers clear the NEW flag
+// once done).  Every claimed slot is published before an error returns, so a
+// failing round leaves no claimed-but-unnamed slot behind.
 template <class Src>
 int insert_names(phip_handle* h, Src src, u32* list, u32 nlist, const int64_t* now_arr, i64 now0,
-                 u32* n_claimed) {
+                 u32* n_claimed, bool* grew = nullptr) {
   u32 *cslot, *cmsg, *retry, *cur = list;
   int rc;
+  *n_claimed = 0;
+  bool g = false;
+  if ((rc = reserve(h, src, list, nlist, nlist, &g))) return rc;
+  if (grew) *grew = g;
   if ((rc = ensure(h, B_CSLOT, nlist, &cslot)) || (rc = ensure(h, B_CMSG, nlist, &cmsg)) ||
       (rc = ensure(h, B_RETRY, nlist, &retry)))
     return rc;
@@ -264,9 +377,6 @@ int insert_names(phip_handle* h, Src src, u32* list, u32 nlist, const int64_t* n
   // name met a slot claimed in that same round), so this terminates; with a
   // 64-bit tag a second round is already rare.
   while (ncur > 0) {
-    if (h->n_buckets >= h->max_load)
-      return set_err(h, PHIP_ERR_FULL, "table load limit reached: %llu buckets of %llu allowed",
-                     (unsigned long long)h->n_buckets, (unsigned long long)h->max_load);
     // ctr[3] is the running claimed count (cumulative), ctr[4] the retry count.
     HIPCHK(h, hipMemsetAsync(h->ctr + 4, 0, sizeof(u32), h->stream));
     {
@@ -276,11 +386,9 @@ int insert_names(phip_handle* h, Src src, u32* list, u32 nlist, const int64_t* n
     }
     HIPCHK(h, hipGetLastError());
     if ((rc = read_ctr(h))) return rc;
-    if ((rc = check_flags(h))) return rc;
     u32 claimed_total = h->ctr_host[3];
     u32 fresh = claimed_total - total;
-    if (fresh == 0 && h->ctr_host[4] != 0)
-      return set_err(h, PHIP_ERR_INVALID, "internal: insert round made no progress");
+    // The round's claims are published before any error is reported.
     if (fresh) {
       Launch l(h, "k_publish");
       k_publish<Src><<<grid_for(fresh), kBlock, 0, h->stream>>>(
@@ -290,12 +398,21 @@ int insert_names(phip_handle* h, Src src, u32* list, u32 nlist, const int64_t* n
     HIPCHK(h, hipGetLastError());
     h->n_buckets += fresh;
     total = claimed_total;
+    *n_claimed = total;
     ncur = h->ctr_host[4];
+    if ((rc = check_flags(h))) return rc;
+    if (fresh == 0 && ncur != 0)
+      return set_err(h, PHIP_ERR_INVALID, "internal: insert round made no progress");
     // next round reads the retries
     cur = nxt;
     nxt = (nxt == retry) ? spare : retry;
   }
   *n_claimed = total;
+  // An arena overflow would show only in the last publish's flags (it cannot
+  // happen after reserve(); checked all the same when long names were inserted).
+  if (h->long_need) {
+    if ((rc = read_ctr(h)) || (rc = check_flags(h))) return rc;
+  }
   return PHIP_OK;
 }
 
@@ -306,6 +423,18 @@ int clear_new(phip_handle* h, u32 n_claimed) {
   k_clear_new<<<grid_for(n_claimed), kBlock, 0, h->stream>>>(cslot, n_claimed, table(h));
   HIPCHK(h, hipGetLastError());
   return PHIP_OK;
+}
+
+// After a failed batch: no slot may keep the NEW flag (the ordered fold reads
+// it as "GetBucket is creating this bucket", phip_kernels.hpp load_state),
+// whichever insert call of the batch claimed it.  Returns rc.
+int after_error(phip_handle* h, int rc) {
+  if (rc == PHIP_OK || rc == PHIP_ERR_HIP) return rc;
+  std::string keep = h->err;
+  k_clear_new_all<<<grid_for(h->cap), kBlock, 0, h->stream>>>(table(h), h->cap);
+  if (hipGetLastError() == hipSuccess) (void)hipStreamSynchronize(h->stream);
+  h->err = keep;
+  return rc;
 }
 
 // ------------------------------------------------------- fast receive ----
@@ -591,13 +720,14 @@ int resolve_all(phip_handle* h, Src src, u32 n, const int64_t* now_arr, i64 now0
   if ((rc = pack_sharded(h, rsh, 2, miss, &nmiss))) return rc;
   if ((rc = check_flags(h))) return rc;
   *n_claimed = 0;
+  bool grew = false;
   if (nmiss >= kManyMisses) {
     // Many new names (an ordered batch on a fresh key range, a large seed):
     // create each once, then resolve the misses again; names k_dedupe
     // dropped for a shared tag miss again and take the general rounds below.
     u32 *dedup, nd = 0;
     if ((rc = dedupe_names(h, src, miss, nmiss, &dedup, &nd)) ||
-        (rc = insert_names(h, src, dedup, nd, now_arr, now0, n_claimed)))
+        (rc = insert_names(h, src, dedup, nd, now_arr, now0, n_claimed, &grew)))
       return rc;
     Sharded r2;
     if ((rc = sharded(h, B_MSHARD, grid_for(nmiss), kBlock, &r2))) return rc;
@@ -611,11 +741,22 @@ int resolve_all(phip_handle* h, Src src, u32 n, const int64_t* now_arr, i64 now0
   }
   if (nmiss) {
     u32 more = 0;
-    if ((rc = insert_names(h, src, miss, nmiss, now_arr, now0, &more))) return rc;
+    bool g2 = false;
+    if ((rc = insert_names(h, src, miss, nmiss, now_arr, now0, &more, &g2))) return rc;
+    grew |= g2;
     *n_claimed += more;
-    Launch l(h, "k_resolve_miss");
-    k_resolve<Src><<<grid_for(nmiss), kBlock, 0, h->stream>>>(src, nmiss, miss, table(h), slot,
-                                                               Sharded{}, h->ctr);
+    if (!grew) {
+      Launch l(h, "k_resolve_miss");
+      k_resolve<Src><<<grid_for(nmiss), kBlock, 0, h->stream>>>(src, nmiss, miss, table(h), slot,
+                                                                 Sharded{}, h->ctr);
+      HIPCHK(h, hipGetLastError());
+    }
+  }
+  if (grew) {
+    // The table was rehashed: every op's slot is looked up again.
+    Launch l(h, "k_resolve");
+    k_resolve<Src><<<grid_for(n), kBlock, 0, h->stream>>>(src, n, nullptr, table(h), slot,
+                                                           Sharded{}, h->ctr);
     HIPCHK(h, hipGetLastError());
   }
   *slot_out = slot;
@@ -881,8 +1022,9 @@ int phip_open(const phip_config* cfg, phip_handle** out) {
   h->device = cfg->device;
   h->L = cfg->log2_slots;
   h->cap = 1ull << h->L;
-  u32 pct = cfg->max_load_pct ? std::min<u32>(cfg->max_load_pct, 95) : 90;
-  h->max_load = h->cap * pct / 100;
+  h->load_pct = cfg->max_load_pct ? std::min<u32>(cfg->max_load_pct, 95) : 90;
+  h->max_load = load_limit(h->cap, h->load_pct);
+  h->grow = !(cfg->flags & PHIP_CFG_NO_GROW);
   h->arena_cap = cfg->arena_bytes ? cfg->arena_bytes : (1ull << 20);
   if (cfg->debug_tag_bits && cfg->debug_tag_bits < 64) h->tag_mask = (1ull << cfg->debug_tag_bits) - 1;
   auto fail = [&](hipError_t e) {
@@ -905,12 +1047,13 @@ int phip_open(const phip_config* cfg, phip_handle** out) {
   if ((e = hipMalloc(&h->aux, h->cap * sizeof(u32))) != hipSuccess) return fail(e);
   if ((e = hipMalloc(&h->arena, h->arena_cap + 64)) != hipSuccess) return fail(e);
   if ((e = hipMalloc(&h->arena_cursor, 64)) != hipSuccess) return fail(e);
-  if ((e = hipMalloc(&h->ctr, 64)) != hipSuccess) return fail(e);
-  if ((e = hipHostMalloc(&h->ctr_host, 64, 0)) != hipSuccess) return fail(e);
+  if ((e = hipMalloc(&h->ctr, kCtrWords * sizeof(u32))) != hipSuccess) return fail(e);
+  if ((e = hipHostMalloc(&h->ctr_host, kCtrWords * sizeof(u32), 0)) != hipSuccess) return fail(e);
   if ((e = hipMemsetAsync(h->recs, 0, h->cap * sizeof(Rec), h->stream)) != hipSuccess) return fail(e);
   if ((e = hipMemsetAsync(h->aux, 0, h->cap * sizeof(u32), h->stream)) != hipSuccess) return fail(e);
   if ((e = hipMemsetAsync(h->arena_cursor, 0, 64, h->stream)) != hipSuccess) return fail(e);
-  if ((e = hipMemsetAsync(h->ctr, 0, 64, h->stream)) != hipSuccess) return fail(e);
+  if ((e = hipMemsetAsync(h->ctr, 0, kCtrWords * sizeof(u32), h->stream)) != hipSuccess)
+    return fail(e);
   if ((e = hipStreamSynchronize(h->stream)) != hipSuccess) return fail(e);
   *out = h;
   return PHIP_OK;
@@ -973,7 +1116,7 @@ int phip_seed(phip_handle* h, const uint8_t* names, const uint32_t* name_offs, u
   if ((rc = stage(h, B_STATES, states, n, dev, &d_st))) return rc;
   u32* slot;
   u32 n_claimed = 0;
-  if ((rc = resolve_all(h, src, n, nullptr, 0, &slot, &n_claimed))) return rc;
+  if ((rc = resolve_all(h, src, n, nullptr, 0, &slot, &n_claimed))) return after_error(h, rc);
   // aux is the per-slot "last writer" scratch: clear, pick the last entry of
   // each name, apply it, clear again.
   k_seed_finish<<<grid_for(n), kBlock, 0, h->stream>>>(slot, n, table(h));
@@ -1073,12 +1216,37 @@ int phip_restore(phip_handle* h, const uint8_t* in, uint64_t len) {
   std::memcpy(&hd, in, sizeof hd);
   if (std::memcmp(hd.magic, kSnapMagic, 8) || hd.abi != PHIP_ABI_VERSION || hd.rec_bytes != sizeof(Rec))
     return set_err(h, PHIP_ERR_INVALID, "not a snapshot of this ABI");
-  if (hd.log2_slots != h->L)
-    return set_err(h, PHIP_ERR_INVALID, "snapshot of 2^%u slots, handle has 2^%u", hd.log2_slots, h->L);
-  if (hd.arena_used > h->arena_cap) return set_err(h, PHIP_ERR_ARENA, "snapshot arena larger than the handle's");
-  if (hd.n_buckets > h->max_load) return set_err(h, PHIP_ERR_FULL, "snapshot above the handle's load limit");
-  if (len != sizeof hd + h->cap * sizeof(Rec) + hd.arena_used)
+  if (hd.log2_slots < 4 || hd.log2_slots > 31)
+    return set_err(h, PHIP_ERR_INVALID, "snapshot of 2^%u slots", hd.log2_slots);
+  const u64 scap = 1ull << hd.log2_slots;
+  if (len != sizeof hd + scap * sizeof(Rec) + hd.arena_used)
     return set_err(h, PHIP_ERR_INVALID, "snapshot truncated");
+  if (hd.n_buckets > load_limit(scap, h->load_pct))
+    return set_err(h, PHIP_ERR_FULL, "snapshot above the handle's load limit");
+  if (hd.arena_used > h->arena_cap) {
+    if (!h->grow) return set_err(h, PHIP_ERR_ARENA, "snapshot arena larger than the handle's");
+    if (int rc = grow_arena(h, 0, hd.arena_used)) return rc;
+  }
+  if (hd.log2_slots != h->L) {
+    // The image's table size wins (the table may have grown since it was
+    // opened): the handle's table is replaced by one of that size.
+    Rec* nrecs = nullptr;
+    u32* naux = nullptr;
+    if (hipMalloc(&nrecs, scap * sizeof(Rec)) != hipSuccess ||
+        hipMalloc(&naux, scap * sizeof(u32)) != hipSuccess) {
+      (void)hipGetLastError();
+      if (nrecs) (void)hipFree(nrecs);
+      return set_err(h, PHIP_ERR_FULL, "restore: no device memory for 2^%u slots", hd.log2_slots);
+    }
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    HIPCHK(h, hipFree(h->recs));
+    HIPCHK(h, hipFree(h->aux));
+    h->recs = nrecs;
+    h->aux = naux;
+    h->L = hd.log2_slots;
+    h->cap = scap;
+    h->max_load = load_limit(scap, h->load_pct);
+  }
   const u8* p = in + sizeof hd;
   HIPCHK(h, hipMemcpyAsync(h->recs, p, h->cap * sizeof(Rec), hipMemcpyHostToDevice, h->stream));
   if (hd.arena_used)
@@ -1124,12 +1292,19 @@ int phip_dump(phip_handle* h, uint8_t* names, uint64_t names_cap, uint64_t* name
   if (int rc0 = begin_call(h)) return rc0;
   int rc;
   u32* list;
-  if ((rc = ensure(h, B_DUMP, h->n_buckets + 1, &list))) return rc;
+  // count the occupied slots first, then size the list by that count
+  if ((rc = reset_ctr(h))) return rc;
+  k_dump_collect<<<grid_for(h->cap), kBlock, 0, h->stream>>>(h->recs, h->cap, nullptr, h->ctr);
+  HIPCHK(h, hipGetLastError());
+  if ((rc = read_ctr(h))) return rc;
+  const u32 occupied = h->ctr_host[2];
+  if ((rc = ensure(h, B_DUMP, (size_t)occupied + 1, &list))) return rc;
   if ((rc = reset_ctr(h))) return rc;
   k_dump_collect<<<grid_for(h->cap), kBlock, 0, h->stream>>>(h->recs, h->cap, list, h->ctr);
   HIPCHK(h, hipGetLastError());
   if ((rc = read_ctr(h))) return rc;
   u32 n = h->ctr_host[2];
+  if (n != occupied) return set_err(h, PHIP_ERR_INVALID, "internal: table changed during dump");
   Rec* d_out;
   if ((rc = ensure(h, B_TEMP, (size_t)n * sizeof(Rec), (u8**)&d_out))) return rc;
   k_dump_gather<<<grid_for(n), kBlock, 0, h->stream>>>(list, n, h->recs, d_out);
@@ -1194,7 +1369,7 @@ int phip_receive_soa(phip_handle* h, const phip_msgs* m, int64_t now, const phip
       (rc = stage(h, B_A, m->added, n, dev, &a)) || (rc = stage(h, B_T, m->taken, n, dev, &t)) ||
       (rc = stage(h, B_E, m->elapsed, n, dev, &e)) || (rc = outputs(h, res, n, dev, &ow)))
     return rc;
-  if ((rc = receive_decoded(h, src, a, t, e, n, now, ow))) return rc;
+  if ((rc = receive_decoded(h, src, a, t, e, n, now, ow))) return after_error(h, rc);
   return copy_outputs(h, res, n, dev, ow);
 }
 
@@ -1217,7 +1392,7 @@ int receive_datagrams_dev(phip_handle* h, const u8* d_bytes, const uint64_t* d_o
   u32 fd = n, nmiss = 0;
   if ((rc = fast_apply(h, WireIn{d_bytes, d_offs}, Datagrams{d_bytes, d_offs}, n, ow.status, &fd,
                        &nmiss)))
-    return rc;
+    return after_error(h, rc);
   const u32 stop = std::min<u32>(h->ctr_host[5], n);
   // Statuses of the short datagram and everything after it (the Go loop exits).
   if (ow.status && stop < n) {
@@ -1239,7 +1414,7 @@ int receive_datagrams_dev(phip_handle* h, const u8* d_bytes, const uint64_t* d_o
       HIPCHK(h, hipGetLastError());
     }
     if ((rc = finish_receive(h, NamesPairs{d_bytes, no, nl}, a, t, e, stop, fd, nmiss, now, ow)))
-      return rc;
+      return after_error(h, rc);
   }
   if ((rc = copy_outputs(h, res, n, dev, ow))) return rc;
   if (dev) HIPCHK(h, hipStreamSynchronize(h->stream));
@@ -1439,7 +1614,7 @@ int phip_upsert_soa(phip_handle* h, const phip_msgs* m, int64_t now, const phip_
   ov.kind0 = PHIP_OP_UPSERT;
   ov.now0 = now;
   ov.a = a; ov.t = t; ov.e = e;
-  if ((rc = ordered(h, src, n, ov, ow))) return rc;
+  if ((rc = ordered(h, src, n, ov, ow))) return after_error(h, rc);
   return copy_outputs(h, res, n, dev, ow);
 }
 
@@ -1477,7 +1652,7 @@ int phip_apply_mixed(phip_handle* h, const phip_ops* ops, const phip_results* re
       (rc = stage(h, B_E, ops->elapsed, n, dev, &ov.e)) || (rc = outputs(h, res, n, dev, &ow)))
     return rc;
   ov.kind = kind;
-  if ((rc = ordered(h, src, n, ov, ow))) return rc;
+  if ((rc = ordered(h, src, n, ov, ow))) return after_error(h, rc);
   return copy_outputs(h, res, n, dev, ow);
 }
 
@@ -1713,8 +1888,9 @@ int phip_set_stream(phip_handle* h, void* stream) {
 int phip_last_stats(phip_handle* h, uint64_t* out, int max) {
   if (!h || !out) return 0;
   std::lock_guard<std::mutex> g(h->mu);
+  const uint64_t v[4] = {h->stats[0], h->stats[1], h->stats[2], h->grows};
   int k = 0;
-  for (; k < max && k < 3; ++k) out[k] = h->stats[k];
+  for (; k < max && k < 4; ++k) out[k] = v[k];
   return k;
 }
 

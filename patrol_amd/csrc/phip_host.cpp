@@ -12,6 +12,7 @@
 #include <string>
 
 #include "patrolhip.h"
+#include "phip_host.hpp"
 
 namespace {
 
@@ -139,6 +140,26 @@ u64 parse_count(const char* s, size_t n) {
 
 }  // namespace
 
+namespace phip_host {
+
+int api_prepare(const uint8_t* name, uint32_t len, const char* rate, uint32_t rate_len,
+                const char* count, uint32_t count_len, int64_t* freq, int64_t* per, uint64_t* n,
+                char* body, uint32_t* body_len) {
+  (void)name;
+  if (len > PHIP_MAX_NAME_LEN) {                                  // api.go:55-58
+    static const char msg[] = "bucket name larger than 231";
+    memcpy(body, msg, sizeof msg - 1);
+    *body_len = sizeof msg - 1;
+    return 400;
+  }
+  phip_parse_rate(rate, rate_len, freq, per);                     // api.go:61, error ignored
+  *n = parse_count(count, count_len);                             // api.go:62-65
+  if (*n == 0) *n = 1;
+  return 0;
+}
+
+}  // namespace phip_host
+
 extern "C" {
 
 int phip_parse_rate(const char* s, uint32_t len, int64_t* freq, int64_t* per) {
@@ -171,16 +192,11 @@ int phip_api_take(phip_handle* h, const uint8_t* name, uint32_t len, const char*
                   uint32_t rate_len, const char* count, uint32_t count_len, int64_t now,
                   char* body, uint32_t* body_len) {
   if (!body || !body_len) return PHIP_ERR_INVALID;
-  if (len > PHIP_MAX_NAME_LEN) {                                  // api.go:55-58
-    static const char msg[] = "bucket name larger than 231";
-    memcpy(body, msg, sizeof msg - 1);
-    *body_len = sizeof msg - 1;
-    return 400;
-  }
   int64_t freq, per;
-  phip_parse_rate(rate, rate_len, &freq, &per);                   // api.go:61, error ignored
-  uint64_t n = parse_count(count, count_len);                     // api.go:62-65
-  if (n == 0) n = 1;
+  uint64_t n;
+  const int pre = phip_host::api_prepare(name, len, rate, rate_len, count, count_len, &freq, &per,
+                                         &n, body, body_len);
+  if (pre) return pre;
   uint32_t offs[2] = {0, len};
   uint8_t empty = 0;
   uint64_t rem = 0;

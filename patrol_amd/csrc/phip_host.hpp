@@ -1,0 +1,15 @@
+// Host helpers shared by the C-ABI entry points (not exported).
+#pragma once
+#include <cstdint>
+
+namespace phip_host {
+
+// The request parsing of API.takeBucket (api.go:55-65): the name-length check
+// (returns 400 with ErrNameTooLarge's text as the body), ParseRate with its
+// error ignored (the Rate Go returns beside the error), count 0 / error -> 1.
+// Returns 0 when the Take should run.
+int api_prepare(const uint8_t* name, uint32_t len, const char* rate, uint32_t rate_len,
+                const char* count, uint32_t count_len, int64_t* freq, int64_t* per, uint64_t* n,
+                char* body, uint32_t* body_len);
+
+}  // namespace phip_host

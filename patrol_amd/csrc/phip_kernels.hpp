@@ -1061,6 +1061,58 @@ __global__ void k_clear_new(const u32* __restrict__ claimed_slot, u32 n, Table T
   T.aux[s] = 0;
 }
 
+// Error paths: the NEW flag (and creator scratch) of every slot, whatever
+// list claimed it, so a refused batch leaves no bucket marked as created.
+__global__ void k_clear_new_all(Table T, u64 cap) {
+  const u64 s = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= cap) return;
+  Rec* r = &T.recs[s];
+  if (r->tag && (rec_flags(*r) & kRecNew)) r->name0 = with_flags(r->name0, kRecPublished);
+  T.aux[s] = 0;
+}
+
+// Arena bytes the names of a list could need (names > kInlineName bytes;
+// duplicates counted once each, so an upper bound), summed into *out.
+template <class Src>
+__global__ __launch_bounds__(kBlock) void k_list_long_bytes(Src src, u32 n,
+                                                            const u32* __restrict__ list,
+                                                            u64* out) {
+  const u32 tid = blockIdx.x * kBlock + threadIdx.x;
+  u64 b = 0;
+  if (tid < n) {
+    u64 off; u32 len;
+    src.get(list[tid], off, len);
+    b = len > kInlineName ? len : 0;
+  }
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) b += (u64)__shfl_xor((long long)b, d);
+  if (__lane_id() == 0 && b) atomicAdd((unsigned long long*)out, (unsigned long long)b);
+}
+
+// Table growth (Go's map never refuses a bucket, repo.go:204-207,225-227):
+// every record of the old table moves to its home in the new one (2x the
+// slots) by linear probing.  Names are distinct, so a slot is claimed by a
+// CAS on its tag and no name is compared; the record (state, name words,
+// created, flags) and its aux word move as they are, arena offsets included.
+__global__ __launch_bounds__(kBlock) void k_rehash(const Rec* __restrict__ old,
+                                                   const u32* __restrict__ old_aux, u64 old_cap,
+                                                   Table T, u32* ctr) {
+  const u64 s = (u64)blockIdx.x * kBlock + threadIdx.x;
+  if (s >= old_cap) return;
+  const Rec r = load_rec(&old[s]);
+  if (!r.tag) return;
+  const u32 mask = T.mask();
+  u32 d = T.home(r.tag);
+  u32 k = 0;
+  for (; k <= mask; ++k, d = (d + 1) & mask)
+    if (atomicCAS(&T.recs[d].tag, 0ull, r.tag) == 0ull) break;
+  if (k > mask) { atomicOr(&ctr[8], 1u); return; }
+  Rec* q = &T.recs[d];
+  q->added = r.added; q->taken = r.taken; q->elapsed = r.elapsed;
+  q->name0 = r.name0; q->name1 = r.name1; q->created = r.created; q->name2 = r.name2;
+  T.aux[d] = old_aux[s];
+}
+
 // --------------------------------------------------------------- decode --
 // UnmarshalBinary (bucket.go:71-91) for a batch of raw datagrams: big-endian
 // fields, name length byte, io.ErrShortBuffer when < 25 bytes or the name is
@@ -1831,11 +1883,12 @@ __global__ void k_seed_finish(const u32* __restrict__ slot_of, u32 n, Table T) {
   T.recs[s].name0 = with_flags(T.recs[s].name0, kRecPublished);
 }
 
+// Occupied slots into list (list == nullptr: count only, into ctr[2]).
 __global__ void k_dump_collect(const Rec* __restrict__ recs, u64 cap, u32* list, u32* ctr) {
   u64 s = (u64)blockIdx.x * blockDim.x + threadIdx.x;
   bool occ = s < cap && recs[s].tag != 0;
   u32 p = wave_append(&ctr[2], occ);
-  if (occ) list[p] = (u32)s;
+  if (occ && list) list[p] = (u32)s;
 }
 __global__ void k_dump_gather(const u32* __restrict__ list, u32 n, const Rec* __restrict__ recs,
                               Rec* out) {

@@ -82,9 +82,10 @@ class GPURepo:
     """A device-resident bucket map (the LocalRepo of repo.go:171-235)."""
 
     def __init__(self, device: int = 0, log2_slots: int = 20, arena_bytes: int = 1 << 24,
-                 max_load_pct: int = 90, debug_tag_bits: int = 0):
+                 max_load_pct: int = 90, debug_tag_bits: int = 0, grow: bool = True):
         self.L = _lib.load()
-        cfg = phip_config(device, log2_slots, arena_bytes, max_load_pct, debug_tag_bits)
+        cfg = phip_config(device, log2_slots, arena_bytes, max_load_pct, debug_tag_bits,
+                          0 if grow else _lib.CFG_NO_GROW, 0)
         h = C.c_void_p()
         rc = self.L.phip_open(C.byref(cfg), C.byref(h))
         if rc != 0:
@@ -144,9 +145,9 @@ class GPURepo:
 
     def last_stats(self):
         """(hot-directory entries, messages folded through it, misses) of the
-        last fast-path Receive batch."""
-        out = (C.c_uint64 * 3)()
-        k = self.L.phip_last_stats(self.h, out, 3)
+        last fast-path Receive batch, and the table's growths since open."""
+        out = (C.c_uint64 * 4)()
+        k = self.L.phip_last_stats(self.h, out, 4)
         return tuple(int(out[i]) for i in range(k))
 
     def timings(self, max_entries: int = 1 << 14):
@@ -214,6 +215,23 @@ class GPURepo:
         buf = np.fromfile(src, np.uint8) if isinstance(src, (str, bytes, os.PathLike)) else \
             np.ascontiguousarray(src, np.uint8)
         self._check(self.L.phip_restore(self.h, buf.ctypes.data, buf.size))
+
+    def dump_arrays(self):
+        """Every bucket as arrays (unordered): (names uint8, offs uint64[n+1],
+        added bits, taken bits, elapsed, created) -- for tables too large for
+        a dict."""
+        n, nb = C.c_uint64(), C.c_uint64()
+        self._check(self.L.phip_dump(self.h, None, 0, None, None, 0, C.byref(n), C.byref(nb)))
+        cnt = n.value
+        names = np.zeros(max(nb.value, 1), np.uint8)
+        offs = np.zeros(cnt + 1, np.uint64)
+        st = np.zeros(max(cnt, 1), dtype=[("a", "<u8"), ("t", "<u8"), ("e", "<i8"), ("c", "<i8")])
+        self._check(self.L.phip_dump(self.h, names.ctypes.data, names.size, offs.ctypes.data,
+                                     st.ctypes.data, cnt, C.byref(n), C.byref(nb)))
+        st = st[:n.value]
+        return (names, offs[:n.value + 1], np.ascontiguousarray(st["a"]),
+                np.ascontiguousarray(st["t"]), np.ascontiguousarray(st["e"]),
+                np.ascontiguousarray(st["c"]))
 
     def dump(self):
         """{name: BucketState} of every bucket."""

@@ -81,50 +81,73 @@ def route_messages(blob, offs, added, taken, elapsed, group=None, repo=None, h=N
     this rank owns.
     """
     world = dist.get_world_size(group)
-    dev = blob.device
+    packed = pack_by_owner(blob, offs, added, taken, elapsed, world, h=h, repo=repo)
+    return exchange_packed(*packed, group=group)
+
+
+def _a2a(out, inp, r_splits=None, s_splits=None, group=None):
+    """all_to_all_single; gloo (the CPU rehearsal backend) takes CPU tensors
+    only, so CUDA tensors are staged through host memory there."""
+    if inp.is_cuda and dist.get_backend(group) == "gloo":
+        o = torch.empty(out.shape, dtype=out.dtype)
+        dist.all_to_all_single(o, inp.cpu(), r_splits, s_splits, group=group)
+        out.copy_(o)
+        return
+    dist.all_to_all_single(out, inp, r_splits, s_splits, group=group)
+
+
+def pack_by_owner(blob, offs, added, taken, elapsed, world, h=None, repo=None):
+    """The pack step of owner routing restated with torch ops: the
+    owner-major, per-owner stable layout phip_route_pack writes (without its
+    sender-side combine).  Returns (names, lens int32, added, taken, elapsed,
+    counts int64[world], name_bytes int64[world])."""
     if h is None:
         h = hash_names(blob, offs, repo)
     own = owner_of(h, world)
     order = torch.sort(own, stable=True).indices
-    send_cnt = torch.bincount(own, minlength=world).to(torch.int64)
     nb, lens, _ = _gather_names(blob, offs, order)
-    send_bytes = torch.zeros(world, dtype=torch.int64, device=dev)
-    send_bytes.index_add_(0, own, (offs[1:] - offs[:-1]).to(torch.int64))
-    recv_cnt = torch.empty_like(send_cnt)
-    recv_bytes = torch.empty_like(send_bytes)
-    dist.all_to_all_single(recv_cnt, send_cnt, group=group)
-    dist.all_to_all_single(recv_bytes, send_bytes, group=group)
-    sc, rc = send_cnt.tolist(), recv_cnt.tolist()
-    sb, rb = send_bytes.tolist(), recv_bytes.tolist()
+    cnt = torch.bincount(own, minlength=world).to(torch.int64)
+    nbytes = torch.zeros(world, dtype=torch.int64, device=blob.device)
+    nbytes.index_add_(0, own, (offs[1:] - offs[:-1]).to(torch.int64))
+    return nb, lens.to(torch.int32), added[order], taken[order], elapsed[order], cnt, nbytes
 
-    def a2a(x, s_splits, r_splits):
-        out = torch.empty(sum(r_splits), dtype=x.dtype, device=dev)
-        dist.all_to_all_single(out, x.contiguous(), r_splits, s_splits, group=group)
-        return out
 
-    r_lens = a2a(lens, sc, rc)
-    r_blob = a2a(nb, sb, rb)
-    r_a = a2a(added[order], sc, rc)
-    r_t = a2a(taken[order], sc, rc)
-    r_e = a2a(elapsed[order], sc, rc)
+def exchange_packed(s_names, s_lens, s_a, s_t, s_e, cnt, nbytes, group=None):
+    """The exchange step of owner routing: one all-to-all of the (messages,
+    name bytes) split sizes, then one all-to-all per column of the
+    owner-major send buffers (phip_route_pack's or pack_by_owner's layout).
+    Returns (names with 8 bytes of read slack, int32 offsets[m+1], added,
+    taken, elapsed) of the m messages this rank owns, sources concatenated
+    by rank, each source's in its order."""
+    world = dist.get_world_size(group)
+    dev = s_names.device
+    sizes = torch.stack([cnt, nbytes], 1)                  # [world, 2]
+    recv_sizes = torch.empty_like(sizes)
+    _a2a(recv_sizes, sizes, group=group)
+    (sc, sb), (rc_, rb) = torch.cat([sizes, recv_sizes], 1).t().reshape(2, 2, world).tolist()
+
+    def a2a(x, s_splits, r_splits, slack=0):
+        total = sum(r_splits)
+        out = torch.zeros(total + slack, dtype=x.dtype, device=dev)
+        _a2a(out[:total], x[:sum(s_splits)], r_splits, s_splits, group=group)
+        return out if slack else out[:total]
+
+    r_lens = a2a(s_lens, sc, rc_)
+    # 8 bytes of read slack past the last name (the ABI's blob rule)
+    r_blob = a2a(s_names, sb, rb, slack=8)
+    r_a, r_t, r_e = a2a(s_a, sc, rc_), a2a(s_t, sc, rc_), a2a(s_e, sc, rc_)
     # name offsets in the received blob: one int32 scan of the lengths
-    r_offs = torch.empty(r_lens.numel() + 1, dtype=torch.int32, device=dev)
-    r_offs[0] = 0
+    r_offs = torch.zeros(r_lens.numel() + 1, dtype=torch.int32, device=dev)
     torch.cumsum(r_lens, 0, dtype=torch.int32, out=r_offs[1:])
     return r_blob, r_offs, r_a, r_t, r_e
 
 
-def route_messages_native(blob, offs, added, taken, elapsed, repo, group=None, combine=False):
-    """route_messages with the partition on the GPU (phip_route_pack: owner
-    hash, stable owner-major pack of names, lengths and states in two
-    passes), then the all-to-all of each column over RCCL.  Same result as
-    route_messages(); with combine=True a clean batch's hot names are
-    max-combined at the sender (PHIP_ROUTE_COMBINE), which leaves every
-    owner's merged state the same with fewer messages moved.  repo's stream
-    must be torch's current stream (GPURepo.use_torch_stream) or the inputs
-    complete."""
+def route_pack_native(blob, offs, added, taken, elapsed, repo, world, combine=False):
+    """phip_route_pack on the GPU (owner hash, stable owner-major pack of
+    names, lengths and states in two passes; with combine=True a clean
+    batch's hot names are max-combined at the sender, PHIP_ROUTE_COMBINE).
+    Returns the send buffers and split sizes exchange_packed() takes."""
     from .engine import phip_msgs
-    world = dist.get_world_size(group)
     dev = blob.device
     n = offs.numel() - 1
     L = _lib.load()
@@ -144,27 +167,18 @@ def route_messages_native(blob, offs, added, taken, elapsed, repo, group=None, c
                            _lib.DEVICE_PTRS | (_lib.ROUTE_COMBINE if combine else 0))
     if rc != 0:
         raise RuntimeError(f"phip_route_pack failed: {rc}")
-    # one exchange of the (messages, name bytes) split sizes, one host sync
-    sizes = torch.stack([cnt, nbytes], 1)                  # [world, 2]
-    recv_sizes = torch.empty_like(sizes)
-    dist.all_to_all_single(recv_sizes, sizes, group=group)
-    (sc, sb), (rc_, rb) = torch.cat([sizes, recv_sizes], 1).t().reshape(2, 2, world).tolist()
+    return s_names, s_lens, s_a, s_t, s_e, cnt, nbytes
 
-    def a2a(x, s_splits, r_splits, slack=0):
-        total = sum(r_splits)
-        out = torch.empty(total + slack, dtype=x.dtype, device=dev)
-        dist.all_to_all_single(out[:total], x[:sum(s_splits)], r_splits, s_splits, group=group)
-        return out if slack else out[:total]
 
-    r_lens = a2a(s_lens, sc, rc_)
-    # 8 bytes of read slack past the last name (the ABI's blob rule)
-    r_blob = a2a(s_names, sb, rb, slack=8)
-    r_a, r_t, r_e = a2a(s_a, sc, rc_), a2a(s_t, sc, rc_), a2a(s_e, sc, rc_)
-    # name offsets in the received blob: one int32 scan of the lengths
-    r_offs = torch.empty(r_lens.numel() + 1, dtype=torch.int32, device=dev)
-    r_offs[0] = 0
-    torch.cumsum(r_lens, 0, dtype=torch.int32, out=r_offs[1:])
-    return r_blob, r_offs, r_a, r_t, r_e
+def route_messages_native(blob, offs, added, taken, elapsed, repo, group=None, combine=False):
+    """route_messages with the partition on the GPU (route_pack_native), then
+    the all-to-all of each column over RCCL (exchange_packed).  Same result
+    as route_messages(); with combine=True every owner's merged state is the
+    same with fewer messages moved.  repo's stream must be torch's current
+    stream (GPURepo.use_torch_stream) or the inputs complete."""
+    world = dist.get_world_size(group)
+    packed = route_pack_native(blob, offs, added, taken, elapsed, repo, world, combine)
+    return exchange_packed(*packed, group=group)
 
 
 # ---------------------------------------------------------- E-encoding ----

@@ -36,7 +36,14 @@ def test_exports_match_header():
     L = _lib.load()
     for name in declared:
         assert hasattr(L, name)
-    assert L.phip_abi_version() == 1
+    assert L.phip_abi_version() == 2
+
+
+def test_config_struct_layout():
+    """phip_config as the header lays it out (a cgo binding mirrors it)."""
+    import ctypes as C
+    assert C.sizeof(_lib.phip_config) == 32
+    assert _lib.phip_config.flags.offset == 24
 
 
 def test_library_is_gfx950_code_object():

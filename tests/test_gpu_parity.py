@@ -469,14 +469,121 @@ def test_datagram_path_matches_soa_path(pa):
     assert_same_dump(gpu_dump(g), o.dump())
 
 
-def test_table_full_is_an_error(pa):
-    g = pa.GPURepo(log2_slots=8, max_load_pct=50)
-    names = _gen.key_names(range(200))
-    a, t, e = _gen.clean_states(np.random.default_rng(0), 200)
+@pytest.mark.parametrize("path", ["receive", "mixed", "seed"])
+def test_table_full_refused_without_growth(pa, path):
+    """PHIP_CFG_NO_GROW: a batch whose new buckets would pass the load limit
+    is refused before any of them is claimed (PHIP_ERR_FULL).  The table then
+    holds what it held plus the merges into existing buckets (merges commute),
+    no slot is left claimed or flagged as new, and later batches that fit
+    still work bit-exactly."""
+    rng = np.random.default_rng(0)
+    g = pa.GPURepo(log2_slots=8, max_load_pct=50, grow=False)     # 128 buckets allowed
+    o = O.Repo()
+    names1 = _gen.key_names(range(100))
+    a, t, e = _gen.clean_states(rng, 100)
+    g.receive_soa(names1, a, t, e, _gen.T0)
+    o.receive_soa(names1, a, t, e, _gen.T0)
+    new = _gen.key_names(range(1000, 1100))
+    old = [names1[i] for i in rng.integers(0, 100, 60)]
+    names2 = old + new
+    rng.shuffle(names2)
+    a2, t2, e2 = _gen.clean_states(rng, len(names2))
     with pytest.raises(pa.PatrolHipError) as ei:
-        g.receive_soa(names[:150], a[:150], t[:150], e[:150], _gen.T0)
-        g.receive_soa(names[150:], a[150:], t[150:], e[150:], _gen.T0)
+        if path == "receive":
+            g.receive_soa(names2, a2, t2, e2, _gen.T0 + SEC)
+        elif path == "mixed":
+            k = np.ones(len(names2), np.uint8)
+            z = np.zeros(len(names2), np.int64)
+            g.apply_mixed(k, names2, z + _gen.T0 + SEC, z, z, z.astype(np.uint64), a2, t2, e2)
+        else:
+            g.seed(names2, a2, t2, e2, np.full(len(names2), _gen.T0 + SEC, np.int64))
     assert ei.value.code == -3
+    assert len(g) == 100
+    if path == "receive":   # the fast path merged the clean prefix's existing buckets
+        keep = [i for i, nm in enumerate(names2) if nm in set(names1)]
+        o.receive_soa([names2[i] for i in keep], a2[keep], t2[keep], e2[keep], _gen.T0 + SEC)
+    assert_same_dump(gpu_dump(g), o.dump())
+    # the table still works: a batch that fits creates and merges exactly
+    names3 = old[:10] + new[:20]
+    a3, t3, e3 = _gen.clean_states(rng, len(names3))
+    out = g.receive_soa(names3, a3, t3, e3, _gen.T0 + 2 * SEC)
+    st, _, _, _ = o.receive_soa(names3, a3, t3, e3, _gen.T0 + 2 * SEC)
+    assert np.array_equal(out["status"], st)
+    assert len(g) == 120
+    assert_same_dump(gpu_dump(g), o.dump())
+
+
+@pytest.mark.parametrize("tag_bits", [0, 12])
+def test_table_grows_vs_oracle(pa, tag_bits):
+    """Go's map never refuses a bucket (repo.go:204-207): a 2^10-slot table
+    takes 60k buckets by rehashing into larger tables (k_rehash) through the
+    fast Receive path (small and large miss lists), the ordered path and
+    seeding, bit-exact throughout (statuses, `created`, the final table)."""
+    rng = np.random.default_rng(303 + tag_bits)
+    g = pa.GPURepo(log2_slots=10, debug_tag_bits=tag_bits)
+    o = O.Repo()
+    # small miss list (k_receive_list) on a table that must grow
+    names = _gen.key_names(rng.integers(0, 3000, 9000))
+    a, t, e = _gen.clean_states(rng, len(names))
+    out = g.receive_soa(names, a, t, e, _gen.T0)
+    st, _, _, _ = o.receive_soa(names, a, t, e, _gen.T0)
+    assert np.array_equal(out["status"], st)
+    # large miss list (k_dedupe + second fast pass)
+    ids = _gen.zipf_ids(rng, 200_000, 40_000) + 3000
+    names = [(b"a-long-name-that-lives-in-the-arena-%d" % i) if i % 53 == 0 else b"b%d" % i
+             for i in ids]
+    a, t, e = _fast_dirty_states(rng, len(names))
+    out = g.receive_soa(names, a, t, e, _gen.T0 + SEC)
+    st, _, _, _ = o.receive_soa(names, a, t, e, _gen.T0 + SEC)
+    assert np.array_equal(out["status"], st)
+    # ordered path creating buckets (slots resolved again after the rehash)
+    args = _mixed_stream(rng, 100_000, 60_000)
+    out = g.apply_mixed(*args)
+    ref = o.apply_mixed(*args)
+    assert np.array_equal(out["status"], ref["status"])
+    assert np.array_equal(out["remaining"], ref["remaining"])
+    # seeding into a table that must grow
+    sn = _gen.key_names(np.arange(500_000, 520_000))
+    sa, stt, se = _gen.clean_states(rng, len(sn))
+    sc = np.full(len(sn), _gen.T0 + 5 * SEC, np.int64)
+    g.seed(sn, sa, stt, se, sc)
+    o.seed(sn, sa, stt, se, sc)
+    assert len(g) == len(o) > 50_000
+    assert g.capacity >= 1 << 17 and g.last_stats()[3] >= 5
+    assert_same_dump(gpu_dump(g), o.dump())
+    g.close()
+
+
+@pytest.mark.parametrize("grow", [True, False])
+def test_long_name_arena_growth(pa, grow):
+    """The long-name arena is reserved before any name is claimed: with
+    growth a 256-byte arena takes thousands of 23..231-byte names exactly;
+    without it the batch is refused (PHIP_ERR_ARENA) with no bucket created
+    and no record pointing at another name's bytes."""
+    rng = np.random.default_rng(17)
+    g = pa.GPURepo(log2_slots=14, arena_bytes=256, grow=grow)
+    o = O.Repo()
+    short = _gen.key_names(range(50))
+    a, t, e = _gen.clean_states(rng, 50)
+    g.receive_soa(short, a, t, e, _gen.T0)
+    o.receive_soa(short, a, t, e, _gen.T0)
+    longs = [bytes(rng.integers(97, 123, int(rng.integers(23, 232)), dtype=np.uint8)) for _ in range(3000)]
+    names = [longs[i] for i in rng.integers(0, len(longs), 20000)] + short[:10]
+    a, t, e = _gen.clean_states(rng, len(names))
+    if grow:
+        out = g.receive_soa(names, a, t, e, _gen.T0 + SEC)
+        st, _, _, _ = o.receive_soa(names, a, t, e, _gen.T0 + SEC)
+        assert np.array_equal(out["status"], st)
+        for nm in longs[:20]:
+            got, want = g.get(nm), o.get(nm)
+            assert (got.added, got.taken, got.elapsed, got.created) == want
+    else:
+        with pytest.raises(pa.PatrolHipError) as ei:
+            g.receive_soa(names, a, t, e, _gen.T0 + SEC)
+        assert ei.value.code == -4
+        assert len(g) == 50
+        o.receive_soa(names[-10:], a[-10:], t[-10:], e[-10:], _gen.T0 + SEC)
+    assert_same_dump(gpu_dump(g), o.dump())
 
 
 def test_merge_laws_at_scale(pa):
@@ -661,9 +768,10 @@ def test_snapshot_restore_round_trip(pa, tmp_path):
     o.apply_mixed(kind, names2, now, freq, per, cnt, a2, t2, e2)
     assert gpu_dump(r) == gpu_dump(g)
     assert_same_dump(gpu_dump(r), o.dump())
-    other = pa.GPURepo(log2_slots=15)
-    with pytest.raises(pa.PatrolHipError):
-        other.restore(path)
+    # a handle opened at another size takes the image's table size
+    other = pa.GPURepo(log2_slots=11)
+    other.restore(path)
+    assert other.capacity == g.capacity and gpu_dump(other) == gpu_dump(g)
 
 
 # ------------------------------------------------ C1 (BASELINE configs[0]) --

@@ -126,6 +126,77 @@ def test_route_messages_gloo_world2():
     assert sum(len(v) for v in res.values()) == world * n
 
 
+def _c4_worker(rank, world, port, n, out_q):
+    """C4's per-rank step with the oracle as the receiving table: pack by
+    owner (the layout phip_route_pack writes), exchange_packed (the same glue
+    bench.py's C4 and owner-routed lines run), then Receive the owned
+    messages into this rank's shard."""
+    from oracle import oracle as O
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        names, blob, offs, a, t, e = _c4_msgs(rank, n)
+        packed = shard.pack_by_owner(blob, offs, a, t, e, world)
+        rb, ro, ra, rt, re = shard.exchange_packed(*packed)
+        m = ro.numel() - 1
+        repo = O.Repo()
+        st, _, _, _ = repo.receive_soa([bytes(rb[ro[i]:ro[i + 1]].numpy()) for i in range(m)],
+                                       ra.numpy().view(np.uint64), rt.numpy().view(np.uint64),
+                                       re.numpy(), 10**18)
+        out_q.put((rank, m, repo.dump()))
+    finally:
+        dist.destroy_process_group()
+
+
+def _c4_msgs(rank, n):
+    rng = np.random.default_rng(300 + rank)
+    ids = rng.zipf(1.3, n) % 4000
+    names = [(b"b%d" % i) if i % 9 else (b"a-longer-bucket-name-%d" % i) for i in ids]
+    lens = torch.tensor([len(x) for x in names], dtype=torch.int64)
+    offs = torch.zeros(n + 1, dtype=torch.int64)
+    offs[1:] = torch.cumsum(lens, 0)
+    blob = torch.tensor(np.frombuffer(b"".join(names) + b"\0" * 8, np.uint8).copy())
+    taken = rng.integers(0, 10**6, n).astype(np.float64)
+    a = torch.from_numpy((taken + rng.random(n) * 100).view(np.int64).copy())
+    t = torch.from_numpy(taken.view(np.int64).copy())
+    e = torch.tensor(rng.integers(1, 1 << 40, n), dtype=torch.int64)
+    return names, blob, offs, a, t, e
+
+
+def test_owner_routed_receive_gloo_world2_equals_oracle():
+    """The owner-routed merge over two gloo ranks: every
+    rank's shard holds only buckets it owns, shards are disjoint, and their
+    union equals one oracle repo that received every rank's messages
+    (repo.go:54-92; merges commute in the clean domain)."""
+    from oracle import oracle as O
+    world, n = 2, 20000
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_c4_worker, args=(r, world, port, n, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {r: (m, d) for r, m, d in (q.get(timeout=120) for _ in range(world))}
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert sum(m for m, _ in res.values()) == world * n
+    whole = O.Repo()
+    for r in range(world):
+        names, blob, offs, a, t, e = _c4_msgs(r, n)
+        whole.receive_soa(names, a.numpy().view(np.uint64), t.numpy().view(np.uint64), e.numpy(),
+                          10**18)
+    union = {}
+    for r in range(world):
+        d = res[r][1]
+        for k in d:
+            assert int(shard.owner_of(torch.tensor([to_i64(G.fnv1a64(k))]), world)) == r
+        assert not (set(d) & set(union))
+        union.update(d)
+    assert union == whole.dump()
+
+
 def _replicas(rank, R, B):
     rng = random.Random(7 + rank)
     pool = [b for b in specials() if b != S] + [G.f2b(float(i)) for i in range(50)]
