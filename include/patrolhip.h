@@ -71,7 +71,8 @@ typedef enum phip_err {
   PHIP_ERR_NAME_TOO_LARGE = -6, /* ErrNameTooLarge (bucket.go:48) */
   PHIP_ERR_NO_DEVICE = -7,
   PHIP_ERR_IO = -8,             /* socket error (phip_udp_*; errno holds the cause) */
-  PHIP_ERR_BUSY = -9            /* ring slot not available (phip_ring_*) */
+  PHIP_ERR_BUSY = -9,           /* ring slot not available (phip_ring_*) */
+  PHIP_ERR_RCCL = -10           /* RCCL call failed (phip_group_*) */
 } phip_err;
 
 /* Per-op status codes (one uint8 per op). */
@@ -279,10 +280,12 @@ int phip_batcher_open(phip_handle* h, const phip_batcher_config* cfg, phip_batch
 /* Runs the requests already queued, then stops the dispatcher. */
 void phip_batcher_close(phip_batcher* b);
 /* GetBucket + Take(now, Rate{freq, per}, count): *remaining and *ok as Go's
- * Take returns them (ok = 1 means HTTP 200, 0 means 429). */
+ * Take returns them (ok = 1 means HTTP 200, 0 means 429).  *seq (optional)
+ * receives the request's arrival number: the requests of a batcher took
+ * effect exactly as Go running them one by one in seq order. */
 int phip_batcher_take(phip_batcher* b, const uint8_t* name, uint32_t len, int64_t now,
                       int64_t freq, int64_t per, uint64_t count, uint64_t* remaining,
-                      uint8_t* ok);
+                      uint8_t* ok, uint64_t* seq);
 /* API.takeBucket (api.go:51-86) through the batcher: phip_api_take's
  * contract (HTTP status 200/429/400, body <= 64 bytes). */
 int phip_batcher_api_take(phip_batcher* b, const uint8_t* name, uint32_t len, const char* rate,
@@ -401,6 +404,52 @@ int phip_ae_local_max(phip_handle* h, const int64_t* replicas, uint32_t nrep, ui
                       int64_t* out, uint32_t flags);
 int phip_ae_apply(phip_handle* h, int64_t* replicas, uint32_t nrep, uint64_t nbuckets,
                   const int64_t* joined, uint32_t flags);
+
+/* ---- shard group: owner routing and anti-entropy over RCCL ----
+ * A group is the set of GPUs the buckets are hash-sharded over (owner =
+ * ((FNV-1a(name) >> 32) * world) >> 32), each GPU one table (a phip_handle)
+ * and one rank of an RCCL communicator (xGMI between the GPUs of a node).
+ * It replaces the single-table Receive loop (repo.go:54-92) of one node by a
+ * sharded one, with no Python or torch on the path:
+ *   - phip_group_open_all: one process driving n GPUs (ncclCommInitAll); the
+ *     group opens and owns a handle per GPU (cfg->device is ignored);
+ *   - phip_group_open_rank: one process per GPU (ncclCommInitRank) around the
+ *     caller's handle; rank 0 makes the id with phip_group_unique_id and the
+ *     caller hands it to every rank by its own means.
+ * Calls taking one argument per local member (index i = local member i) run
+ * the members concurrently, one host thread each. */
+#define PHIP_GROUP_ID_BYTES 128
+typedef struct phip_group phip_group;
+int phip_group_unique_id(uint8_t* id /* PHIP_GROUP_ID_BYTES */);
+int phip_group_open_all(const phip_config* cfg, const int32_t* devices, uint32_t n,
+                        phip_group** out);
+int phip_group_open_rank(phip_handle* h, const uint8_t* id, uint32_t nranks, uint32_t rank,
+                         phip_group** out);
+/* Destroys the communicators, and the handles phip_group_open_all opened. */
+void phip_group_close(phip_group* g);
+const char* phip_group_last_error(const phip_group* g);
+uint32_t phip_group_world(const phip_group* g);
+uint32_t phip_group_local(const phip_group* g);          /* local members */
+phip_handle* phip_group_handle(phip_group* g, uint32_t i);
+/* Owner-routed Receive (the C4 step): batches[i] (device pointers on member
+ * i's GPU, as phip_receive_soa takes them) are the messages that arrived at
+ * member i, addressed to buckets of every shard.  Each member packs its batch
+ * by owner (phip_route_pack; PHIP_ROUTE_COMBINE max-combines a clean batch's
+ * hot names at the sender), the members exchange the packed segments (one
+ * all-to-all of the split sizes, then grouped send/recv per column), and
+ * every owner merges what it received, sources in rank order, each in its
+ * order (phip_receive_soa, `now` for buckets it creates).  sent[i] /
+ * merged[i] (optional) receive the messages member i sent after the combine
+ * and merged. */
+int phip_group_receive(phip_group* g, const phip_msgs* batches, int64_t now, uint64_t* sent,
+                       uint64_t* merged, uint32_t flags);
+/* Anti-entropy round over simulated replicas (BASELINE configs[4]):
+ * replicas[i] holds member i's nrep replicas in phip_ae_local_max's layout
+ * (device memory).  Local join (phip_ae_local_max), RCCL all-reduce(MAX) of
+ * the [3, nbuckets] join across the group, phip_ae_apply: afterwards every
+ * replica of every member is the CvRDT join of all of them. */
+int phip_group_anti_entropy(phip_group* g, int64_t* const* replicas, uint32_t nrep,
+                            uint64_t nbuckets, uint32_t flags);
 
 /* ---- diagnostics ---- */
 /* Per-kernel timing of the last hot-path call (every call since

@@ -6,9 +6,10 @@ build (Makefile -> libpatrolhip.so) and a thin Python binding used by tests
 and bench.py.
 """
 from ._lib import EXPORTS, LIB_PATH, load  # noqa: F401
-from .engine import (BucketState, GPURepo, PatrolHipError, Ring, incast_replies, marshal,  # noqa: F401
-                     names_blob, parse_rate, udp_recv_batch, udp_send_batch)
+from .engine import (BucketState, GPUGroup, GPURepo, PatrolHipError, Ring, TakeBatcher,  # noqa: F401
+                     incast_replies, marshal, names_blob, parse_rate, udp_recv_batch,
+                     udp_send_batch)
 
-__all__ = ["GPURepo", "BucketState", "PatrolHipError", "Ring", "parse_rate", "marshal",
+__all__ = ["GPURepo", "GPUGroup", "BucketState", "PatrolHipError", "Ring", "TakeBatcher", "parse_rate", "marshal",
            "names_blob", "udp_recv_batch", "udp_send_batch", "incast_replies", "load", "LIB_PATH",
            "EXPORTS"]

@@ -24,12 +24,15 @@ EXPORTS = [
     "phip_ring_open", "phip_ring_close", "phip_ring_acquire", "phip_ring_submit",
     "phip_ring_receive", "phip_udp_recv_batch", "phip_incast_replies", "phip_udp_send_batch",
     "phip_batcher_open", "phip_batcher_close", "phip_batcher_take", "phip_batcher_api_take",
-    "phip_batcher_stats",
+    "phip_batcher_stats", "phip_group_unique_id", "phip_group_open_all", "phip_group_open_rank",
+    "phip_group_close", "phip_group_last_error", "phip_group_world", "phip_group_local",
+    "phip_group_handle", "phip_group_receive", "phip_group_anti_entropy",
 ]
 
 PHIP_OK = 0
 PHIP_ERR = {-1: "INVALID", -2: "HIP", -3: "FULL", -4: "ARENA", -5: "SHORT_BUFFER",
-            -6: "NAME_TOO_LARGE", -7: "NO_DEVICE", -8: "IO", -9: "BUSY"}
+            -6: "NAME_TOO_LARGE", -7: "NO_DEVICE", -8: "IO", -9: "BUSY", -10: "RCCL"}
+GROUP_ID_BYTES = 128
 PEER_BYTES = 128   # PHIP_PEER_BYTES = sizeof(struct sockaddr_storage)
 ST_MERGED, ST_INCAST_REPLY, ST_INCAST_NOREPLY, ST_SHORT, ST_NOT_PROCESSED = 1, 2, 3, 4, 5
 ST_TAKE_OK, ST_TAKE_DENIED, ST_UPSERT_INSERTED, ST_CREATED = 6, 7, 8, 0x80
@@ -145,9 +148,26 @@ def load(path: str = LIB_PATH):
     L.phip_batcher_close.argtypes = [vp]
     L.phip_batcher_close.restype = None
     L.phip_batcher_take.argtypes = [vp, C.c_char_p, u32, i64, i64, i64, u64, C.POINTER(u64),
-                                    C.POINTER(C.c_uint8)]
+                                    C.POINTER(C.c_uint8), C.POINTER(u64)]
     L.phip_batcher_api_take.argtypes = [vp, C.c_char_p, u32, C.c_char_p, u32, C.c_char_p, u32,
                                         i64, C.c_char_p, C.POINTER(u32)]
     L.phip_batcher_stats.argtypes = [vp, C.POINTER(u64), C.c_int]
+    L.phip_group_unique_id.argtypes = [C.c_char_p]
+    L.phip_group_open_all.argtypes = [C.POINTER(phip_config), C.POINTER(C.c_int32), u32,
+                                      C.POINTER(vp)]
+    L.phip_group_open_rank.argtypes = [vp, C.c_char_p, u32, u32, C.POINTER(vp)]
+    L.phip_group_close.argtypes = [vp]
+    L.phip_group_close.restype = None
+    L.phip_group_last_error.argtypes = [vp]
+    L.phip_group_last_error.restype = C.c_char_p
+    L.phip_group_world.argtypes = [vp]
+    L.phip_group_world.restype = u32
+    L.phip_group_local.argtypes = [vp]
+    L.phip_group_local.restype = u32
+    L.phip_group_handle.argtypes = [vp, u32]
+    L.phip_group_handle.restype = vp
+    L.phip_group_receive.argtypes = [vp, C.POINTER(phip_msgs), i64, C.POINTER(u64),
+                                     C.POINTER(u64), u32]
+    L.phip_group_anti_entropy.argtypes = [vp, C.POINTER(vp), u32, u64, u32]
     _lib = L
     return L

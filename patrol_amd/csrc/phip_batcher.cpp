@@ -38,6 +38,7 @@ struct Req {
   int64_t now, freq, per;
   uint64_t count;
   uint64_t remaining = 0;
+  uint64_t seq = 0;
   uint8_t status = 0;
   int rc = 0;
   bool done = false;
@@ -58,6 +59,7 @@ struct phip_batcher {
   std::thread th;
   // stats
   uint64_t batches = 0, requests = 0, max_seen = 0, gpu_ns = 0, errors = 0;
+  uint64_t arrivals = 0;   // arrival numbers handed out (under mu)
   // dispatcher scratch (host arrays of one batch)
   std::vector<uint8_t> kind, names, status;
   std::vector<uint32_t> offs;
@@ -139,6 +141,7 @@ int submit_and_wait(phip_batcher* b, Req* r) {
   std::unique_lock<std::mutex> l(b->mu);
   if (b->stop) return PHIP_ERR_INVALID;
   if (b->pending.empty()) b->first_arrival = Clock::now();
+  r->seq = b->arrivals++;
   b->pending.push_back(r);
   if (b->pending.size() == 1 || b->pending.size() >= b->max_batch) b->cv_submit.notify_one();
   b->cv_done.wait(l, [&] { return r->done; });
@@ -181,7 +184,7 @@ void phip_batcher_close(phip_batcher* b) {
 
 int phip_batcher_take(phip_batcher* b, const uint8_t* name, uint32_t len, int64_t now,
                       int64_t freq, int64_t per, uint64_t count, uint64_t* remaining,
-                      uint8_t* ok) {
+                      uint8_t* ok, uint64_t* seq) {
   if (!b || (!name && len)) return PHIP_ERR_INVALID;
   if (len > PHIP_MAX_NAME_LEN) return PHIP_ERR_NAME_TOO_LARGE;
   Req r;
@@ -195,6 +198,7 @@ int phip_batcher_take(phip_batcher* b, const uint8_t* name, uint32_t len, int64_
   if (rc) return rc;
   if (remaining) *remaining = r.remaining;
   if (ok) *ok = (r.status & 0x7F) == PHIP_ST_TAKE_OK;
+  if (seq) *seq = r.seq;
   return PHIP_OK;
 }
 
@@ -210,7 +214,7 @@ int phip_batcher_api_take(phip_batcher* b, const uint8_t* name, uint32_t len, co
   uint64_t rem = 0;
   uint8_t ok = 0;
   const int rc = phip_batcher_take(b, len ? name : (const uint8_t*)"", len, now, freq, per, n,
-                                   &rem, &ok);
+                                   &rem, &ok, nullptr);
   if (rc < 0) return rc;
   const std::string s = std::to_string(rem);              // api.go:84-85
   std::memcpy(body, s.data(), s.size());

@@ -24,6 +24,7 @@
 
 #include "patrolhip.h"
 #include "phip_kernels.hpp"
+#include "phip_host.hpp"
 
 using namespace phip;
 
@@ -55,6 +56,7 @@ enum BufId {
   B_MISS, B_MISS2, B_RETRY, B_CSLOT, B_CMSG,
   B_SLOT, B_IDX, B_SSLOT, B_SIDX, B_USLOT, B_SCNT, B_SSTART, B_LONG, B_HUGE, B_TEMP, B_DUMP,
   B_OPS, B_HOFF, B_HOP, B_HVAL, B_RPOS, B_RST, B_RUNN, B_SEGEX, B_WOFF, B_SUMS, B_WRUN,
+  B_WING, B_SEGXF,
   B_STATES, B_NAME1, B_HOT, B_ROUTE, B_EXPORT, B_MSHARD, B_MSCNT, B_DEDUP, B_DSET, B_COUNT_
 };
 
@@ -839,13 +841,16 @@ int ordered(phip_handle* h, Src src, u32 n, const OpView& ov, const OutView& ow)
     RunState* rst;
     u8* segex;
     WinSum* sums;
+    GMax* wing;
+    u32* segxf;
     const size_t nwin_max = (size_t)n / kFoldWin + nhuge + 1;
     if ((rc = ensure(h, B_WOFF, (size_t)nhuge + 1, &woff)) ||
         (rc = ensure(h, B_SUMS, nwin_max, &sums)) || (rc = ensure(h, B_WRUN, nwin_max, &wrun)) ||
         (rc = ensure(h, B_HOFF, nhuge, &hoff)) || (rc = ensure(h, B_HOP, n, &hop)) ||
         (rc = ensure(h, B_HVAL, n, &hval)) || (rc = ensure(h, B_RPOS, (size_t)n + nhuge, &rpos)) ||
         (rc = ensure(h, B_RST, (size_t)n + nhuge, &rst)) || (rc = ensure(h, B_RUNN, nhuge, &runn)) ||
-        (rc = ensure(h, B_SEGEX, nhuge, &segex)))
+        (rc = ensure(h, B_SEGEX, nhuge, &segex)) || (rc = ensure(h, B_WING, nwin_max, &wing)) ||
+        (rc = ensure(h, B_SEGXF, nhuge, &segxf)))
       return rc;
     HIPCHK(h, hipEventRecord(h->ev_fork, h->stream));
     HIPCHK(h, hipStreamWaitEvent(h->stream2, h->ev_fork, 0));
@@ -861,14 +866,14 @@ int ordered(phip_handle* h, Src src, u32 n, const OpView& ov, const OutView& ow)
     {
       Launch l(h, "k_fold_block", h->stream2);
       kb<<<nhuge, kFoldThreads, 0, h->stream2>>>(huge, nhuge, uslot, hoff, scnt, hval, hop,
-                                                  h->recs, rpos, rst, runn, segex, woff, sums,
-                                                  wrun);
+                                                  h->recs, rpos, rst, runn, segex, segxf, woff,
+                                                  sums, wrun, wing);
     }
     HIPCHK(h, hipGetLastError());
     {
       Launch l(h, "k_huge_outputs", h->stream2);
       k_huge_outputs<<<(unsigned)nwin_max, kBlock, 0, h->stream2>>>(
-          huge, nhuge, hoff, woff, scnt, hval, hop, rpos, rst, runn, segex, wrun, ow);
+          huge, nhuge, hoff, woff, scnt, hval, hop, rpos, rst, runn, segex, segxf, wrun, wing, ow);
     }
     HIPCHK(h, hipGetLastError());
   }
@@ -1895,3 +1900,8 @@ int phip_last_stats(phip_handle* h, uint64_t* out, int max) {
 }
 
 }  // extern "C"
+
+namespace phip_host {
+void* handle_stream(phip_handle* h) { return h ? (void*)h->stream : nullptr; }
+int handle_device(const phip_handle* h) { return h ? h->device : -1; }
+}  // namespace phip_host

@@ -1,0 +1,362 @@
+// Shard group: the buckets of one node hash-sharded by name over
+// its GPUs, one phip_handle and one RCCL rank per GPU.  The reference has a
+// single map behind one mutex (repo.go:171-235) fed by one Receive goroutine
+// (repo.go:54-92); here every GPU owns the buckets whose name hashes to it,
+// messages that arrive anywhere are routed to their owner, and simulated
+// replicas converge by an all-reduce(max).
+//
+// Per member and call, one host thread: it binds its GPU, queues the member's
+// kernels and RCCL calls on the member handle's stream, and synchronises only
+// to read the split sizes of the exchange.  With one process per GPU the
+// calling thread is the member's thread.
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+#include <rocprim/rocprim.hpp>
+
+#include <algorithm>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "patrolhip.h"
+#include "phip_host.hpp"
+
+namespace {
+
+typedef uint64_t u64;
+typedef unsigned int u32;
+
+// A device buffer that only grows.
+struct Buf {
+  void* p = nullptr;
+  size_t cap = 0;
+  hipError_t ensure(size_t bytes) {
+    if (cap >= bytes) return hipSuccess;
+    if (p) {
+      hipError_t e = hipFree(p);
+      if (e != hipSuccess) return e;
+    }
+    const size_t want = std::max(bytes, cap * 3 / 2) + 64;   // +64: 8-byte over-read slack
+    p = nullptr;
+    cap = 0;
+    hipError_t e = hipMalloc(&p, want);
+    if (e == hipSuccess) cap = want;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+struct Member {
+  phip_handle* h = nullptr;
+  bool own = false;            // opened by the group (phip_group_open_all)
+  int device = 0;
+  u32 rank = 0;
+  ncclComm_t comm = nullptr;
+  // send side (phip_route_pack's owner-major buffers), receive side
+  Buf s_names, s_lens, s_a, s_t, s_e, r_names, r_lens, r_offs, r_a, r_t, r_e;
+  Buf sizes, scan_tmp, ae;
+  u64* host_sizes = nullptr;   // pinned [4 * world]: send counts, send bytes, recv counts, recv bytes
+  std::string err;
+};
+
+}  // namespace
+
+struct phip_group {
+  u32 world = 0;
+  std::vector<Member> m;
+  std::string err;
+};
+
+namespace {
+
+int fail(Member& mb, int code, const char* fmt, ...) {
+  char tmp[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(tmp, sizeof tmp, fmt, ap);
+  va_end(ap);
+  mb.err = tmp;
+  return code;
+}
+
+#define GHIP(mb, x)                                                                        \
+  do {                                                                                     \
+    hipError_t e_ = (x);                                                                   \
+    if (e_ != hipSuccess)                                                                  \
+      return fail((mb), PHIP_ERR_HIP, "%s: %s (%s:%d)", #x, hipGetErrorString(e_), __FILE__, \
+                  __LINE__);                                                               \
+  } while (0)
+
+#define GNCCL(mb, x)                                                                        \
+  do {                                                                                      \
+    ncclResult_t r_ = (x);                                                                  \
+    if (r_ != ncclSuccess)                                                                  \
+      return fail((mb), PHIP_ERR_RCCL, "%s: %s (%s:%d)", #x, ncclGetErrorString(r_), __FILE__, \
+                  __LINE__);                                                                \
+  } while (0)
+
+#define GPHIP(mb, x)                                                                   \
+  do {                                                                                 \
+    int rc_ = (x);                                                                     \
+    if (rc_ != PHIP_OK)                                                                \
+      return fail((mb), rc_, "%s: %s", #x, phip_last_error((mb).h));                    \
+  } while (0)
+
+// Run f(member index) on one host thread per local member (the calling
+// thread when there is one); returns the first member's error.
+template <class F>
+int for_members(phip_group* g, F f) {
+  const size_t n = g->m.size();
+  std::vector<int> rc(n, PHIP_OK);
+  if (n == 1) {
+    rc[0] = f(0);
+  } else {
+    std::vector<std::thread> th;
+    th.reserve(n);
+    for (size_t i = 0; i < n; ++i) th.emplace_back([&, i] { rc[i] = f(i); });
+    for (auto& t : th) t.join();
+  }
+  for (size_t i = 0; i < n; ++i)
+    if (rc[i] != PHIP_OK) {
+      g->err = "member " + std::to_string(i) + ": " + g->m[i].err;
+      return rc[i];
+    }
+  g->err.clear();
+  return PHIP_OK;
+}
+
+// One member's owner-routed Receive.
+int member_receive(phip_group* g, Member& mb, const phip_msgs& in, int64_t now, uint64_t* sent,
+                   uint64_t* merged, uint32_t flags) {
+  const u32 W = g->world;
+  const u32 n = in.n;
+  GHIP(mb, hipSetDevice(mb.device));
+  hipStream_t st = (hipStream_t)phip_host::handle_stream(mb.h);
+  // 1. pack by owner (device; phip_route_pack returns when the sizes are written)
+  size_t in_bytes = 0;
+  if (n) {
+    u32 last = 0;
+    GHIP(mb, hipMemcpyAsync(&last, in.name_offs + n, sizeof last, hipMemcpyDeviceToHost, st));
+    GHIP(mb, hipStreamSynchronize(st));
+    in_bytes = last;
+  }
+  GHIP(mb, mb.s_names.ensure(in_bytes + 64));
+  GHIP(mb, mb.s_lens.ensure((size_t)n * 4 + 4));
+  GHIP(mb, mb.s_a.ensure((size_t)n * 8 + 8));
+  GHIP(mb, mb.s_t.ensure((size_t)n * 8 + 8));
+  GHIP(mb, mb.s_e.ensure((size_t)n * 8 + 8));
+  GHIP(mb, mb.sizes.ensure((size_t)4 * W * 8));
+  u64* sz = (u64*)mb.sizes.p;   // [send counts | send bytes | recv counts | recv bytes]
+  GPHIP(mb, phip_route_pack(mb.h, &in, W, (uint8_t*)mb.s_names.p, (uint32_t*)mb.s_lens.p,
+                            (uint64_t*)mb.s_a.p, (uint64_t*)mb.s_t.p, (int64_t*)mb.s_e.p, sz,
+                            sz + W, PHIP_DEVICE_PTRS | (flags & PHIP_ROUTE_COMBINE)));
+  // 2. split sizes: every member learns what each source sends it
+  GNCCL(mb, ncclGroupStart());
+  GNCCL(mb, ncclAllToAll(sz, sz + 2 * W, 1, ncclUint64, mb.comm, st));
+  GNCCL(mb, ncclAllToAll(sz + W, sz + 3 * W, 1, ncclUint64, mb.comm, st));
+  GNCCL(mb, ncclGroupEnd());
+  GHIP(mb, hipMemcpyAsync(mb.host_sizes, sz, 4 * W * sizeof(u64), hipMemcpyDeviceToHost, st));
+  GHIP(mb, hipStreamSynchronize(st));
+  const u64* hs = mb.host_sizes;
+  u64 n_send = 0, n_recv = 0, b_recv = 0;
+  for (u32 p = 0; p < W; ++p) {
+    n_send += hs[p];
+    n_recv += hs[2 * W + p];
+    b_recv += hs[3 * W + p];
+  }
+  if (n_recv > 0xFFFFFFFFull || b_recv > 0xFFFFFFFFull)
+    return fail(mb, PHIP_ERR_INVALID, "routed batch of %llu messages / %llu name bytes exceeds 2^32",
+                (unsigned long long)n_recv, (unsigned long long)b_recv);
+  GHIP(mb, mb.r_names.ensure(b_recv + 64));
+  GHIP(mb, mb.r_lens.ensure(n_recv * 4 + 4));
+  GHIP(mb, mb.r_offs.ensure(n_recv * 4 + 8));
+  GHIP(mb, mb.r_a.ensure(n_recv * 8 + 8));
+  GHIP(mb, mb.r_t.ensure(n_recv * 8 + 8));
+  GHIP(mb, mb.r_e.ensure(n_recv * 8 + 8));
+  // 3. the segments: one send and one receive per peer and column
+  GNCCL(mb, ncclGroupStart());
+  u64 so = 0, sb = 0, ro = 0, rb = 0;
+  for (u32 p = 0; p < W; ++p) {
+    const u64 sc = hs[p], sbytes = hs[W + p], rc = hs[2 * W + p], rbytes = hs[3 * W + p];
+    GNCCL(mb, ncclSend((u32*)mb.s_lens.p + so, sc, ncclUint32, p, mb.comm, st));
+    GNCCL(mb, ncclRecv((u32*)mb.r_lens.p + ro, rc, ncclUint32, p, mb.comm, st));
+    GNCCL(mb, ncclSend((uint8_t*)mb.s_names.p + sb, sbytes, ncclUint8, p, mb.comm, st));
+    GNCCL(mb, ncclRecv((uint8_t*)mb.r_names.p + rb, rbytes, ncclUint8, p, mb.comm, st));
+    GNCCL(mb, ncclSend((u64*)mb.s_a.p + so, sc, ncclUint64, p, mb.comm, st));
+    GNCCL(mb, ncclRecv((u64*)mb.r_a.p + ro, rc, ncclUint64, p, mb.comm, st));
+    GNCCL(mb, ncclSend((u64*)mb.s_t.p + so, sc, ncclUint64, p, mb.comm, st));
+    GNCCL(mb, ncclRecv((u64*)mb.r_t.p + ro, rc, ncclUint64, p, mb.comm, st));
+    GNCCL(mb, ncclSend((u64*)mb.s_e.p + so, sc, ncclUint64, p, mb.comm, st));
+    GNCCL(mb, ncclRecv((u64*)mb.r_e.p + ro, rc, ncclUint64, p, mb.comm, st));
+    so += sc; sb += sbytes; ro += rc; rb += rbytes;
+  }
+  GNCCL(mb, ncclGroupEnd());
+  if (sent) *sent = n_send;
+  if (merged) *merged = n_recv;
+  if (n_recv == 0) return PHIP_OK;
+  // 4. name offsets of the received blob: an inclusive scan of the lengths
+  u32* offs = (u32*)mb.r_offs.p;
+  GHIP(mb, hipMemsetAsync(offs, 0, sizeof(u32), st));
+  size_t tb = 0;
+  GHIP(mb, rocprim::inclusive_scan(nullptr, tb, (const u32*)mb.r_lens.p, offs + 1, (size_t)n_recv,
+                                   rocprim::plus<u32>(), st));
+  GHIP(mb, mb.scan_tmp.ensure(tb));
+  GHIP(mb, rocprim::inclusive_scan(mb.scan_tmp.p, tb, (const u32*)mb.r_lens.p, offs + 1,
+                                   (size_t)n_recv, rocprim::plus<u32>(), st));
+  // 5. the owner's merge
+  phip_msgs rm{};
+  rm.n = (u32)n_recv;
+  rm.names = (const uint8_t*)mb.r_names.p;
+  rm.name_offs = offs;
+  rm.added = (const uint64_t*)mb.r_a.p;
+  rm.taken = (const uint64_t*)mb.r_t.p;
+  rm.elapsed = (const int64_t*)mb.r_e.p;
+  GPHIP(mb, phip_receive_soa(mb.h, &rm, now, nullptr, PHIP_DEVICE_PTRS));
+  return PHIP_OK;
+}
+
+int member_anti_entropy(phip_group* g, Member& mb, int64_t* reps, uint32_t nrep, uint64_t B) {
+  (void)g;
+  GHIP(mb, hipSetDevice(mb.device));
+  hipStream_t st = (hipStream_t)phip_host::handle_stream(mb.h);
+  GHIP(mb, mb.ae.ensure((size_t)3 * B * 8));
+  int64_t* j = (int64_t*)mb.ae.p;
+  GPHIP(mb, phip_ae_local_max(mb.h, reps, nrep, B, j, PHIP_DEVICE_PTRS));
+  GNCCL(mb, ncclAllReduce(j, j, 3 * B, ncclInt64, ncclMax, mb.comm, st));
+  GPHIP(mb, phip_ae_apply(mb.h, reps, nrep, B, j, PHIP_DEVICE_PTRS));
+  return PHIP_OK;
+}
+
+void destroy(phip_group* g) {
+  for (auto& mb : g->m) {
+    (void)hipSetDevice(mb.device);
+    if (mb.h) (void)phip_flush(mb.h);
+    if (mb.comm) (void)ncclCommDestroy(mb.comm);
+    for (Buf* b : {&mb.s_names, &mb.s_lens, &mb.s_a, &mb.s_t, &mb.s_e, &mb.r_names, &mb.r_lens,
+                   &mb.r_offs, &mb.r_a, &mb.r_t, &mb.r_e, &mb.sizes, &mb.scan_tmp, &mb.ae})
+      b->release();
+    if (mb.host_sizes) (void)hipHostFree(mb.host_sizes);
+    if (mb.own && mb.h) phip_close(mb.h);
+  }
+  delete g;
+}
+
+int alloc_host_sizes(phip_group* g) {
+  for (auto& mb : g->m) {
+    if (hipSetDevice(mb.device) != hipSuccess ||
+        hipHostMalloc(&mb.host_sizes, 4 * (size_t)g->world * sizeof(u64), 0) != hipSuccess)
+      return PHIP_ERR_HIP;
+  }
+  return PHIP_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int phip_group_unique_id(uint8_t* id) {
+  if (!id) return PHIP_ERR_INVALID;
+  ncclUniqueId u;
+  if (ncclGetUniqueId(&u) != ncclSuccess) return PHIP_ERR_RCCL;
+  std::memcpy(id, u.internal, PHIP_GROUP_ID_BYTES);
+  return PHIP_OK;
+}
+
+int phip_group_open_all(const phip_config* cfg, const int32_t* devices, uint32_t n,
+                        phip_group** out) {
+  if (!cfg || !devices || !out || n == 0 || n > 64) return PHIP_ERR_INVALID;
+  *out = nullptr;
+  phip_group* g = new phip_group;
+  g->world = n;
+  g->m.resize(n);
+  std::vector<int> devs(devices, devices + n);
+  for (u32 i = 0; i < n; ++i) {
+    phip_config c = *cfg;
+    c.device = devices[i];
+    g->m[i].device = devices[i];
+    g->m[i].rank = i;
+    g->m[i].own = true;
+    int rc = phip_open(&c, &g->m[i].h);
+    if (rc) {
+      destroy(g);
+      return rc;
+    }
+  }
+  std::vector<ncclComm_t> comms(n);
+  if (ncclCommInitAll(comms.data(), (int)n, devs.data()) != ncclSuccess) {
+    destroy(g);
+    return PHIP_ERR_RCCL;
+  }
+  for (u32 i = 0; i < n; ++i) g->m[i].comm = comms[i];
+  if (int rc = alloc_host_sizes(g)) {
+    destroy(g);
+    return rc;
+  }
+  *out = g;
+  return PHIP_OK;
+}
+
+int phip_group_open_rank(phip_handle* h, const uint8_t* id, uint32_t nranks, uint32_t rank,
+                         phip_group** out) {
+  if (!h || !id || !out || nranks == 0 || nranks > 64 || rank >= nranks) return PHIP_ERR_INVALID;
+  *out = nullptr;
+  phip_group* g = new phip_group;
+  g->world = nranks;
+  g->m.resize(1);
+  Member& mb = g->m[0];
+  mb.h = h;
+  mb.device = phip_host::handle_device(h);
+  mb.rank = rank;
+  ncclUniqueId u;
+  std::memcpy(u.internal, id, PHIP_GROUP_ID_BYTES);
+  if (hipSetDevice(mb.device) != hipSuccess ||
+      ncclCommInitRank(&mb.comm, (int)nranks, u, (int)rank) != ncclSuccess) {
+    mb.comm = nullptr;
+    destroy(g);
+    return PHIP_ERR_RCCL;
+  }
+  if (int rc = alloc_host_sizes(g)) {
+    destroy(g);
+    return rc;
+  }
+  *out = g;
+  return PHIP_OK;
+}
+
+void phip_group_close(phip_group* g) {
+  if (g) destroy(g);
+}
+
+const char* phip_group_last_error(const phip_group* g) { return g ? g->err.c_str() : "null group"; }
+uint32_t phip_group_world(const phip_group* g) { return g ? g->world : 0; }
+uint32_t phip_group_local(const phip_group* g) { return g ? (uint32_t)g->m.size() : 0; }
+phip_handle* phip_group_handle(phip_group* g, uint32_t i) {
+  return (g && i < g->m.size()) ? g->m[i].h : nullptr;
+}
+
+int phip_group_receive(phip_group* g, const phip_msgs* batches, int64_t now, uint64_t* sent,
+                       uint64_t* merged, uint32_t flags) {
+  if (!g || !batches || !(flags & PHIP_DEVICE_PTRS)) return PHIP_ERR_INVALID;
+  return for_members(g, [&](size_t i) {
+    return member_receive(g, g->m[i], batches[i], now, sent ? sent + i : nullptr,
+                          merged ? merged + i : nullptr, flags);
+  });
+}
+
+int phip_group_anti_entropy(phip_group* g, int64_t* const* replicas, uint32_t nrep,
+                            uint64_t nbuckets, uint32_t flags) {
+  if (!g || !replicas || nrep == 0 || !(flags & PHIP_DEVICE_PTRS)) return PHIP_ERR_INVALID;
+  if (nbuckets == 0) return PHIP_OK;
+  return for_members(g, [&](size_t i) {
+    return member_anti_entropy(g, g->m[i], replicas[i], nrep, nbuckets);
+  });
+}
+
+}  // extern "C"

@@ -2,7 +2,14 @@
 #pragma once
 #include <cstdint>
 
+struct phip_handle;
+
 namespace phip_host {
+
+// The stream every call of the handle runs on (its own or phip_set_stream's)
+// and its device: the shard group (phip_group.hip) queues its RCCL calls there.
+void* handle_stream(phip_handle* h);
+int handle_device(const phip_handle* h);
 
 // The request parsing of API.takeBucket (api.go:55-65): the name-length check
 // (returns 400 with ErrNameTooLarge's text as the body), ParseRate with its

@@ -1421,6 +1421,7 @@ struct alignas(16) WinSum {
   u32 flags, pad;
 };
 constexpr u32 kSumTake = 1, kSumMixed = 2, kSumMerge = 4;
+constexpr u32 kSumDirty = 8;   // a merge with a -0.0 replica field (E max != Go's merge)
 
 __device__ inline bool window_quiet(const WinSum& q, const FState& S) {
   if (!S.existed) return false;
@@ -1524,7 +1525,7 @@ __global__ __launch_bounds__(kBlock) void k_gather_huge(
   for (u32 k = 0; k < kGatherPer; ++k) r[k] = load_oprec(ops + (v[k] & kOpIdxMask));
   u64 ea = 0, et = 0, ee = 0, nmin = ~0ull, nmax = 0;
   u32 first_take = 0xFFFFFFFFu;
-  bool merge = false;
+  bool merge = false, dirty = false;
 #pragma unroll
   for (u32 k = 0; k < kGatherPer; ++k) {
     const u32 j = p0 + k * kBlock + tid;
@@ -1540,6 +1541,7 @@ __global__ __launch_bounds__(kBlock) void k_gather_huge(
       first_take = min(first_take, j);
     } else if (kind == PHIP_OP_UPSERT || !state_is_zero(r[k].x, r[k].y, (i64)r[k].z)) {
       merge = true;
+      dirty |= r[k].x == kSign || r[k].y == kSign;
       ea = max(ea, enc_replica(r[k].x)); et = max(et, enc_replica(r[k].y));
       ee = max(ee, r[k].z ^ kSign);
     }
@@ -1562,7 +1564,7 @@ __global__ __launch_bounds__(kBlock) void k_gather_huge(
         mixed |= r[k].x != iv || r[k].y != cp || r[k].z != tb;
     }
   }
-  u64 x[6] = {ea, et, ee, ~nmin, nmax, (u64)(merge ? 1 : 0) | (mixed ? 2 : 0)};
+  u64 x[6] = {ea, et, ee, ~nmin, nmax, (u64)(merge ? 1 : 0) | (mixed ? 2 : 0) | (dirty ? 4 : 0)};
 #pragma unroll
   for (int k = 0; k < 6; ++k)
     for (int off = 32; off >= 1; off >>= 1) {
@@ -1584,18 +1586,36 @@ __global__ __launch_bounds__(kBlock) void k_gather_huge(
     q.cap = ft != 0xFFFFFFFFu ? s_par[1] : 0;
     q.t = ft != 0xFFFFFFFFu ? s_par[2] : 0;
     q.flags = (ft != 0xFFFFFFFFu ? kSumTake : 0) | ((x[5] & 2) ? kSumMixed : 0) |
-              ((x[5] & 1) ? kSumMerge : 0);
+              ((x[5] & 1) ? kSumMerge : 0) | ((x[5] & 4) ? kSumDirty : 0);
     q.pad = 0;
     sums[woff[h] + w] = q;
   }
 }
 
 // The hot-bucket fold records the bucket's state history as runs instead of
-// per-op results: run k says "ops [pos_k, pos_{k+1}) of the segment all saw
-// state state_k".  k_huge_outputs then evaluates every op against its run's
-// state on the whole chip and writes the results, so the one workgroup on
-// the sequential critical path only streams ops and tests "does this op
-// change the state?".
+// per-op results: run k says "ops [pos_k, pos_{k+1}) of the segment saw state
+// state_k, raised by the merges between" (below).  k_huge_outputs then
+// evaluates every op against its state on the whole chip and writes the
+// results, so the one workgroup on the sequential critical path only streams
+// ops and tests "does this op change the state?".
+//
+// Absorbing merges.  A hot bucket receives replica states all the time, and
+// many raise it a little (replica `elapsed` values run close behind the local
+// clock), while most of its Takes are denied (it is rate limited).  Treating
+// every such merge as a sequential state change made the fold of a realistic
+// stream 20x slower than its quiet-window fast path.  Instead, while the
+// bucket's state only grows (E order, every field), the state an op sees is
+//     X_k = max(R, G_k)
+// with R the state after the last change that was not a merge (a successful
+// Take) and G_k the running maximum of the replica states merged before op k
+// (E' codes, phip_device.hpp): R already holds every merge before it, and a
+// merge is the E max for replicas without -0.0 fields (kSumDirty).  A window
+// whose Takes are all provably denied for every X_k between its first and last
+// op (window_absorbable) then changes nothing but G, and needs no run.  If a
+// change ever lowers a field (a Take whose refill is negative because tokens
+// exceed capacity, a -0.0 replica) the identity fails from there on: the
+// segment turns "exact" at that run (exact_from) and every later change,
+// merges included, is a run of its own (window_quiet, the strict test).
 struct RunState {
   u64 a, t;   // float64 bits
   i64 e, c;
@@ -1606,11 +1626,61 @@ __device__ inline void put_run(u32* run_pos, RunState* run_st, u32 k, u32 pos, c
   run_st[k] = RunState{as_bits(S.a), as_bits(S.t), S.e, S.c};
 }
 
+// Maxima of merged replica states: E' codes of added and taken (enc_replica)
+// and elapsed biased by 2^63, 0 = none.
+struct alignas(32) GMax {
+  u64 a, t, e, pad;
+};
+__device__ inline GMax gmax(const GMax& x, const GMax& y) {
+  return GMax{x.a > y.a ? x.a : y.a, x.t > y.t ? x.t : y.t, x.e > y.e ? x.e : y.e, 0};
+}
+__device__ inline GMax gmax_of(const WinSum& q) { return GMax{q.ea, q.et, q.ee, 0}; }
+
+// X = max(R, G) in E order, field by field.
+__device__ inline FState join_state(const FState& R, const GMax& g) {
+  FState X = R;
+  if (g.a > enc_f64(as_bits(R.a))) X.a = as_f64(dec_f64(g.a));
+  if (g.t > enc_f64(as_bits(R.t))) X.t = as_f64(dec_f64(g.t));
+  if (g.e > ((u64)R.e ^ kSign)) X.e = (i64)(g.e ^ kSign);
+  return X;
+}
+
+// A change from S to S2 that keeps X_k = max(R, G_k) exact afterwards: no
+// field is lowered in E order.
+__device__ inline bool state_grew(const FState& S, const FState& S2) {
+  return enc_f64(as_bits(S2.a)) >= enc_f64(as_bits(S.a)) &&
+         enc_f64(as_bits(S2.t)) >= enc_f64(as_bits(S.t)) && S2.e >= S.e;
+}
+
+// Window q, whose ops see states between Xs (at its start) and Xe (Xs raised
+// by the window's merge maxima): true when no Take of the window can succeed
+// (then no op changes anything but G).  For every op the state lies between
+// the two ends field by field, and with a shared (interval > 0, capacity, t)
+// Take's `have` (bucket.go:198-216) is bounded by
+//     (Xe.added - Xs.taken) + take_dt(created, Xs.elapsed, max now) / interval,
+// every step being a correctly rounded monotone operation (a refill capped at
+// `missing` is below the uncapped one, and + is monotone).  t > bound then
+// means every Take of the window is denied; added > 0 at the start (it only
+// grows) rules out the added = capacity write of bucket.go:194-196.
+__device__ inline bool window_absorbable(const WinSum& q, const FState& Xs, const FState& Xe) {
+  if (!Xs.existed || (q.flags & kSumDirty)) return false;
+  if (!(q.flags & kSumTake)) return true;
+  if (q.flags & kSumMixed) return false;
+  const i64 iv = (i64)q.interval;
+  if (iv <= 0) return false;
+  if (!(Xs.a > 0.0) || !(Xe.a < __builtin_inf()) || !(Xs.t > -__builtin_inf()) ||
+      !(Xs.t < __builtin_inf()))
+    return false;
+  const double tok = Xe.a - Xs.t;
+  const double add = (double)take_dt(Xs.c, Xs.e, q.now_max) / (double)iv;
+  return as_f64(q.t) > tok + add;
+}
+
 // One workgroup folds one very long segment (a Zipf-hot bucket) from the
-// contiguous copy k_gather_huge made.  Thread t owns ops k*kFoldThreads + t
-// (k < kFoldPer) of each window of kFoldWin ops; two windows are held in
-// registers (buffers A and B, the loop unrolled by two so the loads of the
-// window after next are in flight while one is folded).  Per window:
+// contiguous copy k_gather_huge made.  Windows are tested kSumChunk at a time
+// from their summaries (absorbable, or quiet once the segment is exact), and
+// only a window that may change the state is folded: thread t owns ops
+// k*kFoldThreads + t (k < kFoldPer) of it, and
 //  * parallel round: every thread tests its unretired ops against the
 //    current state; a workgroup min finds the first op that changes it; the
 //    ops before it are retired (they saw the current state);
@@ -1619,8 +1689,7 @@ __device__ inline void put_run(u32* run_pos, RunState* run_st, u32 k, u32 pos, c
 //    a run at every change, until kBurstQuiet ops in a row leave the state
 //    unchanged.  Changes cluster (a merge that raises `added` is followed by a
 //    run of successful Takes) and a round costs far more than one op, so a
-//    cluster costs about one round plus its ops at sequential speed, and the
-//    long unchanged stretches between clusters cost one round per window.
+//    cluster costs about one round plus its ops at sequential speed.
 
 struct FoldWin {
   u32 v[kFoldPer];
@@ -1633,10 +1702,12 @@ struct FoldShared {
   OpRec op[kFoldWin];
   u32 val[kFoldWin];
   WinSum sum[kSumChunk];
+  GMax pinc[kSumChunk];                   // inclusive merge-maxima prefix over the chunk
+  GMax wtot[kFoldThreads / 64];
   u32 wave_min[2][kFoldThreads / 64];
   u32 quiet_min[kFoldThreads / 64];
   u64 state[4];
-  u32 cur, nrun;
+  u32 cur, nrun, exact_from;
 };
 
 // Loads are unconditional (index clamped into the segment): a load under a
@@ -1694,10 +1765,12 @@ __device__ inline void fold_window(const FoldWin& W, u32 pos, u32 lim, FState& S
     // ---- sequential burst (wave 0) from `first`, which changes the state
     if (wv == 0) {
       FState T = S;
-      u32 j = first, quiet = 0, nrun = sh.nrun;
+      u32 j = first, quiet = 0, nrun = sh.nrun, exact_from = sh.exact_from;
       while (j < lim && quiet < kBurstQuiet) {
         FState T2;
         if (apply_sop(make_sop(sh.op[j], sh.val[j]), T, T2)) {
+          // a change that lowers a field ends the absorbing identity
+          if (exact_from == 0xFFFFFFFFu && !state_grew(T, T2)) exact_from = nrun;
           T = T2;
           if (lane == 0) put_run(rp, rs, nrun, pos + j + 1, T);
           ++nrun;
@@ -1712,6 +1785,7 @@ __device__ inline void fold_window(const FoldWin& W, u32 pos, u32 lim, FState& S
         sh.state[2] = (u64)T.e; sh.state[3] = (u64)T.c;
         sh.cur = j;
         sh.nrun = nrun;
+        sh.exact_from = exact_from;
       }
     }
     __syncthreads();
@@ -1722,6 +1796,27 @@ __device__ inline void fold_window(const FoldWin& W, u32 pos, u32 lim, FState& S
   }
 }
 
+__device__ inline u64 shfl_up_u64(u64 v, u32 d) {
+  const u32 lo = __shfl_up((u32)v, d), hi = __shfl_up((u32)(v >> 32), d);
+  return ((u64)hi << 32) | lo;
+}
+
+// Inclusive prefix max of x over the workgroup (kFoldThreads lanes, thread
+// order) into sh.pinc[tid].
+__device__ inline void block_prefix_gmax(GMax x, FoldShared& sh, u32 tid) {
+  const u32 lane = tid & 63, wv = tid >> 6;
+#pragma unroll
+  for (u32 d = 1; d < 64; d <<= 1) {
+    const GMax y{shfl_up_u64(x.a, d), shfl_up_u64(x.t, d), shfl_up_u64(x.e, d), 0};
+    if (lane >= d) x = gmax(x, y);
+  }
+  if (lane == 63) sh.wtot[wv] = x;
+  __syncthreads();
+  for (u32 y = 0; y < wv; ++y) x = gmax(x, sh.wtot[y]);
+  sh.pinc[tid] = x;
+  __syncthreads();
+}
+
 // Ablation variants (tools only, PHIP_FOLD_VARIANT): 1 = no state test
 // (every op unchanged: streaming cost alone).
 template <int V = 0>
@@ -1730,8 +1825,9 @@ __global__ __launch_bounds__(kFoldThreads) void k_fold_block(
     const u64* __restrict__ hoff, const u32* __restrict__ seg_count,
     const u32* __restrict__ hval, const OpRec* __restrict__ hop, Rec* recs,
     u32* __restrict__ run_pos, RunState* __restrict__ run_st, u32* __restrict__ run_n,
-    u8* __restrict__ seg_existed, const u64* __restrict__ woff, const WinSum* __restrict__ sums,
-    u32* __restrict__ win_run) {
+    u8* __restrict__ seg_existed, u32* __restrict__ seg_exact_from,
+    const u64* __restrict__ woff, const WinSum* __restrict__ sums, u32* __restrict__ win_run,
+    GMax* __restrict__ win_g) {
   __shared__ FoldShared sh;
   if (blockIdx.x >= nhuge) return;
   const u32 g = huge_list[blockIdx.x];
@@ -1745,22 +1841,26 @@ __global__ __launch_bounds__(kFoldThreads) void k_fold_block(
   u32* rp = run_pos + base + blockIdx.x;
   RunState* rs = run_st + base + blockIdx.x;
 
-  FState S = load_state(load_rec(r));
+  FState R = load_state(load_rec(r));   // run state (see the module comment)
+  GMax G{0, 0, 0, 0};                   // merges absorbed so far
   if (tid == 0) {
-    put_run(rp, rs, 0, 0, S);
-    seg_existed[blockIdx.x] = S.existed;
+    put_run(rp, rs, 0, 0, R);
+    seg_existed[blockIdx.x] = R.existed;
     sh.nrun = 1;
+    sh.exact_from = 0xFFFFFFFFu;
   }
+  __syncthreads();
   const u32 nwin = (cnt + kFoldWin - 1) / kFoldWin;
   const WinSum* __restrict__ ws = sums + woff[blockIdx.x];
   u32* __restrict__ wr = win_run + woff[blockIdx.x];
+  GMax* __restrict__ wg = win_g + woff[blockIdx.x];
   u32 round = 0;
   FoldWin A;
-  // Quiet windows are found kSumChunk at a time: every thread tests one
-  // window's summary against the current state and a workgroup min picks
-  // the first window that may change it.  The windows before it keep the
-  // state, so a long rate-limited stretch costs one test per thread instead
-  // of one sequential test per window; only the found window is folded.
+  // Windows are tested kSumChunk at a time: every thread tests one window's
+  // summary (with the merge maxima of the windows before it in the chunk)
+  // and a workgroup min picks the first window that may change the state.
+  // The windows before it change nothing but G, so a long rate-limited
+  // stretch costs one test per thread; only the found window is folded.
   u32 staged = 0xFFFFFFFFu;
   for (u32 w = 0; w < nwin;) {
     const u32 cb = w - w % kSumChunk;
@@ -1772,7 +1872,17 @@ __global__ __launch_bounds__(kFoldThreads) void k_fold_block(
     }
     const u32 lim = min(cb + kSumChunk, nwin);
     const u32 mine = cb + tid;
-    u32 m = (mine >= w && mine < lim && !window_quiet(sh.sum[tid], S)) ? mine : 0xFFFFFFFFu;
+    const bool in = mine >= w && mine < lim;
+    const bool exact = sh.exact_from != 0xFFFFFFFFu;
+    block_prefix_gmax(in ? gmax_of(sh.sum[tid]) : GMax{0, 0, 0, 0}, sh, tid);
+    const GMax gs = gmax(G, (in && mine > w) ? sh.pinc[tid - 1] : GMax{0, 0, 0, 0});
+    bool quiet = false;
+    if (in) {
+      if (exact) quiet = window_quiet(sh.sum[tid], R);
+      else quiet = window_absorbable(sh.sum[tid], join_state(R, gs),
+                                     join_state(R, gmax(G, sh.pinc[tid])));
+    }
+    u32 m = (in && !quiet) ? mine : 0xFFFFFFFFu;
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) m = min(m, (u32)__shfl_xor((int)m, off));
     if ((tid & 63) == 0) sh.quiet_min[tid >> 6] = m;
@@ -1781,36 +1891,78 @@ __global__ __launch_bounds__(kFoldThreads) void k_fold_block(
 #pragma unroll
     for (u32 x = 0; x < kFoldThreads / 64; ++x) first = min(first, sh.quiet_min[x]);
     const u32 stop = first == 0xFFFFFFFFu ? lim : first;
-    const u32 run_now = sh.nrun - 1;   // run in effect at each quiet window's first op
-    for (u32 x = w + tid; x < stop; x += kFoldThreads) wr[x] = run_now;
-    __syncthreads();   // quiet_min and nrun are rewritten below
+    const u32 run_now = sh.nrun - 1;   // run in effect at each such window's first op
+    if (in && mine <= stop && mine < lim) {
+      wr[mine] = run_now;
+      wg[mine] = gs;
+    }
+    // G after the windows before `stop` (their merges are absorbed)
+    if (stop > w) G = gmax(G, sh.pinc[stop - 1 - cb]);
+    __syncthreads();   // quiet_min, pinc and nrun are rewritten below
     if (first == 0xFFFFFFFFu) {
       w = lim;
       continue;
     }
-    if (tid == 0) wr[first] = run_now;
     const u32 pos = first * kFoldWin;
+    FState X = exact ? R : join_state(R, G);
+    if (!exact && (sh.sum[first - cb].flags & kSumDirty)) {
+      // A -0.0 replica: Go's merge is not the E max for it, so the segment is
+      // exact from here on, starting with a run that holds the true state.
+      // Nothing absorbed yet (G empty): the current run is already exact
+      // (and may be the bucket's not-yet-created initial state, which a new
+      // run could not express).
+      if (tid == 0) {
+        if (G.a | G.t | G.e) {
+          put_run(rp, rs, sh.nrun, pos, X);
+          sh.exact_from = sh.nrun;
+          ++sh.nrun;
+        } else {
+          sh.exact_from = sh.nrun - 1;
+        }
+      }
+      __syncthreads();
+    }
     fold_load(A, sv, so, pos, last, tid);
-    fold_window<V>(A, pos, min(kFoldWin, cnt - pos), S, round, sh, rp, rs, tid);
+    fold_window<V>(A, pos, min(kFoldWin, cnt - pos), X, round, sh, rp, rs, tid);
+    // the window's ops are applied exactly: X is the state after it, and it
+    // holds the window's merges
+    R = X;
+    G = gmax(G, gmax_of(sh.sum[first - cb]));
     w = first + 1;
   }
   if (tid == 0) {
-    store_state(r, S);
+    store_state(r, join_state(R, sh.exact_from == 0xFFFFFFFFu ? G : GMax{0, 0, 0, 0}));
     run_n[blockIdx.x] = sh.nrun;
+    seg_exact_from[blockIdx.x] = sh.exact_from;
   }
 }
 
 // Results of every op of the huge segments: op j of segment h saw the state
-// of the last run of h starting at or before j.  One block per fold window;
-// the fold recorded the run in effect at each window start, so the search
-// only spans the runs that begin inside the window (usually none).
+// of the last run of h starting at or before j, raised by the merges before
+// j (G: the window's starting maximum k_fold_block recorded, then a prefix
+// max over the window) unless that run is exact.  One block per fold
+// window; each thread takes kFoldWin / kBlock consecutive ops, so the
+// in-window prefix is a thread-local scan plus a workgroup scan of thread
+// totals.  The fold recorded the run in effect at each window start, so the
+// run search only spans the runs that begin inside the window (usually none).
+constexpr u32 kOutPer = kFoldWin / kBlock;
+
+__device__ inline GMax merge_contrib(const OpRec& r, u32 v) {
+  const u32 kind = v >> kOpIdxBits;
+  if (kind == PHIP_OP_TAKE || (kind == PHIP_OP_RECEIVE && state_is_zero(r.x, r.y, (i64)r.z)))
+    return GMax{0, 0, 0, 0};
+  return GMax{enc_replica(r.x), enc_replica(r.y), r.z ^ kSign, 0};
+}
+
 __global__ __launch_bounds__(kBlock) void k_huge_outputs(
     const u32* __restrict__ huge_list, u32 nhuge, const u64* __restrict__ hoff,
     const u64* __restrict__ woff, const u32* __restrict__ seg_count,
     const u32* __restrict__ hval, const OpRec* __restrict__ hop,
     const u32* __restrict__ run_pos, const RunState* __restrict__ run_st,
     const u32* __restrict__ run_n, const u8* __restrict__ seg_existed,
-    const u32* __restrict__ win_run, OutView ow) {
+    const u32* __restrict__ seg_exact_from, const u32* __restrict__ win_run,
+    const GMax* __restrict__ win_g, OutView ow) {
+  __shared__ GMax wtot[kBlock / 64];
   u32 h, w;
   if (!huge_window(woff, nhuge, blockIdx.x, h, w)) return;
   const u32 cnt = seg_count[huge_list[h]];
@@ -1821,9 +1973,39 @@ __global__ __launch_bounds__(kBlock) void k_huge_outputs(
   const u32 k0 = win_run[woff[h] + w];
   const u32 k1 = w + 1 < nwin ? win_run[woff[h] + w + 1] : run_n[h] - 1;
   const bool existed0 = seg_existed[h];
+  const u32 exact_from = seg_exact_from[h];
+  const GMax g0 = win_g[woff[h] + w];
   const u32 p0 = w * kFoldWin, p1 = min(cnt, p0 + kFoldWin);
-  for (u32 j = p0 + threadIdx.x; j < p1; j += kBlock) {
-    u32 lo = k0, hi = k1;   // last k in [k0, k1] with rp[k] <= j
+  const u32 tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const u32 j0 = p0 + tid * kOutPer;
+  OpRec op[kOutPer];
+  u32 val[kOutPer];
+  GMax tot{0, 0, 0, 0};
+#pragma unroll
+  for (u32 k = 0; k < kOutPer; ++k) {
+    const u32 j = min(j0 + k, p1 - 1);
+    op[k] = load_oprec(hop + base + j);
+    val[k] = hval[base + j];
+    if (j0 + k < p1) tot = gmax(tot, merge_contrib(op[k], val[k]));
+  }
+  // exclusive prefix of the thread totals over the workgroup
+  GMax inc = tot;
+#pragma unroll
+  for (u32 d = 1; d < 64; d <<= 1) {
+    const GMax y{shfl_up_u64(inc.a, d), shfl_up_u64(inc.t, d), shfl_up_u64(inc.e, d), 0};
+    if (lane >= d) inc = gmax(inc, y);
+  }
+  if (lane == 63) wtot[wv] = inc;
+  GMax exc{shfl_up_u64(inc.a, 1), shfl_up_u64(inc.t, 1), shfl_up_u64(inc.e, 1), 0};
+  if (lane == 0) exc = GMax{0, 0, 0, 0};
+  __syncthreads();
+  for (u32 y = 0; y < wv; ++y) exc = gmax(exc, wtot[y]);
+  GMax gj = gmax(g0, exc);
+#pragma unroll
+  for (u32 k = 0; k < kOutPer; ++k) {
+    const u32 j = j0 + k;
+    if (j >= p1) break;
+    u32 lo = k0, hi = k1;   // last run in [k0, k1] with rp[run] <= j
     while (lo < hi) {
       const u32 mid = (lo + hi + 1) >> 1;
       if (rp[mid] <= j) lo = mid; else hi = mid - 1;
@@ -1832,11 +2014,13 @@ __global__ __launch_bounds__(kBlock) void k_huge_outputs(
     FState S;
     S.a = as_f64(q.a); S.t = as_f64(q.t); S.e = q.e; S.c = q.c;
     S.existed = lo > 0 || existed0;
-    const SOp op = make_sop(load_oprec(hop + base + j), hval[base + j]);
+    if (lo < exact_from) S = join_state(S, gj);
+    const SOp sop = make_sop(op[k], val[k]);
     FState S2;
     OpOut o;
-    eval_sop(op, S, S2, o);
-    write_out(ow, op.idx, o, S);
+    eval_sop(sop, S, S2, o);
+    write_out(ow, sop.idx, o, S);
+    gj = gmax(gj, merge_contrib(op[k], val[k]));
   }
 }
 

@@ -92,12 +92,20 @@ class GPURepo:
             raise PatrolHipError(rc, "phip_open failed")
         self.h = h
         self.device = device
+        self.owned = True
+
+    @classmethod
+    def wrap(cls, handle, device: int):
+        """A GPURepo over a handle someone else owns (a GPUGroup member)."""
+        r = cls.__new__(cls)
+        r.L, r.h, r.device, r.owned = _lib.load(), C.c_void_p(handle), device, False
+        return r
 
     # ------------------------------------------------------------ basics --
     def close(self):
-        if getattr(self, "h", None):
+        if getattr(self, "h", None) and getattr(self, "owned", True):
             self.L.phip_close(self.h)
-            self.h = None
+        self.h = None
 
     def __del__(self):
         try:
@@ -366,6 +374,143 @@ class GPURepo:
         code = self._check(self.L.phip_api_take(self.h, name, len(name), rate, len(rate), count,
                                                 len(count), int(now), body, C.byref(bl)))
         return code, body.raw[:bl.value].decode()
+
+
+class GPUGroup:
+    """A shard group over RCCL (phip_group_*, include/patrolhip.h): the
+    buckets hash-sharded by name over several GPUs, owner-routed Receive and
+    anti-entropy in the C library (no torch on the data path).
+
+    open_all(devices): one process, every listed GPU (ncclCommInitAll);
+    open_rank(repo, uid, nranks, rank): one process per GPU around `repo`
+    (ncclCommInitRank), `uid` from unique_id() on rank 0."""
+
+    def __init__(self, g, L, repos):
+        self.g, self.L, self.repos = g, L, repos
+
+    @staticmethod
+    def unique_id() -> bytes:
+        L = _lib.load()
+        buf = C.create_string_buffer(_lib.GROUP_ID_BYTES)
+        rc = L.phip_group_unique_id(buf)
+        if rc != 0:
+            raise PatrolHipError(rc, "phip_group_unique_id failed")
+        return buf.raw
+
+    @classmethod
+    def open_all(cls, devices, log2_slots: int = 20, arena_bytes: int = 1 << 24,
+                 max_load_pct: int = 90):
+        L = _lib.load()
+        cfg = phip_config(0, log2_slots, arena_bytes, max_load_pct, 0, 0, 0)
+        devs = (C.c_int32 * len(devices))(*devices)
+        g = C.c_void_p()
+        rc = L.phip_group_open_all(C.byref(cfg), devs, len(devices), C.byref(g))
+        if rc != 0:
+            raise PatrolHipError(rc, "phip_group_open_all failed")
+        repos = [GPURepo.wrap(L.phip_group_handle(g, i), devices[i]) for i in range(len(devices))]
+        return cls(g, L, repos)
+
+    @classmethod
+    def open_rank(cls, repo: "GPURepo", uid: bytes, nranks: int, rank: int):
+        L = repo.L
+        g = C.c_void_p()
+        rc = L.phip_group_open_rank(repo.h, uid, nranks, rank, C.byref(g))
+        if rc != 0:
+            raise PatrolHipError(rc, "phip_group_open_rank failed")
+        return cls(g, L, [repo])
+
+    @property
+    def world(self) -> int:
+        return int(self.L.phip_group_world(self.g))
+
+    def _check(self, rc):
+        if rc != 0:
+            raise PatrolHipError(rc, self.L.phip_group_last_error(self.g).decode(errors="replace"))
+
+    def receive(self, batches, now: int, combine: bool = True):
+        """batches: one (names uint8, name_offs int32[n+1], added, taken, elapsed)
+        tuple of CUDA tensors per local member -> (sent, merged) lists."""
+        k = len(batches)
+        msgs = (phip_msgs * k)()
+        for i, (names, offs, a, t, e) in enumerate(batches):
+            msgs[i] = phip_msgs(offs.numel() - 1, 0, _ptr(names), _ptr(offs), _ptr(a), _ptr(t),
+                                _ptr(e))
+        sent, merged = (C.c_uint64 * k)(), (C.c_uint64 * k)()
+        self._check(self.L.phip_group_receive(self.g, msgs, int(now), sent, merged,
+                                              DEVICE_PTRS | (_lib.ROUTE_COMBINE if combine else 0)))
+        return [int(x) for x in sent], [int(x) for x in merged]
+
+    def anti_entropy(self, replicas):
+        """replicas: one contiguous int64 CUDA tensor [R, 3, B] per local member."""
+        R, three, B = replicas[0].shape
+        ptrs = (C.c_void_p * len(replicas))(*[x.data_ptr() for x in replicas])
+        self._check(self.L.phip_group_anti_entropy(self.g, ptrs, R, B, DEVICE_PTRS))
+
+    def close(self):
+        if getattr(self, "g", None):
+            for r in self.repos:
+                if not r.owned:
+                    r.h = None
+            self.L.phip_group_close(self.g)
+            self.g = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class TakeBatcher:
+    """Request-coalescing Take batcher over a GPURepo (phip_batcher_*,
+    include/patrolhip.h): the drop-in form of the POST /take handler
+    (api.go:51-86) for one-request-per-thread callers.  take()/api_take()
+    block until the request's batch ran; they release the GIL (ctypes), so
+    many Python threads can wait at once."""
+
+    def __init__(self, repo: "GPURepo", window_us: int = 20, max_batch: int = 0):
+        self.repo, self.L = repo, repo.L
+        b = C.c_void_p()
+        cfg = _lib.phip_batcher_config(window_us, max_batch)
+        repo._check(self.L.phip_batcher_open(repo.h, C.byref(cfg), C.byref(b)))
+        self.b = b
+
+    def close(self):
+        if getattr(self, "b", None):
+            self.L.phip_batcher_close(self.b)
+            self.b = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def take(self, name: bytes, now: int, freq: int, per: int, count: int):
+        """-> (remaining, ok, arrival seq)."""
+        rem, ok, seq = C.c_uint64(), C.c_uint8(), C.c_uint64()
+        rc = self.L.phip_batcher_take(self.b, name, len(name), int(now), int(freq), int(per),
+                                      int(count), C.byref(rem), C.byref(ok), C.byref(seq))
+        if rc != 0:
+            raise PatrolHipError(rc, "phip_batcher_take failed")
+        return rem.value, bool(ok.value), seq.value
+
+    def api_take(self, name: bytes, rate: bytes, count: bytes, now: int):
+        """API.takeBucket through the batcher: (HTTP status, body)."""
+        body = C.create_string_buffer(64)
+        bl = C.c_uint32()
+        code = self.L.phip_batcher_api_take(self.b, name, len(name), rate, len(rate), count,
+                                            len(count), int(now), body, C.byref(bl))
+        if code < 0:
+            raise PatrolHipError(code, "phip_batcher_api_take failed")
+        return code, body.raw[:bl.value].decode()
+
+    def stats(self):
+        """dict(batches, requests, max_batch, gpu_ns, errors)."""
+        out = (C.c_uint64 * 5)()
+        k = self.L.phip_batcher_stats(self.b, out, 5)
+        keys = ("batches", "requests", "max_batch", "gpu_ns", "errors")
+        return {keys[i]: int(out[i]) for i in range(k)}
 
 
 class Ring:

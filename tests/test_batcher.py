@@ -1,0 +1,101 @@
+"""The request-coalescing Take batcher (phip_batcher_*)
+against the oracle: many threads submit Takes concurrently; every request's
+(remaining, ok) equals the Go reference running the same requests one by one
+in the batcher's arrival order (api.go:67-74, bucket.go:186-225), and the
+HTTP handler form reproduces the reference's API table (api_test.go:34-73).
+"""
+import json
+import os
+import threading
+import time
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+from oracle import oracle as O  # noqa: E402
+from tests import _gen  # noqa: E402
+
+SEC = 10**9
+
+
+@pytest.fixture(scope="module")
+def pa():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import patrol_amd
+    return patrol_amd
+
+
+@pytest.mark.parametrize("window_us", [0, 50])
+def test_batcher_threads_vs_oracle_in_arrival_order(pa, window_us):
+    threads, per_thread, K = 48, 150, 120
+    repo = pa.GPURepo(log2_slots=12)
+    b = pa.TakeBatcher(repo, window_us=window_us)
+    rng = np.random.default_rng(window_us)
+    plan = []
+    for tid in range(threads):
+        ids = _gen.zipf_ids(rng, per_thread, K)
+        freq = rng.choice(np.array([100, 100, 100, 5, 3, 0], np.int64), per_thread)
+        per = rng.choice(np.array([SEC, SEC, 60 * SEC, 1], np.int64), per_thread)
+        cnt = rng.integers(1, 4, per_thread).astype(np.uint64)
+        now = _gen.T0 + np.sort(rng.integers(0, 5 * SEC, per_thread))
+        plan.append([(b"b%d" % ids[k], int(now[k]), int(freq[k]), int(per[k]), int(cnt[k]))
+                     for k in range(per_thread)])
+    results = [[] for _ in range(threads)]
+    lat = [[] for _ in range(threads)]
+    start = threading.Barrier(threads)
+
+    def worker(tid):
+        start.wait()
+        for req in plan[tid]:
+            t0 = time.perf_counter()
+            rem, ok, seq = b.take(*req)
+            lat[tid].append(time.perf_counter() - t0)
+            results[tid].append((seq, req, rem, ok))
+
+    ts = [threading.Thread(target=worker, args=(t,)) for t in range(threads)]
+    t0 = time.perf_counter()
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    wall = time.perf_counter() - t0
+    st = b.stats()
+    b.close()
+    allr = sorted(r for rs in results for r in rs)
+    n = threads * per_thread
+    assert [r[0] for r in allr] == list(range(n))          # every arrival number once
+    assert st["requests"] == n and st["errors"] == 0
+    assert st["batches"] < n // 4                           # requests were coalesced
+    names = [r[1][0] for r in allr]
+    o = O.Repo()
+    ref = o.apply_mixed(np.zeros(n, np.uint8), names, [r[1][1] for r in allr],
+                        [r[1][2] for r in allr], [r[1][3] for r in allr], [r[1][4] for r in allr],
+                        np.zeros(n, np.uint64), np.zeros(n, np.uint64), np.zeros(n, np.int64))
+    assert [r[2] for r in allr] == [int(x) for x in ref["remaining"]]
+    assert [r[3] for r in allr] == [bool(s & 0x7F == 6) for s in ref["status"]]
+    assert {k: (v.added, v.taken, v.elapsed, v.created) for k, v in repo.dump().items()} == o.dump()
+    ls = np.array([x for l in lat for x in l]) * 1e6
+    print(json.dumps({"window_us": window_us, "threads": threads, "requests": n,
+                      "takes_per_s": n / wall, "p50_us": float(np.percentile(ls, 50)),
+                      "p99_us": float(np.percentile(ls, 99)), "batches": st["batches"],
+                      "max_batch": st["max_batch"]}))
+    repo.close()
+
+
+def test_batcher_api_take_reference_table(pa):
+    """api_test.go:34-73 through the batcher's handler form."""
+    with open(os.path.join(os.path.dirname(__file__), "golden", "api_table.json")) as f:
+        g = json.load(f)
+    repo = pa.GPURepo(log2_slots=10)
+    sb = g["seed_bucket"]
+    repo.seed([sb["name"].encode()], [0], [0], [0], [sb["created"]])
+    b = pa.TakeBatcher(repo, window_us=10)
+    for r in g["requests"]:
+        assert b.api_take(r["name"].encode(), r["rate"].encode(), r["count"].encode(), r["now"]) == \
+               (r["code"], r["body"]), r
+    b.close()
+    repo.close()

@@ -406,6 +406,60 @@ def test_hot_bucket_quiet_window_skips(pa, freq, per):
     _check_mixed(pa, [kind, names, now, fr, pe, cnt, a, t, e], 10, reply=True)
 
 
+@pytest.mark.parametrize("variant", ["below", "over_capacity", "negzero", "rates", "seeded"])
+def test_hot_bucket_absorbing_merges(pa, variant):
+    """k_fold_block absorbs merges into the running replica maximum when a
+    window's Takes are provably denied (window_absorbable): the C3 shape with
+    replica `elapsed` below the local clock, so merges raise the hot buckets
+    all the time while Takes refill now and then.  Variants that break the
+    max(R, G) identity must switch the segment to exact runs: replicas whose
+    tokens exceed capacity (negative refill lowers `added`), -0.0 replica
+    fields, and windows of mixed rates; 'seeded' starts from existing
+    buckets.  Three buckets of ~45k ops each plus a cold tail."""
+    rng = np.random.default_rng({"below": 1, "over_capacity": 2, "negzero": 3, "rates": 4,
+                                 "seeded": 5}[variant])
+    n = 150000
+    ids = np.where(rng.random(n) < 0.9, rng.integers(0, 3, n), rng.integers(3, 3000, n))
+    names = [b"hot%d" % i if i < 3 else b"b%d" % i for i in ids]
+    kind = (rng.random(n) < 0.5).astype(np.uint8)
+    now = _gen.T0 + np.arange(n, dtype=np.int64) * 20_000
+    fr = np.full(n, 100, np.int64)
+    pe = np.full(n, SEC, np.int64)
+    cnt = np.ones(n, np.uint64)
+    taken = rng.integers(0, 10**4, n).astype(np.float64)
+    added = taken + rng.random(n) * 100
+    if variant == "over_capacity":
+        sel = rng.random(n) < 0.001
+        added[sel] = taken[sel] + 150.0
+    a, t = added.view(np.uint64).copy(), taken.view(np.uint64).copy()
+    e = (rng.random(n) * (now - _gen.T0)).astype(np.int64)
+    if variant == "negzero":
+        sel = (rng.random(n) < 0.0005) & (kind == 1)
+        t[sel] = np.uint64(0x8000000000000000)
+    if variant == "rates":
+        sel = rng.random(n) < 0.002
+        fr[sel] = 7
+        cnt[rng.random(n) < 0.002] = 2
+    args = [kind, names, now, fr, pe, cnt, a, t, e]
+    if variant != "seeded":
+        _check_mixed(pa, args, 12, reply=False)
+        return
+    g = pa.GPURepo(log2_slots=12)
+    o = O.Repo()
+    seed = [b"hot0", b"hot1", b"hot2"]
+    sa = np.array([50.0, 0.0, 1e4 + 99.5]).view(np.uint64)
+    st = np.array([10.0, 0.0, 1e4]).view(np.uint64)
+    for r in (g, o):
+        r.seed(seed, sa, st, [0, 0, 0], [_gen.T0 - SEC] * 3)
+    out = g.apply_mixed(*args)
+    ref = o.apply_mixed(*args)
+    assert np.array_equal(out["status"], ref["status"])
+    assert np.array_equal(out["remaining"], ref["remaining"])
+    take = kind == 0
+    assert np.array_equal(out["have"][take], ref["have"][take])
+    assert_same_dump(gpu_dump(g), o.dump())
+
+
 def test_tag_collisions_names_always_compared(pa):
     """With the probe tag cut to 3 bits nearly every lookup meets other names
     with an equal tag: results must still be exact."""
@@ -549,7 +603,7 @@ def test_table_grows_vs_oracle(pa, tag_bits):
     g.seed(sn, sa, stt, se, sc)
     o.seed(sn, sa, stt, se, sc)
     assert len(g) == len(o) > 50_000
-    assert g.capacity >= 1 << 17 and g.last_stats()[3] >= 5
+    assert g.capacity * 9 // 10 >= len(g) and g.capacity >= 1 << 16 and g.last_stats()[3] >= 2
     assert_same_dump(gpu_dump(g), o.dump())
     g.close()
 
@@ -753,7 +807,8 @@ def test_snapshot_restore_round_trip(pa, tmp_path):
     r = pa.GPURepo(log2_slots=14)
     r.restore(path)
     assert len(r) == len(g)
-    assert gpu_dump(r) == gpu_dump(g)
+    d0 = gpu_dump(g)
+    assert gpu_dump(r) == d0
     ids2 = _gen.zipf_ids(rng, n, K + 1200)
     names2 = [(b"an-arena-length-bucket-name-%d" % i) if i % 7 == 0 else (b"b%d" % i) for i in ids2]
     kind = rng.choice(np.array([0, 1, 2], np.uint8), n, p=[0.5, 0.45, 0.05])
@@ -771,7 +826,7 @@ def test_snapshot_restore_round_trip(pa, tmp_path):
     # a handle opened at another size takes the image's table size
     other = pa.GPURepo(log2_slots=11)
     other.restore(path)
-    assert other.capacity == g.capacity and gpu_dump(other) == gpu_dump(g)
+    assert other.capacity == g.capacity and gpu_dump(other) == d0
 
 
 # ------------------------------------------------ C1 (BASELINE configs[0]) --

@@ -1,0 +1,90 @@
+"""The shard group through the C ABI (phip_group_*): owner-routed
+Receive and anti-entropy over RCCL with no torch.distributed on the data
+path, against the oracle.  The box has one GPU, so the group is world 1 in
+both forms (ncclCommInitAll over [0]; ncclCommInitRank with 1 rank); the
+multi-rank exchange glue is covered on CPU (test_shard.py, gloo world 2)
+and the N-GPU runs are the driver's.
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from oracle import oracle as O  # noqa: E402
+from tests import _gen  # noqa: E402
+
+
+@pytest.fixture(scope="module")
+def pa():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import patrol_amd
+    return patrol_amd
+
+
+def _batch(rng, n, K, dev):
+    from patrol_amd.engine import names_blob
+    ids = _gen.zipf_ids(rng, n, K)
+    names = [(b"an-arena-length-bucket-name-%d" % i) if i % 97 == 0 else b"b%d" % i for i in ids]
+    a, t, e = _gen.clean_states(rng, n)
+    blob, offs = names_blob(names)
+    dv = [torch.from_numpy(blob).to(dev), torch.from_numpy(offs.view(np.int32)).to(dev)]
+    dv += [torch.from_numpy(x.view(np.int64)).to(dev) for x in (a, t, e)]
+    return names, a, t, e, dv
+
+
+def _dump(repo):
+    return {k: (v.added, v.taken, v.elapsed, v.created) for k, v in repo.dump().items()}
+
+
+@pytest.mark.parametrize("mode", ["all", "rank"])
+def test_group_receive_vs_oracle(pa, mode):
+    """Two owner-routed batches (the second large enough for the sender-side
+    combine) merged through phip_group_receive equal the oracle's Receive of
+    the same messages."""
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(61)
+    if mode == "all":
+        g = pa.GPUGroup.open_all([0], log2_slots=14)
+        repo = g.repos[0]
+    else:
+        repo = pa.GPURepo(log2_slots=14)
+        g = pa.GPUGroup.open_rank(repo, pa.GPUGroup.unique_id(), 1, 0)
+    assert g.world == 1
+    o = O.Repo()
+    for k, n in enumerate((5000, 1 << 21)):
+        names, a, t, e, dv = _batch(rng, n, 20000, dev)
+        torch.cuda.synchronize()
+        sent, merged = g.receive([dv], _gen.T0 + k, combine=True)
+        assert sent == merged and 0 < merged[0] <= n
+        if n >= 1 << 20:
+            assert merged[0] < n          # hot names were combined at the sender
+        o.receive_soa(names, a, t, e, _gen.T0 + k)
+    got = _dump(repo)
+    want = o.dump()
+    assert len(got) == len(want)
+    assert all(got.get(k) == v for k, v in want.items())
+    g.close()
+    if mode == "rank":
+        repo.close()
+
+
+def test_group_anti_entropy_equals_torch_restatement(pa):
+    from patrol_amd import shard
+    R, B = 5, 4000
+    rng = np.random.default_rng(3)
+    x = torch.zeros((R, 3, B), dtype=torch.int64)
+    for k in range(R):
+        taken = rng.integers(0, 10**6, B).astype(np.float64)
+        x[k, 0] = shard.e_encode(torch.from_numpy((taken + rng.random(B) * 100).view(np.int64)))
+        x[k, 1] = shard.e_encode(torch.from_numpy(taken.view(np.int64)))
+        x[k, 2] = torch.from_numpy(rng.integers(0, 1 << 40, B))
+    want = shard.anti_entropy(x.clone())
+    g = pa.GPUGroup.open_all([0], log2_slots=10)
+    xd = x.cuda()
+    torch.cuda.synchronize()
+    g.anti_entropy([xd])
+    torch.cuda.synchronize()
+    assert torch.equal(xd.cpu(), want)
+    g.close()
