@@ -56,7 +56,7 @@ enum BufId {
   B_MISS, B_MISS2, B_RETRY, B_CSLOT, B_CMSG,
   B_SLOT, B_IDX, B_SSLOT, B_SIDX, B_USLOT, B_SCNT, B_SSTART, B_LONG, B_HUGE, B_TEMP, B_DUMP,
   B_OPS, B_HOFF, B_HOP, B_HVAL, B_RPOS, B_RST, B_RUNN, B_SEGEX, B_WOFF, B_SUMS, B_WRUN,
-  B_WING, B_SEGXF,
+  B_WING, B_SEGXF, B_FOLDDBG,
   B_STATES, B_NAME1, B_HOT, B_ROUTE, B_EXPORT, B_MSHARD, B_MSCNT, B_DEDUP, B_DSET, B_COUNT_
 };
 
@@ -862,12 +862,17 @@ int ordered(phip_handle* h, Src src, u32 n, const OpView& ov, const OutView& ow)
     }
     HIPCHK(h, hipGetLastError());
     static const int variant = getenv("PHIP_FOLD_VARIANT") ? atoi(getenv("PHIP_FOLD_VARIANT")) : 0;
+    // PHIP_FOLD_STATS=1 (diagnostics): per hot segment, ops / windows /
+    // windows folded / rounds / bursts / ops walked / runs / cycles, to stderr
+    static const bool fold_stats = getenv("PHIP_FOLD_STATS") != nullptr;
+    u64* fold_dbg = nullptr;
+    if (fold_stats && (rc = ensure(h, B_FOLDDBG, (size_t)nhuge * 8, &fold_dbg))) return rc;
     auto kb = variant == 1 ? k_fold_block<1> : k_fold_block<0>;
     {
       Launch l(h, "k_fold_block", h->stream2);
       kb<<<nhuge, kFoldThreads, 0, h->stream2>>>(huge, nhuge, uslot, hoff, scnt, hval, hop,
                                                   h->recs, rpos, rst, runn, segex, segxf, woff,
-                                                  sums, wrun, wing);
+                                                  sums, wrun, wing, fold_dbg);
     }
     HIPCHK(h, hipGetLastError());
     {
@@ -876,6 +881,21 @@ int ordered(phip_handle* h, Src src, u32 n, const OpView& ov, const OutView& ow)
           huge, nhuge, hoff, woff, scnt, hval, hop, rpos, rst, runn, segex, segxf, wrun, wing, ow);
     }
     HIPCHK(h, hipGetLastError());
+    if (fold_dbg) {
+      std::vector<u64> d((size_t)nhuge * 8);
+      HIPCHK(h, hipMemcpyAsync(d.data(), fold_dbg, d.size() * 8, hipMemcpyDeviceToHost, h->stream2));
+      HIPCHK(h, hipStreamSynchronize(h->stream2));
+      std::vector<u32> ord(nhuge);
+      for (u32 k = 0; k < nhuge; ++k) ord[k] = k;
+      std::sort(ord.begin(), ord.end(), [&](u32 x, u32 y) { return d[8 * x + 7] > d[8 * y + 7]; });
+      fprintf(stderr, "fold: %u huge segments\n", nhuge);
+      for (u32 i = 0; i < nhuge && i < 6; ++i) {
+        const u32 k = ord[i];
+        fprintf(stderr, "fold[%u] ops %llu windows %llu folded %llu rounds %llu bursts %llu walked "
+                "%llu runs %llu us %.1f\n", k, d[8 * k], d[8 * k + 1], d[8 * k + 2],
+                d[8 * k + 3], d[8 * k + 4], d[8 * k + 5], d[8 * k + 6], d[8 * k + 7] / 100.0);
+      }
+    }
   }
   if (nlong) {
     Launch l(h, "k_fold_wave");

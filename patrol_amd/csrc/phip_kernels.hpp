@@ -1628,13 +1628,14 @@ __device__ inline void put_run(u32* run_pos, RunState* run_st, u32 k, u32 pos, c
 
 // Maxima of merged replica states: E' codes of added and taken (enc_replica)
 // and elapsed biased by 2^63, 0 = none.
-struct alignas(32) GMax {
-  u64 a, t, e, pad;
+struct GMax {
+  u64 a, t, e;
 };
 __device__ inline GMax gmax(const GMax& x, const GMax& y) {
-  return GMax{x.a > y.a ? x.a : y.a, x.t > y.t ? x.t : y.t, x.e > y.e ? x.e : y.e, 0};
+  return GMax{x.a > y.a ? x.a : y.a, x.t > y.t ? x.t : y.t, x.e > y.e ? x.e : y.e};
 }
-__device__ inline GMax gmax_of(const WinSum& q) { return GMax{q.ea, q.et, q.ee, 0}; }
+__device__ inline GMax gmax_of(const WinSum& q) { return GMax{q.ea, q.et, q.ee}; }
+__device__ inline bool gmax_empty(const GMax& g) { return !(g.a | g.t | g.e); }
 
 // X = max(R, G) in E order, field by field.
 __device__ inline FState join_state(const FState& R, const GMax& g) {
@@ -1678,23 +1679,15 @@ __device__ inline bool window_absorbable(const WinSum& q, const FState& Xs, cons
 
 // One workgroup folds one very long segment (a Zipf-hot bucket) from the
 // contiguous copy k_gather_huge made.  Windows are tested kSumChunk at a time
-// from their summaries (absorbable, or quiet once the segment is exact), and
-// only a window that may change the state is folded: thread t owns ops
-// k*kFoldThreads + t (k < kFoldPer) of it, and
-//  * parallel round: every thread tests its unretired ops against the
-//    current state; a workgroup min finds the first op that changes it; the
-//    ops before it are retired (they saw the current state);
-//  * sequential burst (only when a round found a change): the window is
-//    staged in LDS and wave 0 applies ops one by one from that op, appending
-//    a run at every change, until kBurstQuiet ops in a row leave the state
-//    unchanged.  Changes cluster (a merge that raises `added` is followed by a
-//    run of successful Takes) and a round costs far more than one op, so a
-//    cluster costs about one round plus its ops at sequential speed.
-
-struct FoldWin {
-  u32 v[kFoldPer];
-  OpRec r[kFoldPer];
-};
+// from their summaries (quiet, absorbable, or quiet once the segment is
+// exact), and only a window that may change the state is staged in LDS and
+// folded (fold_window_absorb, or fold_window once exact):
+//  * parallel round: every thread tests its unretired ops (k*kFoldThreads +
+//    t, k < kFoldPer) against the state they see; a workgroup min finds the
+//    first op that changes it; the ops before it saw exactly that state;
+//  * burst from that op by wave 0, until the state stops changing.
+// The window lives in LDS while it is folded; registers hold per-op values
+// only, so the kernel keeps its working set without spilling.
 
 constexpr u32 kSumChunk = kFoldThreads;   // window summaries staged in LDS at a time
 
@@ -1704,73 +1697,91 @@ struct FoldShared {
   WinSum sum[kSumChunk];
   GMax pinc[kSumChunk];                   // inclusive merge-maxima prefix over the chunk
   GMax wtot[kFoldThreads / 64];
+  GMax wtot4[kFoldPer][kFoldThreads / 64];
   u32 wave_min[2][kFoldThreads / 64];
   u32 quiet_min[kFoldThreads / 64];
-  u64 state[4];
+  u64 state[8];
   u32 cur, nrun, exact_from;
+  u32 n_burst, n_walk;   // diagnostics (k_fold_block's dbg)
 };
 
-// Loads are unconditional (index clamped into the segment): a load under a
-// runtime condition makes hipcc branch around it and wait for it on the spot
-// (cdna_hip_programming.md, "traps that silently de-pipeline").
-__device__ inline void fold_load(FoldWin& W, const u32* __restrict__ sv,
-                                 const OpRec* __restrict__ so, u32 pos, u32 last, u32 tid) {
+// Window [pos, pos + kFoldWin) of the segment into LDS (sh.op / sh.val, op k
+// of the window at index k).  Loads are unconditional (index clamped into the
+// segment) and issued together: a load under a runtime condition makes hipcc
+// branch around it and wait for it on the spot (cdna_hip_programming.md,
+// "traps that silently de-pipeline").
+__device__ inline void fold_stage(const u32* __restrict__ sv, const OpRec* __restrict__ so, u32 pos,
+                                  u32 last, u32 tid, FoldShared& sh) {
+  u32 v[kFoldPer];
+  OpRec r[kFoldPer];
 #pragma unroll
   for (u32 k = 0; k < kFoldPer; ++k) {
     const u32 j = min(pos + k * kFoldThreads + tid, last);
-    W.v[k] = sv[j];
-    W.r[k] = load_oprec(so + j);
+    v[k] = sv[j];
+    r[k] = load_oprec(so + j);
   }
+#pragma unroll
+  for (u32 k = 0; k < kFoldPer; ++k) {
+    sh.op[k * kFoldThreads + tid] = r[k];
+    sh.val[k * kFoldThreads + tid] = v[k];
+  }
+  __syncthreads();
 }
 
+__device__ inline SOp staged_sop(const FoldShared& sh, u32 i) { return make_sop(sh.op[i], sh.val[i]); }
+
+__device__ inline void publish_state(FoldShared& sh, const FState& T) {
+  sh.state[0] = as_bits(T.a); sh.state[1] = as_bits(T.t);
+  sh.state[2] = (u64)T.e; sh.state[3] = (u64)T.c;
+}
+__device__ inline FState read_state(const FoldShared& sh) {
+  FState S;
+  S.a = as_f64(sh.state[0]); S.t = as_f64(sh.state[1]);
+  S.e = (i64)sh.state[2]; S.c = (i64)sh.state[3]; S.existed = true;
+  return S;
+}
+
+// Workgroup min of u32 (alternating buffers: one barrier per round).
+__device__ inline u32 block_min(u32 m, FoldShared& sh, u32& round, u32 tid) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) m = min(m, (u32)__shfl_xor((int)m, off));
+  u32* wm = sh.wave_min[round & 1];
+  ++round;
+  if ((tid & 63) == 0) wm[tid >> 6] = m;
+  __syncthreads();
+  u32 r = 0xFFFFFFFFu;
+#pragma unroll
+  for (u32 x = 0; x < kFoldThreads / 64; ++x) r = min(r, wm[x]);
+  return r;
+}
+
+// Exact fold of a staged window: every change of the state is a run.
 template <int V>
-__device__ inline void fold_window(const FoldWin& W, u32 pos, u32 lim, FState& S, u32& round,
-                                   FoldShared& sh, u32* rp, RunState* rs, u32 tid) {
+__device__ inline void fold_window(u32 pos, u32 lim, FState& S, u32& round, FoldShared& sh, u32* rp,
+                                   RunState* rs, u32 tid) {
   const u32 lane = tid & 63, wv = tid >> 6;
   u32 cur = 0;
-  bool staged = false;
   while (cur < lim) {
     u32 my_first = 0xFFFFFFFFu;
     if constexpr (!(V & 1)) {
-#pragma unroll
+#pragma unroll 1
       for (u32 k = 0; k < kFoldPer; ++k) {
         const u32 w = k * kFoldThreads + tid;
         if (w >= cur && w < lim && my_first == 0xFFFFFFFFu) {
           FState S2;
-          if (apply_sop(make_sop(W.r[k], W.v[k]), S, S2)) my_first = w;
+          if (apply_sop(staged_sop(sh, w), S, S2)) my_first = w;
         }
       }
     }
-    u32 m = my_first;
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) m = min(m, (u32)__shfl_xor((int)m, off));
-    u32* wm = sh.wave_min[round & 1];   // alternating: one barrier per round suffices
-    ++round;
-    if (lane == 0) wm[wv] = m;
-    __syncthreads();
-    u32 first = 0xFFFFFFFFu;
-#pragma unroll
-    for (u32 x = 0; x < kFoldThreads / 64; ++x) first = min(first, wm[x]);
+    const u32 first = block_min(my_first, sh, round, tid);
     if (first == 0xFFFFFFFFu) return;
-    if (!staged) {
-#pragma unroll
-      for (u32 k = 0; k < kFoldPer; ++k) {
-        const u32 w = k * kFoldThreads + tid;
-        sh.op[w] = W.r[k];
-        sh.val[w] = W.v[k];
-      }
-      staged = true;
-      __syncthreads();
-    }
     // ---- sequential burst (wave 0) from `first`, which changes the state
     if (wv == 0) {
       FState T = S;
-      u32 j = first, quiet = 0, nrun = sh.nrun, exact_from = sh.exact_from;
+      u32 j = first, quiet = 0, nrun = sh.nrun;
       while (j < lim && quiet < kBurstQuiet) {
         FState T2;
-        if (apply_sop(make_sop(sh.op[j], sh.val[j]), T, T2)) {
-          // a change that lowers a field ends the absorbing identity
-          if (exact_from == 0xFFFFFFFFu && !state_grew(T, T2)) exact_from = nrun;
+        if (apply_sop(staged_sop(sh, j), T, T2)) {
           T = T2;
           if (lane == 0) put_run(rp, rs, nrun, pos + j + 1, T);
           ++nrun;
@@ -1781,16 +1792,15 @@ __device__ inline void fold_window(const FoldWin& W, u32 pos, u32 lim, FState& S
         ++j;
       }
       if (lane == 0) {
-        sh.state[0] = as_bits(T.a); sh.state[1] = as_bits(T.t);
-        sh.state[2] = (u64)T.e; sh.state[3] = (u64)T.c;
+        sh.n_burst += 1;
+        sh.n_walk += j - first;
+        publish_state(sh, T);
         sh.cur = j;
         sh.nrun = nrun;
-        sh.exact_from = exact_from;
       }
     }
     __syncthreads();
-    S.a = as_f64(sh.state[0]); S.t = as_f64(sh.state[1]);
-    S.e = (i64)sh.state[2]; S.c = (i64)sh.state[3]; S.existed = true;
+    S = read_state(sh);
     cur = sh.cur;
     __syncthreads();   // state / cur are rewritten by the next burst
   }
@@ -1800,6 +1810,9 @@ __device__ inline u64 shfl_up_u64(u64 v, u32 d) {
   const u32 lo = __shfl_up((u32)v, d), hi = __shfl_up((u32)(v >> 32), d);
   return ((u64)hi << 32) | lo;
 }
+__device__ inline GMax shfl_up_gmax(const GMax& g, u32 d) {
+  return GMax{shfl_up_u64(g.a, d), shfl_up_u64(g.t, d), shfl_up_u64(g.e, d)};
+}
 
 // Inclusive prefix max of x over the workgroup (kFoldThreads lanes, thread
 // order) into sh.pinc[tid].
@@ -1807,14 +1820,180 @@ __device__ inline void block_prefix_gmax(GMax x, FoldShared& sh, u32 tid) {
   const u32 lane = tid & 63, wv = tid >> 6;
 #pragma unroll
   for (u32 d = 1; d < 64; d <<= 1) {
-    const GMax y{shfl_up_u64(x.a, d), shfl_up_u64(x.t, d), shfl_up_u64(x.e, d), 0};
+    const GMax y = shfl_up_gmax(x, d);
     if (lane >= d) x = gmax(x, y);
   }
   if (lane == 63) sh.wtot[wv] = x;
   __syncthreads();
   for (u32 y = 0; y < wv; ++y) x = gmax(x, sh.wtot[y]);
-  sh.pinc[tid] = x;
+  if (tid < kSumChunk) sh.pinc[tid] = x;
   __syncthreads();
+}
+
+// A merge op's contribution to the running replica maximum G (E' codes,
+// elapsed biased; 0 for Takes and incast requests, which merge nothing).
+__device__ inline GMax merge_contrib(const OpRec& r, u32 v) {
+  const u32 kind = v >> kOpIdxBits;
+  if (kind == PHIP_OP_TAKE || (kind == PHIP_OP_RECEIVE && state_is_zero(r.x, r.y, (i64)r.z)))
+    return GMax{0, 0, 0};
+  return GMax{enc_replica(r.x), enc_replica(r.y), r.z ^ kSign};
+}
+
+// g[k] = the replica maximum before op k*kFoldThreads + tid of the staged
+// window (gstart, then the window's merges in op order); *gend after the
+// whole window.  Four rows of kFoldThreads ops, each a wave scan plus the
+// totals of the waves and rows before it.
+__device__ inline void window_prefix(u32 lim, GMax gstart, GMax (&g)[kFoldPer], GMax& gend,
+                                     FoldShared& sh, u32 tid) {
+  const u32 lane = tid & 63, wv = tid >> 6;
+  GMax inc[kFoldPer];
+#pragma unroll
+  for (u32 k = 0; k < kFoldPer; ++k) {
+    const u32 i = k * kFoldThreads + tid;
+    inc[k] = i < lim ? merge_contrib(sh.op[i], sh.val[i]) : GMax{0, 0, 0};
+#pragma unroll
+    for (u32 d = 1; d < 64; d <<= 1) {
+      const GMax y = shfl_up_gmax(inc[k], d);
+      if (lane >= d) inc[k] = gmax(inc[k], y);
+    }
+    if (lane == 63) sh.wtot4[k][wv] = inc[k];
+  }
+  __syncthreads();
+  GMax acc = gstart;
+#pragma unroll
+  for (u32 k = 0; k < kFoldPer; ++k) {
+    GMax before = acc;
+    for (u32 y = 0; y < wv; ++y) before = gmax(before, sh.wtot4[k][y]);
+    const GMax ex = shfl_up_gmax(inc[k], 1);
+    g[k] = lane ? gmax(before, ex) : before;
+#pragma unroll
+    for (u32 y = 0; y < kFoldThreads / 64; ++y) acc = gmax(acc, sh.wtot4[k][y]);
+  }
+  gend = acc;
+  __syncthreads();   // wtot4 is rewritten by the next window
+}
+
+// g[k] for a runtime k without indexing the register array (a dynamic
+// index would put it in scratch memory).
+__device__ inline GMax pick(const GMax (&g)[kFoldPer], u32 k) {
+  GMax r = g[0];
+#pragma unroll
+  for (u32 x = 1; x < kFoldPer; ++x) {
+    const bool s = k == x;
+    r.a = s ? g[x].a : r.a;
+    r.t = s ? g[x].t : r.t;
+    r.e = s ? g[x].e : r.e;
+  }
+  return r;
+}
+
+// Fold a staged window that neither window test could clear, in the
+// absorbing model: merges only raise G, so the ops that need a run are those
+// that change the state otherwise (a successful Take, a denied Take's added =
+// capacity write, the op creating the bucket).  A parallel round evaluates
+// every such op against its own X_k = max(R, G_k) and finds the first that
+// changes it; the ops before it saw exactly those states.  Wave 0 then runs
+// wave rounds from there carrying the true state X (lane l looks at op
+// cur + l; the first op that changes X decides: a merge that raises it is
+// applied with no run, a Take that changes it is applied and starts one)
+// until two rounds in a row change nothing; the workgroup round follows.  A
+// change that lowers a field ends the identity: the run it starts is exact
+// (sh.exact_from) and the rest of the window is applied one op at a time,
+// every change a run.  R and G are updated in place.
+template <int V>
+__device__ inline void fold_window_absorb(u32 pos, u32 lim, FState& R, GMax& G, u32& round,
+                                          FoldShared& sh, u32* rp, RunState* rs, u32 tid) {
+  const u32 lane = tid & 63, wv = tid >> 6;
+  GMax g[kFoldPer], gend;
+  window_prefix(lim, G, g, gend, sh, tid);
+  u32 cur = 0;
+  while (cur < lim) {
+    u32 my_first = 0xFFFFFFFFu;
+    if constexpr (!(V & 1)) {
+#pragma unroll 1
+      for (u32 k = 0; k < kFoldPer; ++k) {
+        const u32 idx = k * kFoldThreads + tid;
+        if (idx >= cur && idx < lim && my_first == 0xFFFFFFFFu) {
+          const SOp op = staged_sop(sh, idx);
+          const FState X = join_state(R, pick(g, k));
+          if (op.kind == PHIP_OP_TAKE || !X.existed) {
+            FState X2;
+            if (apply_sop(op, X, X2)) my_first = idx;
+          }
+        }
+      }
+    }
+    const u32 p = block_min(my_first, sh, round, tid);
+    if (p == 0xFFFFFFFFu) break;
+    if (tid == p % kFoldThreads) {   // G before op p, for the burst
+      const GMax gp = pick(g, p / kFoldThreads);
+      sh.state[4] = gp.a; sh.state[5] = gp.t; sh.state[6] = gp.e;
+    }
+    __syncthreads();
+    if (wv == 0) {
+      FState X = join_state(R, GMax{sh.state[4], sh.state[5], sh.state[6]});
+      u32 j = p, quiet = 0, nrun = sh.nrun, exact_from = sh.exact_from;
+      while (j < lim && quiet < 2 && exact_from == 0xFFFFFFFFu) {
+        const u32 i = j + lane;
+        const bool valid = i < lim;
+        const SOp op = staged_sop(sh, min(i, lim - 1));
+        const bool is_take = op.kind == PHIP_OP_TAKE || !X.existed;
+        const bool is_merge = !is_take &&
+                              (op.kind != PHIP_OP_RECEIVE || !state_is_zero(op.x, op.y, (i64)op.z));
+        bool raise = false;
+        FState X2 = X;
+        if (valid && is_merge) {
+          go_merge(X2.a, X2.t, X2.e, as_f64(op.x), as_f64(op.y), (i64)op.z);   // bucket.go:250-260
+          raise = as_bits(X2.a) != as_bits(X.a) || as_bits(X2.t) != as_bits(X.t) || X2.e != X.e;
+        }
+        bool chg = false;
+        if (valid && is_take) chg = apply_sop(op, X, X2);
+        const u64 mb = __ballot(raise | chg);
+        if (!mb) {
+          j += 64;
+          ++quiet;
+          continue;
+        }
+        const u32 q = (u32)__ffsll((long long)mb) - 1;
+        FState Y;
+        Y.a = shfl_f64(X2.a, q); Y.t = shfl_f64(X2.t, q);
+        Y.e = shfl_i64(X2.e, q); Y.c = shfl_i64(X2.c, q);
+        Y.existed = true;
+        if (__shfl((int)chg, q) != 0) {
+          if (!state_grew(X, Y)) exact_from = nrun;
+          if (lane == 0) put_run(rp, rs, nrun, pos + j + q + 1, Y);
+          ++nrun;
+          quiet = 0;
+        }
+        X = Y;
+        j += q + 1;
+      }
+      if (exact_from != 0xFFFFFFFFu) {   // exact from here: one op at a time, every change a run
+        for (; j < lim; ++j) {
+          FState X2;
+          if (apply_sop(staged_sop(sh, j), X, X2)) {
+            X = X2;
+            if (lane == 0) put_run(rp, rs, nrun, pos + j + 1, X);
+            ++nrun;
+          }
+        }
+      }
+      j = min(j, lim);
+      if (lane == 0) {
+        sh.n_burst += 1;
+        sh.n_walk += j - p;
+        publish_state(sh, X);
+        sh.cur = j;
+        sh.nrun = nrun;
+        sh.exact_from = exact_from;
+      }
+    }
+    __syncthreads();
+    R = read_state(sh);
+    cur = sh.cur;
+    __syncthreads();   // state / cur are rewritten by the next burst
+  }
+  G = gend;
 }
 
 // Ablation variants (tools only, PHIP_FOLD_VARIANT): 1 = no state test
@@ -1827,9 +2006,11 @@ __global__ __launch_bounds__(kFoldThreads) void k_fold_block(
     u32* __restrict__ run_pos, RunState* __restrict__ run_st, u32* __restrict__ run_n,
     u8* __restrict__ seg_existed, u32* __restrict__ seg_exact_from,
     const u64* __restrict__ woff, const WinSum* __restrict__ sums, u32* __restrict__ win_run,
-    GMax* __restrict__ win_g) {
+    GMax* __restrict__ win_g, u64* __restrict__ dbg) {
   __shared__ FoldShared sh;
   if (blockIdx.x >= nhuge) return;
+  const u64 t_begin = wall_clock64();
+  u32 n_folded = 0;
   const u32 g = huge_list[blockIdx.x];
   const u32 tid = threadIdx.x;
   Rec* r = &recs[seg_slot[g]];
@@ -1842,12 +2023,14 @@ __global__ __launch_bounds__(kFoldThreads) void k_fold_block(
   RunState* rs = run_st + base + blockIdx.x;
 
   FState R = load_state(load_rec(r));   // run state (see the module comment)
-  GMax G{0, 0, 0, 0};                   // merges absorbed so far
+  GMax G{0, 0, 0};                      // merges absorbed so far
   if (tid == 0) {
     put_run(rp, rs, 0, 0, R);
     seg_existed[blockIdx.x] = R.existed;
     sh.nrun = 1;
     sh.exact_from = 0xFFFFFFFFu;
+    sh.n_burst = 0;
+    sh.n_walk = 0;
   }
   __syncthreads();
   const u32 nwin = (cnt + kFoldWin - 1) / kFoldWin;
@@ -1855,7 +2038,6 @@ __global__ __launch_bounds__(kFoldThreads) void k_fold_block(
   u32* __restrict__ wr = win_run + woff[blockIdx.x];
   GMax* __restrict__ wg = win_g + woff[blockIdx.x];
   u32 round = 0;
-  FoldWin A;
   // Windows are tested kSumChunk at a time: every thread tests one window's
   // summary (with the merge maxima of the windows before it in the chunk)
   // and a workgroup min picks the first window that may change the state.
@@ -1874,22 +2056,22 @@ __global__ __launch_bounds__(kFoldThreads) void k_fold_block(
     const u32 mine = cb + tid;
     const bool in = mine >= w && mine < lim;
     const bool exact = sh.exact_from != 0xFFFFFFFFu;
-    block_prefix_gmax(in ? gmax_of(sh.sum[tid]) : GMax{0, 0, 0, 0}, sh, tid);
-    const GMax gs = gmax(G, (in && mine > w) ? sh.pinc[tid - 1] : GMax{0, 0, 0, 0});
+    block_prefix_gmax(in ? gmax_of(sh.sum[tid]) : GMax{0, 0, 0}, sh, tid);
+    const GMax gs = gmax(G, (in && mine > w) ? sh.pinc[tid - 1] : GMax{0, 0, 0});
     bool quiet = false;
     if (in) {
-      if (exact) quiet = window_quiet(sh.sum[tid], R);
-      else quiet = window_absorbable(sh.sum[tid], join_state(R, gs),
-                                     join_state(R, gmax(G, sh.pinc[tid])));
+      if (exact) {
+        quiet = window_quiet(sh.sum[tid], R);
+      } else {
+        // merges that raise nothing and Takes denied at the extreme clock
+        // (the strict test), or Takes denied for every state the window's
+        // merges lead through (the absorbing bound)
+        const FState Xs = join_state(R, gs);
+        quiet = window_quiet(sh.sum[tid], Xs) ||
+                window_absorbable(sh.sum[tid], Xs, join_state(R, gmax(G, sh.pinc[tid])));
+      }
     }
-    u32 m = (in && !quiet) ? mine : 0xFFFFFFFFu;
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) m = min(m, (u32)__shfl_xor((int)m, off));
-    if ((tid & 63) == 0) sh.quiet_min[tid >> 6] = m;
-    __syncthreads();
-    u32 first = 0xFFFFFFFFu;
-#pragma unroll
-    for (u32 x = 0; x < kFoldThreads / 64; ++x) first = min(first, sh.quiet_min[x]);
+    const u32 first = block_min((in && !quiet) ? mine : 0xFFFFFFFFu, sh, round, tid);
     const u32 stop = first == 0xFFFFFFFFu ? lim : first;
     const u32 run_now = sh.nrun - 1;   // run in effect at each such window's first op
     if (in && mine <= stop && mine < lim) {
@@ -1898,21 +2080,22 @@ __global__ __launch_bounds__(kFoldThreads) void k_fold_block(
     }
     // G after the windows before `stop` (their merges are absorbed)
     if (stop > w) G = gmax(G, sh.pinc[stop - 1 - cb]);
-    __syncthreads();   // quiet_min, pinc and nrun are rewritten below
+    __syncthreads();   // wave_min, pinc and nrun are rewritten below
     if (first == 0xFFFFFFFFu) {
       w = lim;
       continue;
     }
     const u32 pos = first * kFoldWin;
-    FState X = exact ? R : join_state(R, G);
+    const u32 wlim = min(kFoldWin, cnt - pos);
     if (!exact && (sh.sum[first - cb].flags & kSumDirty)) {
       // A -0.0 replica: Go's merge is not the E max for it, so the segment is
       // exact from here on, starting with a run that holds the true state.
       // Nothing absorbed yet (G empty): the current run is already exact
       // (and may be the bucket's not-yet-created initial state, which a new
       // run could not express).
+      const FState X = join_state(R, G);
       if (tid == 0) {
-        if (G.a | G.t | G.e) {
+        if (!gmax_empty(G)) {
           put_run(rp, rs, sh.nrun, pos, X);
           sh.exact_from = sh.nrun;
           ++sh.nrun;
@@ -1920,20 +2103,29 @@ __global__ __launch_bounds__(kFoldThreads) void k_fold_block(
           sh.exact_from = sh.nrun - 1;
         }
       }
+      R = X;
       __syncthreads();
     }
-    fold_load(A, sv, so, pos, last, tid);
-    fold_window<V>(A, pos, min(kFoldWin, cnt - pos), X, round, sh, rp, rs, tid);
-    // the window's ops are applied exactly: X is the state after it, and it
-    // holds the window's merges
-    R = X;
-    G = gmax(G, gmax_of(sh.sum[first - cb]));
+    const GMax gw = gmax_of(sh.sum[first - cb]);
+    fold_stage(sv, so, pos, last, tid, sh);
+    ++n_folded;
+    if (sh.exact_from == 0xFFFFFFFFu) {
+      fold_window_absorb<V>(pos, wlim, R, G, round, sh, rp, rs, tid);
+    } else {
+      fold_window<V>(pos, wlim, R, round, sh, rp, rs, tid);   // R: the exact state after
+      G = gmax(G, gw);
+    }
     w = first + 1;
   }
   if (tid == 0) {
-    store_state(r, join_state(R, sh.exact_from == 0xFFFFFFFFu ? G : GMax{0, 0, 0, 0}));
+    store_state(r, join_state(R, sh.exact_from == 0xFFFFFFFFu ? G : GMax{0, 0, 0}));
     run_n[blockIdx.x] = sh.nrun;
     seg_exact_from[blockIdx.x] = sh.exact_from;
+    if (dbg) {
+      u64* d = dbg + (u64)blockIdx.x * 8;
+      d[0] = cnt; d[1] = nwin; d[2] = n_folded; d[3] = round; d[4] = sh.n_burst;
+      d[5] = sh.n_walk; d[6] = sh.nrun; d[7] = wall_clock64() - t_begin;
+    }
   }
 }
 
@@ -1946,13 +2138,6 @@ __global__ __launch_bounds__(kFoldThreads) void k_fold_block(
 // totals.  The fold recorded the run in effect at each window start, so the
 // run search only spans the runs that begin inside the window (usually none).
 constexpr u32 kOutPer = kFoldWin / kBlock;
-
-__device__ inline GMax merge_contrib(const OpRec& r, u32 v) {
-  const u32 kind = v >> kOpIdxBits;
-  if (kind == PHIP_OP_TAKE || (kind == PHIP_OP_RECEIVE && state_is_zero(r.x, r.y, (i64)r.z)))
-    return GMax{0, 0, 0, 0};
-  return GMax{enc_replica(r.x), enc_replica(r.y), r.z ^ kSign, 0};
-}
 
 __global__ __launch_bounds__(kBlock) void k_huge_outputs(
     const u32* __restrict__ huge_list, u32 nhuge, const u64* __restrict__ hoff,
@@ -1980,7 +2165,7 @@ __global__ __launch_bounds__(kBlock) void k_huge_outputs(
   const u32 j0 = p0 + tid * kOutPer;
   OpRec op[kOutPer];
   u32 val[kOutPer];
-  GMax tot{0, 0, 0, 0};
+  GMax tot{0, 0, 0};
 #pragma unroll
   for (u32 k = 0; k < kOutPer; ++k) {
     const u32 j = min(j0 + k, p1 - 1);
@@ -1992,12 +2177,12 @@ __global__ __launch_bounds__(kBlock) void k_huge_outputs(
   GMax inc = tot;
 #pragma unroll
   for (u32 d = 1; d < 64; d <<= 1) {
-    const GMax y{shfl_up_u64(inc.a, d), shfl_up_u64(inc.t, d), shfl_up_u64(inc.e, d), 0};
+    const GMax y = shfl_up_gmax(inc, d);
     if (lane >= d) inc = gmax(inc, y);
   }
   if (lane == 63) wtot[wv] = inc;
-  GMax exc{shfl_up_u64(inc.a, 1), shfl_up_u64(inc.t, 1), shfl_up_u64(inc.e, 1), 0};
-  if (lane == 0) exc = GMax{0, 0, 0, 0};
+  GMax exc = shfl_up_gmax(inc, 1);
+  if (lane == 0) exc = GMax{0, 0, 0};
   __syncthreads();
   for (u32 y = 0; y < wv; ++y) exc = gmax(exc, wtot[y]);
   GMax gj = gmax(g0, exc);
