@@ -89,6 +89,10 @@ def parse():
                    help="c2: pad every bucket name to this many bytes (e.g. 32: the arena path)")
     p.add_argument("--no-routed", action="store_true",
                    help="c2: skip the owner_routed (strong-scaling) object")
+    p.add_argument("--route-path", default="c", choices=["c", "torch"],
+                   help="owner routing / anti-entropy through the C shard group (phip_group_*, "
+                        "RCCL inside libpatrolhip) or the torch.distributed glue; the gloo "
+                        "rehearsal backend always takes the glue")
     return p.parse_args()
 
 
@@ -372,17 +376,41 @@ def run_c4(args, torch, dev, repo, rank, world, K, gen):
     torch.cuda.synchronize()
 
     merged = []
+    group = repo._group = open_group(args, dist_module(), repo, rank, world)
 
     def step(j):
         a, t, e = batches[j]
-        rb, ro, ra, rt, re = shard.route_messages_native(blob, offs, a, t, e, repo,
-                                                         combine=not args.no_combine)
-        m = ro.numel() - 1
+        if group is not None:
+            _, got = group.receive([(blob, offs, a, t, e)], T0 + j, combine=not args.no_combine)
+            m = got[0]
+        else:
+            rb, ro, ra, rt, re = shard.route_messages_native(blob, offs, a, t, e, repo,
+                                                             combine=not args.no_combine)
+            m = ro.numel() - 1
+            if m:
+                repo.receive_soa(rb, ra, rt, re, T0 + j, name_offs=ro, n=m, device=True)
         if j >= args.warmup:
             merged.append(m)
-        if m:
-            repo.receive_soa(rb, ra, rt, re, T0 + j, name_offs=ro, n=m, device=True)
     return n, step, owned, merged
+
+
+def dist_module():
+    import torch.distributed as dist
+    return dist
+
+
+def open_group(args, dist, repo, rank, world):
+    """The shard group of the C library (phip_group_open_rank: RCCL owner
+    routing and all-reduce with no torch on the data path), its id handed
+    out over torch.distributed (bootstrap only).  None under the gloo
+    rehearsal backend, where ranks may share one GPU (RCCL refuses that):
+    the torch.distributed glue (patrol_amd.shard) stands in."""
+    if args.dist_backend != "nccl" or args.route_path != "c":
+        return None
+    import patrol_amd
+    obj = [patrol_amd.GPUGroup.unique_id() if rank == 0 else None]
+    dist.broadcast_object_list(obj, src=0)
+    return patrol_amd.GPUGroup.open_rank(repo, obj[0], world, rank)
 
 
 def run_routed(args, torch, dist, dev, local, rank, world):
@@ -419,15 +447,21 @@ def run_routed(args, torch, dist, dev, local, rank, world):
     batches = [replica_states(torch, gen, m, j, dev) for j in range(args.warmup + args.steps)]
     torch.cuda.synchronize()
     merged = []
+    group = open_group(args, dist, repo, rank, world)
 
     def step(j):
         a, t, e = batches[j]
-        rb, ro, ra, rt, re = shard.route_messages_native(blob, offs, a, t, e, repo, combine=True)
-        k = ro.numel() - 1
+        if group is not None:
+            _, got = group.receive([(blob, offs, a, t, e)], T0 + j, combine=True)
+            k = got[0]
+        else:
+            rb, ro, ra, rt, re = shard.route_messages_native(blob, offs, a, t, e, repo,
+                                                             combine=True)
+            k = ro.numel() - 1
+            if k:
+                repo.receive_soa(rb, ra, rt, re, T0 + j, name_offs=ro, n=k, device=True)
         if j >= args.warmup:
             merged.append(k)
-        if k:
-            repo.receive_soa(rb, ra, rt, re, T0 + j, name_offs=ro, n=k, device=True)
 
     for j in range(args.warmup):
         step(j)
@@ -445,6 +479,8 @@ def run_routed(args, torch, dist, dev, local, rank, world):
     dist.all_reduce(mx, op=dist.ReduceOp.MAX)
     sm = tt.clone()
     dist.all_reduce(sm, op=dist.ReduceOp.SUM)
+    if group is not None:
+        group.close()
     repo.close()
     del batches, blob, offs
     el = float(mx[0])
@@ -455,8 +491,10 @@ def run_routed(args, torch, dist, dev, local, rank, world):
         "messages_per_step_total": n, "messages_per_step_per_gpu": m, "buckets_total": K,
         "merged_per_step_total": float(sm[1]), "merged_per_step_max_gpu": float(mx[1]),
         "buckets_max_gpu": int(mx[2]), "slots_per_gpu": 1 << L, "sender_combine": True,
-        "step": "phip_route_pack (owner partition + sender-side combine) -> RCCL all-to-all per "
-                "column -> phip_receive_soa on the owner",
+        "step": ("phip_group_receive (C ABI: phip_route_pack with sender-side combine, RCCL "
+                 "all-to-all of the split sizes, grouped send/recv per column, phip_receive_soa "
+                 "on the owner)" if group is not None else
+                 "phip_route_pack + torch.distributed all-to-all per column + phip_receive_soa"),
     }
 
 
@@ -487,14 +525,16 @@ def run_c5(args, torch, dev, repo, rank, world, gen):
                        torch.randint(1, 10**6, (R * nw,), device=dev, generator=gen)))
     flat = reps.view(-1)
     torch.cuda.synchronize()
+    group = repo._group = open_group(args, dist_module(), repo, rank, world)
 
     def step(j):
         idx, dt, de = rounds[j]
         flat.index_add_(0, idx + B, dt)
         flat.index_add_(0, idx + 2 * B, de)
-        tl = []
-        shard.anti_entropy_native(reps, repo, timings=tl)
-        return tl
+        if group is not None:
+            group.anti_entropy([reps])      # phip_group_anti_entropy: local max, RCCL max, apply
+        else:
+            shard.anti_entropy_native(reps, repo)
 
     def check():
         ok = bool((reps == reps[0:1]).all())
@@ -655,7 +695,7 @@ def main():
     # HIP events around every kernel of the timed steps, kept by the library
     # and read once after the timed region (reading them synchronises).
     # (c5's step reads its own per-call timings from the shard layer.)
-    repo.set_timing(True, accumulate=args.workload != "c5")
+    repo.set_timing(True, accumulate=True)
     kern = {}
     if world > 1:
         dist.barrier()
@@ -787,6 +827,8 @@ def main():
         out["cpu_baseline"] = None
     if args.ring and args.workload == "c2":
         ring.close()
+    if getattr(repo, "_group", None) is not None:
+        repo._group.close()
     repo.close()
     if routed:
         # the C2 batches are freed first: the owner-routed line has its own

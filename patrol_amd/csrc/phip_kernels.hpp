@@ -73,12 +73,74 @@ struct Datagrams {
   }
 };
 
+// Bytes [8k, 8k + 8) of a byte string that starts `sh` bits into the
+// aligned word p[0], assembled from aligned 8-byte loads; `lastw` is the
+// word holding the string's last byte, so no load runs past it (bytes past
+// the string come back as garbage: callers mask them).
+__device__ inline u64 str_word(const u64* p, u32 sh, u32 k, u32 lastw) {
+  const u64 lo = p[k < lastw ? k : lastw], hi = p[k + 1 < lastw ? k + 1 : lastw];
+  return sh ? (lo >> sh) | (hi << (64 - sh)) : lo;
+}
+__device__ inline u64 low_bytes(u64 w, u32 n) { return n >= 8 ? w : (w & ((1ull << (8 * n)) - 1)); }
+
+// One FNV-1a step on the hash held as 32-bit halves:
+// h*0x100000001b3 = h*0x1b3 + (h << 40), so hi' = hi*0x1b3 + carry + (lo << 8).
+__device__ inline void fnv_step32(u32& lo, u32& hi, u32 c) {
+  lo ^= c;
+  const u64 p = (u64)lo * 0x1b3u;
+  hi = (u32)((u64)hi * 0x1b3u + (p >> 32)) + (lo << 8);
+  lo = (u32)p;
+}
+// FNV-1a over the low n (<= 8) bytes of w.
+__device__ inline void fnv_word32(u32& lo, u32& hi, u64 w, u32 n) {
+#pragma unroll
+  for (u32 b = 0; b < 8; ++b)
+    if (b < n) fnv_step32(lo, hi, (u32)(w >> (8 * b)) & 0xFFu);
+}
+
+// A name longer than kInlineName bytes read with aligned 8-byte loads (any
+// alignment): FNV-1a and the canonical words of a long name (Rec: len in
+// word 0, the first 16 bytes in words 1-2; the arena offset is the
+// record's).
+__device__ inline void load_name_long(const u8* src, u64 off, u32 len, Name& nm) {
+  const u64* p = reinterpret_cast<const u64*>(src + (off & ~7ull));
+  const u32 sh = (u32)(off & 7) * 8;
+  const u32 lastw = ((u32)(off & 7) + len - 1) >> 3;
+  u32 lo = (u32)kFnvOffset, hi = (u32)(kFnvOffset >> 32);
+  const u64 w1 = str_word(p, sh, 0, lastw), w2 = str_word(p, sh, 1, lastw);   // len > 16
+  fnv_word32(lo, hi, w1, 8);
+  fnv_word32(lo, hi, w2, 8);
+  for (u32 k = 16; k < len; k += 8) {
+    const u32 n = len - k < 8 ? len - k : 8;
+    fnv_word32(lo, hi, str_word(p, sh, k >> 3, lastw), n);
+  }
+  nm.h = ((u64)hi << 32) | lo; nm.len = len; nm.off = off;
+  nm.w0 = len; nm.w1 = w1; nm.w2 = w2;
+}
+
+// Bytes [16, len) of a long name equal the arena copy at aoff (both read as
+// words from aligned loads).
+__device__ inline bool long_tail_equal(const u8* arena, u64 aoff, const u8* src, u64 off, u32 len) {
+  const u64 a0 = aoff + 16, s0 = off + 16;
+  const u32 n = len - 16;
+  const u64* pa = reinterpret_cast<const u64*>(arena + (a0 & ~7ull));
+  const u64* ps = reinterpret_cast<const u64*>(src + (s0 & ~7ull));
+  const u32 sha = (u32)(a0 & 7) * 8, shs = (u32)(s0 & 7) * 8;
+  const u32 la = ((u32)(a0 & 7) + n - 1) >> 3, ls = ((u32)(s0 & 7) + n - 1) >> 3;
+  for (u32 k = 0; k < n; k += 8) {
+    const u32 m = n - k < 8 ? n - k : 8;
+    if (low_bytes(str_word(pa, sha, k >> 3, la), m) != low_bytes(str_word(ps, shs, k >> 3, ls), m))
+      return false;
+  }
+  return true;
+}
+
 // Name read with aligned 8-byte loads (up to 4 per name) instead of one
 // byte load per character.  Needs the blob 8-byte aligned and readable up to
 // the next 8-byte boundary past its last name (the ABI's slack rule).
 template <bool NT>
 __device__ inline void load_name_wide(const u8* src, u64 off, u32 len, Name& nm) {
-  if (len > kInlineName) { load_name(src, off, len, nm); return; }
+  if (len > kInlineName) { load_name_long(src, off, len, nm); return; }
   const u32 sh = (u32)(off & 7) * 8;
   const u32 nw = ((u32)(off & 7) + len + 7) >> 3;
   const u64* p = reinterpret_cast<const u64*>(src + (off & ~7ull));
@@ -90,12 +152,11 @@ __device__ inline void load_name_wide(const u8* src, u64 off, u32 len, Name& nm)
   if (len < 8) { b0 = len ? b0 & ((1ull << (8 * len)) - 1) : 0; b1 = 0; b2 = 0; }
   else if (len < 16) { b1 = len > 8 ? b1 & ((1ull << (8 * (len - 8))) - 1) : 0; b2 = 0; }
   else if (len < 24) { b2 = len > 16 ? b2 & ((1ull << (8 * (len - 16))) - 1) : 0; }
-  u64 h = kFnvOffset;
-  for (u32 k = 0; k < len; ++k) {
-    const u64 w = k < 8 ? b0 : (k < 16 ? b1 : b2);
-    h = fnv_step(h, (u8)(w >> ((k & 7) * 8)));
-  }
-  nm.h = h; nm.len = len; nm.off = off;
+  u32 lo = (u32)kFnvOffset, hi = (u32)(kFnvOffset >> 32);
+  fnv_word32(lo, hi, b0, len);
+  if (len > 8) fnv_word32(lo, hi, b1, len - 8);
+  if (len > 16) fnv_word32(lo, hi, b2, len - 16);
+  nm.h = ((u64)hi << 32) | lo; nm.len = len; nm.off = off;
   nm.w0 = (u64)len | (b0 << 16);           // name byte k sits at canonical byte k+2
   nm.w1 = (b0 >> 48) | (b1 << 16);
   nm.w2 = (b1 >> 48) | (b2 << 16);
@@ -177,10 +238,7 @@ __device__ inline bool name_equal(const Rec& r, const Name& nm, const u8* src, c
   if ((r0 & 0xFFu) != (nm.w0 & 0xFFu)) return false;
   if (nm.len <= kInlineName) return r0 == nm.w0 && r.name1 == nm.w1 && r.name2 == nm.w2;
   if (r.name1 != nm.w1 || r.name2 != nm.w2) return false;
-  u64 aoff = r.name0 >> 32;
-  for (u32 k = 16; k < nm.len; ++k)
-    if (arena[aoff + k] != src[nm.off + k]) return false;
-  return true;
+  return long_tail_equal(arena, r.name0 >> 32, src, nm.off, nm.len);
 }
 
 enum ProbeResult : int { kFound = 0, kMiss = 1, kPending = 2, kFull = 3 };
@@ -325,15 +383,6 @@ __device__ inline void load_words3(const u8* blob, u64 off, u32 len, u64& w0, u6
   w2 = ld<NT>(p + (wb + 2 < we ? wb + 2 : we));
 }
 
-// One FNV-1a step on the hash held as 32-bit halves:
-// h*0x100000001b3 = h*0x1b3 + (h << 40), so hi' = hi*0x1b3 + carry + (lo << 8).
-__device__ inline void fnv_step32(u32& lo, u32& hi, u32 c) {
-  lo ^= c;
-  const u64 p = (u64)lo * 0x1b3u;
-  hi = (u32)((u64)hi * 0x1b3u + (p >> 32)) + (lo << 8);
-  lo = (u32)p;
-}
-
 // FNV-1a and the canonical words of a name of <= kShortName bytes from the
 // words load_words3 returned (bytes past the name's end are ignored).
 __device__ inline void short_name(u64 w0, u64 w1, u64 w2, u64 off, u32 len, Name& nm) {
@@ -404,9 +453,14 @@ constexpr u32 kRouteMinBatch = 1u << 20;   // the route combine's (phip_route_pa
 #endif
 constexpr u32 kManyMisses = PHIP_MANY_MISSES;
 
+// Hot names of up to kHotTailName bytes are matched from LDS alone: the
+// directory also holds bytes [16, len) of an arena name (tail words).
+constexpr u32 kHotTailName = 40;
+constexpr u32 kHotTailWords = (kHotTailName - 16) / 8;
 struct HotEntry {
-  u64 tag, w0, w1;   // table tag and canonical name words 0-1 (flags byte cleared)
-  u32 slot, pad;
+  u64 tag, w0, w1, w2;   // table tag and canonical name words (flags byte and arena offset cleared)
+  u64 tail[kHotTailWords];   // arena names of <= kHotTailName bytes: bytes [16, len), zero-padded
+  u32 slot, aoff;        // record slot; arena offset of a name longer than kInlineName
 };
 struct HotHdr {
   u32 n;             // directory entries
@@ -416,7 +470,7 @@ struct HotHdr {
 
 __device__ inline u32 hot_home(u64 tag) { return (u32)(tag ^ (tag >> 29)) & (kHotLds - 1); }
 
-// Sample j = message j*stride: resolve it (short names only) and count its
+// Sample j = message j*stride: resolve it and count its
 // slot, aggregated per workgroup in LDS first (a hot slot is sampled by most
 // lanes; one global atomic per workgroup and slot keeps it off one address).
 template <class Src>
@@ -433,7 +487,6 @@ __global__ __launch_bounds__(256) void k_hot_sample(Src src, u32 n, u32 stride, 
     if (j >= nsample || i >= n) continue;
     u64 off; u32 len;
     src.template get<true>((u32)i, off, len);
-    if (len > kShortName) continue;
     Name nm;
     load_name_wide<true>(src.blob, off, len, nm);
     u32 s;
@@ -506,11 +559,24 @@ __global__ void k_hot_build(const u32* __restrict__ ckeys, const u32* __restrict
   const u32 s = ckeys[e] - 1;
   const Rec r = load_rec(&T.recs[s]);
   HotEntry d;
+  const bool arena = (r.name0 & 0xFFu) > kInlineName;
   d.tag = r.tag;
-  d.w0 = r.name0 & ~0xFF00ull;
+  d.w0 = arena ? (r.name0 & 0xFFu) : (r.name0 & ~0xFF00ull);
   d.w1 = r.name1;
+  d.w2 = r.name2;
   d.slot = s;
-  d.pad = 0;
+  d.aoff = arena ? (u32)(r.name0 >> 32) : 0u;
+  const u32 len = (u32)(r.name0 & 0xFFu);
+  for (u32 k = 0; k < kHotTailWords; ++k) d.tail[k] = 0;
+  if (arena && len <= kHotTailName) {
+    const u64 a0 = (r.name0 >> 32) + 16;
+    const u64* p = reinterpret_cast<const u64*>(T.arena + (a0 & ~7ull));
+    const u32 sh = (u32)(a0 & 7) * 8, lastw = ((u32)(a0 & 7) + len - 17) >> 3;
+    for (u32 k = 0; 8 * k < len - 16; ++k) {
+      const u32 m = len - 16 - 8 * k;
+      d.tail[k] = low_bytes(str_word(p, sh, k, lastw), m);
+    }
+  }
   dir[idx] = d;
 }
 
@@ -696,13 +762,42 @@ __global__ __launch_bounds__(kBlock) void k_classify_soa2(const uint64_t* __rest
   note_dirty(d, at, ctr);
 }
 
+// load_name_long for kInlineName < len <= kHotTailName, also returning the
+// tail words (bytes [16, len), zero-padded).
+__device__ inline void load_name_tail(const u8* src, u64 off, u32 len, Name& nm, u64 (&tail)[kHotTailWords]) {
+  const u64* p = reinterpret_cast<const u64*>(src + (off & ~7ull));
+  const u32 sh = (u32)(off & 7) * 8;
+  const u32 lastw = ((u32)(off & 7) + len - 1) >> 3;
+  u32 lo = (u32)kFnvOffset, hi = (u32)(kFnvOffset >> 32);
+  const u64 w1 = str_word(p, sh, 0, lastw), w2 = str_word(p, sh, 1, lastw);
+  fnv_word32(lo, hi, w1, 8);
+  fnv_word32(lo, hi, w2, 8);
+#pragma unroll
+  for (u32 k = 0; k < kHotTailWords; ++k) {
+    const u32 m = len > 16 + 8 * k ? len - 16 - 8 * k : 0;
+    const u64 w = m ? low_bytes(str_word(p, sh, k + 2, lastw), m) : 0;
+    fnv_word32(lo, hi, w, m);
+    tail[k] = w;
+  }
+  nm.h = ((u64)hi << 32) | lo; nm.len = len; nm.off = off;
+  nm.w0 = len; nm.w1 = w1; nm.w2 = w2;
+}
+__device__ inline bool tail_match(const u64 (&htail)[kHotTailWords][kHotMax], u32 j,
+                                  const u64 (&tail)[kHotTailWords]) {
+  bool eq = true;
+#pragma unroll
+  for (u32 k = 0; k < kHotTailWords; ++k) eq &= htail[k][j] == tail[k];
+  return eq;
+}
+
 template <class In>
 __global__ __launch_bounds__(kFastBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_receive_fast(
     In in, u32 n, Table T, u8* __restrict__ status, Sharded miss, u32* ctr,
     const HotHdr* __restrict__ hot, const HotEntry* __restrict__ hot_dir) {
   __shared__ u32 hslot[kHotLds];        // directory index + 1 (0 = empty)
-  __shared__ u64 htag[kHotMax], hw0[kHotMax], hw1[kHotMax];
-  __shared__ u32 hrec[kHotMax];
+  __shared__ u64 htag[kHotMax], hw0[kHotMax], hw1[kHotMax], hw2[kHotMax];
+  __shared__ u32 hrec[kHotMax], haoff[kHotMax];
+  __shared__ u64 htail[kHotTailWords][kHotMax];
   __shared__ u64 hmax[3][kHotMax];      // per-workgroup maxima (elapsed biased by 2^63)
   __shared__ u32 hhits;
 
@@ -720,7 +815,9 @@ __global__ __launch_bounds__(kFastBlock) __attribute__((amdgpu_waves_per_eu(8, 8
   __syncthreads();
   for (u32 j = threadIdx.x; j < nh; j += kFastBlock) {
     const HotEntry d = hot_dir[j];
-    htag[j] = d.tag; hw0[j] = d.w0; hw1[j] = d.w1; hrec[j] = d.slot;
+    htag[j] = d.tag; hw0[j] = d.w0; hw1[j] = d.w1; hw2[j] = d.w2;
+    hrec[j] = d.slot; haoff[j] = d.aoff;
+    for (u32 k = 0; k < kHotTailWords; ++k) htail[k][j] = d.tail[k];
     u32 hs = hot_home(d.tag);
     while (atomicCAS(&hslot[hs], 0u, j + 1) != 0) hs = (hs + 1) & (kHotLds - 1);
   }
@@ -755,17 +852,33 @@ __global__ __launch_bounds__(kFastBlock) __attribute__((amdgpu_waves_per_eu(8, 8
     Name nm;
     short_name(w0, w1, w2, off, len, nm);
     const bool shortname = len <= kShortName;
+    // Longer names (rare on the headline batches, all of a 32-byte-name
+    // batch): the full canonical words and hash, word loads from the blob;
+    // an arena name of <= kHotTailName bytes also keeps its tail words for
+    // the directory match.
+    u64 tail[kHotTailWords] = {};
+    if (!shortname) {
+      // (decoded batches only: the datagram form keeps its registers for
+      // the wire decode)
+      if (In::kSoa && len > kInlineName && len <= kHotTailName) load_name_tail(in.blob(), off, len, nm, tail);
+      else load_name_wide<true>(in.blob(), off, len, nm);
+    }
     const u64 tag = T.tag(nm.h);
     const u64 ea = enc_replica_nz(ra), et = enc_replica_nz(rt), ee = (u64)re ^ kSign;
 
     bool missed = false;
     if (valid) {
       int hidx = -1;
-      if (nh && shortname) {
+      if (nh) {
         for (u32 hs = hot_home(tag);; hs = (hs + 1) & (kHotLds - 1)) {
           const u32 e = hslot[hs];
           if (!e) break;
-          if (htag[e - 1] == tag && hw0[e - 1] == nm.w0 && hw1[e - 1] == nm.w1) {
+          if (htag[e - 1] == tag && hw0[e - 1] == nm.w0 && hw1[e - 1] == nm.w1 &&
+              (shortname || (hw2[e - 1] == nm.w2 &&
+                             (len <= kInlineName ||
+                              (In::kSoa && len <= kHotTailName
+                                   ? tail_match(htail, e - 1, tail)
+                                   : long_tail_equal(T.arena, haoff[e - 1], in.blob(), off, len)))))) {
             hidx = (int)e - 1;
             break;
           }
@@ -788,7 +901,6 @@ __global__ __launch_bounds__(kFastBlock) __attribute__((amdgpu_waves_per_eu(8, 8
           if (shortname && cur.tag == 0) {
             pr = kMiss;
           } else {
-            if (!shortname) load_name_wide<true>(in.blob(), off, len, nm);
             pr = probe(T, nm, in.blob(), &s, &cur);
           }
         }
@@ -943,7 +1055,7 @@ __global__ void k_mark_created(Src src, u32 n, const u32* __restrict__ list, Tab
   u64 off; u32 len;
   src.get(i, off, len);
   Name nm;
-  load_name(src.blob, off, len, nm);
+  load_name_wide<false>(src.blob, off, len, nm);
   u32 s;
   Rec r;
   if (probe(T, nm, src.blob, &s, &r) != kFound) return;
@@ -964,7 +1076,7 @@ __global__ __launch_bounds__(kBlock) void k_resolve(Src src, u32 n, const u32* _
     u64 off; u32 len;
     src.get(i, off, len);
     Name nm;
-    load_name(src.blob, off, len, nm);
+    load_name_wide<false>(src.blob, off, len, nm);
     u32 s;
     Rec r;
     int pr = probe(T, nm, src.blob, &s, &r);
@@ -994,7 +1106,7 @@ __global__ __launch_bounds__(kBlock) void k_claim(Src src, u32 n, const u32* __r
     u64 off; u32 len;
     src.get(i, off, len);
     Name nm;
-    load_name(src.blob, off, len, nm);
+    load_name_wide<false>(src.blob, off, len, nm);
     const u64 tag = T.tag(nm.h);
     const u32 mask = T.mask();
     s = T.home(tag);
@@ -1033,7 +1145,7 @@ __global__ void k_publish(Src src, u32 base, u32 n, const u32* __restrict__ clai
   u64 off; u32 len;
   src.get(i, off, len);
   Name nm;
-  load_name(src.blob, off, len, nm);
+  load_name_wide<false>(src.blob, off, len, nm);
   Rec r;
   r.tag = T.tag(nm.h);
   r.added = kEPosZero;
@@ -2709,7 +2821,7 @@ __global__ void k_hash_names(NamesOffs src, u32 n, uint64_t* out) {
   u64 off; u32 len;
   src.get(i, off, len);
   Name nm;
-  load_name(src.blob, off, len, nm);
+  load_name_wide<false>(src.blob, off, len, nm);
   out[i] = nm.h;
 }
 
@@ -2725,7 +2837,7 @@ __global__ void k_export(NamesOffs src, u32 n, Table T, u8* __restrict__ out,
   u64 off; u32 len;
   src.get(i, off, len);
   Name nm;
-  load_name(src.blob, off, len, nm);
+  load_name_wide<false>(src.blob, off, len, nm);
   u32 s;
   Rec r;
   const bool hit = probe(T, nm, src.blob, &s, &r) == kFound;
@@ -2747,7 +2859,7 @@ __global__ void k_export(NamesOffs src, u32 n, Table T, u8* __restrict__ out,
 __global__ void k_get_one(const u8* name, u32 len, Table T, Rec* out, int* found) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   Name nm;
-  load_name(name, 0, len, nm);
+  load_name_wide<false>(name, 0, len, nm);
   u32 s;
   Rec r;
   int pr = probe(T, nm, name, &s, &r);

@@ -504,6 +504,39 @@ def test_long_names_and_edges(pa):
             assert (got.added, got.taken, got.elapsed, got.created) == want
 
 
+@pytest.mark.parametrize("form", ["soa", "wire"])
+def test_hot_long_names(pa, form):
+    """Skewed batches (hot directory on) of 15..60-byte names that share their
+    first 16 bytes and differ only in the tail: the directory's match of an
+    arena name (LDS tail words up to 40 bytes, the arena beyond) is exact."""
+    import struct
+    rng = np.random.default_rng(43)
+    K, n = 3000, 1 << 18
+    lens = rng.integers(15, 61, K)
+    names_k = [(b"shared-prefix-AB" + (b"%d" % k).rjust(max(int(L) - 16, 0), b"-"))[-int(L):]
+               if L < 16 else (b"%d" % k).rjust(int(L), b"~") for k, L in enumerate(lens)]
+    assert len(set(names_k)) == K
+    g = pa.GPURepo(log2_slots=14, arena_bytes=1 << 20)
+    o = O.Repo()
+    for step in range(2):
+        ids = _gen.zipf_ids(rng, n, K)
+        names = [names_k[i] for i in ids]
+        a, t, e = _gen.clean_states(rng, n)
+        now = _gen.T0 + step
+        if form == "soa":
+            out = g.receive_soa(names, a, t, e, now)
+        else:
+            dgs = [struct.pack(">QQQ", int(a[i]), int(t[i]), int(e[i]) & (2**64 - 1))
+                   + bytes([len(names[i])]) + names[i] for i in range(n)]
+            out = g.receive_datagrams(dgs, now)
+        st, _, _, _ = o.receive_soa(names, a, t, e, now)
+        assert np.array_equal(out["status"], st)
+        if step == 1:
+            hot, folded = g.last_stats()[:2]
+            assert hot > 0 and folded > n // 4   # the directory carried the hot names
+    assert_same_dump(gpu_dump(g), o.dump())
+
+
 def test_datagram_path_matches_soa_path(pa):
     """Raw wire datagrams (device decode) == pre-decoded states."""
     import struct
