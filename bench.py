@@ -728,10 +728,12 @@ def main():
     kms = {k: float(np.mean(v)) for k, v in kern.items()}
     extra = {}
     if args.workload == "c5":
-        # bytes of the two local passes per round (reads R*24 + 24, writes 24;
-        # then reads 24 + R*24, writes R*24 per bucket) over their kernel time
+        # bytes of the two local passes per round (reads R*24, writes 24;
+        # then reads 24 + R*24 per bucket) over their kernel time; k_ae_apply
+        # writes only the fields the join changed, data-dependent and not
+        # counted (profiles/r02_c5_kernels.json has the measured writes)
         R, B = args.replicas, args.buckets
-        bpo = (3 * R + 2) * 24 / R
+        bpo = (2 * R + 2) * 24 / R
         dom_name = "k_ae_local_max+k_ae_apply"
         dom_ms = kms.get("k_ae_local_max", float("nan")) + kms.get("k_ae_apply", float("nan"))
         unit, metric = "merges/s", METRIC + " [C5: anti-entropy replica-bucket joins/sec]"

@@ -2770,7 +2770,9 @@ __global__ void k_route_totals(const u32* __restrict__ cnt, const u32* __restric
 //
 // k_ae_local_max: m[f][i] = max over the R local replicas, in the signed
 // form RCCL's all-reduce(MAX) takes; k_ae_apply: every local replica becomes
-// max(own, m) after the all-reduce (one read and one write per replica).
+// max(own, m) after the all-reduce (one read per replica, and a write only
+// where the join differs: a round that changed a few buckets rewrites those,
+// not every replica plane).
 __global__ __launch_bounds__(kBlock) void k_ae_local_max(const int64_t* __restrict__ rep, u32 R,
                                                          u64 B, int64_t* __restrict__ m) {
   const u64 i = (u64)blockIdx.x * kBlock + threadIdx.x;
@@ -2808,9 +2810,9 @@ __global__ __launch_bounds__(kBlock) void k_ae_apply(int64_t* __restrict__ rep, 
     const int64_t own = p[r * stride];
     if (f < 2) {
       const u64 theirs = (u64)mv ^ kSign;   // already NaN-free
-      p[r * stride] = (int64_t)((u64)own > theirs ? (u64)own : theirs);
+      if (theirs > (u64)own) p[r * stride] = (int64_t)theirs;
     } else {
-      p[r * stride] = own > mv ? own : mv;
+      if (mv > own) p[r * stride] = mv;
     }
   }
 }
