@@ -413,6 +413,9 @@ def open_group(args, dist, repo, rank, world):
     return patrol_amd.GPUGroup.open_rank(repo, obj[0], world, rank)
 
 
+ROUTED_LIMIT_S = 300   # the owner-routed leg's watchdog (main())
+
+
 def run_routed(args, torch, dist, dev, local, rank, world):
     """The owner_routed object (SURVEY §8d/§8e strong scaling): C2's fixed
     total of K buckets and n messages per step, the buckets hash-sharded by
@@ -839,7 +842,25 @@ def main():
             del batches, blob, offs, ids
         torch.cuda.synchronize()
         torch.cuda.empty_cache()
-        out["owner_routed"] = run_routed(args, torch, dist, dev, local, rank, world)
+        # The routed leg is an extra object in the line: an error or a hang
+        # there (one rank failing inside a collective leaves the others
+        # waiting) must not cost the headline.  A watchdog on every rank
+        # prints the line without it and ends the process.
+        import threading
+
+        def give_up():
+            if rank == 0:
+                out["owner_routed"] = {"error": f"timed out after {ROUTED_LIMIT_S} s"}
+                print(json.dumps(out), file=json_out, flush=True)
+            os._exit(0)
+        dog = threading.Timer(ROUTED_LIMIT_S, give_up)
+        dog.daemon = True
+        dog.start()
+        try:
+            out["owner_routed"] = run_routed(args, torch, dist, dev, local, rank, world)
+        except Exception as ex:
+            out["owner_routed"] = {"error": repr(ex)}
+        dog.cancel()
     if rank == 0:
         print(json.dumps(out), file=json_out, flush=True)
     if dist.is_initialized():
