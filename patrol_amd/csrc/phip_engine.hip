@@ -866,7 +866,7 @@ int ordered(phip_handle* h, Src src, u32 n, const OpView& ov, const OutView& ow)
     // windows folded / rounds / bursts / ops walked / runs / cycles, to stderr
     static const bool fold_stats = getenv("PHIP_FOLD_STATS") != nullptr;
     u64* fold_dbg = nullptr;
-    if (fold_stats && (rc = ensure(h, B_FOLDDBG, (size_t)nhuge * 8, &fold_dbg))) return rc;
+    if (fold_stats && (rc = ensure(h, B_FOLDDBG, (size_t)nhuge * 16, &fold_dbg))) return rc;
     auto kb = variant == 1 ? k_fold_block<1> : k_fold_block<0>;
     {
       Launch l(h, "k_fold_block", h->stream2);
@@ -882,18 +882,20 @@ int ordered(phip_handle* h, Src src, u32 n, const OpView& ov, const OutView& ow)
     }
     HIPCHK(h, hipGetLastError());
     if (fold_dbg) {
-      std::vector<u64> d((size_t)nhuge * 8);
+      std::vector<u64> d((size_t)nhuge * 16);
       HIPCHK(h, hipMemcpyAsync(d.data(), fold_dbg, d.size() * 8, hipMemcpyDeviceToHost, h->stream2));
       HIPCHK(h, hipStreamSynchronize(h->stream2));
       std::vector<u32> ord(nhuge);
       for (u32 k = 0; k < nhuge; ++k) ord[k] = k;
-      std::sort(ord.begin(), ord.end(), [&](u32 x, u32 y) { return d[8 * x + 7] > d[8 * y + 7]; });
+      std::sort(ord.begin(), ord.end(), [&](u32 x, u32 y) { return d[16 * x + 7] > d[16 * y + 7]; });
       fprintf(stderr, "fold: %u huge segments\n", nhuge);
       for (u32 i = 0; i < nhuge && i < 6; ++i) {
         const u32 k = ord[i];
+        const u64* e = &d[16 * k];
         fprintf(stderr, "fold[%u] ops %llu windows %llu folded %llu rounds %llu bursts %llu walked "
-                "%llu runs %llu us %.1f\n", k, d[8 * k], d[8 * k + 1], d[8 * k + 2],
-                d[8 * k + 3], d[8 * k + 4], d[8 * k + 5], d[8 * k + 6], d[8 * k + 7] / 100.0);
+                "%llu runs %llu us %.1f | scan %.1f stage %.1f prefix %.1f round %.1f burst %.1f\n",
+                k, e[0], e[1], e[2], e[3], e[4], e[5], e[6], e[7] / 100.0, e[8] / 100.0,
+                e[9] / 100.0, e[10] / 100.0, e[11] / 100.0, e[12] / 100.0);
       }
     }
   }

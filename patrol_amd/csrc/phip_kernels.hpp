@@ -1420,8 +1420,14 @@ __device__ inline void store_state(Rec* r, const FState& S) {
 
 constexpr u32 kLongSeg = 32;        // longer segments: one wave each (k_fold_wave)
 constexpr u32 kHugeSeg = 16384;     // longer still: one workgroup each (k_fold_block)
-constexpr u32 kFoldThreads = 512;   // k_fold_block: threads, ops per thread per window
-constexpr u32 kFoldPer = 4;
+#ifndef PHIP_FOLD_THREADS
+#define PHIP_FOLD_THREADS 512
+#endif
+#ifndef PHIP_FOLD_PER
+#define PHIP_FOLD_PER 1
+#endif
+constexpr u32 kFoldThreads = PHIP_FOLD_THREADS;   // k_fold_block: threads, ops per thread per window
+constexpr u32 kFoldPer = PHIP_FOLD_PER;
 constexpr u32 kFoldWin = kFoldThreads * kFoldPer;
 constexpr u32 kBurstQuiet = 16;     // a sequential burst ends after this many unchanged ops
 
@@ -1450,14 +1456,21 @@ __global__ __launch_bounds__(kBlock) void k_fold_thread(
   store_state(r, S);
 }
 
-__device__ inline double shfl_f64(double v, int src) {
-  u64 b = as_bits(v);
-  u32 lo = __shfl((u32)b, src), hi = __shfl((u32)(b >> 32), src);
-  return as_f64(((u64)hi << 32) | lo);
+// Lane l's value when l is wave-uniform (a ballot's first set lane): a
+// v_readlane into a scalar register instead of an LDS permute.
+__device__ inline u64 lane_u64(u64 v, u32 l) {
+  const u32 lo = (u32)__builtin_amdgcn_readlane((int)(u32)v, (int)l);
+  const u32 hi = (u32)__builtin_amdgcn_readlane((int)(u32)(v >> 32), (int)l);
+  return ((u64)hi << 32) | lo;
 }
-__device__ inline i64 shfl_i64(i64 v, int src) {
-  u32 lo = __shfl((u32)(u64)v, src), hi = __shfl((u32)((u64)v >> 32), src);
-  return (i64)(((u64)hi << 32) | lo);
+__device__ inline FState lane_state(const FState& x, u32 l) {
+  FState y;
+  y.a = as_f64(lane_u64(as_bits(x.a), l));
+  y.t = as_f64(lane_u64(as_bits(x.t), l));
+  y.e = (i64)lane_u64((u64)x.e, l);
+  y.c = (i64)lane_u64((u64)x.c, l);
+  y.existed = true;
+  return y;
 }
 
 // One wave folds one long segment, 64 ops per window, the window held in
@@ -1499,11 +1512,7 @@ __global__ __launch_bounds__(64) void k_fold_wave(
       const u32 p = m ? (u32)(__ffsll((long long)m) - 1) : 64u;
       if (active && lane <= p) write_out(ow, op.idx, o, S);
       if (p >= 64) break;
-      S.a = shfl_f64(S2.a, p);
-      S.t = shfl_f64(S2.t, p);
-      S.e = shfl_i64(S2.e, p);
-      S.c = shfl_i64(S2.c, p);
-      S.existed = true;
+      S = lane_state(S2, p);
       c = p + 1;
     }
     op = nx;
@@ -1815,7 +1824,19 @@ struct FoldShared {
   u64 state[8];
   u32 cur, nrun, exact_from;
   u32 n_burst, n_walk;   // diagnostics (k_fold_block's dbg)
+  u64 prof[6];           // diagnostics: wall-clock ticks per phase (dbg only)
+  u32 profiling;
 };
+
+// Phase timing of k_fold_block (PHIP_FOLD_STATS): thread 0 adds the ticks
+// since *t to sh.prof[k] (the workgroup's threads run every phase together).
+__device__ inline void prof_mark(FoldShared& sh, u32 k, u64& t) {
+  if (sh.profiling && threadIdx.x == 0) {
+    const u64 now = wall_clock64();
+    sh.prof[k] += now - t;
+    t = now;
+  }
+}
 
 // Window [pos, pos + kFoldWin) of the segment into LDS (sh.op / sh.val, op k
 // of the window at index k).  Loads are unconditional (index clamped into the
@@ -1926,15 +1947,39 @@ __device__ inline GMax shfl_up_gmax(const GMax& g, u32 d) {
   return GMax{shfl_up_u64(g.a, d), shfl_up_u64(g.t, d), shfl_up_u64(g.e, d)};
 }
 
+// Wave-wide max scans of GMax with DPP moves (no LDS round trip per step:
+// the fold runs one wave per SIMD, so every step's latency is exposed).
+// Lanes with no source read 0, the identity of the unsigned max.  All 64
+// lanes must be active.
+template <int Ctrl, int RowMask = 0xF>
+__device__ inline u64 dpp_u64(u64 v) {
+  const u32 lo = (u32)__builtin_amdgcn_update_dpp(0, (int)(u32)v, Ctrl, RowMask, 0xF, true);
+  const u32 hi = (u32)__builtin_amdgcn_update_dpp(0, (int)(u32)(v >> 32), Ctrl, RowMask, 0xF, true);
+  return ((u64)hi << 32) | lo;
+}
+template <int Ctrl, int RowMask = 0xF>
+__device__ inline GMax dpp_gmax(const GMax& g) {
+  return GMax{dpp_u64<Ctrl, RowMask>(g.a), dpp_u64<Ctrl, RowMask>(g.t), dpp_u64<Ctrl, RowMask>(g.e)};
+}
+// inclusive: row_shr 1/2/4/8 within rows of 16, then row_bcast15 into rows
+// 1 and 3, row_bcast31 into rows 2 and 3
+__device__ inline GMax wave_incl_max(GMax x) {
+  x = gmax(x, dpp_gmax<0x111>(x));
+  x = gmax(x, dpp_gmax<0x112>(x));
+  x = gmax(x, dpp_gmax<0x114>(x));
+  x = gmax(x, dpp_gmax<0x118>(x));
+  x = gmax(x, dpp_gmax<0x142, 0xA>(x));
+  x = gmax(x, dpp_gmax<0x143, 0xC>(x));
+  return x;
+}
+// the value of lane - 1 (wave_shr:1; lane 0 reads 0)
+__device__ inline GMax wave_shr1(const GMax& x) { return dpp_gmax<0x138>(x); }
+
 // Inclusive prefix max of x over the workgroup (kFoldThreads lanes, thread
 // order) into sh.pinc[tid].
 __device__ inline void block_prefix_gmax(GMax x, FoldShared& sh, u32 tid) {
   const u32 lane = tid & 63, wv = tid >> 6;
-#pragma unroll
-  for (u32 d = 1; d < 64; d <<= 1) {
-    const GMax y = shfl_up_gmax(x, d);
-    if (lane >= d) x = gmax(x, y);
-  }
+  x = wave_incl_max(x);
   if (lane == 63) sh.wtot[wv] = x;
   __syncthreads();
   for (u32 y = 0; y < wv; ++y) x = gmax(x, sh.wtot[y]);
@@ -1962,12 +2007,7 @@ __device__ inline void window_prefix(u32 lim, GMax gstart, GMax (&g)[kFoldPer], 
 #pragma unroll
   for (u32 k = 0; k < kFoldPer; ++k) {
     const u32 i = k * kFoldThreads + tid;
-    inc[k] = i < lim ? merge_contrib(sh.op[i], sh.val[i]) : GMax{0, 0, 0};
-#pragma unroll
-    for (u32 d = 1; d < 64; d <<= 1) {
-      const GMax y = shfl_up_gmax(inc[k], d);
-      if (lane >= d) inc[k] = gmax(inc[k], y);
-    }
+    inc[k] = wave_incl_max(i < lim ? merge_contrib(sh.op[i], sh.val[i]) : GMax{0, 0, 0});
     if (lane == 63) sh.wtot4[k][wv] = inc[k];
   }
   __syncthreads();
@@ -1976,8 +2016,7 @@ __device__ inline void window_prefix(u32 lim, GMax gstart, GMax (&g)[kFoldPer], 
   for (u32 k = 0; k < kFoldPer; ++k) {
     GMax before = acc;
     for (u32 y = 0; y < wv; ++y) before = gmax(before, sh.wtot4[k][y]);
-    const GMax ex = shfl_up_gmax(inc[k], 1);
-    g[k] = lane ? gmax(before, ex) : before;
+    g[k] = gmax(before, wave_shr1(inc[k]));   // lane 0: 0, the identity
 #pragma unroll
     for (u32 y = 0; y < kFoldThreads / 64; ++y) acc = gmax(acc, sh.wtot4[k][y]);
   }
@@ -2017,7 +2056,9 @@ __device__ inline void fold_window_absorb(u32 pos, u32 lim, FState& R, GMax& G, 
                                           FoldShared& sh, u32* rp, RunState* rs, u32 tid) {
   const u32 lane = tid & 63, wv = tid >> 6;
   GMax g[kFoldPer], gend;
+  u64 tp = sh.profiling ? wall_clock64() : 0;
   window_prefix(lim, G, g, gend, sh, tid);
+  prof_mark(sh, 2, tp);
   u32 cur = 0;
   while (cur < lim) {
     u32 my_first = 0xFFFFFFFFu;
@@ -2036,6 +2077,7 @@ __device__ inline void fold_window_absorb(u32 pos, u32 lim, FState& R, GMax& G, 
       }
     }
     const u32 p = block_min(my_first, sh, round, tid);
+    prof_mark(sh, 3, tp);
     if (p == 0xFFFFFFFFu) break;
     if (tid == p % kFoldThreads) {   // G before op p, for the burst
       const GMax gp = pick(g, p / kFoldThreads);
@@ -2067,11 +2109,8 @@ __device__ inline void fold_window_absorb(u32 pos, u32 lim, FState& R, GMax& G, 
           continue;
         }
         const u32 q = (u32)__ffsll((long long)mb) - 1;
-        FState Y;
-        Y.a = shfl_f64(X2.a, q); Y.t = shfl_f64(X2.t, q);
-        Y.e = shfl_i64(X2.e, q); Y.c = shfl_i64(X2.c, q);
-        Y.existed = true;
-        if (__shfl((int)chg, q) != 0) {
+        const FState Y = lane_state(X2, q);
+        if ((__ballot(chg) >> q) & 1) {
           if (!state_grew(X, Y)) exact_from = nrun;
           if (lane == 0) put_run(rp, rs, nrun, pos + j + q + 1, Y);
           ++nrun;
@@ -2104,6 +2143,7 @@ __device__ inline void fold_window_absorb(u32 pos, u32 lim, FState& R, GMax& G, 
     R = read_state(sh);
     cur = sh.cur;
     __syncthreads();   // state / cur are rewritten by the next burst
+    prof_mark(sh, 4, tp);
   }
   G = gend;
 }
@@ -2143,8 +2183,11 @@ __global__ __launch_bounds__(kFoldThreads) void k_fold_block(
     sh.exact_from = 0xFFFFFFFFu;
     sh.n_burst = 0;
     sh.n_walk = 0;
+    sh.profiling = dbg != nullptr;
+    for (u32 k = 0; k < 6; ++k) sh.prof[k] = 0;
   }
   __syncthreads();
+  u64 tp = dbg ? wall_clock64() : 0;
   const u32 nwin = (cnt + kFoldWin - 1) / kFoldWin;
   const WinSum* __restrict__ ws = sums + woff[blockIdx.x];
   u32* __restrict__ wr = win_run + woff[blockIdx.x];
@@ -2219,7 +2262,9 @@ __global__ __launch_bounds__(kFoldThreads) void k_fold_block(
       __syncthreads();
     }
     const GMax gw = gmax_of(sh.sum[first - cb]);
+    prof_mark(sh, 0, tp);
     fold_stage(sv, so, pos, last, tid, sh);
+    prof_mark(sh, 1, tp);
     ++n_folded;
     if (sh.exact_from == 0xFFFFFFFFu) {
       fold_window_absorb<V>(pos, wlim, R, G, round, sh, rp, rs, tid);
@@ -2227,16 +2272,19 @@ __global__ __launch_bounds__(kFoldThreads) void k_fold_block(
       fold_window<V>(pos, wlim, R, round, sh, rp, rs, tid);   // R: the exact state after
       G = gmax(G, gw);
     }
+    if (sh.profiling && tid == 0) tp = wall_clock64();
     w = first + 1;
   }
+  prof_mark(sh, 0, tp);
   if (tid == 0) {
     store_state(r, join_state(R, sh.exact_from == 0xFFFFFFFFu ? G : GMax{0, 0, 0}));
     run_n[blockIdx.x] = sh.nrun;
     seg_exact_from[blockIdx.x] = sh.exact_from;
     if (dbg) {
-      u64* d = dbg + (u64)blockIdx.x * 8;
+      u64* d = dbg + (u64)blockIdx.x * 16;
       d[0] = cnt; d[1] = nwin; d[2] = n_folded; d[3] = round; d[4] = sh.n_burst;
       d[5] = sh.n_walk; d[6] = sh.nrun; d[7] = wall_clock64() - t_begin;
+      for (u32 k = 0; k < 6; ++k) d[8 + k] = sh.prof[k];
     }
   }
 }
