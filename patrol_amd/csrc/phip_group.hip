@@ -133,6 +133,30 @@ int for_members(phip_group* g, F f) {
 }
 
 // One member's owner-routed Receive.
+// The owner's merge of n received messages (lengths, packed names, states):
+// name offsets by an inclusive scan of the lengths, then phip_receive_soa
+// (sources in rank order, each in its order).
+int merge_received(Member& mb, hipStream_t st, const u32* lens, const uint8_t* names, const u64* a,
+                   const u64* t, const int64_t* e, u64 n, int64_t now) {
+  GHIP(mb, mb.r_offs.ensure(n * 4 + 8));
+  u32* offs = (u32*)mb.r_offs.p;
+  GHIP(mb, hipMemsetAsync(offs, 0, sizeof(u32), st));
+  size_t tb = 0;
+  GHIP(mb, rocprim::inclusive_scan(nullptr, tb, lens, offs + 1, (size_t)n, rocprim::plus<u32>(), st));
+  GHIP(mb, mb.scan_tmp.ensure(tb));
+  GHIP(mb, rocprim::inclusive_scan(mb.scan_tmp.p, tb, lens, offs + 1, (size_t)n,
+                                   rocprim::plus<u32>(), st));
+  phip_msgs rm{};
+  rm.n = (u32)n;
+  rm.names = names;
+  rm.name_offs = offs;
+  rm.added = a;
+  rm.taken = t;
+  rm.elapsed = e;
+  GPHIP(mb, phip_receive_soa(mb.h, &rm, now, nullptr, PHIP_DEVICE_PTRS));
+  return PHIP_OK;
+}
+
 int member_receive(phip_group* g, Member& mb, const phip_msgs& in, int64_t now, uint64_t* sent,
                    uint64_t* merged, uint32_t flags) {
   const u32 W = g->world;
@@ -174,17 +198,41 @@ int member_receive(phip_group* g, Member& mb, const phip_msgs& in, int64_t now, 
   if (n_recv > 0xFFFFFFFFull || b_recv > 0xFFFFFFFFull)
     return fail(mb, PHIP_ERR_INVALID, "routed batch of %llu messages / %llu name bytes exceeds 2^32",
                 (unsigned long long)n_recv, (unsigned long long)b_recv);
+  if (sent) *sent = n_send;
+  if (merged) *merged = n_recv;
+  if (W == 1) {   // the whole batch stays here: merge straight from the packed buffers
+    if (n_recv == 0) return PHIP_OK;
+    return merge_received(mb, st, (const u32*)mb.s_lens.p, (const uint8_t*)mb.s_names.p,
+                          (const u64*)mb.s_a.p, (const u64*)mb.s_t.p, (const int64_t*)mb.s_e.p, n_recv,
+                          now);
+  }
   GHIP(mb, mb.r_names.ensure(b_recv + 64));
   GHIP(mb, mb.r_lens.ensure(n_recv * 4 + 4));
   GHIP(mb, mb.r_offs.ensure(n_recv * 4 + 8));
   GHIP(mb, mb.r_a.ensure(n_recv * 8 + 8));
   GHIP(mb, mb.r_t.ensure(n_recv * 8 + 8));
   GHIP(mb, mb.r_e.ensure(n_recv * 8 + 8));
-  // 3. the segments: one send and one receive per peer and column
+  // 3. the segments: one send and one receive per peer and column; this
+  // member's own segment is a device copy (no RCCL round trip through its
+  // buffers)
   GNCCL(mb, ncclGroupStart());
   u64 so = 0, sb = 0, ro = 0, rb = 0;
   for (u32 p = 0; p < W; ++p) {
     const u64 sc = hs[p], sbytes = hs[W + p], rc = hs[2 * W + p], rbytes = hs[3 * W + p];
+    if (p == mb.rank) {
+      GHIP(mb, hipMemcpyAsync((u32*)mb.r_lens.p + ro, (u32*)mb.s_lens.p + so, sc * 4,
+                              hipMemcpyDeviceToDevice, st));
+      GHIP(mb, hipMemcpyAsync((uint8_t*)mb.r_names.p + rb, (uint8_t*)mb.s_names.p + sb, sbytes,
+                              hipMemcpyDeviceToDevice, st));
+      GHIP(mb, hipMemcpyAsync((u64*)mb.r_a.p + ro, (u64*)mb.s_a.p + so, sc * 8,
+                              hipMemcpyDeviceToDevice, st));
+      GHIP(mb, hipMemcpyAsync((u64*)mb.r_t.p + ro, (u64*)mb.s_t.p + so, sc * 8,
+                              hipMemcpyDeviceToDevice, st));
+      GHIP(mb, hipMemcpyAsync((u64*)mb.r_e.p + ro, (u64*)mb.s_e.p + so, sc * 8,
+                              hipMemcpyDeviceToDevice, st));
+      so += sc; sb += sbytes; ro += rc; rb += rbytes;
+      continue;
+    }
     GNCCL(mb, ncclSend((u32*)mb.s_lens.p + so, sc, ncclUint32, p, mb.comm, st));
     GNCCL(mb, ncclRecv((u32*)mb.r_lens.p + ro, rc, ncclUint32, p, mb.comm, st));
     GNCCL(mb, ncclSend((uint8_t*)mb.s_names.p + sb, sbytes, ncclUint8, p, mb.comm, st));
@@ -198,28 +246,10 @@ int member_receive(phip_group* g, Member& mb, const phip_msgs& in, int64_t now, 
     so += sc; sb += sbytes; ro += rc; rb += rbytes;
   }
   GNCCL(mb, ncclGroupEnd());
-  if (sent) *sent = n_send;
-  if (merged) *merged = n_recv;
   if (n_recv == 0) return PHIP_OK;
-  // 4. name offsets of the received blob: an inclusive scan of the lengths
-  u32* offs = (u32*)mb.r_offs.p;
-  GHIP(mb, hipMemsetAsync(offs, 0, sizeof(u32), st));
-  size_t tb = 0;
-  GHIP(mb, rocprim::inclusive_scan(nullptr, tb, (const u32*)mb.r_lens.p, offs + 1, (size_t)n_recv,
-                                   rocprim::plus<u32>(), st));
-  GHIP(mb, mb.scan_tmp.ensure(tb));
-  GHIP(mb, rocprim::inclusive_scan(mb.scan_tmp.p, tb, (const u32*)mb.r_lens.p, offs + 1,
-                                   (size_t)n_recv, rocprim::plus<u32>(), st));
-  // 5. the owner's merge
-  phip_msgs rm{};
-  rm.n = (u32)n_recv;
-  rm.names = (const uint8_t*)mb.r_names.p;
-  rm.name_offs = offs;
-  rm.added = (const uint64_t*)mb.r_a.p;
-  rm.taken = (const uint64_t*)mb.r_t.p;
-  rm.elapsed = (const int64_t*)mb.r_e.p;
-  GPHIP(mb, phip_receive_soa(mb.h, &rm, now, nullptr, PHIP_DEVICE_PTRS));
-  return PHIP_OK;
+  return merge_received(mb, st, (const u32*)mb.r_lens.p, (const uint8_t*)mb.r_names.p,
+                        (const u64*)mb.r_a.p, (const u64*)mb.r_t.p, (const int64_t*)mb.r_e.p, n_recv,
+                        now);
 }
 
 int member_anti_entropy(phip_group* g, Member& mb, int64_t* reps, uint32_t nrep, uint64_t B) {

@@ -2732,7 +2732,7 @@ __global__ __launch_bounds__(kRouteBlock) void k_route_scatter(
   const u64 t0 = (u64)tile * span, t1 = min((u64)n, t0 + span);
   for (u64 b0 = t0; b0 < t1; b0 += 64 * kRU) {
     u32 c[kRU], len[kRU];
-    u64 off[kRU], va[kRU], vt[kRU];
+    u64 off[kRU], va[kRU], vt[kRU], w0[kRU], w1[kRU], w2[kRU];
     i64 ve[kRU];
     bool valid[kRU];
 #pragma unroll
@@ -2744,6 +2744,9 @@ __global__ __launch_bounds__(kRouteBlock) void k_route_scatter(
       src.get(ic, off[u], len[u]);
       va[u] = a[ic]; vt[u] = t[ic]; ve[u] = e[ic];
     }
+    // the name as three aligned words (all of a name of <= 16 bytes)
+#pragma unroll
+    for (u32 u = 0; u < kRU; ++u) load_words3<false>(src.blob, off[u], len[u], w0[u], w1[u], w2[u]);
 #pragma unroll
     for (u32 u = 0; u < kRU; ++u) {
       const bool comb = valid[u] && (c[u] & kRouteHot);
@@ -2764,7 +2767,16 @@ __global__ __launch_bounds__(kRouteBlock) void k_route_scatter(
       out_a[dst] = va[u];
       out_t[dst] = vt[u];
       out_e[dst] = ve[u];
-      for (u32 k = 0; k < len[u]; ++k) out_names[dby + k] = src.blob[off[u] + k];
+      if (len[u] <= 16) {   // bytes from the words already in registers
+        const u32 sh = (u32)(off[u] & 7) * 8;
+        const u64 n0 = sh ? (w0[u] >> sh) | (w1[u] << (64 - sh)) : w0[u];
+        const u64 n1 = sh ? (w1[u] >> sh) | (w2[u] << (64 - sh)) : w1[u];
+#pragma unroll
+        for (u32 k = 0; k < 16; ++k)
+          if (k < len[u]) out_names[dby + k] = (u8)((k < 8 ? n0 >> (8 * k) : n1 >> (8 * (k - 8))) & 0xFFu);
+      } else {
+        for (u32 k = 0; k < len[u]; ++k) out_names[dby + k] = src.blob[off[u] + k];
+      }
     }
   }
   __syncthreads();
