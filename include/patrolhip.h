@@ -101,6 +101,8 @@ enum {
 
 /* phip_config.flags */
 #define PHIP_CFG_NO_GROW 0x1u   /* refuse (PHIP_ERR_FULL / PHIP_ERR_ARENA) instead of growing */
+#define PHIP_CFG_NO_SMALL 0x2u  /* ordered batches of <= 1024 host ops also take the large,
+                                   multi-launch path (by default they run as one launch) */
 
 typedef struct phip_config {
   int32_t device;        /* HIP device ordinal                                          */

@@ -39,6 +39,7 @@ ST_TAKE_OK, ST_TAKE_DENIED, ST_UPSERT_INSERTED, ST_CREATED = 6, 7, 8, 0x80
 OP_TAKE, OP_RECEIVE, OP_UPSERT = 0, 1, 2
 DEVICE_PTRS = 0x1
 CFG_NO_GROW = 0x1
+CFG_NO_SMALL = 0x2
 ROUTE_COMBINE = 0x2
 
 

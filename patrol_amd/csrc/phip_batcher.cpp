@@ -42,9 +42,12 @@ struct Req {
   uint8_t status = 0;
   int rc = 0;
   bool done = false;
+  std::condition_variable cv;   // its caller waits here (woken alone, not with every waiter)
 };
 
 }  // namespace
+
+constexpr uint32_t kSpinWindowUs = 500;   // windows up to this long are yield-waited
 
 struct phip_batcher {
   phip_handle* h = nullptr;
@@ -52,7 +55,6 @@ struct phip_batcher {
   uint32_t max_batch = 1u << 16;
   std::mutex mu;
   std::condition_variable cv_submit;   // the dispatcher waits for requests
-  std::condition_variable cv_done;     // callers wait for their batch
   std::vector<Req*> pending;
   Clock::time_point first_arrival;
   bool stop = false;
@@ -118,8 +120,18 @@ void phip_batcher::run() {
     cv_submit.wait(l, [&] { return stop || !pending.empty(); });
     if (pending.empty()) break;   // stop, nothing left
     const auto deadline = first_arrival + std::chrono::microseconds(window_us);
-    while (!stop && pending.size() < max_batch && Clock::now() < deadline)
-      cv_submit.wait_until(l, deadline);
+    // A short window is waited out by yielding, not by a timed sleep: the
+    // kernel's timer slack (50 us by default) would stretch a 20 us window
+    // to ~70 us.
+    while (!stop && pending.size() < max_batch && Clock::now() < deadline) {
+      if (deadline - Clock::now() > std::chrono::microseconds(kSpinWindowUs)) {
+        cv_submit.wait_until(l, deadline);
+      } else {
+        l.unlock();
+        std::this_thread::yield();
+        l.lock();
+      }
+    }
     const size_t take = std::min<size_t>(pending.size(), max_batch);
     batch.assign(pending.begin(), pending.begin() + take);
     pending.erase(pending.begin(), pending.begin() + take);
@@ -127,11 +139,16 @@ void phip_batcher::run() {
     l.unlock();
     dispatch(batch);
     l.lock();
-    for (Req* r : batch) r->done = true;
     ++batches;
     requests += batch.size();
     max_seen = std::max<uint64_t>(max_seen, batch.size());
-    cv_done.notify_all();
+    // each caller is woken on its own (notified under the lock: a caller
+    // cannot see `done` and return, destroying its Req, before this loop
+    // let go of it)
+    for (Req* r : batch) {
+      r->done = true;
+      r->cv.notify_one();
+    }
   }
 }
 
@@ -144,7 +161,7 @@ int submit_and_wait(phip_batcher* b, Req* r) {
   r->seq = b->arrivals++;
   b->pending.push_back(r);
   if (b->pending.size() == 1 || b->pending.size() >= b->max_batch) b->cv_submit.notify_one();
-  b->cv_done.wait(l, [&] { return r->done; });
+  r->cv.wait(l, [&] { return r->done; });
   return r->rc;
 }
 

@@ -56,7 +56,7 @@ enum BufId {
   B_MISS, B_MISS2, B_RETRY, B_CSLOT, B_CMSG,
   B_SLOT, B_IDX, B_SSLOT, B_SIDX, B_USLOT, B_SCNT, B_SSTART, B_LONG, B_HUGE, B_TEMP, B_DUMP,
   B_OPS, B_HOFF, B_HOP, B_HVAL, B_RPOS, B_RST, B_RUNN, B_SEGEX, B_WOFF, B_SUMS, B_WRUN,
-  B_WING, B_SEGXF, B_FOLDDBG,
+  B_WING, B_SEGXF, B_FOLDDBG, B_SMALL,
   B_STATES, B_NAME1, B_HOT, B_ROUTE, B_EXPORT, B_MSHARD, B_MSCNT, B_DEDUP, B_DSET, B_COUNT_
 };
 
@@ -87,6 +87,7 @@ struct phip_handle {
   u64 max_load = 0;
   u32 load_pct = 90;
   bool grow = true;          // !PHIP_CFG_NO_GROW
+  bool small = true;         // !PHIP_CFG_NO_SMALL
   u64 grows = 0;             // table rehashes so far
   u64 long_need = 0;         // arena bytes the last reserve() counted
   Rec* recs = nullptr;
@@ -104,6 +105,8 @@ struct phip_handle {
   std::vector<Timing> timings;
   std::vector<Timing> event_pool;
   size_t pool_used = 0;
+  u8* small_pin = nullptr;   // pinned staging of small ordered batches (both ways)
+  size_t small_pin_cap = 0;
 };
 
 namespace {
@@ -1052,6 +1055,7 @@ int phip_open(const phip_config* cfg, phip_handle** out) {
   h->load_pct = cfg->max_load_pct ? std::min<u32>(cfg->max_load_pct, 95) : 90;
   h->max_load = load_limit(h->cap, h->load_pct);
   h->grow = !(cfg->flags & PHIP_CFG_NO_GROW);
+  h->small = !(cfg->flags & PHIP_CFG_NO_SMALL);
   h->arena_cap = cfg->arena_bytes ? cfg->arena_bytes : (1ull << 20);
   if (cfg->debug_tag_bits && cfg->debug_tag_bits < 64) h->tag_mask = (1ull << cfg->debug_tag_bits) - 1;
   auto fail = [&](hipError_t e) {
@@ -1105,6 +1109,7 @@ void phip_close(phip_handle* h) {
   if (h->arena_cursor) (void)hipFree(h->arena_cursor);
   if (h->ctr) (void)hipFree(h->ctr);
   if (h->ctr_host) (void)hipHostFree(h->ctr_host);
+  if (h->small_pin) (void)hipHostFree(h->small_pin);
   if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
   if (h->ev_join) (void)hipEventDestroy(h->ev_join);
   if (h->stream2) (void)hipStreamDestroy(h->stream2);
@@ -1645,6 +1650,115 @@ int phip_upsert_soa(phip_handle* h, const phip_msgs* m, int64_t now, const phip_
   return copy_outputs(h, res, n, dev, ow);
 }
 
+// A host-pointer batch of at most kSmallMax ops through k_small_mixed: one
+// pinned copy in, one launch, one pinned copy out (the large path takes a
+// dozen launches and several host round trips, ~0.2 ms whatever the size).
+// *done = false leaves the batch to the large path with nothing changed: too
+// many ops or name bytes, a bucket bound past the load limit (the large path
+// grows the table), or a long-name arena the kernel found too small.
+int small_mixed(phip_handle* h, const phip_ops* ops, const phip_results* res, bool* done) {
+  *done = false;
+  const u32 n = ops->n;
+  if (n > kSmallMax || h->n_buckets + n > h->max_load) return PHIP_OK;
+  const u64 nbytes = ops->name_offs[n];
+  if (nbytes > (u64)kSmallMax * PHIP_MAX_NAME_LEN) return PHIP_OK;
+  auto al = [](size_t x) { return (x + 15) & ~(size_t)15; };
+  const bool take = ops->freq != nullptr, state = ops->added != nullptr;
+  // inputs: offsets | kind | now | freq per count | added taken elapsed | names
+  const size_t o_kind = al(4 * ((size_t)n + 1)), o_now = o_kind + al(n), o_freq = o_now + 8 * n;
+  const size_t o_per = o_freq + 8 * n, o_count = o_per + 8 * n, o_a = o_count + 8 * n;
+  const size_t o_t = o_a + 8 * n, o_e = o_t + 8 * n, o_names = o_e + 8 * n;
+  const size_t in_bytes = al(o_names + nbytes + 8);
+  // outputs: header | status | remaining | have | reply
+  const size_t o_st = sizeof(SmallHdr), o_rem = al(o_st + n), o_have = o_rem + 8 * n;
+  const size_t o_reply = o_have + 8 * n, out_bytes = o_reply + sizeof(phip_state) * n;
+  const size_t total = in_bytes + out_bytes;
+  if (h->small_pin_cap < total) {
+    if (h->small_pin) HIPCHK(h, hipHostFree(h->small_pin));
+    h->small_pin = nullptr;
+    h->small_pin_cap = 0;
+    const size_t want = std::max<size_t>(total, 1 << 20);
+    HIPCHK(h, hipHostMalloc(&h->small_pin, want, 0));
+    h->small_pin_cap = want;
+  }
+  u8 *d = nullptr, *pin = h->small_pin;
+  int rc;
+  if ((rc = ensure(h, B_SMALL, total, &d))) return rc;
+  std::memcpy(pin, ops->name_offs, 4 * ((size_t)n + 1));
+  std::memcpy(pin + o_kind, ops->kind, n);
+  std::memcpy(pin + o_now, ops->now, 8 * n);
+  if (take) {
+    std::memcpy(pin + o_freq, ops->freq, 8 * n);
+    std::memcpy(pin + o_per, ops->per, 8 * n);
+    std::memcpy(pin + o_count, ops->count, 8 * n);
+  }
+  if (state) {
+    std::memcpy(pin + o_a, ops->added, 8 * n);
+    std::memcpy(pin + o_t, ops->taken, 8 * n);
+    std::memcpy(pin + o_e, ops->elapsed, 8 * n);
+  }
+  std::memcpy(pin + o_names, ops->names, nbytes);
+  std::memset(pin + o_names + nbytes, 0, 8);
+  std::memset(pin + in_bytes, 0, sizeof(SmallHdr));
+  HIPCHK(h, hipMemcpyAsync(d, pin, in_bytes + sizeof(SmallHdr), hipMemcpyHostToDevice, h->stream));
+  NamesOffs src{d + o_names, (const u32*)d};
+  OpView ov{};
+  ov.kind = d + o_kind;
+  ov.now = (const int64_t*)(d + o_now);
+  if (take) {
+    ov.freq = (const int64_t*)(d + o_freq);
+    ov.per = (const int64_t*)(d + o_per);
+    ov.count = (const uint64_t*)(d + o_count);
+  }
+  if (state) {
+    ov.a = (const uint64_t*)(d + o_a);
+    ov.t = (const uint64_t*)(d + o_t);
+    ov.e = (const int64_t*)(d + o_e);
+  }
+  u8* dout = d + in_bytes;
+  phip_results r{};
+  if (res) r = *res;
+  OutView ow{};
+  ow.status = r.status ? dout + o_st : nullptr;
+  ow.remaining = r.remaining ? (uint64_t*)(dout + o_rem) : nullptr;
+  ow.have = r.have ? (uint64_t*)(dout + o_have) : nullptr;
+  ow.reply = r.reply ? (phip_state*)(dout + o_reply) : nullptr;
+  {
+    Launch l(h, "k_small_mixed");
+    k_small_mixed<<<1, kSmallMax, 0, h->stream>>>(src, ov, n, table(h), h->arena, h->arena_cap,
+                                                  h->arena_cursor, ow, (SmallHdr*)dout);
+  }
+  HIPCHK(h, hipGetLastError());
+  // the header and the columns the caller asked for, in one copy
+  const size_t back = r.reply ? out_bytes : r.have ? o_reply : r.remaining ? o_have : o_rem;
+  u8* pout = pin + in_bytes;
+  HIPCHK(h, hipMemcpyAsync(pout, dout, back, hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  SmallHdr hd;
+  std::memcpy(&hd, pout, sizeof hd);
+  h->n_buckets += hd.created;
+  if (hd.fallback) return PHIP_OK;
+  if (hd.full) return set_err(h, PHIP_ERR_FULL, "internal: small batch probe wrapped the table");
+  if (r.status) std::memcpy(r.status, pout + o_st, n);
+  if (r.remaining) std::memcpy(r.remaining, pout + o_rem, 8 * n);
+  if (r.have) std::memcpy(r.have, pout + o_have, 8 * n);
+  if (r.reply) {
+    // an op's reply is defined only for INCAST_REPLY statuses; copy those
+    const phip_state* src_r = (const phip_state*)(pout + o_reply);
+    std::vector<u8> st;
+    const u8* stp = r.status;
+    if (!stp) {
+      st.assign(n, 0);
+      HIPCHK(h, hipMemcpy(st.data(), dout + o_st, n, hipMemcpyDeviceToHost));
+      stp = st.data();
+    }
+    for (u32 i = 0; i < n; ++i)
+      if ((stp[i] & 0x7F) == PHIP_ST_INCAST_REPLY) r.reply[i] = src_r[i];
+  }
+  *done = true;
+  return PHIP_OK;
+}
+
 int phip_apply_mixed(phip_handle* h, const phip_ops* ops, const phip_results* res, uint32_t flags) {
   if (!h || !ops) return PHIP_ERR_INVALID;
   std::lock_guard<std::mutex> g(h->mu);
@@ -1664,6 +1778,11 @@ int phip_apply_mixed(phip_handle* h, const phip_ops* ops, const phip_results* re
     if (need_state && (!ops->added || !ops->taken || !ops->elapsed)) return PHIP_ERR_INVALID;
   }
   int rc;
+  if (!dev && h->small) {
+    bool done = false;
+    if ((rc = small_mixed(h, ops, res, &done))) return after_error(h, rc);
+    if (done) return PHIP_OK;
+  }
   NamesOffs src;
   OpView ov{};
   const u8* kind;

@@ -77,8 +77,16 @@ struct Datagrams {
 // aligned word p[0], assembled from aligned 8-byte loads; `lastw` is the
 // word holding the string's last byte, so no load runs past it (bytes past
 // the string come back as garbage: callers mask them).
+// Device-scope coherent load (past the CU's L1): for data other threads of
+// the same kernel may have just written (k_small_mixed's inserts).
+__device__ inline u64 ld_co(const u64* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <bool Co = false>
 __device__ inline u64 str_word(const u64* p, u32 sh, u32 k, u32 lastw) {
-  const u64 lo = p[k < lastw ? k : lastw], hi = p[k + 1 < lastw ? k + 1 : lastw];
+  const u64* a = p + (k < lastw ? k : lastw);
+  const u64* b = p + (k + 1 < lastw ? k + 1 : lastw);
+  const u64 lo = Co ? ld_co(a) : *a, hi = Co ? ld_co(b) : *b;
   return sh ? (lo >> sh) | (hi << (64 - sh)) : lo;
 }
 __device__ inline u64 low_bytes(u64 w, u32 n) { return n >= 8 ? w : (w & ((1ull << (8 * n)) - 1)); }
@@ -119,7 +127,8 @@ __device__ inline void load_name_long(const u8* src, u64 off, u32 len, Name& nm)
 }
 
 // Bytes [16, len) of a long name equal the arena copy at aoff (both read as
-// words from aligned loads).
+// words from aligned loads; Co: the arena side coherently).
+template <bool Co = false>
 __device__ inline bool long_tail_equal(const u8* arena, u64 aoff, const u8* src, u64 off, u32 len) {
   const u64 a0 = aoff + 16, s0 = off + 16;
   const u32 n = len - 16;
@@ -129,7 +138,7 @@ __device__ inline bool long_tail_equal(const u8* arena, u64 aoff, const u8* src,
   const u32 la = ((u32)(a0 & 7) + n - 1) >> 3, ls = ((u32)(s0 & 7) + n - 1) >> 3;
   for (u32 k = 0; k < n; k += 8) {
     const u32 m = n - k < 8 ? n - k : 8;
-    if (low_bytes(str_word(pa, sha, k >> 3, la), m) != low_bytes(str_word(ps, shs, k >> 3, ls), m))
+    if (low_bytes(str_word<Co>(pa, sha, k >> 3, la), m) != low_bytes(str_word(ps, shs, k >> 3, ls), m))
       return false;
   }
   return true;
@@ -233,12 +242,13 @@ __global__ __launch_bounds__(256) void k_shard_compact(const u32* __restrict__ b
 }
 
 // Full-name equality for a candidate record (names > 22 bytes live in the arena).
+template <bool Co = false>
 __device__ inline bool name_equal(const Rec& r, const Name& nm, const u8* src, const u8* arena) {
   const u64 r0 = r.name0 & ~0xFF00ull;   // drop the flags byte
   if ((r0 & 0xFFu) != (nm.w0 & 0xFFu)) return false;
   if (nm.len <= kInlineName) return r0 == nm.w0 && r.name1 == nm.w1 && r.name2 == nm.w2;
   if (r.name1 != nm.w1 || r.name2 != nm.w2) return false;
-  return long_tail_equal(arena, r.name0 >> 32, src, nm.off, nm.len);
+  return long_tail_equal<Co>(arena, r.name0 >> 32, src, nm.off, nm.len);
 }
 
 enum ProbeResult : int { kFound = 0, kMiss = 1, kPending = 2, kFull = 3 };
@@ -1518,6 +1528,207 @@ __global__ __launch_bounds__(64) void k_fold_wave(
     op = nx;
   }
   if (lane == 0) store_state(r, S);
+}
+
+// ---- small ordered batches: one workgroup, one launch ------------------
+// A batch of at most kSmallMax ops (the Take batcher's batches, single HTTP
+// takes, small mixed streams) in one kernel instead of the ordered
+// pipeline's dozen launches and host round trips: resolve every op, create
+// the missing buckets, order the ops by (slot, seq) and fold every bucket's
+// ops in that order with the same per-op code as the large path (eval_sop).
+//   * resolve: probe() per op (the table is quiescent at kernel start);
+//   * capacity: the host checked the bucket bound; the arena bytes the
+//     missing long names could need are checked here, before any claim: if
+//     they do not fit, hdr->fallback is set and nothing is written (the host
+//     then runs the large path, which grows the arena);
+//   * create: rounds of CAS claims from each missing name's home slot; a
+//     claimer publishes its record (zero state, NEW flag) and a lookup that
+//     meets an unpublished slot with its tag retries after the round's
+//     barrier; later lookups read records and arena coherently (ld_co), as
+//     other waves of this kernel wrote them;
+//   * order: op i's rank among the (slot << 32 | i) keys, counted over LDS;
+//   * fold: one thread per bucket with <= kLongSeg ops, one wave per longer
+//     one (rounds of 64 ops against the current state, as k_fold_wave).
+// The NEW flag of a created bucket is consumed by its fold (store_state), and
+// the creating op gets PHIP_ST_CREATED from step_sop, as on the large path.
+constexpr u32 kSmallMax = 1024;
+struct SmallHdr {
+  u32 created;    // buckets this launch created
+  u32 fallback;   // 1: nothing was done, run the large path
+  u32 full;       // a probe wrapped the table (cannot happen below the load limit)
+  u32 pad;
+};
+
+__device__ inline Rec load_rec_co(const Rec* p) {
+  const u64* q = reinterpret_cast<const u64*>(p);
+  Rec r;
+  r.tag = ld_co(q); r.added = ld_co(q + 1); r.taken = ld_co(q + 2); r.elapsed = (i64)ld_co(q + 3);
+  r.name0 = ld_co(q + 4); r.name1 = ld_co(q + 5); r.created = (i64)ld_co(q + 6); r.name2 = ld_co(q + 7);
+  return r;
+}
+
+__global__ __launch_bounds__(kSmallMax) void k_small_mixed(NamesOffs src, OpView ov, u32 n, Table T,
+                                                         u8* arena, u64 arena_cap,
+                                                         u64* arena_cursor, OutView ow,
+                                                         SmallHdr* hdr) {
+  __shared__ OpRec sop[kSmallMax];
+  __shared__ u32 sval[kSmallMax];
+  __shared__ u64 skey[kSmallMax];
+  __shared__ u32 sorted[kSmallMax];
+  __shared__ u32 lstart[kSmallMax / kLongSeg + 1], lcnt[kSmallMax / kLongSeg + 1];
+  __shared__ u32 nlong, long_need, pending, created, full;
+  const u32 i = threadIdx.x;
+  const bool valid = i < n;
+  if (i == 0) { nlong = 0; long_need = 0; pending = 0; created = 0; full = 0; }
+  // 1. the op (k_pack_ops' record) and its name's slot
+  Name nm{};
+  u32 slot = 0;
+  bool miss = false;
+  if (valid) {
+    const u32 kind = ov.kind ? ov.kind[i] : ov.kind0;
+    OpRec r;
+    r.now = ov.now ? ov.now[i] : ov.now0;
+    if (kind == PHIP_OP_TAKE) {
+      const i64 f = ov.freq[i], pr = ov.per[i];
+      r.x = (u64)rate_interval(f, pr);
+      r.y = as_bits((double)f);             // bucket.go:192
+      r.z = as_bits((double)ov.count[i]);   // bucket.go:215
+    } else {
+      r.x = ov.a[i]; r.y = ov.t[i]; r.z = (u64)ov.e[i];
+    }
+    sop[i] = r;
+    sval[i] = i | (kind << kOpIdxBits);
+    u64 off; u32 len;
+    src.get(i, off, len);
+    load_name_wide<false>(src.blob, off, len, nm);
+    Rec rr;
+    const int pr = probe(T, nm, src.blob, &slot, &rr);
+    miss = pr != kFound;
+  }
+  __syncthreads();
+  // 2. arena room for the missing long names (an upper bound), before any claim
+  if (miss && nm.len > kInlineName) atomicAdd(&long_need, nm.len);
+  __syncthreads();
+  if (long_need && ld_co(arena_cursor) + long_need > arena_cap) {
+    if (i == 0) hdr->fallback = 1;
+    return;
+  }
+  // 3. create the missing buckets, in rounds
+  const u32 mask = T.mask();
+  for (;;) {
+    if (miss) {
+      const u64 tag = T.tag(nm.h);
+      u32 s = T.home(tag), k = 0;
+      for (; k <= mask; ++k, s = (s + 1) & mask) {
+        u64 t = ld_co(&T.recs[s].tag);
+        if (t == 0) {
+          t = atomicCAS(&T.recs[s].tag, 0ull, tag);
+          if (t == 0) {   // claimed: publish (k_publish's record)
+            Rec* q = &T.recs[s];
+            q->added = kEPosZero; q->taken = kEPosZero; q->elapsed = 0;
+            q->created = sop[i].now;
+            q->name1 = nm.w1; q->name2 = nm.w2;
+            u64 w0 = nm.w0;
+            if (nm.len > kInlineName) {
+              const u64 a = atomicAdd(arena_cursor, (u64)nm.len);   // room checked above
+              u64 off; u32 len;
+              src.get(i, off, len);
+              for (u32 b = 0; b < len; ++b) arena[a + b] = src.blob[off + b];
+              w0 = (nm.w0 & 0xFFu) | (a << 32);
+            }
+            T.aux[s] = 0;
+            __threadfence();
+            q->name0 = with_flags(w0, kRecPublished | kRecNew);
+            atomicAdd(&created, 1u);
+            slot = s;
+            miss = false;
+            break;
+          }
+        }
+        if (t == tag) {
+          const Rec r = load_rec_co(&T.recs[s]);
+          if (!(rec_flags(r) & kRecPublished)) { pending = 1; break; }   // its claimer publishes this round
+          if (name_equal<true>(r, nm, src.blob, T.arena)) { slot = s; miss = false; break; }
+        }
+      }
+      if (k > mask) { full = 1; miss = false; }
+    }
+    __threadfence();
+    __syncthreads();
+    const bool again = pending != 0;
+    __syncthreads();
+    if (!again) break;
+    if (i == 0) pending = 0;
+    __syncthreads();
+  }
+  if (full) {   // cannot happen below the load limit the host checked; nothing is folded
+    if (i == 0) { hdr->full = 1; hdr->created = created; }
+    return;
+  }
+  // 4. order: rank of (slot, seq)
+  const u64 key = valid ? ((u64)slot << 32 | i) : ~0ull;
+  skey[i] = key;
+  __syncthreads();
+  if (valid) {
+    u32 rank = 0;
+    for (u32 j = 0; j < n; ++j) rank += skey[j] < key;
+    sorted[rank] = i;
+  }
+  __syncthreads();
+  // 5. fold: position r starts a bucket's segment when its slot differs
+  //    from position r - 1's
+  if (valid) {
+    const u32 sl = (u32)(skey[sorted[i]] >> 32);
+    if (i == 0 || (u32)(skey[sorted[i - 1]] >> 32) != sl) {
+      u32 cnt = 1;
+      while (i + cnt < n && (u32)(skey[sorted[i + cnt]] >> 32) == sl) ++cnt;
+      if (cnt > kLongSeg) {
+        const u32 l = atomicAdd(&nlong, 1u);
+        lstart[l] = i;
+        lcnt[l] = cnt;
+      } else {
+        Rec* rec = &T.recs[sl];
+        FState S = load_state(load_rec_co(rec)), S2;
+        for (u32 j = 0; j < cnt; ++j) {
+          const u32 o = sorted[i + j];
+          const SOp op = make_sop(sop[o], sval[o]);
+          OpOut out;
+          eval_sop(op, S, S2, out);
+          write_out(ow, op.idx, out, S);
+          S = S2;
+        }
+        store_state(rec, S);
+      }
+    }
+  }
+  __syncthreads();
+  const u32 lane = i & 63, wave = i >> 6;
+  for (u32 l = wave; l < nlong; l += kSmallMax / 64) {
+    const u32 r0 = lstart[l], cnt = lcnt[l];
+    Rec* rec = &T.recs[(u32)(skey[sorted[r0]] >> 32)];
+    FState S = load_state(load_rec_co(rec));
+    for (u32 base = 0; base < cnt; base += 64) {
+      const u32 lim = min(64u, cnt - base);
+      const u32 o = sorted[r0 + base + min(lane, lim - 1)];
+      const SOp op = make_sop(sop[o], sval[o]);
+      u32 c = 0;
+      while (c < lim) {   // k_fold_wave's round
+        const bool active = lane >= c && lane < lim;
+        FState S2;
+        OpOut out;
+        bool ch = false;
+        if (active) ch = eval_sop(op, S, S2, out);
+        const u64 m = __ballot(ch);
+        const u32 p = m ? (u32)(__ffsll((long long)m) - 1) : 64u;
+        if (active && lane <= p) write_out(ow, op.idx, out, S);
+        if (p >= 64) break;
+        S = lane_state(S2, p);
+        c = p + 1;
+      }
+    }
+    if (lane == 0) store_state(rec, S);
+  }
+  if (i == 0) hdr->created = created;
 }
 
 // ---- window summaries: skip provably quiet windows of a hot bucket -------

@@ -82,10 +82,11 @@ class GPURepo:
     """A device-resident bucket map (the LocalRepo of repo.go:171-235)."""
 
     def __init__(self, device: int = 0, log2_slots: int = 20, arena_bytes: int = 1 << 24,
-                 max_load_pct: int = 90, debug_tag_bits: int = 0, grow: bool = True):
+                 max_load_pct: int = 90, debug_tag_bits: int = 0, grow: bool = True,
+                 small: bool = True):
         self.L = _lib.load()
-        cfg = phip_config(device, log2_slots, arena_bytes, max_load_pct, debug_tag_bits,
-                          0 if grow else _lib.CFG_NO_GROW, 0)
+        flags = (0 if grow else _lib.CFG_NO_GROW) | (0 if small else _lib.CFG_NO_SMALL)
+        cfg = phip_config(device, log2_slots, arena_bytes, max_load_pct, debug_tag_bits, flags, 0)
         h = C.c_void_p()
         rc = self.L.phip_open(C.byref(cfg), C.byref(h))
         if rc != 0:

@@ -325,6 +325,51 @@ def test_mixed_hot_adversarial_all_fold_kinds(pa):
     _check_mixed(pa, args, 13, reply=True)
 
 
+def test_small_batches_one_launch_vs_large_path_and_oracle(pa):
+    """Ordered batches of <= 1024 host ops run as one launch (k_small_mixed).
+    A stream of small batches exercises every op kind: odd rates, dirty
+    states with incast replies, upserts, new short and long names repeated
+    inside a batch, and a bucket with more than 32 ops in one batch (the
+    wave fold). Each batch must give the same statuses, remaining, have and
+    replies, and the same table, on the small path, on the large path
+    (PHIP_CFG_NO_SMALL) and in the oracle."""
+    rng = np.random.default_rng(9090)
+    small = pa.GPURepo(log2_slots=12, arena_bytes=1 << 16)
+    large = pa.GPURepo(log2_slots=12, arena_bytes=1 << 16, small=False)
+    o = O.Repo()
+    longs = [b"a-long-bucket-name-for-the-arena-%03d" % k for k in range(40)]
+    t0 = _gen.T0
+    for step, n in enumerate([1, 2, 33, 500, 1024, 1025, 700, 64, 1024]):
+        args = list(_mixed_stream(rng, n, 300))
+        names = list(args[1])
+        for k in np.nonzero(rng.random(n) < 0.1)[0]:
+            names[k] = longs[int(rng.integers(0, len(longs)))]
+        hot = rng.random(n) < 0.2
+        for k in np.nonzero(hot)[0]:
+            names[k] = b"hot-bucket"
+        args[1] = names
+        args[0] = rng.choice(np.array([0, 1, 2], np.uint8), n, p=[0.5, 0.4, 0.1])
+        a, t, e = _gen.dirty_states(rng, n, 0.1)
+        args[6], args[7], args[8] = a, t, e
+        args[2] = t0 + step * SEC + np.arange(n, dtype=np.int64) * 1000
+        outs = [r.apply_mixed(*args) for r in (small, large)]
+        ref = o.apply_mixed(*args)
+        take = args[0] == 0
+        rep = (ref["status"] & 0x7F) == 2
+        for out in outs:
+            assert np.array_equal(out["status"], ref["status"]), step
+            assert np.array_equal(out["remaining"], ref["remaining"]), step
+            assert np.array_equal(out["have"][take], ref["have"][take]), step
+            r = out["reply"][rep]
+            assert np.array_equal(r["a"], ref["reply_added"][rep]), step
+            assert np.array_equal(r["t"], ref["reply_taken"][rep]), step
+            assert np.array_equal(r["e"], ref["reply_elapsed"][rep]), step
+    want = o.dump()
+    assert_same_dump(gpu_dump(small), want)
+    assert_same_dump(gpu_dump(large), want)
+    assert len(small) == len(large) == len(want)
+
+
 def test_mixed_c3_shape_clamped_clock(pa):
     """The bench's C3 shape: replica elapsed far ahead of the local clock, so
     Take's `last` is clamped to now (bucket.go:199-201) and tokens come only
