@@ -747,6 +747,12 @@ def main():
         step_s = el / args.steps
         extra["allreduce_bytes"] = allreduce_bytes
         extra["replicas_total"] = R * world
+        ar_ms = kms.get("rccl_allreduce")
+        if ar_ms:   # HIP events around the RCCL call (phip_group_anti_entropy)
+            algbw = allreduce_bytes / (ar_ms / 1e3) / 1e9
+            extra["allreduce_ms"] = ar_ms
+            extra["allreduce_algbw_GBps"] = algbw
+            extra["allreduce_busbw_GBps"] = algbw * 2 * (world - 1) / world
     elif args.workload == "c4":
         bpo = BYTES_PER_MERGE
         dom_name, dom_ms = DOMINANT, float(np.mean(kern.get(DOMINANT, [float("nan")])))
@@ -759,6 +765,8 @@ def main():
         # the sender-side combine, not the n messages it sent
         extra["messages_sent_per_step_rank0"] = n
         extra["messages_merged_per_step_rank0"] = float(np.mean(c4_merged))
+        if "rccl_exchange" in kms:   # the grouped send/recv of the packed segments
+            extra["exchange_ms"] = kms["rccl_exchange"]
     elif args.workload == "c3":
         # Take 89 B (op 24 + state read 32 + write 24 + result 9), Merge 88 B.
         bpo = 88.5

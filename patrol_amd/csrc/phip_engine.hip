@@ -2045,4 +2045,14 @@ int phip_last_stats(phip_handle* h, uint64_t* out, int max) {
 namespace phip_host {
 void* handle_stream(phip_handle* h) { return h ? (void*)h->stream : nullptr; }
 int handle_device(const phip_handle* h) { return h ? h->device : -1; }
+void* timing_begin(phip_handle* h, const char* name) {
+  if (!h) return nullptr;
+  std::lock_guard<std::mutex> g(h->mu);
+  return h->timing ? new Launch(h, name) : nullptr;
+}
+void timing_end(phip_handle* h, void* token) {
+  if (!h || !token) return;
+  std::lock_guard<std::mutex> g(h->mu);
+  delete static_cast<Launch*>(token);   // records the end event
+}
 }  // namespace phip_host

@@ -215,6 +215,7 @@ int member_receive(phip_group* g, Member& mb, const phip_msgs& in, int64_t now, 
   // 3. the segments: one send and one receive per peer and column; this
   // member's own segment is a device copy (no RCCL round trip through its
   // buffers)
+  void* tm = phip_host::timing_begin(mb.h, "rccl_exchange");
   GNCCL(mb, ncclGroupStart());
   u64 so = 0, sb = 0, ro = 0, rb = 0;
   for (u32 p = 0; p < W; ++p) {
@@ -246,6 +247,7 @@ int member_receive(phip_group* g, Member& mb, const phip_msgs& in, int64_t now, 
     so += sc; sb += sbytes; ro += rc; rb += rbytes;
   }
   GNCCL(mb, ncclGroupEnd());
+  phip_host::timing_end(mb.h, tm);
   if (n_recv == 0) return PHIP_OK;
   return merge_received(mb, st, (const u32*)mb.r_lens.p, (const uint8_t*)mb.r_names.p,
                         (const u64*)mb.r_a.p, (const u64*)mb.r_t.p, (const int64_t*)mb.r_e.p, n_recv,
@@ -259,7 +261,9 @@ int member_anti_entropy(phip_group* g, Member& mb, int64_t* reps, uint32_t nrep,
   GHIP(mb, mb.ae.ensure((size_t)3 * B * 8));
   int64_t* j = (int64_t*)mb.ae.p;
   GPHIP(mb, phip_ae_local_max(mb.h, reps, nrep, B, j, PHIP_DEVICE_PTRS));
+  void* tm = phip_host::timing_begin(mb.h, "rccl_allreduce");
   GNCCL(mb, ncclAllReduce(j, j, 3 * B, ncclInt64, ncclMax, mb.comm, st));
+  phip_host::timing_end(mb.h, tm);
   GPHIP(mb, phip_ae_apply(mb.h, reps, nrep, B, j, PHIP_DEVICE_PTRS));
   return PHIP_OK;
 }

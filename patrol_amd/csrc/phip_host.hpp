@@ -11,6 +11,12 @@ namespace phip_host {
 void* handle_stream(phip_handle* h);
 int handle_device(const phip_handle* h);
 
+// A timed region on the handle's stream (HIP events, like the engine's own
+// kernels; nothing when timing is off): the group's RCCL calls show up in
+// phip_last_timings under `name`.  timing_end takes what timing_begin gave.
+void* timing_begin(phip_handle* h, const char* name);
+void timing_end(phip_handle* h, void* token);
+
 // The request parsing of API.takeBucket (api.go:55-65): the name-length check
 // (returns 400 with ErrNameTooLarge's text as the body), ParseRate with its
 // error ignored (the Rate Go returns beside the error), count 0 / error -> 1.
