@@ -412,6 +412,26 @@ __device__ inline void short_name(u64 w0, u64 w1, u64 w2, u64 off, u32 len, Name
   nm.w2 = 0;
 }
 
+// FNV-1a and canonical words of an inline name of kShortName < len <=
+// kInlineName bytes from the words the fast kernel already loaded (w0..w2 as
+// load_words3 returns them) and the next word w3 (clamped like them).
+__device__ inline void inline_name(u64 w0, u64 w1, u64 w2, u64 w3, u64 off, u32 len, Name& nm) {
+  const u32 sh = (u32)(off & 7) * 8;
+  const u64 b0 = sh ? (w0 >> sh) | (w1 << (64 - sh)) : w0;
+  u64 b1 = sh ? (w1 >> sh) | (w2 << (64 - sh)) : w1;
+  u64 b2 = sh ? (w2 >> sh) | (w3 << (64 - sh)) : w2;
+  b1 = low_bytes(b1, len - 8);
+  b2 = len > 16 ? low_bytes(b2, len - 16) : 0;
+  u32 lo = (u32)kFnvOffset, hi = (u32)(kFnvOffset >> 32);
+  fnv_word32(lo, hi, b0, 8);
+  fnv_word32(lo, hi, b1, len - 8);
+  if (len > 16) fnv_word32(lo, hi, b2, len - 16);
+  nm.h = ((u64)hi << 32) | lo; nm.len = len; nm.off = off;
+  nm.w0 = (u64)len | (b0 << 16);     // name byte k sits at canonical byte k+2
+  nm.w1 = (b0 >> 48) | (b1 << 16);
+  nm.w2 = (b1 >> 48) | (b2 << 16);
+}
+
 // enc_replica for a replica field that is not -0.0 (the fast path's batches
 // hold none), without branches.
 __device__ inline u64 enc_replica_nz(u64 b) {
@@ -868,10 +888,17 @@ __global__ __launch_bounds__(kFastBlock) __attribute__((amdgpu_waves_per_eu(8, 8
     // the directory match.
     u64 tail[kHotTailWords] = {};
     if (!shortname) {
-      // (decoded batches only: the datagram form keeps its registers for
-      // the wire decode)
-      if (In::kSoa && len > kInlineName && len <= kHotTailName) load_name_tail(in.blob(), off, len, nm, tail);
-      else load_name_wide<true>(in.blob(), off, len, nm);
+      if (len <= kInlineName) {   // one more word than round 2 loaded
+        const u64* bw = reinterpret_cast<const u64*>(in.blob());
+        const u64 last = (off + len - 1) >> 3, w3i = (off >> 3) + 3;
+        inline_name(w0, w1, w2, bw[w3i < last ? w3i : last], off, len, nm);
+      } else if (In::kSoa && len <= kHotTailName) {
+        // (decoded batches only: the datagram form keeps its registers
+        // for the wire decode)
+        load_name_tail(in.blob(), off, len, nm, tail);
+      } else {
+        load_name_wide<true>(in.blob(), off, len, nm);
+      }
     }
     const u64 tag = T.tag(nm.h);
     const u64 ea = enc_replica_nz(ra), et = enc_replica_nz(rt), ee = (u64)re ^ kSign;
