@@ -896,9 +896,10 @@ int ordered(phip_handle* h, Src src, u32 n, const OpView& ov, const OutView& ow)
         const u32 k = ord[i];
         const u64* e = &d[16 * k];
         fprintf(stderr, "fold[%u] ops %llu windows %llu folded %llu rounds %llu bursts %llu walked "
-                "%llu runs %llu us %.1f | scan %.1f stage %.1f prefix %.1f round %.1f burst %.1f\n",
+                "%llu runs %llu us %.1f | scan %.1f stage %.1f prefix %.1f round %.1f burst %.1f "
+                "| burst iterations %llu (stopped at a merge %llu)\n",
                 k, e[0], e[1], e[2], e[3], e[4], e[5], e[6], e[7] / 100.0, e[8] / 100.0,
-                e[9] / 100.0, e[10] / 100.0, e[11] / 100.0, e[12] / 100.0);
+                e[9] / 100.0, e[10] / 100.0, e[11] / 100.0, e[12] / 100.0, e[13], e[14]);
       }
     }
   }

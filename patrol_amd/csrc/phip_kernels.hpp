@@ -2062,6 +2062,7 @@ struct FoldShared {
   u64 state[8];
   u32 cur, nrun, exact_from;
   u32 n_burst, n_walk;   // diagnostics (k_fold_block's dbg)
+  u32 n_iter, n_raise;   // burst iterations; those that stopped at a merge
   u64 prof[6];           // diagnostics: wall-clock ticks per phase (dbg only)
   u32 profiling;
 };
@@ -2348,7 +2349,9 @@ __device__ inline void fold_window_absorb(u32 pos, u32 lim, FState& R, GMax& G, 
         }
         const u32 q = (u32)__ffsll((long long)mb) - 1;
         const FState Y = lane_state(X2, q);
-        if ((__ballot(chg) >> q) & 1) {
+        const bool q_chg = (__ballot(chg) >> q) & 1;
+        if (lane == 0) { ++sh.n_iter; sh.n_raise += !q_chg; }
+        if (q_chg) {
           if (!state_grew(X, Y)) exact_from = nrun;
           if (lane == 0) put_run(rp, rs, nrun, pos + j + q + 1, Y);
           ++nrun;
@@ -2421,6 +2424,8 @@ __global__ __launch_bounds__(kFoldThreads) void k_fold_block(
     sh.exact_from = 0xFFFFFFFFu;
     sh.n_burst = 0;
     sh.n_walk = 0;
+    sh.n_iter = 0;
+    sh.n_raise = 0;
     sh.profiling = dbg != nullptr;
     for (u32 k = 0; k < 6; ++k) sh.prof[k] = 0;
   }
@@ -2522,7 +2527,9 @@ __global__ __launch_bounds__(kFoldThreads) void k_fold_block(
       u64* d = dbg + (u64)blockIdx.x * 16;
       d[0] = cnt; d[1] = nwin; d[2] = n_folded; d[3] = round; d[4] = sh.n_burst;
       d[5] = sh.n_walk; d[6] = sh.nrun; d[7] = wall_clock64() - t_begin;
-      for (u32 k = 0; k < 6; ++k) d[8 + k] = sh.prof[k];
+      for (u32 k = 0; k < 5; ++k) d[8 + k] = sh.prof[k];
+      d[13] = sh.n_iter;
+      d[14] = sh.n_raise;
     }
   }
 }
