@@ -1035,6 +1035,191 @@ int receive_decoded(phip_handle* h, Src src, const uint64_t* a, const uint64_t* 
   return finish_receive(h, src, a, t, e, n, fd, nmiss, now, ow);
 }
 
+// A host-pointer batch of at most kSmallMax ops through k_small_mixed: one
+// pinned copy in, one launch, one pinned copy out (the large path takes a
+// dozen launches and several host round trips, ~0.2 ms whatever the size).
+// *done = false leaves the batch to the large path with nothing changed: too
+// many ops or name bytes, a bucket bound past the load limit (the large path
+// grows the table), or a long-name arena the kernel found too small.
+int small_mixed(phip_handle* h, const phip_ops* ops, const phip_results* res, bool* done) {
+  *done = false;
+  const u32 n = ops->n;
+  if (n > kSmallMax || h->n_buckets + n > h->max_load) return PHIP_OK;
+  const u64 nbytes = ops->name_offs[n];
+  if (nbytes > (u64)kSmallMax * PHIP_MAX_NAME_LEN) return PHIP_OK;
+  auto al = [](size_t x) { return (x + 15) & ~(size_t)15; };
+  const bool take = ops->freq != nullptr, state = ops->added != nullptr;
+  // inputs: offsets | kind | now | freq per count | added taken elapsed | names
+  const size_t o_kind = al(4 * ((size_t)n + 1)), o_now = o_kind + al(n), o_freq = o_now + 8 * n;
+  const size_t o_per = o_freq + 8 * n, o_count = o_per + 8 * n, o_a = o_count + 8 * n;
+  const size_t o_t = o_a + 8 * n, o_e = o_t + 8 * n, o_names = o_e + 8 * n;
+  const size_t in_bytes = al(o_names + nbytes + 8);
+  // outputs: header | status | remaining | have | reply
+  const size_t o_st = sizeof(SmallHdr), o_rem = al(o_st + n), o_have = o_rem + 8 * n;
+  const size_t o_reply = o_have + 8 * n, out_bytes = o_reply + sizeof(phip_state) * n;
+  const size_t total = in_bytes + out_bytes;
+  if (h->small_pin_cap < total) {
+    if (h->small_pin) HIPCHK(h, hipHostFree(h->small_pin));
+    h->small_pin = nullptr;
+    h->small_pin_cap = 0;
+    const size_t want = std::max<size_t>(total, 1 << 20);
+    HIPCHK(h, hipHostMalloc(&h->small_pin, want, 0));
+    h->small_pin_cap = want;
+  }
+  u8 *d = nullptr, *pin = h->small_pin;
+  int rc;
+  if ((rc = ensure(h, B_SMALL, total, &d))) return rc;
+  std::memcpy(pin, ops->name_offs, 4 * ((size_t)n + 1));
+  std::memcpy(pin + o_kind, ops->kind, n);
+  std::memcpy(pin + o_now, ops->now, 8 * n);
+  if (take) {
+    std::memcpy(pin + o_freq, ops->freq, 8 * n);
+    std::memcpy(pin + o_per, ops->per, 8 * n);
+    std::memcpy(pin + o_count, ops->count, 8 * n);
+  }
+  if (state) {
+    std::memcpy(pin + o_a, ops->added, 8 * n);
+    std::memcpy(pin + o_t, ops->taken, 8 * n);
+    std::memcpy(pin + o_e, ops->elapsed, 8 * n);
+  }
+  std::memcpy(pin + o_names, ops->names, nbytes);
+  std::memset(pin + o_names + nbytes, 0, 8);
+  std::memset(pin + in_bytes, 0, sizeof(SmallHdr));
+  HIPCHK(h, hipMemcpyAsync(d, pin, in_bytes + sizeof(SmallHdr), hipMemcpyHostToDevice, h->stream));
+  NamesOffs src{d + o_names, (const u32*)d};
+  OpView ov{};
+  ov.kind = d + o_kind;
+  ov.now = (const int64_t*)(d + o_now);
+  if (take) {
+    ov.freq = (const int64_t*)(d + o_freq);
+    ov.per = (const int64_t*)(d + o_per);
+    ov.count = (const uint64_t*)(d + o_count);
+  }
+  if (state) {
+    ov.a = (const uint64_t*)(d + o_a);
+    ov.t = (const uint64_t*)(d + o_t);
+    ov.e = (const int64_t*)(d + o_e);
+  }
+  u8* dout = d + in_bytes;
+  phip_results r{};
+  if (res) r = *res;
+  OutView ow{};
+  ow.status = r.status ? dout + o_st : nullptr;
+  ow.remaining = r.remaining ? (uint64_t*)(dout + o_rem) : nullptr;
+  ow.have = r.have ? (uint64_t*)(dout + o_have) : nullptr;
+  ow.reply = r.reply ? (phip_state*)(dout + o_reply) : nullptr;
+  {
+    Launch l(h, "k_small_mixed");
+    k_small_mixed<<<1, kSmallMax, 0, h->stream>>>(src, ov, n, table(h), h->arena, h->arena_cap,
+                                                  h->arena_cursor, ow, (SmallHdr*)dout);
+  }
+  HIPCHK(h, hipGetLastError());
+  // the header and the columns the caller asked for, in one copy
+  const size_t back = r.reply ? out_bytes : r.have ? o_reply : r.remaining ? o_have : o_rem;
+  u8* pout = pin + in_bytes;
+  HIPCHK(h, hipMemcpyAsync(pout, dout, back, hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  SmallHdr hd;
+  std::memcpy(&hd, pout, sizeof hd);
+  h->n_buckets += hd.created;
+  if (hd.fallback) return PHIP_OK;
+  if (hd.full) return set_err(h, PHIP_ERR_FULL, "internal: small batch probe wrapped the table");
+  if (r.status) std::memcpy(r.status, pout + o_st, n);
+  if (r.remaining) std::memcpy(r.remaining, pout + o_rem, 8 * n);
+  if (r.have) std::memcpy(r.have, pout + o_have, 8 * n);
+  if (r.reply) {
+    // an op's reply is defined only for INCAST_REPLY statuses; copy those
+    const phip_state* src_r = (const phip_state*)(pout + o_reply);
+    std::vector<u8> st;
+    const u8* stp = r.status;
+    if (!stp) {
+      st.assign(n, 0);
+      HIPCHK(h, hipMemcpy(st.data(), dout + o_st, n, hipMemcpyDeviceToHost));
+      stp = st.data();
+    }
+    for (u32 i = 0; i < n; ++i)
+      if ((stp[i] & 0x7F) == PHIP_ST_INCAST_REPLY) r.reply[i] = src_r[i];
+  }
+  *done = true;
+  return PHIP_OK;
+}
+
+
+// A uniform-kind host batch (Receive or Upsert of decoded states, all at one
+// clock reading) through small_mixed: the ordered code is the same Go loop
+// (repo.go:78-90, :215-235), so statuses, replies and states are those of
+// the large paths.
+int small_uniform(phip_handle* h, const phip_msgs* m, u8 kind, int64_t now, const phip_results* res,
+                  bool* done) {
+  *done = false;
+  if (!h->small || m->n > kSmallMax) return PHIP_OK;
+  std::vector<u8> kinds(m->n, kind);
+  std::vector<int64_t> nows(m->n, now);
+  phip_ops ops{};
+  ops.n = m->n;
+  ops.kind = kinds.data();
+  ops.names = m->names;
+  ops.name_offs = m->name_offs;
+  ops.now = nows.data();
+  ops.added = m->added;
+  ops.taken = m->taken;
+  ops.elapsed = m->elapsed;
+  return small_mixed(h, &ops, res, done);
+}
+
+// ReplicatedRepo.Receive over at most kSmallMax host datagrams: decoded on
+// the host (UnmarshalBinary, bucket.go:71-91: a datagram under 25 bytes or
+// shorter than its name is io.ErrShortBuffer, where the Go loop stops), the
+// prefix before the first short one through small_mixed.
+int small_datagrams(phip_handle* h, const uint8_t* bytes, const uint64_t* offs, uint32_t n,
+                    int64_t now, const phip_results* res, uint32_t* stop_index, bool* done) {
+  *done = false;
+  if (!h->small || n > kSmallMax) return PHIP_OK;
+  std::vector<uint64_t> a(n), t(n);
+  std::vector<int64_t> e(n);
+  std::vector<uint32_t> no(n + 1);
+  std::vector<uint8_t> names;
+  names.reserve((size_t)n * 16 + 8);
+  auto be64 = [](const uint8_t* p) {
+    uint64_t v = 0;
+    for (int k = 0; k < 8; ++k) v = (v << 8) | p[k];
+    return v;
+  };
+  u32 stop = n;
+  for (u32 i = 0; i < n; ++i) {
+    const uint8_t* d = bytes + offs[i];
+    const uint64_t sz = offs[i + 1] - offs[i];
+    if (sz < PHIP_BUCKET_FIXED_SIZE || sz - PHIP_BUCKET_FIXED_SIZE < d[24]) { stop = i; break; }
+    a[i] = be64(d);
+    t[i] = be64(d + 8);
+    e[i] = (int64_t)be64(d + 16);
+    no[i] = (uint32_t)names.size();
+    names.insert(names.end(), d + PHIP_BUCKET_FIXED_SIZE, d + PHIP_BUCKET_FIXED_SIZE + d[24]);
+  }
+  no[stop] = (uint32_t)names.size();
+  names.resize(names.size() + 8, 0);
+  if (stop) {
+    phip_msgs m{};
+    m.n = stop;
+    m.names = names.data();
+    m.name_offs = no.data();
+    m.added = a.data();
+    m.taken = t.data();
+    m.elapsed = e.data();
+    bool ok = false;
+    int rc;
+    if ((rc = small_uniform(h, &m, PHIP_OP_RECEIVE, now, res, &ok))) return rc;
+    if (!ok) return PHIP_OK;   // the large path takes the whole batch
+  }
+  if (res && res->status && stop < n) {   // the short datagram and everything after it
+    std::memset(res->status + stop, PHIP_ST_NOT_PROCESSED, n - stop);
+    res->status[stop] = PHIP_ST_SHORT;
+  }
+  if (stop_index) *stop_index = stop;
+  *done = true;
+  if (stop < n) return set_err(h, PHIP_ERR_SHORT_BUFFER, "short buffer at datagram %u", stop);
+  return PHIP_OK;
+}
 }  // namespace
 
 // ===================================================================== ABI
@@ -1394,6 +1579,11 @@ int phip_receive_soa(phip_handle* h, const phip_msgs* m, int64_t now, const phip
   bool dev = flags & PHIP_DEVICE_PTRS;
   if (!dev && !names_ok(m->name_offs, n)) return set_err(h, PHIP_ERR_NAME_TOO_LARGE, "name > 231 bytes");
   int rc;
+  if (!dev) {
+    bool done = false;
+    if ((rc = small_uniform(h, m, PHIP_OP_RECEIVE, now, res, &done))) return after_error(h, rc);
+    if (done) return PHIP_OK;
+  }
   NamesOffs src;
   const uint64_t *a, *t;
   const int64_t* e;
@@ -1473,6 +1663,11 @@ int phip_receive_datagrams(phip_handle* h, const uint8_t* bytes, const uint64_t*
   const u8* d_bytes;
   if (!dev && !datagrams_ok(offs, n))
     return set_err(h, PHIP_ERR_INVALID, "datagram offsets decrease");
+  if (!dev) {
+    bool done = false;
+    rc = small_datagrams(h, bytes, offs, n, now, res, stop_index, &done);
+    if (done || (rc && rc != PHIP_ERR_SHORT_BUFFER)) return rc == PHIP_ERR_SHORT_BUFFER ? rc : after_error(h, rc);
+  }
   if ((rc = stage(h, B_DOFFS, offs, (size_t)n + 1, dev, &d_offs))) return rc;
   size_t nb = dev ? 0 : offs[n];
   if ((rc = stage(h, B_BYTES, bytes, nb, dev, &d_bytes))) return rc;
@@ -1635,6 +1830,11 @@ int phip_upsert_soa(phip_handle* h, const phip_msgs* m, int64_t now, const phip_
   bool dev = flags & PHIP_DEVICE_PTRS;
   if (!dev && !names_ok(m->name_offs, n)) return set_err(h, PHIP_ERR_NAME_TOO_LARGE, "name > 231 bytes");
   int rc;
+  if (!dev) {
+    bool done = false;
+    if ((rc = small_uniform(h, m, PHIP_OP_UPSERT, now, res, &done))) return after_error(h, rc);
+    if (done) return PHIP_OK;
+  }
   NamesOffs src;
   const uint64_t *a, *t;
   const int64_t* e;
@@ -1649,115 +1849,6 @@ int phip_upsert_soa(phip_handle* h, const phip_msgs* m, int64_t now, const phip_
   ov.a = a; ov.t = t; ov.e = e;
   if ((rc = ordered(h, src, n, ov, ow))) return after_error(h, rc);
   return copy_outputs(h, res, n, dev, ow);
-}
-
-// A host-pointer batch of at most kSmallMax ops through k_small_mixed: one
-// pinned copy in, one launch, one pinned copy out (the large path takes a
-// dozen launches and several host round trips, ~0.2 ms whatever the size).
-// *done = false leaves the batch to the large path with nothing changed: too
-// many ops or name bytes, a bucket bound past the load limit (the large path
-// grows the table), or a long-name arena the kernel found too small.
-int small_mixed(phip_handle* h, const phip_ops* ops, const phip_results* res, bool* done) {
-  *done = false;
-  const u32 n = ops->n;
-  if (n > kSmallMax || h->n_buckets + n > h->max_load) return PHIP_OK;
-  const u64 nbytes = ops->name_offs[n];
-  if (nbytes > (u64)kSmallMax * PHIP_MAX_NAME_LEN) return PHIP_OK;
-  auto al = [](size_t x) { return (x + 15) & ~(size_t)15; };
-  const bool take = ops->freq != nullptr, state = ops->added != nullptr;
-  // inputs: offsets | kind | now | freq per count | added taken elapsed | names
-  const size_t o_kind = al(4 * ((size_t)n + 1)), o_now = o_kind + al(n), o_freq = o_now + 8 * n;
-  const size_t o_per = o_freq + 8 * n, o_count = o_per + 8 * n, o_a = o_count + 8 * n;
-  const size_t o_t = o_a + 8 * n, o_e = o_t + 8 * n, o_names = o_e + 8 * n;
-  const size_t in_bytes = al(o_names + nbytes + 8);
-  // outputs: header | status | remaining | have | reply
-  const size_t o_st = sizeof(SmallHdr), o_rem = al(o_st + n), o_have = o_rem + 8 * n;
-  const size_t o_reply = o_have + 8 * n, out_bytes = o_reply + sizeof(phip_state) * n;
-  const size_t total = in_bytes + out_bytes;
-  if (h->small_pin_cap < total) {
-    if (h->small_pin) HIPCHK(h, hipHostFree(h->small_pin));
-    h->small_pin = nullptr;
-    h->small_pin_cap = 0;
-    const size_t want = std::max<size_t>(total, 1 << 20);
-    HIPCHK(h, hipHostMalloc(&h->small_pin, want, 0));
-    h->small_pin_cap = want;
-  }
-  u8 *d = nullptr, *pin = h->small_pin;
-  int rc;
-  if ((rc = ensure(h, B_SMALL, total, &d))) return rc;
-  std::memcpy(pin, ops->name_offs, 4 * ((size_t)n + 1));
-  std::memcpy(pin + o_kind, ops->kind, n);
-  std::memcpy(pin + o_now, ops->now, 8 * n);
-  if (take) {
-    std::memcpy(pin + o_freq, ops->freq, 8 * n);
-    std::memcpy(pin + o_per, ops->per, 8 * n);
-    std::memcpy(pin + o_count, ops->count, 8 * n);
-  }
-  if (state) {
-    std::memcpy(pin + o_a, ops->added, 8 * n);
-    std::memcpy(pin + o_t, ops->taken, 8 * n);
-    std::memcpy(pin + o_e, ops->elapsed, 8 * n);
-  }
-  std::memcpy(pin + o_names, ops->names, nbytes);
-  std::memset(pin + o_names + nbytes, 0, 8);
-  std::memset(pin + in_bytes, 0, sizeof(SmallHdr));
-  HIPCHK(h, hipMemcpyAsync(d, pin, in_bytes + sizeof(SmallHdr), hipMemcpyHostToDevice, h->stream));
-  NamesOffs src{d + o_names, (const u32*)d};
-  OpView ov{};
-  ov.kind = d + o_kind;
-  ov.now = (const int64_t*)(d + o_now);
-  if (take) {
-    ov.freq = (const int64_t*)(d + o_freq);
-    ov.per = (const int64_t*)(d + o_per);
-    ov.count = (const uint64_t*)(d + o_count);
-  }
-  if (state) {
-    ov.a = (const uint64_t*)(d + o_a);
-    ov.t = (const uint64_t*)(d + o_t);
-    ov.e = (const int64_t*)(d + o_e);
-  }
-  u8* dout = d + in_bytes;
-  phip_results r{};
-  if (res) r = *res;
-  OutView ow{};
-  ow.status = r.status ? dout + o_st : nullptr;
-  ow.remaining = r.remaining ? (uint64_t*)(dout + o_rem) : nullptr;
-  ow.have = r.have ? (uint64_t*)(dout + o_have) : nullptr;
-  ow.reply = r.reply ? (phip_state*)(dout + o_reply) : nullptr;
-  {
-    Launch l(h, "k_small_mixed");
-    k_small_mixed<<<1, kSmallMax, 0, h->stream>>>(src, ov, n, table(h), h->arena, h->arena_cap,
-                                                  h->arena_cursor, ow, (SmallHdr*)dout);
-  }
-  HIPCHK(h, hipGetLastError());
-  // the header and the columns the caller asked for, in one copy
-  const size_t back = r.reply ? out_bytes : r.have ? o_reply : r.remaining ? o_have : o_rem;
-  u8* pout = pin + in_bytes;
-  HIPCHK(h, hipMemcpyAsync(pout, dout, back, hipMemcpyDeviceToHost, h->stream));
-  HIPCHK(h, hipStreamSynchronize(h->stream));
-  SmallHdr hd;
-  std::memcpy(&hd, pout, sizeof hd);
-  h->n_buckets += hd.created;
-  if (hd.fallback) return PHIP_OK;
-  if (hd.full) return set_err(h, PHIP_ERR_FULL, "internal: small batch probe wrapped the table");
-  if (r.status) std::memcpy(r.status, pout + o_st, n);
-  if (r.remaining) std::memcpy(r.remaining, pout + o_rem, 8 * n);
-  if (r.have) std::memcpy(r.have, pout + o_have, 8 * n);
-  if (r.reply) {
-    // an op's reply is defined only for INCAST_REPLY statuses; copy those
-    const phip_state* src_r = (const phip_state*)(pout + o_reply);
-    std::vector<u8> st;
-    const u8* stp = r.status;
-    if (!stp) {
-      st.assign(n, 0);
-      HIPCHK(h, hipMemcpy(st.data(), dout + o_st, n, hipMemcpyDeviceToHost));
-      stp = st.data();
-    }
-    for (u32 i = 0; i < n; ++i)
-      if ((stp[i] & 0x7F) == PHIP_ST_INCAST_REPLY) r.reply[i] = src_r[i];
-  }
-  *done = true;
-  return PHIP_OK;
 }
 
 int phip_apply_mixed(phip_handle* h, const phip_ops* ops, const phip_results* res, uint32_t flags) {

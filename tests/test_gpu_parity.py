@@ -370,6 +370,53 @@ def test_small_batches_one_launch_vs_large_path_and_oracle(pa):
     assert len(small) == len(large) == len(want)
 
 
+def test_small_receive_upsert_datagrams_one_launch_vs_large_path(pa):
+    """Host Receive / Upsert / datagram batches of <= 1024 messages run as one
+    launch too (small_uniform, small_datagrams): statuses, incast replies,
+    the short-datagram stop and the table equal the large paths' and the
+    oracle's."""
+    import struct
+    rng = np.random.default_rng(4242)
+    small = pa.GPURepo(log2_slots=12, arena_bytes=1 << 16)
+    large = pa.GPURepo(log2_slots=12, arena_bytes=1 << 16, small=False)
+    o = O.Repo()
+    longs = [b"receive-path-long-name-for-the-arena-%02d" % k for k in range(20)]
+    for step, n in enumerate([1, 40, 777, 1024, 1025, 300]):
+        ids = _gen.zipf_ids(rng, n, 500)
+        names = [longs[i % 20] if i % 7 == 0 else b"r%d" % i for i in ids]
+        a, t, e = _gen.dirty_states(rng, n, 0.15)
+        now = _gen.T0 + step * SEC
+        mode = step % 3
+        if mode == 0:
+            outs = [r.receive_soa(names, a, t, e, now) for r in (small, large)]
+            st, ra, rt, re_ = o.receive_soa(names, a, t, e, now)
+            rep = (st & 0x7F) == 2
+            for out in outs:
+                assert np.array_equal(out["status"], st), step
+                r = out["reply"][rep]
+                assert np.array_equal(r["a"], ra[rep]) and np.array_equal(r["t"], rt[rep]), step
+                assert np.array_equal(r["e"], re_[rep]), step
+        elif mode == 1:
+            outs = [r.upsert_soa(names, a, t, e, now) for r in (small, large)]
+            merged = o.upsert_soa(names, a, t, e, now)
+            assert np.array_equal(outs[0]["status"], outs[1]["status"]), step
+            assert np.array_equal((outs[0]["status"] & 0x7F) == 1, merged.astype(bool)), step
+        else:
+            dgs = [struct.pack(">QQQ", int(a[i]), int(t[i]), int(e[i]) & (2**64 - 1))
+                   + bytes([len(names[i])]) + names[i] for i in range(n)]
+            cut = n // 2
+            dgs[cut] = dgs[cut][:20]                      # io.ErrShortBuffer there
+            outs = [r.receive_datagrams(dgs, now) for r in (small, large)]
+            st, _, _, _ = o.receive_soa(names[:cut], a[:cut], t[:cut], e[:cut], now)
+            for out in outs:
+                assert out["stop"] == cut, step
+                assert np.array_equal(out["status"][:cut], st), step
+                assert out["status"][cut] == 4 and (out["status"][cut + 1:] == 5).all(), step
+    want = o.dump()
+    assert_same_dump(gpu_dump(small), want)
+    assert_same_dump(gpu_dump(large), want)
+
+
 def test_mixed_c3_shape_clamped_clock(pa):
     """The bench's C3 shape: replica elapsed far ahead of the local clock, so
     Take's `last` is clamped to now (bucket.go:199-201) and tokens come only
