@@ -1802,13 +1802,29 @@ int phip_ring_receive(phip_ring* r, uint32_t slot, int64_t now, const phip_resul
     std::lock_guard<std::mutex> g(h->mu);
     if ((rc = begin_call(h))) return rc;
     if (stop_index) *stop_index = s->n;
-    hipError_t e = hipStreamWaitEvent(h->stream, s->copied, 0);
-    if (e != hipSuccess)
-      rc = set_err(h, PHIP_ERR_HIP, "hipStreamWaitEvent: %s", hipGetErrorString(e));
-    else if (s->n == 0)
-      rc = PHIP_OK;
-    else
-      rc = receive_datagrams_dev(h, s->dbytes, s->doffs, s->n, now, res, stop_index, false);
+    // A small slot is merged from its pinned host bytes in one launch (the
+    // device copy is not waited for; the slot is freed only after it
+    // finished, below); a larger one from the device copy.
+    bool done = false;
+    if (s->n && s->n <= kSmallMax) {
+      rc = small_datagrams(h, s->hbytes, s->hoffs, s->n, now, res, stop_index, &done);
+      if (done || (rc && rc != PHIP_ERR_SHORT_BUFFER)) {
+        if (rc && rc != PHIP_ERR_SHORT_BUFFER) rc = after_error(h, rc);
+        done = true;
+        const hipError_t ce = hipEventSynchronize(s->copied);
+        if (ce != hipSuccess && rc == PHIP_OK)
+          rc = set_err(h, PHIP_ERR_HIP, "hipEventSynchronize: %s", hipGetErrorString(ce));
+      }
+    }
+    if (!done) {
+      hipError_t e = hipStreamWaitEvent(h->stream, s->copied, 0);
+      if (e != hipSuccess)
+        rc = set_err(h, PHIP_ERR_HIP, "hipStreamWaitEvent: %s", hipGetErrorString(e));
+      else if (s->n == 0)
+        rc = PHIP_OK;
+      else
+        rc = receive_datagrams_dev(h, s->dbytes, s->doffs, s->n, now, res, stop_index, false);
+    }
     // On success the stream has drained (results copied back), so the slot's
     // host and device buffers are free; after an error wait for them first.
     if (rc) (void)hipStreamSynchronize(h->stream);  // drain; rc already set

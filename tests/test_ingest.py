@@ -213,10 +213,12 @@ def _batches(rng, K, nb, n):
 
 
 @pytest.mark.gpu
-def test_ring_pipeline_vs_oracle(lib):
+@pytest.mark.parametrize("n", [40000, 700])
+def test_ring_pipeline_vs_oracle(lib, n):
     """Slots submitted one ahead of the receive (copy k+1 overlaps merge k):
     statuses, replies, stop index and the final table equal the oracle's
-    Receive loop over the same datagrams."""
+    Receive loop over the same datagrams (700: small slots, merged from the
+    pinned host bytes in one launch)."""
     import torch
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
@@ -229,8 +231,8 @@ def test_ring_pipeline_vs_oracle(lib):
     g.seed(names, a, t, e, created)
     o = O.Repo()
     o.seed(names, a, t, e, created)
-    batches = _batches(rng, K, 6, 40000)
-    ring = lib.Ring(g, nslots=3, max_msgs=40000)
+    batches = _batches(rng, K, 6, n)
+    ring = lib.Ring(g, nslots=3, max_msgs=n)
     pending = []
     for k, dgs in enumerate(batches):
         slot, n = ring.fill(dgs)
