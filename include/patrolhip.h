@@ -414,7 +414,11 @@ int phip_ae_apply(phip_handle* h, int64_t* replicas, uint32_t nrep, uint64_t nbu
  * It replaces the single-table Receive loop (repo.go:54-92) of one node by a
  * sharded one, with no Python or torch on the path:
  *   - phip_group_open_all: one process driving n GPUs (ncclCommInitAll); the
- *     group opens and owns a handle per GPU (cfg->device is ignored);
+ *     group opens and owns a handle per GPU (cfg->device is ignored).  A
+ *     device listed more than once (all entries the same device) gives n
+ *     shards on that one GPU, which exchange by device copies instead of
+ *     RCCL (RCCL takes one rank per device): the same packing, segments and
+ *     merge order, to rehearse an n-GPU group on one;
  *   - phip_group_open_rank: one process per GPU (ncclCommInitRank) around the
  *     caller's handle; rank 0 makes the id with phip_group_unique_id and the
  *     caller hands it to every rank by its own means.

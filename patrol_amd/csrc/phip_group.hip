@@ -9,6 +9,15 @@
 // kernels and RCCL calls on the member handle's stream, and synchronises only
 // to read the split sizes of the exchange.  With one process per GPU the
 // calling thread is the member's thread.
+//
+// Members sharing one GPU (phip_group_open_all with a device listed more
+// than once: several shards' tables on one device, e.g. to rehearse an
+// N-GPU group on one) exchange without RCCL, which refuses two ranks on one
+// device: the member threads meet at a barrier once every member's packed
+// send buffers and split sizes are ready, and each copies its segments from
+// its peers' buffers with device copies; the all-reduce is an element-wise
+// max over the members' joins.  The packing, segment offsets, source order
+// and merge are the same code as the RCCL path.
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -17,6 +26,8 @@
 #include <rocprim/rocprim.hpp>
 
 #include <algorithm>
+#include <condition_variable>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -68,10 +79,46 @@ struct Member {
 
 }  // namespace
 
+// A reusable barrier of the member threads of one call (shared-device
+// exchange).  abort() releases every waiter with false: a member that fails
+// before a barrier must not leave the others waiting.
+struct Barrier {
+  std::mutex mu;
+  std::condition_variable cv;
+  u32 n = 0, count = 0, gen = 0;
+  bool aborted = false;
+  bool wait() {
+    std::unique_lock<std::mutex> l(mu);
+    if (aborted) return false;
+    const u32 g0 = gen;
+    if (++count == n) {
+      count = 0;
+      ++gen;
+      cv.notify_all();
+      return true;
+    }
+    cv.wait(l, [&] { return gen != g0 || aborted; });
+    return !aborted;
+  }
+  void abort() {
+    std::lock_guard<std::mutex> l(mu);
+    aborted = true;
+    cv.notify_all();
+  }
+  void reset(u32 members) {
+    std::lock_guard<std::mutex> l(mu);
+    n = members;
+    count = 0;
+    aborted = false;
+  }
+};
+
 struct phip_group {
   u32 world = 0;
   std::vector<Member> m;
   std::string err;
+  bool shared = false;   // every member on one device: exchange by device copies (no RCCL)
+  Barrier bar;
 };
 
 namespace {
@@ -110,17 +157,23 @@ int fail(Member& mb, int code, const char* fmt, ...) {
   } while (0)
 
 // Run f(member index) on one host thread per local member (the calling
-// thread when there is one); returns the first member's error.
+// thread when there is one); returns the first member's error.  A member
+// that fails releases the others from the call's barriers.
 template <class F>
 int for_members(phip_group* g, F f) {
   const size_t n = g->m.size();
   std::vector<int> rc(n, PHIP_OK);
+  g->bar.reset((u32)n);
   if (n == 1) {
     rc[0] = f(0);
   } else {
     std::vector<std::thread> th;
     th.reserve(n);
-    for (size_t i = 0; i < n; ++i) th.emplace_back([&, i] { rc[i] = f(i); });
+    for (size_t i = 0; i < n; ++i)
+      th.emplace_back([&, i] {
+        rc[i] = f(i);
+        if (rc[i] != PHIP_OK) g->bar.abort();
+      });
     for (auto& t : th) t.join();
   }
   for (size_t i = 0; i < n; ++i)
@@ -182,12 +235,22 @@ int member_receive(phip_group* g, Member& mb, const phip_msgs& in, int64_t now, 
                             (uint64_t*)mb.s_a.p, (uint64_t*)mb.s_t.p, (int64_t*)mb.s_e.p, sz,
                             sz + W, PHIP_DEVICE_PTRS | (flags & PHIP_ROUTE_COMBINE)));
   // 2. split sizes: every member learns what each source sends it
-  GNCCL(mb, ncclGroupStart());
-  GNCCL(mb, ncclAllToAll(sz, sz + 2 * W, 1, ncclUint64, mb.comm, st));
-  GNCCL(mb, ncclAllToAll(sz + W, sz + 3 * W, 1, ncclUint64, mb.comm, st));
-  GNCCL(mb, ncclGroupEnd());
-  GHIP(mb, hipMemcpyAsync(mb.host_sizes, sz, 4 * W * sizeof(u64), hipMemcpyDeviceToHost, st));
-  GHIP(mb, hipStreamSynchronize(st));
+  if (g->shared) {
+    GHIP(mb, hipMemcpyAsync(mb.host_sizes, sz, 2 * W * sizeof(u64), hipMemcpyDeviceToHost, st));
+    GHIP(mb, hipStreamSynchronize(st));
+    if (!g->bar.wait()) return fail(mb, PHIP_ERR_INVALID, "another member failed");
+    for (u32 p = 0; p < W; ++p) {   // what member p packed for this one
+      mb.host_sizes[2 * W + p] = g->m[p].host_sizes[mb.rank];
+      mb.host_sizes[3 * W + p] = g->m[p].host_sizes[W + mb.rank];
+    }
+  } else {
+    GNCCL(mb, ncclGroupStart());
+    GNCCL(mb, ncclAllToAll(sz, sz + 2 * W, 1, ncclUint64, mb.comm, st));
+    GNCCL(mb, ncclAllToAll(sz + W, sz + 3 * W, 1, ncclUint64, mb.comm, st));
+    GNCCL(mb, ncclGroupEnd());
+    GHIP(mb, hipMemcpyAsync(mb.host_sizes, sz, 4 * W * sizeof(u64), hipMemcpyDeviceToHost, st));
+    GHIP(mb, hipStreamSynchronize(st));
+  }
   const u64* hs = mb.host_sizes;
   u64 n_send = 0, n_recv = 0, b_recv = 0;
   for (u32 p = 0; p < W; ++p) {
@@ -215,6 +278,35 @@ int member_receive(phip_group* g, Member& mb, const phip_msgs& in, int64_t now, 
   // 3. the segments: one send and one receive per peer and column; this
   // member's own segment is a device copy (no RCCL round trip through its
   // buffers)
+  if (g->shared) {   // each segment copied from its source member's packed buffers
+    u64 ro = 0, rb = 0;
+    for (u32 p = 0; p < W; ++p) {
+      const Member& src = g->m[p];
+      const u64* ps = src.host_sizes;
+      u64 so = 0, sb = 0;   // the source's segment for this member
+      for (u32 o = 0; o < mb.rank; ++o) { so += ps[o]; sb += ps[W + o]; }
+      const u64 rc = hs[2 * W + p], rbytes = hs[3 * W + p];
+      GHIP(mb, hipMemcpyAsync((u32*)mb.r_lens.p + ro, (const u32*)src.s_lens.p + so, rc * 4,
+                              hipMemcpyDeviceToDevice, st));
+      GHIP(mb, hipMemcpyAsync((uint8_t*)mb.r_names.p + rb, (const uint8_t*)src.s_names.p + sb, rbytes,
+                              hipMemcpyDeviceToDevice, st));
+      GHIP(mb, hipMemcpyAsync((u64*)mb.r_a.p + ro, (const u64*)src.s_a.p + so, rc * 8,
+                              hipMemcpyDeviceToDevice, st));
+      GHIP(mb, hipMemcpyAsync((u64*)mb.r_t.p + ro, (const u64*)src.s_t.p + so, rc * 8,
+                              hipMemcpyDeviceToDevice, st));
+      GHIP(mb, hipMemcpyAsync((int64_t*)mb.r_e.p + ro, (const int64_t*)src.s_e.p + so, rc * 8,
+                              hipMemcpyDeviceToDevice, st));
+      ro += rc; rb += rbytes;
+    }
+    // every member copied what it needs before any packs again (the next
+    // call's route_pack overwrites the send buffers)
+    GHIP(mb, hipStreamSynchronize(st));
+    if (!g->bar.wait()) return fail(mb, PHIP_ERR_INVALID, "another member failed");
+    if (n_recv == 0) return PHIP_OK;
+    return merge_received(mb, st, (const u32*)mb.r_lens.p, (const uint8_t*)mb.r_names.p,
+                          (const u64*)mb.r_a.p, (const u64*)mb.r_t.p, (const int64_t*)mb.r_e.p,
+                          n_recv, now);
+  }
   void* tm = phip_host::timing_begin(mb.h, "rccl_exchange");
   GNCCL(mb, ncclGroupStart());
   u64 so = 0, sb = 0, ro = 0, rb = 0;
@@ -254,13 +346,31 @@ int member_receive(phip_group* g, Member& mb, const phip_msgs& in, int64_t now, 
                         now);
 }
 
+__global__ void k_max_into(int64_t* __restrict__ dst, const int64_t* __restrict__ src, u64 n) {
+  const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n && src[i] > dst[i]) dst[i] = src[i];
+}
+
 int member_anti_entropy(phip_group* g, Member& mb, int64_t* reps, uint32_t nrep, uint64_t B) {
-  (void)g;
   GHIP(mb, hipSetDevice(mb.device));
   hipStream_t st = (hipStream_t)phip_host::handle_stream(mb.h);
-  GHIP(mb, mb.ae.ensure((size_t)3 * B * 8));
+  GHIP(mb, mb.ae.ensure((size_t)3 * B * 8 * (g->shared ? 2 : 1)));
   int64_t* j = (int64_t*)mb.ae.p;
   GPHIP(mb, phip_ae_local_max(mb.h, reps, nrep, B, j, PHIP_DEVICE_PTRS));
+  if (g->shared) {   // the all-reduce: every member's join, max'd element-wise
+    if (!g->bar.wait()) return fail(mb, PHIP_ERR_INVALID, "another member failed");
+    int64_t* jm = j + 3 * B;
+    GHIP(mb, hipMemcpyAsync(jm, j, 3 * B * 8, hipMemcpyDeviceToDevice, st));
+    for (const Member& p : g->m) {
+      if (&p == &mb) continue;
+      k_max_into<<<(unsigned)((3 * B + 255) / 256), 256, 0, st>>>(jm, (const int64_t*)p.ae.p, 3 * B);
+      GHIP(mb, hipGetLastError());
+    }
+    GHIP(mb, hipStreamSynchronize(st));
+    if (!g->bar.wait()) return fail(mb, PHIP_ERR_INVALID, "another member failed");
+    GPHIP(mb, phip_ae_apply(mb.h, reps, nrep, B, jm, PHIP_DEVICE_PTRS));
+    return PHIP_OK;
+  }
   void* tm = phip_host::timing_begin(mb.h, "rccl_allreduce");
   GNCCL(mb, ncclAllReduce(j, j, 3 * B, ncclInt64, ncclMax, mb.comm, st));
   phip_host::timing_end(mb.h, tm);
@@ -323,12 +433,25 @@ int phip_group_open_all(const phip_config* cfg, const int32_t* devices, uint32_t
       return rc;
     }
   }
-  std::vector<ncclComm_t> comms(n);
-  if (ncclCommInitAll(comms.data(), (int)n, devs.data()) != ncclSuccess) {
-    destroy(g);
-    return PHIP_ERR_RCCL;
+  // one device listed more than once: RCCL takes one rank per device, so the
+  // members exchange by device copies (all of them on that one device)
+  std::vector<int> sorted = devs;
+  std::sort(sorted.begin(), sorted.end());
+  const bool repeated = std::adjacent_find(sorted.begin(), sorted.end()) != sorted.end();
+  if (repeated) {
+    if (sorted.front() != sorted.back()) {   // mixed: some devices shared, some not
+      destroy(g);
+      return PHIP_ERR_INVALID;
+    }
+    g->shared = n > 1;
+  } else {
+    std::vector<ncclComm_t> comms(n);
+    if (ncclCommInitAll(comms.data(), (int)n, devs.data()) != ncclSuccess) {
+      destroy(g);
+      return PHIP_ERR_RCCL;
+    }
+    for (u32 i = 0; i < n; ++i) g->m[i].comm = comms[i];
   }
-  for (u32 i = 0; i < n; ++i) g->m[i].comm = comms[i];
   if (int rc = alloc_host_sizes(g)) {
     destroy(g);
     return rc;

@@ -23,11 +23,11 @@ def pa():
     return patrol_amd
 
 
-def _batch(rng, n, K, dev):
+def _batch(rng, n, K, dev, dirty=0.0):
     from patrol_amd.engine import names_blob
     ids = _gen.zipf_ids(rng, n, K)
     names = [(b"an-arena-length-bucket-name-%d" % i) if i % 97 == 0 else b"b%d" % i for i in ids]
-    a, t, e = _gen.clean_states(rng, n)
+    a, t, e = _gen.dirty_states(rng, n, dirty) if dirty else _gen.clean_states(rng, n)
     blob, offs = names_blob(names)
     dv = [torch.from_numpy(blob).to(dev), torch.from_numpy(offs.view(np.int32)).to(dev)]
     dv += [torch.from_numpy(x.view(np.int64)).to(dev) for x in (a, t, e)]
@@ -87,4 +87,64 @@ def test_group_anti_entropy_equals_torch_restatement(pa):
     g.anti_entropy([xd])
     torch.cuda.synchronize()
     assert torch.equal(xd.cpu(), want)
+    g.close()
+
+
+@pytest.mark.parametrize("world,dirty", [(2, 0.0), (3, 0.0), (3, 0.05)])
+def test_shared_device_group_receive_vs_oracle(pa, world, dirty):
+    """A group of `world` shards on one GPU (phip_group_open_all with the
+    device listed `world` times): the multi-member exchange (split sizes,
+    each source's segment, sources merged in rank order) without RCCL, which
+    takes one rank per device.  Member i sends batch i; every bucket lands
+    on its owner, the members' tables together equal the oracle's Receive of
+    batch 0, then 1, ... (per-bucket order), and a batch with incasts and
+    -0.0 fields is packed without the sender-side combine."""
+    from patrol_amd import shard
+    from oracle import go_semantics as G
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(700 + world)
+    g = pa.GPUGroup.open_all([0] * world, log2_slots=14)
+    assert g.world == world
+    o = O.Repo()
+    for k, n in enumerate((3000, 1 << 20)):
+        per = [_batch(rng, n, 30000, dev, dirty) for _ in range(world)]
+        torch.cuda.synchronize()
+        sent, merged = g.receive([b[4] for b in per], _gen.T0 + k, combine=True)
+        assert sum(sent) == sum(merged) and sum(merged) <= world * n
+        for names, a, t, e, _ in per:
+            o.receive_soa(names, a, t, e, _gen.T0 + k)
+    want = o.dump()
+    got = {}
+    for r, repo in enumerate(g.repos):
+        d = _dump(repo)
+        for name in d:
+            h = torch.tensor([int(np.array([G.fnv1a64(name)], np.uint64).view(np.int64)[0])])
+            assert int(shard.owner_of(h, world)) == r
+        got.update(d)
+    assert len(got) == len(want)
+    assert all(got.get(k) == v for k, v in want.items())
+    g.close()
+
+
+def test_shared_device_group_anti_entropy(pa):
+    from patrol_amd import shard
+    R, B, world = 3, 5000, 3
+    rng = np.random.default_rng(17)
+    xs = []
+    for _ in range(world):
+        x = torch.zeros((R, 3, B), dtype=torch.int64)
+        for k in range(R):
+            taken = rng.integers(0, 10**6, B).astype(np.float64)
+            x[k, 0] = shard.e_encode(torch.from_numpy((taken + rng.random(B) * 100).view(np.int64)))
+            x[k, 1] = shard.e_encode(torch.from_numpy(taken.view(np.int64)))
+            x[k, 2] = torch.from_numpy(rng.integers(0, 1 << 40, B))
+        xs.append(x)
+    want = shard.anti_entropy(torch.cat(xs).clone())[:R]
+    g = pa.GPUGroup.open_all([0] * world, log2_slots=10)
+    xd = [x.cuda() for x in xs]
+    torch.cuda.synchronize()
+    g.anti_entropy(xd)
+    torch.cuda.synchronize()
+    for x in xd:
+        assert torch.equal(x.cpu(), want)
     g.close()
