@@ -85,6 +85,8 @@ def parse():
                    help="c3: replica elapsed drawn below the local clock (U[0, now - created): "
                         "Takes refill, succeed and deny) or ahead of it (round 1's input: every "
                         "Take clamps last to now, dt = 0)")
+    p.add_argument("--no-status", action="store_true",
+                   help="A/B only: the C2 step does not write the per-message status column")
     p.add_argument("--name-len", type=int, default=0,
                    help="c2: pad every bucket name to this many bytes (e.g. 32: the arena path)")
     p.add_argument("--no-routed", action="store_true",
@@ -626,7 +628,7 @@ def main():
         blob, offs = names_for_ids(torch, ids + base, args.name_len)
         batches = [replica_states(torch, gen, n, j, dev) for j in range(args.warmup + args.steps)]
         # the per-message status column a Receive caller reads (merge vs incast)
-        c2_status = torch.empty(n, dtype=torch.uint8, device=dev)
+        c2_status = None if args.no_status else torch.empty(n, dtype=torch.uint8, device=dev)
         if args.insert:
             # SURVEY C2's insert-on-miss variant: every step names a fresh
             # key range (same Zipf shape), so each step creates the buckets it

@@ -611,6 +611,10 @@ __global__ void k_hot_build(const u32* __restrict__ ckeys, const u32* __restrict
 }
 
 // ----------------------------------------------------- fast receive --------
+// Statuses: the caller's status column is filled with PHIP_ST_MERGED
+// before the kernel (fast_apply, beside the classification); every message
+// the kernel does not merge is written again later (misses by the miss path,
+// the dirty suffix by the ordered path).
 // Persistent workgroups; every wave walks its own 64-message chunks
 // (grid-stride over waves, no workgroup barrier inside the loop, so a wave
 // waiting on a table read never holds up another).  Per message:
@@ -822,7 +826,7 @@ __device__ inline bool tail_match(const u64 (&htail)[kHotTailWords][kHotMax], u3
 
 template <class In>
 __global__ __launch_bounds__(kFastBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_receive_fast(
-    In in, u32 n, Table T, u8* __restrict__ status, Sharded miss, u32* ctr,
+    In in, u32 n, Table T, Sharded miss, u32* ctr,
     const HotHdr* __restrict__ hot, const HotEntry* __restrict__ hot_dir) {
   __shared__ u32 hslot[kHotLds];        // directory index + 1 (0 = empty)
   __shared__ u64 htag[kHotMax], hw0[kHotMax], hw1[kHotMax], hw2[kHotMax];
@@ -926,7 +930,6 @@ __global__ __launch_bounds__(kFastBlock) __attribute__((amdgpu_waves_per_eu(8, 8
         if (ea > hmax[0][hidx]) atomicMax(&hmax[0][hidx], ea);
         if (et > hmax[1][hidx]) atomicMax(&hmax[1][hidx], et);
         if (ee > hmax[2][hidx]) atomicMax(&hmax[2][hidx], ee);
-        if (status) status[i] = PHIP_ST_MERGED;
       } else {
         // round 3: the home slot
         u32 s = T.home(tag);
@@ -946,7 +949,6 @@ __global__ __launch_bounds__(kFastBlock) __attribute__((amdgpu_waves_per_eu(8, 8
           if (ea > cur.added) atomicMax(&r->added, ea);
           if (et > cur.taken) atomicMax(&r->taken, et);
           if (ee > ((u64)cur.elapsed ^ kSign)) atomicMax(&r->elapsed, (i64)(ee ^ kSign));
-          if (status) status[i] = PHIP_ST_MERGED;
         } else {
           missed = true;
           if (pr == kFull) atomicOr(&ctr[8], 1u);
