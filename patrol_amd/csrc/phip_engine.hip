@@ -56,7 +56,7 @@ enum BufId {
   B_MISS, B_MISS2, B_RETRY, B_CSLOT, B_CMSG,
   B_SLOT, B_IDX, B_SSLOT, B_SIDX, B_USLOT, B_SCNT, B_SSTART, B_LONG, B_HUGE, B_TEMP, B_DUMP,
   B_OPS, B_HOFF, B_HOP, B_HVAL, B_RPOS, B_RST, B_RUNN, B_SEGEX, B_WOFF, B_SUMS, B_WRUN,
-  B_WING, B_SEGXF, B_FOLDDBG, B_SMALL,
+  B_WING, B_SEGXF, B_FOLDDBG, B_SMALL, B_HUGE2,
   B_STATES, B_NAME1, B_HOT, B_ROUTE, B_EXPORT, B_MSHARD, B_MSCNT, B_DEDUP, B_DSET, B_COUNT_
 };
 
@@ -79,7 +79,10 @@ struct phip_handle {
   hipStream_t stream = nullptr;      // the stream every call runs on (own_stream or the caller's)
   hipStream_t own_stream = nullptr;  // created by phip_open
   hipStream_t stream2 = nullptr;   // second stream: the hot-bucket fold overlaps the others
+  hipStream_t stream3 = nullptr;   // third stream: the other huge segments beside the largest
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  hipEvent_t ev_fork3 = nullptr, ev_join3 = nullptr;
+  hipEvent_t ev_gather = nullptr, ev_gather3 = nullptr;   // huge-segment gathers done
   std::mutex mu;
   std::string err;
   u32 L = 0;
@@ -868,15 +871,30 @@ int ordered(phip_handle* h, Src src, u32 n, const OpView& ov, const OutView& ow)
         (rc = ensure(h, B_SEGEX, nhuge, &segex)) || (rc = ensure(h, B_WING, nwin_max, &wing)) ||
         (rc = ensure(h, B_SEGXF, nhuge, &segxf)))
       return rc;
+    // The largest huge segments (kFirst of them, moved to the front of the
+    // list) run gather -> fold -> outputs on stream2, the other huge segments
+    // the same chain on stream3, beside the wave and thread folds on the
+    // main stream: the largest segments' folds are the longest sequential
+    // chains, so they start as soon as their own (smaller) gather is done.
+    static const u32 first_env =
+        getenv("PHIP_HUGE_FIRST") ? (u32)atoi(getenv("PHIP_HUGE_FIRST")) : PHIP_HUGE_FIRST;
+    const u32 kFirst = std::min<u32>(first_env, kHugeFirstMax);
+    const bool split = kFirst > 0 && nhuge > kFirst;
+    const u32 hsplit = split ? kFirst : nhuge;
+    u32* hl = huge;
+    if (split && (rc = ensure(h, B_HUGE2, nhuge, &hl))) return rc;
     HIPCHK(h, hipEventRecord(h->ev_fork, h->stream));
     HIPCHK(h, hipStreamWaitEvent(h->stream2, h->ev_fork, 0));
-    {
-      Launch l(h, "k_gather_huge", h->stream2);
-      k_huge_offsets<<<1, 1024, 0, h->stream2>>>(huge, nhuge, scnt, hoff, woff);
-      k_gather_huge<<<(unsigned)nwin_max, kBlock, 0, h->stream2>>>(huge, nhuge, hoff, woff, sstart,
-                                                                    scnt, sidx, opr, hop, hval, sums);
+    if (split) {
+      k_huge_order<<<1, 1024, 0, h->stream2>>>(huge, nhuge, scnt, kFirst, hl);
+      HIPCHK(h, hipGetLastError());
     }
+    k_huge_offsets<<<1, 1024, 0, h->stream2>>>(hl, nhuge, scnt, hoff, woff);
     HIPCHK(h, hipGetLastError());
+    if (split) {
+      HIPCHK(h, hipEventRecord(h->ev_fork3, h->stream2));
+      HIPCHK(h, hipStreamWaitEvent(h->stream3, h->ev_fork3, 0));
+    }
     static const int variant = getenv("PHIP_FOLD_VARIANT") ? atoi(getenv("PHIP_FOLD_VARIANT")) : 0;
     // PHIP_FOLD_STATS=1 (diagnostics): per hot segment, ops / windows /
     // windows folded / rounds / bursts / ops walked / runs / cycles, to stderr
@@ -884,19 +902,49 @@ int ordered(phip_handle* h, Src src, u32 n, const OpView& ov, const OutView& ow)
     u64* fold_dbg = nullptr;
     if (fold_stats && (rc = ensure(h, B_FOLDDBG, (size_t)nhuge * 16, &fold_dbg))) return rc;
     auto kb = variant == 1 ? k_fold_block<1> : k_fold_block<0>;
-    {
-      Launch l(h, "k_fold_block", h->stream2);
-      kb<<<nhuge, kFoldThreads, 0, h->stream2>>>(huge, nhuge, uslot, hoff, scnt, hval, hop,
-                                                  h->recs, rpos, rst, runn, segex, segxf, woff,
-                                                  sums, wrun, wing, fold_dbg);
+    // one chain per group: segments [h0, h1) of the list on stream st; the
+    // main stream's wave and thread folds wait for the gathers (ev): the
+    // gathers alone, then the latency-bound block folds beside those
+    // bandwidth-bound folds, is the shorter schedule.
+    static const bool gather_first = !getenv("PHIP_C3_GATHER_BESIDE");
+    auto chain = [&](u32 h0, u32 h1, hipStream_t st, hipEvent_t ev, const char* ng,
+                     const char* nf, const char* no) -> int {
+      {
+        Launch l(h, ng, st);
+        k_gather_huge<<<(unsigned)nwin_max, kBlock, 0, st>>>(hl, h1, hoff, woff, sstart, scnt, sidx,
+                                                              opr, hop, hval, sums, h0);
+      }
+      HIPCHK(h, hipGetLastError());
+      if (gather_first) {
+        HIPCHK(h, hipEventRecord(ev, st));
+        HIPCHK(h, hipStreamWaitEvent(h->stream, ev, 0));
+      }
+      {
+        Launch l(h, nf, st);
+        kb<<<h1 - h0, kFoldThreads, 0, st>>>(hl, h1, uslot, hoff, scnt, hval, hop, h->recs, rpos,
+                                             rst, runn, segex, segxf, woff, sums, wrun, wing,
+                                             fold_dbg, h0);
+      }
+      HIPCHK(h, hipGetLastError());
+      {
+        Launch l(h, no, st);
+        k_huge_outputs<<<(unsigned)nwin_max, kBlock, 0, st>>>(hl, h1, hoff, woff, scnt, hval, hop,
+                                                               rpos, rst, runn, segex, segxf, wrun,
+                                                               wing, ow, h0);
+      }
+      HIPCHK(h, hipGetLastError());
+      return PHIP_OK;
+    };
+    if ((rc = chain(0, hsplit, h->stream2, h->ev_gather, "k_gather_huge", "k_fold_block",
+                    "k_huge_outputs")))
+      return rc;
+    if (split) {
+      if ((rc = chain(hsplit, nhuge, h->stream3, h->ev_gather3, "k_gather_huge2", "k_fold_block2",
+                      "k_huge_outputs2")))
+        return rc;
+      HIPCHK(h, hipEventRecord(h->ev_join3, h->stream3));
+      HIPCHK(h, hipStreamWaitEvent(h->stream2, h->ev_join3, 0));
     }
-    HIPCHK(h, hipGetLastError());
-    {
-      Launch l(h, "k_huge_outputs", h->stream2);
-      k_huge_outputs<<<(unsigned)nwin_max, kBlock, 0, h->stream2>>>(
-          huge, nhuge, hoff, woff, scnt, hval, hop, rpos, rst, runn, segex, segxf, wrun, wing, ow);
-    }
-    HIPCHK(h, hipGetLastError());
     if (fold_dbg) {
       std::vector<u64> d((size_t)nhuge * 16);
       HIPCHK(h, hipMemcpyAsync(d.data(), fold_dbg, d.size() * 8, hipMemcpyDeviceToHost, h->stream2));
@@ -1271,8 +1319,14 @@ int phip_open(const phip_config* cfg, phip_handle** out) {
     return fail(e);
   h->stream = h->own_stream;
   if ((e = hipStreamCreateWithFlags(&h->stream2, hipStreamNonBlocking)) != hipSuccess) return fail(e);
+  if ((e = hipStreamCreateWithFlags(&h->stream3, hipStreamNonBlocking)) != hipSuccess) return fail(e);
   if ((e = hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming)) != hipSuccess) return fail(e);
   if ((e = hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming)) != hipSuccess) return fail(e);
+  if ((e = hipEventCreateWithFlags(&h->ev_fork3, hipEventDisableTiming)) != hipSuccess) return fail(e);
+  if ((e = hipEventCreateWithFlags(&h->ev_join3, hipEventDisableTiming)) != hipSuccess) return fail(e);
+  if ((e = hipEventCreateWithFlags(&h->ev_gather, hipEventDisableTiming)) != hipSuccess) return fail(e);
+  if ((e = hipEventCreateWithFlags(&h->ev_gather3, hipEventDisableTiming)) != hipSuccess)
+    return fail(e);
   if ((e = hipMalloc(&h->recs, h->cap * sizeof(Rec))) != hipSuccess) return fail(e);
   if ((e = hipMalloc(&h->aux, h->cap * sizeof(u32))) != hipSuccess) return fail(e);
   if ((e = hipMalloc(&h->arena, h->arena_cap + 64)) != hipSuccess) return fail(e);
@@ -1296,6 +1350,7 @@ void phip_close(phip_handle* h) {
   (void)hipSetDevice(h->device);
   if (h->stream) (void)hipStreamSynchronize(h->stream);
   if (h->stream2) (void)hipStreamSynchronize(h->stream2);
+  if (h->stream3) (void)hipStreamSynchronize(h->stream3);
   for (auto& b : h->buf)
     if (b.p) (void)hipFree(b.p);
   for (auto& t : h->event_pool) {
@@ -1311,7 +1366,12 @@ void phip_close(phip_handle* h) {
   if (h->small_pin) (void)hipHostFree(h->small_pin);
   if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
   if (h->ev_join) (void)hipEventDestroy(h->ev_join);
+  if (h->ev_fork3) (void)hipEventDestroy(h->ev_fork3);
+  if (h->ev_join3) (void)hipEventDestroy(h->ev_join3);
+  if (h->ev_gather) (void)hipEventDestroy(h->ev_gather);
+  if (h->ev_gather3) (void)hipEventDestroy(h->ev_gather3);
   if (h->stream2) (void)hipStreamDestroy(h->stream2);
+  if (h->stream3) (void)hipStreamDestroy(h->stream3);
   if (h->own_stream) {
     (void)hipStreamSynchronize(h->own_stream);
     (void)hipStreamDestroy(h->own_stream);

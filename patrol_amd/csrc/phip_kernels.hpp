@@ -1459,6 +1459,12 @@ __device__ inline void store_state(Rec* r, const FState& S) {
 
 constexpr u32 kLongSeg = 32;        // longer segments: one wave each (k_fold_wave)
 constexpr u32 kHugeSeg = 16384;     // longer still: one workgroup each (k_fold_block)
+// The largest huge segments (at most this many) fold on a stream of their own.
+#ifndef PHIP_HUGE_FIRST
+#define PHIP_HUGE_FIRST 4
+#endif
+constexpr u32 kHugeFirstMax = 16;
+static_assert(PHIP_HUGE_FIRST <= kHugeFirstMax, "PHIP_HUGE_FIRST");
 #ifndef PHIP_FOLD_THREADS
 #define PHIP_FOLD_THREADS 512
 #endif
@@ -1829,6 +1835,47 @@ __device__ inline void huge_scan(const u32* __restrict__ huge_list, u32 nhuge,
   __syncthreads();
 }
 
+// The huge segment list with its nfirst largest segments moved to the front
+// (the rest keep their order): the largest segments' folds are the step's
+// longest sequential chains, so they get their own stream and start first
+// (one block; out must not alias huge_list).
+__global__ __launch_bounds__(1024) void k_huge_order(const u32* __restrict__ huge_list, u32 nhuge,
+                                                     const u32* __restrict__ seg_count, u32 nfirst,
+                                                     u32* __restrict__ out) {
+  __shared__ u64 part[1024];
+  __shared__ u32 sel[kHugeFirstMax];
+  const u32 tid = threadIdx.x;
+  for (u32 r = 0; r < nfirst; ++r) {
+    u64 best = 0;   // (count, ~index): the largest count, then the lowest index
+    for (u32 h = tid; h < nhuge; h += 1024) {
+      bool taken = false;
+      for (u32 q = 0; q < r; ++q) taken |= sel[q] == h;
+      if (!taken) best = max(best, ((u64)seg_count[huge_list[h]] << 32) | (0xFFFFFFFFu - h));
+    }
+    part[tid] = best;
+    __syncthreads();
+    for (u32 off = 512; off; off >>= 1) {
+      if (tid < off) part[tid] = max(part[tid], part[tid + off]);
+      __syncthreads();
+    }
+    if (tid == 0) {
+      const u32 h = 0xFFFFFFFFu - (u32)part[0];
+      sel[r] = h;
+      out[r] = huge_list[h];
+    }
+    __syncthreads();
+  }
+  for (u32 h = tid; h < nhuge; h += 1024) {
+    u32 below = 0;
+    bool taken = false;
+    for (u32 q = 0; q < nfirst; ++q) {
+      below += sel[q] < h;
+      taken |= sel[q] == h;
+    }
+    if (!taken) out[nfirst + h - below] = huge_list[h];
+  }
+}
+
 // Offsets of the huge segments in the contiguous staging arrays (ops) and in
 // the window-summary array (one block).
 __global__ __launch_bounds__(1024) void k_huge_offsets(const u32* __restrict__ huge_list, u32 nhuge,
@@ -1866,12 +1913,13 @@ __global__ __launch_bounds__(kBlock) void k_gather_huge(
     const u64* __restrict__ woff, const u32* __restrict__ seg_start,
     const u32* __restrict__ seg_count, const u32* __restrict__ sval,
     const OpRec* __restrict__ ops, OpRec* __restrict__ hop, u32* __restrict__ hval,
-    WinSum* __restrict__ sums) {
+    WinSum* __restrict__ sums, u32 h_begin) {
   __shared__ u64 red[6][kBlock / 64];
   __shared__ u32 s_first;
   __shared__ u64 s_par[3];
   u32 h, w;
-  if (!huge_window(woff, nhuge, blockIdx.x, h, w)) return;
+  // segments [h_begin, nhuge) of the list: their windows follow woff[h_begin]
+  if (!huge_window(woff, nhuge, (u32)woff[h_begin] + blockIdx.x, h, w)) return;
   const u32 g = huge_list[h];
   const u32 st = seg_start[g], cnt = seg_count[g];
   const u64 dst = hoff[h];
@@ -2401,27 +2449,28 @@ __global__ __launch_bounds__(kFoldThreads) void k_fold_block(
     u32* __restrict__ run_pos, RunState* __restrict__ run_st, u32* __restrict__ run_n,
     u8* __restrict__ seg_existed, u32* __restrict__ seg_exact_from,
     const u64* __restrict__ woff, const WinSum* __restrict__ sums, u32* __restrict__ win_run,
-    GMax* __restrict__ win_g, u64* __restrict__ dbg) {
+    GMax* __restrict__ win_g, u64* __restrict__ dbg, u32 h_begin) {
   __shared__ FoldShared sh;
-  if (blockIdx.x >= nhuge) return;
+  const u32 hs = h_begin + blockIdx.x;   // segments [h_begin, nhuge) of the list
+  if (hs >= nhuge) return;
   const u64 t_begin = wall_clock64();
   u32 n_folded = 0;
-  const u32 g = huge_list[blockIdx.x];
+  const u32 g = huge_list[hs];
   const u32 tid = threadIdx.x;
   Rec* r = &recs[seg_slot[g]];
   const u32 cnt = seg_count[g], last = cnt - 1;
-  const u64 base = hoff[blockIdx.x];
+  const u64 base = hoff[hs];
   const u32* __restrict__ sv = hval + base;
   const OpRec* __restrict__ so = hop + base;
   // this segment's runs: at most one per op plus the initial one
-  u32* rp = run_pos + base + blockIdx.x;
-  RunState* rs = run_st + base + blockIdx.x;
+  u32* rp = run_pos + base + hs;
+  RunState* rs = run_st + base + hs;
 
   FState R = load_state(load_rec(r));   // run state (see the module comment)
   GMax G{0, 0, 0};                      // merges absorbed so far
   if (tid == 0) {
     put_run(rp, rs, 0, 0, R);
-    seg_existed[blockIdx.x] = R.existed;
+    seg_existed[hs] = R.existed;
     sh.nrun = 1;
     sh.exact_from = 0xFFFFFFFFu;
     sh.n_burst = 0;
@@ -2434,9 +2483,9 @@ __global__ __launch_bounds__(kFoldThreads) void k_fold_block(
   __syncthreads();
   u64 tp = dbg ? wall_clock64() : 0;
   const u32 nwin = (cnt + kFoldWin - 1) / kFoldWin;
-  const WinSum* __restrict__ ws = sums + woff[blockIdx.x];
-  u32* __restrict__ wr = win_run + woff[blockIdx.x];
-  GMax* __restrict__ wg = win_g + woff[blockIdx.x];
+  const WinSum* __restrict__ ws = sums + woff[hs];
+  u32* __restrict__ wr = win_run + woff[hs];
+  GMax* __restrict__ wg = win_g + woff[hs];
   u32 round = 0;
   // Windows are tested kSumChunk at a time: every thread tests one window's
   // summary (with the merge maxima of the windows before it in the chunk)
@@ -2523,10 +2572,10 @@ __global__ __launch_bounds__(kFoldThreads) void k_fold_block(
   prof_mark(sh, 0, tp);
   if (tid == 0) {
     store_state(r, join_state(R, sh.exact_from == 0xFFFFFFFFu ? G : GMax{0, 0, 0}));
-    run_n[blockIdx.x] = sh.nrun;
-    seg_exact_from[blockIdx.x] = sh.exact_from;
+    run_n[hs] = sh.nrun;
+    seg_exact_from[hs] = sh.exact_from;
     if (dbg) {
-      u64* d = dbg + (u64)blockIdx.x * 16;
+      u64* d = dbg + (u64)hs * 16;
       d[0] = cnt; d[1] = nwin; d[2] = n_folded; d[3] = round; d[4] = sh.n_burst;
       d[5] = sh.n_walk; d[6] = sh.nrun; d[7] = wall_clock64() - t_begin;
       for (u32 k = 0; k < 5; ++k) d[8 + k] = sh.prof[k];
@@ -2553,10 +2602,11 @@ __global__ __launch_bounds__(kBlock) void k_huge_outputs(
     const u32* __restrict__ run_pos, const RunState* __restrict__ run_st,
     const u32* __restrict__ run_n, const u8* __restrict__ seg_existed,
     const u32* __restrict__ seg_exact_from, const u32* __restrict__ win_run,
-    const GMax* __restrict__ win_g, OutView ow) {
+    const GMax* __restrict__ win_g, OutView ow, u32 h_begin) {
   __shared__ GMax wtot[kBlock / 64];
   u32 h, w;
-  if (!huge_window(woff, nhuge, blockIdx.x, h, w)) return;
+  // segments [h_begin, nhuge) of the list: their windows follow woff[h_begin]
+  if (!huge_window(woff, nhuge, (u32)woff[h_begin] + blockIdx.x, h, w)) return;
   const u32 cnt = seg_count[huge_list[h]];
   const u64 base = hoff[h];
   const u32* rp = run_pos + base + h;
