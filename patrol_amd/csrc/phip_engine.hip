@@ -721,6 +721,28 @@ int join_hot(phip_handle* h, const HotHdr* hot) {
 
 // ------------------------------------------------------------ ordered ----
 
+// A launch for the run-time output mask (out_mask): CALL(M) with M a
+// compile-time constant.
+#define PHIP_OUT_DISPATCH(mask, CALL) \
+  switch (mask) {                     \
+    case 0: CALL(0); break;           \
+    case 1: CALL(1); break;           \
+    case 2: CALL(2); break;           \
+    case 3: CALL(3); break;           \
+    case 4: CALL(4); break;           \
+    case 5: CALL(5); break;           \
+    case 6: CALL(6); break;           \
+    case 7: CALL(7); break;           \
+    case 8: CALL(8); break;           \
+    case 9: CALL(9); break;           \
+    case 10: CALL(10); break;         \
+    case 11: CALL(11); break;         \
+    case 12: CALL(12); break;         \
+    case 13: CALL(13); break;         \
+    case 14: CALL(14); break;         \
+    default: CALL(15); break;         \
+  }
+
 template <class Src>
 int resolve_all(phip_handle* h, Src src, u32 n, const int64_t* now_arr, i64 now0, u32** slot_out,
                 u32* n_claimed) {
@@ -966,14 +988,20 @@ int ordered(phip_handle* h, Src src, u32 n, const OpView& ov, const OutView& ow)
   }
   if (nlong) {
     Launch l(h, "k_fold_wave");
-    k_fold_wave<<<nlong, 64, 0, h->stream>>>(lng, nlong, uslot, sstart, scnt, sidx, opr, h->recs,
-                                             ow);
+#define PHIP_FOLD_WAVE(M)                                                                  \
+  k_fold_wave<M><<<nlong, 64, 0, h->stream>>>(lng, nlong, uslot, sstart, scnt, sidx, opr, \
+                                              h->recs, ow)
+    PHIP_OUT_DISPATCH(out_mask(ow), PHIP_FOLD_WAVE);
+#undef PHIP_FOLD_WAVE
     HIPCHK(h, hipGetLastError());
   }
   {
     Launch l(h, "k_fold_thread");
-    k_fold_thread<<<grid_for(nseg), kBlock, 0, h->stream>>>(uslot, sstart, scnt, nseg, sidx,
-                                                             opr, h->recs, ow);
+#define PHIP_FOLD_THREAD(M)                                                            \
+  k_fold_thread<M><<<grid_for(nseg), kBlock, 0, h->stream>>>(uslot, sstart, scnt, nseg, sidx, \
+                                                             opr, h->recs, ow)
+    PHIP_OUT_DISPATCH(out_mask(ow), PHIP_FOLD_THREAD);
+#undef PHIP_FOLD_THREAD
     HIPCHK(h, hipGetLastError());
   }
   if (nhuge) {

@@ -1439,6 +1439,31 @@ __device__ inline void write_out(const OutView& o, u32 i, const OpOut& r, const 
   }
 }
 
+// write_out with the outputs present fixed at compile time (kOut: kOutStatus
+// | kOutRem | kOutHave | kOutReply): no branch around a store, so the loops
+// that store have a fixed number of vector memory instructions per
+// iteration and the compiler's vmcnt waits for a load need not wait for
+// the stores issued after it (gfx9 counts loads and stores in one in-order
+// counter: with a variable count it waits for everything, vmcnt(0)).
+constexpr u32 kOutStatus = 1, kOutRem = 2, kOutHave = 4, kOutReply = 8;
+inline u32 out_mask(const OutView& o) {
+  return (o.status ? kOutStatus : 0) | (o.remaining ? kOutRem : 0) | (o.have ? kOutHave : 0) |
+         (o.reply ? kOutReply : 0);
+}
+template <u32 kOut>
+__device__ inline void write_out_m(const OutView& o, u32 i, const OpOut& r, const FState& S) {
+  if constexpr ((kOut & kOutStatus) != 0) o.status[i] = r.st;
+  if constexpr ((kOut & kOutRem) != 0) o.remaining[i] = r.rem;
+  if constexpr ((kOut & kOutHave) != 0) o.have[i] = r.have;
+  if constexpr ((kOut & kOutReply) != 0) {
+    if (r.has_reply) {
+      phip_state st;
+      st.added = as_bits(S.a); st.taken = as_bits(S.t); st.elapsed = S.e; st.created = S.c;
+      o.reply[i] = st;
+    }
+  }
+}
+
 __device__ inline FState load_state(const Rec& r) {
   FState S;
   S.a = as_f64(dec_f64(r.added));
@@ -1477,6 +1502,7 @@ constexpr u32 kFoldWin = kFoldThreads * kFoldPer;
 constexpr u32 kBurstQuiet = 16;     // a sequential burst ends after this many unchanged ops
 
 // One thread folds one short bucket segment in seq order.
+template <u32 kOut>
 __global__ __launch_bounds__(kBlock) void k_fold_thread(
     const u32* __restrict__ seg_slot, const u32* __restrict__ seg_start,
     const u32* __restrict__ seg_count, u32 nseg, const u32* __restrict__ sval,
@@ -1488,15 +1514,20 @@ __global__ __launch_bounds__(kBlock) void k_fold_thread(
   Rec* r = &recs[seg_slot[g]];
   const u32 st = seg_start[g];
   SOp op = load_sop(ops, sval[st]);
+  u32 v1 = sval[st + min(1u, cnt - 1)];
   FState S = load_state(load_rec(r)), S2;
   for (u32 j = 0; j < cnt; ++j) {
-    // next op in flight during this one (unconditional, clamped: see k_fold_block)
-    SOp nx = load_sop(ops, sval[st + min(j + 1, cnt - 1)]);
+    // The next op in flight during this one and the sort value of the one
+    // after (unconditional, clamped: see k_fold_block): the record load
+    // never waits on a sort value loaded after this op's stores.
+    const u32 v2 = sval[st + min(j + 2, cnt - 1)];
+    SOp nx = load_sop(ops, v1);
     OpOut o;
     eval_sop(op, S, S2, o);
-    write_out(ow, op.idx, o, S);
+    write_out_m<kOut>(ow, op.idx, o, S);
     S = S2;
     op = nx;
+    v1 = v2;
   }
   store_state(r, S);
 }
@@ -1527,6 +1558,7 @@ __device__ inline FState lane_state(const FState& x, u32 l) {
 // that op's result state becomes the current one.  A round costs one op
 // evaluation, so a change costs what a sequential fold step costs, and a run
 // of unchanged ops (denied Takes, no-op merges) retires up to 64 ops at once.
+template <u32 kOut>
 __global__ __launch_bounds__(64) void k_fold_wave(
     const u32* __restrict__ long_list, u32 nlong, const u32* __restrict__ seg_slot,
     const u32* __restrict__ seg_start, const u32* __restrict__ seg_count,
@@ -1539,13 +1571,27 @@ __global__ __launch_bounds__(64) void k_fold_wave(
   const u32 st = seg_start[g], cnt = seg_count[g];
   // unconditional loads, index clamped into the segment (see k_fold_block)
   const u32 last = st + cnt - 1;
+  FState S = load_state(load_rec(r));
   SOp op = load_sop(ops, sval[min(st + lane, last)]);
   u32 v_nx = sval[min(st + 64 + lane, last)];
-  FState S = load_state(load_rec(r));
+  // Each lane's result is kept in registers and stored at the top of the
+  // next window, ahead of that window's loads, with no store inside the
+  // round loop: every iteration issues the same stores before the same
+  // loads, so the compiler's in-order wait for a window's records (gfx9
+  // counts loads and stores in one counter) never waits for the stores
+  // issued after them.  Window 0 starts with placeholder stores to its own
+  // outputs, rewritten with its results.
+  // (Incast replies, rare, are stored where their op retires.)
+  constexpr u32 kDefer = kOut & ~kOutReply;
+  const FState none{};
+  OpOut po{};
+  u32 pidx = op.idx;
   for (u32 base = 0; base < cnt; base += 64) {
+    write_out_m<kDefer>(ow, pidx, po, none);
     SOp nx = load_sop(ops, v_nx);
     v_nx = sval[min(st + base + 128 + lane, last)];
     const u32 lim = min(64u, cnt - base);
+    OpOut mo{};
     u32 c = 0;
     while (c < lim) {
       const bool active = lane >= c && lane < lim;
@@ -1555,13 +1601,33 @@ __global__ __launch_bounds__(64) void k_fold_wave(
       if (active) ch = eval_sop(op, S, S2, o);
       const u64 m = __ballot(ch);
       const u32 p = m ? (u32)(__ffsll((long long)m) - 1) : 64u;
-      if (active && lane <= p) write_out(ow, op.idx, o, S);
+      if (active && lane <= p) {
+        mo = o;
+        if constexpr ((kOut & kOutReply) != 0) {
+          if (o.has_reply) write_out_m<kOutReply>(ow, op.idx, o, S);
+        }
+      }
       if (p >= 64) break;
       S = lane_state(S2, p);
       c = p + 1;
     }
+    if (lim < 64) {
+      // lanes past the segment's end hold its last op (clamped loads): they
+      // store lane lim-1's results again, so every lane stores (the reads
+      // of lane q run on every lane, outside any branch)
+      const u32 q = lim - 1;
+      const bool past = lane > q;
+      const u32 qst = (u32)__builtin_amdgcn_readlane((int)(u32)mo.st, (int)q);
+      const u64 qrem = lane_u64(mo.rem, q), qhave = lane_u64(mo.have, q);
+      mo.st = past ? (u8)qst : mo.st;
+      mo.rem = past ? qrem : mo.rem;
+      mo.have = past ? qhave : mo.have;
+    }
+    po = mo;
+    pidx = op.idx;
     op = nx;
   }
+  write_out_m<kDefer>(ow, pidx, po, none);
   if (lane == 0) store_state(r, S);
 }
 
