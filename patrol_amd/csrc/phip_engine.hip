@@ -56,7 +56,7 @@ enum BufId {
   B_MISS, B_MISS2, B_RETRY, B_CSLOT, B_CMSG,
   B_SLOT, B_IDX, B_SSLOT, B_SIDX, B_USLOT, B_SCNT, B_SSTART, B_LONG, B_HUGE, B_TEMP, B_DUMP,
   B_OPS, B_HOFF, B_HOP, B_HVAL, B_RPOS, B_RST, B_RUNN, B_SEGEX, B_WOFF, B_SUMS, B_WRUN,
-  B_WING, B_SEGXF, B_FOLDDBG, B_SMALL, B_HUGE2,
+  B_WING, B_SEGXF, B_FOLDDBG, B_SMALL, B_HUGE2, B_LONG2,
   B_STATES, B_NAME1, B_HOT, B_ROUTE, B_EXPORT, B_MSHARD, B_MSCNT, B_DEDUP, B_DSET, B_COUNT_
 };
 
@@ -987,6 +987,20 @@ int ordered(phip_handle* h, Src src, u32 n, const OpView& ov, const OutView& ow)
     }
   }
   if (nlong) {
+    // the long segments over kBigLongSeg ops first (their sequential chains
+    // are the longest), then the rest
+    static const bool big_first = !getenv("PHIP_LONG_SLOT_ORDER");
+    if (big_first && nlong > 1) {
+      u32* lng2;
+      if ((rc = ensure(h, B_LONG2, nlong, &lng2))) return rc;
+      size_t tb7 = 0;
+      HIPCHK(h, rocprim::partition(nullptr, tb7, lng, lng2, h->ctr + 14, (size_t)nlong,
+                                   BigLongSeg{scnt}, h->stream));
+      if ((rc = ensure(h, B_TEMP, tb7, &temp))) return rc;
+      HIPCHK(h, rocprim::partition(temp, tb7, lng, lng2, h->ctr + 14, (size_t)nlong,
+                                   BigLongSeg{scnt}, h->stream));
+      lng = lng2;
+    }
     Launch l(h, "k_fold_wave");
 #define PHIP_FOLD_WAVE(M)                                                                  \
   k_fold_wave<M><<<nlong, 64, 0, h->stream>>>(lng, nlong, uslot, sstart, scnt, sidx, opr, \

@@ -2742,6 +2742,14 @@ struct HugeSeg {
   const u32* cnt;
   __device__ bool operator()(u32 g) const { return cnt[g] > kHugeSeg; }
 };
+// Long segments whose wave fold starts first (k_fold_wave takes the list in
+// block order): a segment's fold is a sequential chain, so the longest ones
+// must not start last.
+constexpr u32 kBigLongSeg = 1024;
+struct BigLongSeg {
+  const u32* cnt;
+  __device__ bool operator()(u32 g) const { return cnt[g] > kBigLongSeg; }
+};
 
 // Sorted-slot segments from run-length output (counts -> starts is a scan).
 __global__ void k_seg_mark(const u32* __restrict__ sorted_slot, u32 n, u32* head) {
