@@ -924,6 +924,9 @@ int ordered(phip_handle* h, Src src, u32 n, const OpView& ov, const OutView& ow)
     u64* fold_dbg = nullptr;
     if (fold_stats && (rc = ensure(h, B_FOLDDBG, (size_t)nhuge * 16, &fold_dbg))) return rc;
     auto kb = variant == 1 ? k_fold_block<1> : k_fold_block<0>;
+    // gather / outputs: window-striding grids of 8 workgroups per CU (the
+    // window count is known on the device only)
+    const unsigned hgrid = (unsigned)std::min<size_t>(nwin_max, (size_t)h->ncu * 8);
     // one chain per group: segments [h0, h1) of the list on stream st; the
     // main stream's wave and thread folds wait for the gathers (ev): the
     // gathers alone, then the latency-bound block folds beside those
@@ -933,8 +936,8 @@ int ordered(phip_handle* h, Src src, u32 n, const OpView& ov, const OutView& ow)
                      const char* nf, const char* no) -> int {
       {
         Launch l(h, ng, st);
-        k_gather_huge<<<(unsigned)nwin_max, kBlock, 0, st>>>(hl, h1, hoff, woff, sstart, scnt, sidx,
-                                                              opr, hop, hval, sums, h0);
+        k_gather_huge<<<hgrid, kBlock, 0, st>>>(hl, h1, hoff, woff, sstart, scnt, sidx, opr, hop,
+                                                 hval, sums, h0);
       }
       HIPCHK(h, hipGetLastError());
       if (gather_first) {
@@ -950,9 +953,8 @@ int ordered(phip_handle* h, Src src, u32 n, const OpView& ov, const OutView& ow)
       HIPCHK(h, hipGetLastError());
       {
         Launch l(h, no, st);
-        k_huge_outputs<<<(unsigned)nwin_max, kBlock, 0, st>>>(hl, h1, hoff, woff, scnt, hval, hop,
-                                                               rpos, rst, runn, segex, segxf, wrun,
-                                                               wing, ow, h0);
+        k_huge_outputs<<<hgrid, kBlock, 0, st>>>(hl, h1, hoff, woff, scnt, hval, hop, rpos, rst,
+                                                  runn, segex, segxf, wrun, wing, ow, h0);
       }
       HIPCHK(h, hipGetLastError());
       return PHIP_OK;

@@ -1983,9 +1983,12 @@ __global__ __launch_bounds__(kBlock) void k_gather_huge(
   __shared__ u64 red[6][kBlock / 64];
   __shared__ u32 s_first;
   __shared__ u64 s_par[3];
+  // segments [h_begin, nhuge) of the list: their windows follow
+  // woff[h_begin]; a grid of a few blocks per CU walks them
+  const u32 b_end = (u32)woff[nhuge];
+  for (u32 b = (u32)woff[h_begin] + blockIdx.x; b < b_end; b += gridDim.x) {
   u32 h, w;
-  // segments [h_begin, nhuge) of the list: their windows follow woff[h_begin]
-  if (!huge_window(woff, nhuge, (u32)woff[h_begin] + blockIdx.x, h, w)) return;
+  huge_window(woff, nhuge, b, h, w);
   const u32 g = huge_list[h];
   const u32 st = seg_start[g], cnt = seg_count[g];
   const u64 dst = hoff[h];
@@ -2064,6 +2067,8 @@ __global__ __launch_bounds__(kBlock) void k_gather_huge(
               ((x[5] & 1) ? kSumMerge : 0) | ((x[5] & 4) ? kSumDirty : 0);
     q.pad = 0;
     sums[woff[h] + w] = q;
+  }
+  __syncthreads();   // the window's shared arrays are reused by the next
   }
 }
 
@@ -2670,9 +2675,12 @@ __global__ __launch_bounds__(kBlock) void k_huge_outputs(
     const u32* __restrict__ seg_exact_from, const u32* __restrict__ win_run,
     const GMax* __restrict__ win_g, OutView ow, u32 h_begin) {
   __shared__ GMax wtot[kBlock / 64];
+  // segments [h_begin, nhuge) of the list: their windows follow
+  // woff[h_begin]; a grid of a few blocks per CU walks them
+  const u32 b_end = (u32)woff[nhuge];
+  for (u32 b = (u32)woff[h_begin] + blockIdx.x; b < b_end; b += gridDim.x) {
   u32 h, w;
-  // segments [h_begin, nhuge) of the list: their windows follow woff[h_begin]
-  if (!huge_window(woff, nhuge, (u32)woff[h_begin] + blockIdx.x, h, w)) return;
+  huge_window(woff, nhuge, b, h, w);
   const u32 cnt = seg_count[huge_list[h]];
   const u64 base = hoff[h];
   const u32* rp = run_pos + base + h;
@@ -2729,6 +2737,8 @@ __global__ __launch_bounds__(kBlock) void k_huge_outputs(
     eval_sop(sop, S, S2, o);
     write_out(ow, sop.idx, o, S);
     gj = gmax(gj, merge_contrib(op[k], val[k]));
+  }
+  __syncthreads();   // the window's shared arrays are reused by the next
   }
 }
 
