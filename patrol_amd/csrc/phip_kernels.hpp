@@ -403,9 +403,20 @@ __device__ inline void short_name(u64 w0, u64 w1, u64 w2, u64 off, u32 len, Name
   b1 = len > 8 ? (b1 & ((1ull << (8 * (len - 8))) - 1)) : 0;
   u32 lo = (u32)kFnvOffset, hi = (u32)(kFnvOffset >> 32);
   const u32 q[4] = {(u32)b0, (u32)(b0 >> 32), (u32)b1, (u32)(b1 >> 32)};
+#ifndef PHIP_FNV_FULL
+  // A wave whose names all fit in 8 bytes (most of a batch of short names)
+  // hashes 8 bytes, not 14 (a wave-uniform branch on one ballot).
+  if (__builtin_amdgcn_ballot_w64(len > 8) == 0) {
 #pragma unroll
-  for (u32 k = 0; k < kShortName; ++k)
-    if (k < len) fnv_step32(lo, hi, (q[k >> 2] >> (8 * (k & 3))) & 0xFFu);
+    for (u32 k = 0; k < 8; ++k)
+      if (k < len) fnv_step32(lo, hi, (q[k >> 2] >> (8 * (k & 3))) & 0xFFu);
+  } else
+#endif
+  {
+#pragma unroll
+    for (u32 k = 0; k < kShortName; ++k)
+      if (k < len) fnv_step32(lo, hi, (q[k >> 2] >> (8 * (k & 3))) & 0xFFu);
+  }
   nm.h = ((u64)hi << 32) | lo; nm.len = len; nm.off = off;
   nm.w0 = (u64)len | (b0 << 16);     // name byte k sits at canonical byte k+2
   nm.w1 = (b0 >> 48) | (b1 << 16);
@@ -1483,7 +1494,10 @@ __device__ inline void store_state(Rec* r, const FState& S) {
 }
 
 constexpr u32 kLongSeg = 32;        // longer segments: one wave each (k_fold_wave)
-constexpr u32 kHugeSeg = 16384;     // longer still: one workgroup each (k_fold_block)
+#ifndef PHIP_HUGE_SEG
+#define PHIP_HUGE_SEG 16384
+#endif
+constexpr u32 kHugeSeg = PHIP_HUGE_SEG;   // longer still: one workgroup each (k_fold_block)
 // The largest huge segments (at most this many) fold on a stream of their own.
 #ifndef PHIP_HUGE_FIRST
 #define PHIP_HUGE_FIRST 4
