@@ -1495,7 +1495,7 @@ __device__ inline void store_state(Rec* r, const FState& S) {
 
 constexpr u32 kLongSeg = 32;        // longer segments: one wave each (k_fold_wave)
 #ifndef PHIP_HUGE_SEG
-#define PHIP_HUGE_SEG 16384
+#define PHIP_HUGE_SEG 32768   // C3: 16384 7.04-7.10 ms, 32768 6.70-6.76, 65536 6.83
 #endif
 constexpr u32 kHugeSeg = PHIP_HUGE_SEG;   // longer still: one workgroup each (k_fold_block)
 // The largest huge segments (at most this many) fold on a stream of their own.
@@ -2461,6 +2461,7 @@ __device__ inline void fold_window_absorb(u32 pos, u32 lim, FState& R, GMax& G, 
     if (wv == 0) {
       FState X = join_state(R, GMax{sh.state[4], sh.state[5], sh.state[6]});
       u32 j = p, quiet = 0, nrun = sh.nrun, exact_from = sh.exact_from;
+      const bool prof = sh.profiling;   // diagnostics counters only when asked (an LDS update per round)
       while (j < lim && quiet < 2 && exact_from == 0xFFFFFFFFu) {
         const u32 i = j + lane;
         const bool valid = i < lim;
@@ -2485,7 +2486,7 @@ __device__ inline void fold_window_absorb(u32 pos, u32 lim, FState& R, GMax& G, 
         const u32 q = (u32)__ffsll((long long)mb) - 1;
         const FState Y = lane_state(X2, q);
         const bool q_chg = (__ballot(chg) >> q) & 1;
-        if (lane == 0) { ++sh.n_iter; sh.n_raise += !q_chg; }
+        if (prof && lane == 0) { ++sh.n_iter; sh.n_raise += !q_chg; }
         if (q_chg) {
           if (!state_grew(X, Y)) exact_from = nrun;
           if (lane == 0) put_run(rp, rs, nrun, pos + j + q + 1, Y);

@@ -309,9 +309,10 @@ def _check_mixed(pa, args, log2_slots, reply=False):
 def test_mixed_hot_adversarial_all_fold_kinds(pa):
     """Thread, wave and workgroup folds on one stream with every op kind:
     Take (odd rates), Receive of dirty states (incast replies, -0.0, NaN,
-    negatives) and Upsert, with 3 buckets hot enough for k_fold_block."""
+    negatives) and Upsert, with 3 buckets hot enough for k_fold_block
+    (about 75k, 50k and 35k ops: over the 32768-op huge threshold)."""
     rng = np.random.default_rng(5150)
-    n, K = 200000, 3000
+    n, K = 500000, 3000
     args = list(_mixed_stream(rng, n, K))
     ids = _gen.zipf_ids(rng, n, K)
     hot = rng.random(n)
