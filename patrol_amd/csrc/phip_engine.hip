@@ -953,8 +953,11 @@ int ordered(phip_handle* h, Src src, u32 n, const OpView& ov, const OutView& ow)
       HIPCHK(h, hipGetLastError());
       {
         Launch l(h, no, st);
-        k_huge_outputs<<<hgrid, kBlock, 0, st>>>(hl, h1, hoff, woff, scnt, hval, hop, rpos, rst,
-                                                  runn, segex, segxf, wrun, wing, ow, h0);
+#define PHIP_HUGE_OUT(M)                                                                      \
+  k_huge_outputs<M><<<hgrid, kBlock, 0, st>>>(hl, h1, hoff, woff, scnt, hval, hop, rpos, rst, \
+                                              runn, segex, segxf, wrun, wing, ow, h0)
+        PHIP_OUT_DISPATCH(out_mask(ow), PHIP_HUGE_OUT);
+#undef PHIP_HUGE_OUT
       }
       HIPCHK(h, hipGetLastError());
       return PHIP_OK;

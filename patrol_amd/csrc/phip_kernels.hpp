@@ -2681,6 +2681,7 @@ __global__ __launch_bounds__(kFoldThreads) void k_fold_block(
 // run search only spans the runs that begin inside the window (usually none).
 constexpr u32 kOutPer = kFoldWin / kBlock;
 
+template <u32 kOut>
 __global__ __launch_bounds__(kBlock) void k_huge_outputs(
     const u32* __restrict__ huge_list, u32 nhuge, const u64* __restrict__ hoff,
     const u64* __restrict__ woff, const u32* __restrict__ seg_count,
@@ -2732,27 +2733,40 @@ __global__ __launch_bounds__(kBlock) void k_huge_outputs(
   __syncthreads();
   for (u32 y = 0; y < wv; ++y) exc = gmax(exc, wtot[y]);
   GMax gj = gmax(g0, exc);
+  // Every op's run first (its loads), then the evaluations, then the
+  // stores: with the stores last and specialised on the outputs present
+  // (write_out_m), no run load waits for an earlier op's stores (gfx9's
+  // in-order vmcnt).
+  u32 lo[kOutPer];
+  RunState q[kOutPer];
 #pragma unroll
   for (u32 k = 0; k < kOutPer; ++k) {
-    const u32 j = j0 + k;
-    if (j >= p1) break;
-    u32 lo = k0, hi = k1;   // last run in [k0, k1] with rp[run] <= j
-    while (lo < hi) {
-      const u32 mid = (lo + hi + 1) >> 1;
-      if (rp[mid] <= j) lo = mid; else hi = mid - 1;
+    const u32 j = min(j0 + k, p1 - 1);
+    u32 l = k0, hi = k1;   // last run in [k0, k1] with rp[run] <= j
+    while (l < hi) {
+      const u32 mid = (l + hi + 1) >> 1;
+      if (rp[mid] <= j) l = mid; else hi = mid - 1;
     }
-    const RunState q = rs[lo];
+    lo[k] = l;
+    q[k] = rs[l];
+  }
+  OpOut o[kOutPer];
+  FState seen[kOutPer];
+#pragma unroll
+  for (u32 k = 0; k < kOutPer; ++k) {
     FState S;
-    S.a = as_f64(q.a); S.t = as_f64(q.t); S.e = q.e; S.c = q.c;
-    S.existed = lo > 0 || existed0;
-    if (lo < exact_from) S = join_state(S, gj);
+    S.a = as_f64(q[k].a); S.t = as_f64(q[k].t); S.e = q[k].e; S.c = q[k].c;
+    S.existed = lo[k] > 0 || existed0;
+    if (lo[k] < exact_from) S = join_state(S, gj);
     const SOp sop = make_sop(op[k], val[k]);
     FState S2;
-    OpOut o;
-    eval_sop(sop, S, S2, o);
-    write_out(ow, sop.idx, o, S);
-    gj = gmax(gj, merge_contrib(op[k], val[k]));
+    eval_sop(sop, S, S2, o[k]);
+    seen[k] = S;
+    if (j0 + k < p1) gj = gmax(gj, merge_contrib(op[k], val[k]));
   }
+#pragma unroll
+  for (u32 k = 0; k < kOutPer; ++k)
+    if (j0 + k < p1) write_out_m<kOut>(ow, val[k] & kOpIdxMask, o[k], seen[k]);
   __syncthreads();   // the window's shared arrays are reused by the next
   }
 }
