@@ -560,9 +560,12 @@ int fast_apply(phip_handle* h, In in, HotSrc hsrc, u32 n, u8* status, u32* first
   // kernel leaves is written again after it (k_receive_list and
   // k_mark_created for misses, the ordered path for the dirty suffix).
   // Byte stores from the kernel's lanes cost it 2%.
-  if (status && !with_hot) HIPCHK(h, hipMemsetAsync(status, PHIP_ST_MERGED, n, h->stream));
+  // A batch whose directory chain goes first (a small one) keeps the chain
+  // short: its fill runs on the main stream, which waits for the chain anyway.
+  const bool fill_main = !with_hot || hot_first;
   if (with_hot) HIPCHK(h, hipEventRecord(h->ev_fork, h->stream));
-  if (with_hot && hot_first && (rc = fork_hot(h, hsrc, n, &hot, &hot_dir, status, n))) return rc;
+  if (with_hot && hot_first && (rc = fork_hot(h, hsrc, n, &hot, &hot_dir))) return rc;
+  if (status && fill_main) HIPCHK(h, hipMemsetAsync(status, PHIP_ST_MERGED, n, h->stream));
   {
     Launch l(h, "k_classify");
     bool done = false;
