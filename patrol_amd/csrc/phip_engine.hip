@@ -530,8 +530,7 @@ int pack_sharded(phip_handle* h, const Sharded& sh, u32 total_slot, u32* out, u3
 }
 
 template <class Src>
-int fork_hot(phip_handle* h, Src src, u32 n, const HotHdr** hot, const HotEntry** hot_dir,
-             u8* fill = nullptr, u32 nfill = 0);
+int fork_hot(phip_handle* h, Src src, u32 n, const HotHdr** hot, const HotEntry** hot_dir);
 
 // Enqueue order matters at this size (2 ms per 100M messages): the counter
 // reset and the classification go first, so the GPU starts reading the batch
@@ -555,17 +554,15 @@ int fast_apply(phip_handle* h, In in, HotSrc hsrc, u32 n, u8* status, u32* first
   const HotHdr* hot = nullptr;
   const HotEntry* hot_dir = nullptr;
   // Statuses: the fast kernel merges most of the batch and writes none; the
-  // column is filled with PHIP_ST_MERGED up front (on stream2 beside the
-  // classification when there is a directory chain), and every message the
-  // kernel leaves is written again after it (k_receive_list and
-  // k_mark_created for misses, the ordered path for the dirty suffix).
-  // Byte stores from the kernel's lanes cost it 2%.
-  // A batch whose directory chain goes first (a small one) keeps the chain
-  // short: its fill runs on the main stream, which waits for the chain anyway.
-  const bool fill_main = !with_hot || hot_first;
+  // column is filled with PHIP_ST_MERGED up front on the main stream, and
+  // every message the kernel leaves is written again after it
+  // (k_receive_list and k_mark_created for misses, the ordered path for the
+  // dirty suffix).  Byte stores from the kernel's lanes cost it 2%; the
+  // fill on stream2 beside the classification slowed the classification
+  // more than it cost here.
   if (with_hot) HIPCHK(h, hipEventRecord(h->ev_fork, h->stream));
   if (with_hot && hot_first && (rc = fork_hot(h, hsrc, n, &hot, &hot_dir))) return rc;
-  if (status && fill_main) HIPCHK(h, hipMemsetAsync(status, PHIP_ST_MERGED, n, h->stream));
+  if (status) HIPCHK(h, hipMemsetAsync(status, PHIP_ST_MERGED, n, h->stream));
   {
     Launch l(h, "k_classify");
     bool done = false;
@@ -579,7 +576,7 @@ int fast_apply(phip_handle* h, In in, HotSrc hsrc, u32 n, u8* status, u32* first
     if (!done) k_classify<In><<<grid_for(n), kBlock, 0, h->stream>>>(in, n, h->ctr);
   }
   HIPCHK(h, hipGetLastError());
-  if (with_hot && !hot_first && (rc = fork_hot(h, hsrc, n, &hot, &hot_dir, status, n))) return rc;
+  if (with_hot && !hot_first && (rc = fork_hot(h, hsrc, n, &hot, &hot_dir))) return rc;
   // The fast kernel is enqueued behind the classification without a host
   // round trip; it reads the counters itself.
   if ((rc = join_hot(h, hot))) return rc;
@@ -599,8 +596,7 @@ int fast_apply(phip_handle* h, In in, HotSrc hsrc, u32 n, u8* status, u32* first
 }
 
 template <class Src>
-int fork_hot(phip_handle* h, Src src, u32 n, const HotHdr** hot, const HotEntry** hot_dir,
-             u8* fill, u32 nfill);
+int fork_hot(phip_handle* h, Src src, u32 n, const HotHdr** hot, const HotEntry** hot_dir);
 
 // One message per distinct name of list[0..n) (k_dedupe) into B_DEDUP.
 template <class Src>
@@ -700,17 +696,13 @@ int finish_misses(phip_handle* h, Src src, const uint64_t* a, const uint64_t* t,
 
 // Start the hot directory of a fast batch on stream2 (joined by join_hot).
 template <class Src>
-int fork_hot(phip_handle* h, Src src, u32 n, const HotHdr** hot, const HotEntry** hot_dir,
-             u8* fill, u32 nfill) {
+int fork_hot(phip_handle* h, Src src, u32 n, const HotHdr** hot, const HotEntry** hot_dir) {
   *hot = nullptr;
   *hot_dir = nullptr;
   if (n < kHotMinBatch) return PHIP_OK;
   // ev_fork: recorded by fast_apply before the classification (stream2 waits
   // only for the batch's producers, not for k_classify)
   HIPCHK(h, hipStreamWaitEvent(h->stream2, h->ev_fork, 0));
-  // The status column's PHIP_ST_MERGED fill (fast_apply) beside the
-  // classification, joined with the directory before the fast kernel.
-  if (fill) HIPCHK(h, hipMemsetAsync(fill, PHIP_ST_MERGED, nfill, h->stream2));
   int rc;
   if ((rc = build_hot(h, src, n, h->stream2, hot, hot_dir))) return rc;
   HIPCHK(h, hipEventRecord(h->ev_join, h->stream2));
