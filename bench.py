@@ -189,20 +189,32 @@ def replica_states(torch, gen, n, step, dev):
 
 
 # ---------------------------------------------------------- CPU baseline ---
-def cpu_baseline(args, K, ids_host, threads):
+def cpu_thread_counts(args):
+    """1, the box's CPU share (16) and nproc threads (1 and nproc)."""
+    nproc = os.cpu_count() or 1
+    if args.cpu_threads:
+        return [args.cpu_threads]
+    return sorted({1, min(16, nproc), nproc})
+
+
+def cpu_baseline(args, K, ids_host):
     """The Go-structured C++ restatement (global RWMutex + map + per-bucket
     RWMutex, repo.go:171-235 / bucket.go:240-263) timed on this host on a
-    bounded sample of the same workload."""
+    bounded sample of the same workload, at 1, 16 and nproc threads (each on
+    a freshly seeded map); `value` is the nproc figure."""
     import torch
     from oracle import oracle as O
     L = O.lib()
-    repo = O.Repo()
     keys = torch.arange(K, dtype=torch.int64)
     kb, ko = names_for_ids(torch, keys, args.name_len)
-    z = np.zeros(K, np.uint64)
-    L.orc_repo_seed(repo.h, kb.numpy(), ko.numpy().astype(np.uint32), K, z, z,
-                    np.zeros(K, np.int64), np.full(K, T0, np.int64))
+    kb_np, ko_np = kb.numpy(), ko.numpy().astype(np.uint32)
     del kb, ko, keys
+    z = np.zeros(K, np.uint64)
+
+    def seeded():
+        repo = O.Repo()
+        L.orc_repo_seed(repo.h, kb_np, ko_np, K, z, z, np.zeros(K, np.int64), np.full(K, T0, np.int64))
+        return repo
     n = min(args.cpu_sample, ids_host.numel())
     ids = ids_host[:n]
     blob, offs = names_for_ids(torch, ids, args.name_len)
@@ -210,19 +222,24 @@ def cpu_baseline(args, K, ids_host, threads):
     a, t, e = replica_states(torch, g, n, 0, "cpu")
     blob_np, offs_np = blob.numpy(), offs.numpy().astype(np.uint32)
     a_np, t_np, e_np = a.numpy().view(np.uint64), t.numpy().view(np.uint64), e.numpy()
-    secs = L.orc_bench_receive(repo.h, blob_np, offs_np, n, a_np, t_np, e_np, T0, threads)
-    n1 = min(n, 2_000_000)
-    # single goroutine, as the reference's Receive loop runs (repo.go:54)
-    repo1 = O.Repo()
-    kb, ko = names_for_ids(torch, torch.arange(K, dtype=torch.int64), args.name_len)
-    L.orc_repo_seed(repo1.h, kb.numpy(), ko.numpy().astype(np.uint32), K, z, z,
-                    np.zeros(K, np.int64), np.full(K, T0, np.int64))
-    secs1 = L.orc_bench_receive(repo1.h, blob_np, offs_np, n1, a_np, t_np, e_np, T0, 1)
-    return dict(value=n / secs, unit="merges/s", cores=threads, kind="port", **host_cpu(),
+    runs = {}
+    for th in cpu_thread_counts(args):
+        # one goroutine (the reference's Receive loop, repo.go:54) gets a
+        # smaller sample: it runs at a few M merges/s
+        m = n if th > 1 else min(n, 2_000_000)
+        repo = seeded()
+        secs = L.orc_bench_receive(repo.h, blob_np, offs_np, m, a_np, t_np, e_np, T0, th)
+        del repo
+        runs[th] = dict(value=m / secs, messages=m)
+    top = max(runs)
+    return dict(value=runs[top]["value"], unit="merges/s", cores=top, kind="port", **host_cpu(),
                 sample=f"{n} of the step-0 messages (Zipf {args.zipf} over {K} buckets) into a "
-                       f"{K}-bucket Go-structured map, {threads} threads",
-                single_thread=dict(value=n1 / secs1, sample=f"{n1} messages, 1 thread (the "
-                                   "reference's single Receive goroutine)"))
+                       f"{K}-bucket Go-structured map, {top} threads (nproc); 1 thread: "
+                       f"{runs[min(runs)]['messages']} messages",
+                by_threads={str(k): v["value"] for k, v in sorted(runs.items())},
+                single_thread=dict(value=runs[min(runs)]["value"],
+                                   sample=f"{runs[min(runs)]['messages']} messages, 1 thread (the "
+                                          "reference's single Receive goroutine)"))
 
 
 def host_cpu():
@@ -324,31 +341,44 @@ def run_c3(args, torch, dev, repo, rank, K, base, gen):
                                 status=status, remaining=rem)
 
     def cpu():
-        """The same stream through the Go-structured restatement (oracle,
-        orc_bench_mixed) on a bounded prefix, one thread: a mixed stream
-        with per-bucket order is applied in stream order (the reference
-        serialises each bucket under its mutex; one goroutine per request)."""
+        """The same stream through the Go-structured restatement (oracle) on a
+        bounded prefix: one thread in stream order (orc_bench_mixed), and 16 /
+        nproc threads (orc_bench_mixed_mt: each bucket's ops on one worker in
+        stream order, the global map lock and the bucket mutex per op, as
+        concurrent Go handlers take them).  `value` is the nproc figure."""
         from oracle import oracle as O
         L = O.lib()
-        orepo = O.Repo()
         keys = torch.arange(base, base + K, dtype=torch.int64)
         kb, ko = names_for_ids(torch, keys)
-        z = np.zeros(K, np.uint64)
-        L.orc_repo_seed(orepo.h, kb.numpy(), ko.numpy().astype(np.uint32), K, z, z,
-                        np.zeros(K, np.int64), np.full(K, T0, np.int64))
+        kb_np, ko_np = kb.numpy(), ko.numpy().astype(np.uint32)
         del kb, ko, keys
+        z = np.zeros(K, np.uint64)
         m = min(args.cpu_sample // 2, n)
         sb, so = names_for_ids(torch, ids[:m].cpu() + base)
+        sb_np, so_np = sb.numpy(), so.numpy().astype(np.uint32)
         now, a, t, e = steps[args.warmup]
         cols = [x[:m].cpu().numpy() for x in (kind, now, freq, per, cnt, a, t, e)]
-        st = np.zeros(m, np.uint8)
-        rm = np.zeros(m, np.uint64)
-        secs = L.orc_bench_mixed(orepo.h, cols[0], sb.numpy(), so.numpy().astype(np.uint32), m,
-                                 cols[1], cols[2], cols[3], cols[4].view(np.uint64),
-                                 cols[5].view(np.uint64), cols[6].view(np.uint64), cols[7], st, rm)
-        return dict(value=m / secs, unit="ops/s", cores=1, kind="port", **host_cpu(),
+        runs = {}
+        for th in cpu_thread_counts(args):
+            orepo = O.Repo()
+            L.orc_repo_seed(orepo.h, kb_np, ko_np, K, z, z, np.zeros(K, np.int64),
+                            np.full(K, T0, np.int64))
+            st = np.zeros(m, np.uint8)
+            rm = np.zeros(m, np.uint64)
+            f = L.orc_bench_mixed if th == 1 else L.orc_bench_mixed_mt
+            extra = () if th == 1 else (th,)
+            secs = f(orepo.h, cols[0], sb_np, so_np, m, cols[1], cols[2], cols[3],
+                     cols[4].view(np.uint64), cols[5].view(np.uint64), cols[6].view(np.uint64),
+                     cols[7], st, rm, *extra)
+            del orepo
+            runs[th] = m / secs
+        top = max(runs)
+        return dict(value=runs[top], unit="ops/s", cores=top, kind="port", **host_cpu(),
                     sample=f"first {m} ops of the timed stream (Zipf {args.zipf} over {K} "
-                           f"buckets) through the Go-structured restatement, 1 thread")
+                           f"buckets) through the Go-structured restatement, {top} threads "
+                           "(nproc; each bucket's ops on one worker, in stream order)",
+                    by_threads={str(k): v for k, v in sorted(runs.items())},
+                    single_thread=dict(value=runs[min(runs)], sample=f"the same {m} ops, 1 thread"))
     return n, step, cpu
 
 
@@ -416,6 +446,7 @@ def open_group(args, dist, repo, rank, world):
 
 
 ROUTED_LIMIT_S = 300   # the owner-routed leg's watchdog (main())
+ROUTED_TIMEOUT_EXIT = 3   # exit status when the watchdog fired
 
 
 def run_routed(args, torch, dist, dev, local, rank, world):
@@ -828,9 +859,8 @@ def main():
     }
     out["config"].update(extra)
     if rank == 0 and world == 1 and not args.no_cpu and args.workload == "c2":
-        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
         try:
-            out["cpu_baseline"] = cpu_baseline(args, K, ids.cpu(), threads)
+            out["cpu_baseline"] = cpu_baseline(args, K, ids.cpu())
         except Exception as ex:  # the baseline must never hide the GPU result
             out["cpu_baseline"] = {"error": repr(ex)}
     elif rank == 0 and world == 1 and not args.no_cpu and c3_cpu is not None:
@@ -859,10 +889,12 @@ def main():
         import threading
 
         def give_up():
+            # the line still carries the headline, but the exit status says
+            # the routed leg hung (a driver or CI must be able to tell)
             if rank == 0:
                 out["owner_routed"] = {"error": f"timed out after {ROUTED_LIMIT_S} s"}
                 print(json.dumps(out), file=json_out, flush=True)
-            os._exit(0)
+            os._exit(ROUTED_TIMEOUT_EXIT)
         dog = threading.Timer(ROUTED_LIMIT_S, give_up)
         dog.daemon = True
         dog.start()

@@ -52,7 +52,7 @@
 extern "C" {
 #endif
 
-#define PHIP_ABI_VERSION 2
+#define PHIP_ABI_VERSION 3
 
 /* bucket.go:36-44 */
 #define PHIP_BUCKET_FIXED_SIZE 25
@@ -98,11 +98,18 @@ enum {
 /* Call flags. */
 #define PHIP_DEVICE_PTRS 0x1u   /* all pointers of the call are device memory */
 #define PHIP_ROUTE_COMBINE 0x2u /* phip_route_pack: combine hot names at the sender */
+#define PHIP_GROUP_RCCL_SELF 0x4u /* phip_group_receive (testing): a member's own segment also
+                                     travels through RCCL (ncclSend/ncclRecv to itself) instead
+                                     of a device copy, and a world-1 group exchanges through
+                                     RCCL instead of merging its send buffers in place, so the
+                                     per-peer RCCL exchange runs on a single GPU */
 
 /* phip_config.flags */
 #define PHIP_CFG_NO_GROW 0x1u   /* refuse (PHIP_ERR_FULL / PHIP_ERR_ARENA) instead of growing */
 #define PHIP_CFG_NO_SMALL 0x2u  /* ordered batches of <= 1024 host ops also take the large,
                                    multi-launch path (by default they run as one launch) */
+#define PHIP_CFG_FIXED_SEED 0x4u /* place buckets with hash_seed as given (0: the unseeded
+                                    placement) instead of a random per-handle seed */
 
 typedef struct phip_config {
   int32_t device;        /* HIP device ordinal                                          */
@@ -113,7 +120,17 @@ typedef struct phip_config {
                               force tag collisions (names are always compared)          */
   uint32_t flags;        /* PHIP_CFG_*                                                   */
   uint32_t reserved;
+  uint64_t hash_seed;    /* only with PHIP_CFG_FIXED_SEED (see "Placement" below)        */
 } phip_config;
+/*
+ * Placement.  A bucket's tag is FNV-1a 64 of its name (also the shard map's
+ * key, phip_group_*); its home slot is the top log2_slots bits of a 64-bit
+ * mix of (tag ^ seed), with a seed drawn from the OS for every handle.  Go's
+ * map, which the reference keeps its buckets in (repo.go:175), hashes with a
+ * per-process random seed too: names chosen to collide under one placement
+ * do not pile up on one probe chain under another.  Names are always
+ * compared, so the seed never changes results, only where records lie.
+ */
 /*
  * Capacity.  Go's map never refuses a bucket (repo.go:204-207,225-227), so by
  * default the table and the long-name arena grow: before a batch creates
@@ -173,7 +190,16 @@ typedef struct phip_results {
   uint8_t* status;           /* PHIP_ST_* (| PHIP_ST_CREATED)                   */
   uint64_t* remaining;       /* TAKE: uint64(remaining) as Go returns it        */
   uint64_t* have;            /* TAKE: float64 bits of the value truncated       */
-  phip_state* reply;         /* INCAST_REPLY: local state to unicast back       */
+  phip_state* reply;         /* the bucket's state right after the op, for:
+                                  TAKE: what UpsertBucket broadcasts after the take
+                                        (api.go:74, repo.go:123-127);
+                                  UPSERT: the upserted bucket (repo.go:123-127);
+                                  RECEIVE of a zero state (incast): the local state,
+                                        unchanged by it: the unicast payload of an
+                                        INCAST_REPLY (repo.go:86-90), and what
+                                        GetBucket found or created (repo.go:189-211).
+                                  Not written for a merged replica (PHIP_ST_MERGED of
+                                  a RECEIVE op).                                    */
 } phip_results;
 
 /* ---- lifecycle ---- */
@@ -297,6 +323,30 @@ int phip_batcher_api_take(phip_batcher* b, const uint8_t* name, uint32_t len, co
  * out[3] ns spent in phip_apply_mixed, out[4] batches that failed.
  * Returns the number written (<= 5). */
 int phip_batcher_stats(phip_batcher* b, uint64_t* out, int max);
+/* Everything the reference handler does after GetBucket -> Take ->
+ * UpsertBucket (api.go:67-74), from the same batched launch: whether the
+ * Take's GetBucket created the bucket (ReplicatedRepo.GetBucket then sends
+ * its zero-state incast request, repo.go:96-106: datagram bytes [24, len)
+ * with 24 zero bytes in front) and the MarshalBinary datagram of the state
+ * right after the Take, which UpsertBucket broadcasts (repo.go:123-158). */
+typedef struct phip_take_reply {
+  uint64_t remaining;      /* uint64(remaining) as Take returns it (the HTTP body)          */
+  uint8_t ok;              /* 1: HTTP 200, 0: 429                                            */
+  uint8_t created;         /* this request's GetBucket created the bucket                    */
+  uint16_t datagram_len;   /* 25 + len(name); 0 when nothing was taken (HTTP 400)           */
+  uint32_t reserved;
+  uint64_t seq;            /* arrival number (phip_batcher_take)                             */
+  phip_state state;        /* the bucket right after the Take                                */
+  uint8_t datagram[PHIP_BUCKET_PACKET_SIZE]; /* MarshalBinary(state) (bucket.go:51-68)       */
+} phip_take_reply;
+int phip_batcher_take_reply(phip_batcher* b, const uint8_t* name, uint32_t len, int64_t now,
+                            int64_t freq, int64_t per, uint64_t count, phip_take_reply* out);
+/* API.takeBucket (api.go:51-86) through the batcher, as phip_batcher_api_take,
+ * plus *out for the replication it triggers (out->datagram_len = 0 on 400). */
+int phip_batcher_api_take_reply(phip_batcher* b, const uint8_t* name, uint32_t len,
+                                const char* rate, uint32_t rate_len, const char* count,
+                                uint32_t count_len, int64_t now, char* body, uint32_t* body_len,
+                                phip_take_reply* out);
 
 /* ---- batched UDP ingest (command.go's replicator) ----
  * The reference's Receive goroutine reads ONE datagram per iteration into a
@@ -472,6 +522,11 @@ void phip_set_timing(phip_handle* h, int on);
  * that missed the table (inserted); out[3] table growths (rehashes) since
  * phip_open.  Returns the number written (<= 4). */
 int phip_last_stats(phip_handle* h, uint64_t* out, int max);
+/* Placement quality of the table (one scan of the slots): out[0] buckets,
+ * out[1] slots, out[2] the longest probe distance of a bucket from its home
+ * slot, out[3] the sum of those distances.  Returns the number written
+ * (<= 4) or < 0. */
+int phip_table_stats(phip_handle* h, uint64_t* out, int max);
 
 #ifdef __cplusplus
 }

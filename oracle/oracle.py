@@ -48,7 +48,7 @@ def lib():
                                   u8p, u64p, u64p, i64p]
     L.orc_upsert_soa.argtypes = [vp, u8p, u32p, C.c_uint32, u64p, u64p, i64p, C.c_int64, u8p]
     L.orc_apply_mixed.argtypes = [vp, u8p, u8p, u32p, C.c_uint32, i64p, i64p, i64p, u64p,
-                                  u64p, u64p, i64p, u8p, u64p, u64p, u64p, u64p, i64p]
+                                  u64p, u64p, i64p, u8p, u64p, u64p, u64p, u64p, i64p, i64p]
     L.orc_get.argtypes = [vp, C.c_char_p, C.c_uint32, C.POINTER(C.c_uint64),
                           C.POINTER(C.c_uint64), C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
     L.orc_get.restype = C.c_int
@@ -87,6 +87,9 @@ def lib():
     L.orc_bench_mixed.argtypes = [vp, u8p, u8p, u32p, C.c_uint32, i64p, i64p, i64p, u64p, u64p,
                                   u64p, i64p, u8p, u64p]
     L.orc_bench_mixed.restype = C.c_double
+    L.orc_bench_mixed_mt.argtypes = [vp, u8p, u8p, u32p, C.c_uint32, i64p, i64p, i64p, u64p,
+                                     u64p, u64p, i64p, u8p, u64p, C.c_int]
+    L.orc_bench_mixed_mt.restype = C.c_double
     L.orc_check_dump.argtypes = [vp, u8p, u64p, C.c_uint64, u64p, u64p, i64p, i64p,
                                  C.POINTER(C.c_uint64)]
     L.orc_check_dump.restype = C.c_uint64
@@ -175,6 +178,7 @@ class Repo:
         ra = np.zeros(z, np.uint64)
         rt = np.zeros(z, np.uint64)
         re = np.zeros(z, np.int64)
+        rc = np.zeros(z, np.int64)
 
         def a(x, t):
             x = np.ascontiguousarray(x, t)
@@ -182,9 +186,9 @@ class Repo:
         self.L.orc_apply_mixed(self.h, a(kind, np.uint8), blob, offs, n, a(now, np.int64),
                                a(freq, np.int64), a(per, np.int64), a(count, np.uint64),
                                a(added_bits, np.uint64), a(taken_bits, np.uint64),
-                               a(elapsed, np.int64), st, rem, have, ra, rt, re)
+                               a(elapsed, np.int64), st, rem, have, ra, rt, re, rc)
         return dict(status=st[:n], remaining=rem[:n], have=have[:n], reply_added=ra[:n],
-                    reply_taken=rt[:n], reply_elapsed=re[:n])
+                    reply_taken=rt[:n], reply_elapsed=re[:n], reply_created=rc[:n])
 
     def get(self, name: bytes):
         a, t, e, c = C.c_uint64(), C.c_uint64(), C.c_int64(), C.c_int64()

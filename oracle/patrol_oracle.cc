@@ -492,12 +492,26 @@ void orc_upsert_soa(void* r, const uint8_t* names, const uint32_t* offs, uint32_
 // Mixed ordered stream: kind 0 = Take (api.go:67-74 minus HTTP), kind 1 =
 // received replica state (repo.go:78-90), kind 2 = UpsertBucket (repo.go:215-235).  Ops apply in index order; each op
 // carries its own clock reading `now`, also used as `created` on a miss.
+// reply_* (any may be null) receive the bucket's state right after the op
+// for a Take (what UpsertBucket broadcasts next, api.go:74 -> repo.go:123-127),
+// an Upsert (the upserted bucket, repo.go:123-127) and an incast (the local
+// state: the unicast payload of repo.go:86-90 when it is sent); merged
+// replicas leave them untouched.
+static inline void put_reply(const Bucket* b, uint32_t i, uint64_t* ra, uint64_t* rt, int64_t* re,
+                             int64_t* rc) {
+  std::shared_lock<std::shared_mutex> l(b->mu);
+  if (ra) ra[i] = f2b(b->added);
+  if (rt) rt[i] = f2b(b->taken);
+  if (re) re[i] = b->elapsed;
+  if (rc) rc[i] = b->created;
+}
+
 void orc_apply_mixed(void* r, const uint8_t* kind, const uint8_t* names, const uint32_t* offs,
                      uint32_t n, const int64_t* now, const int64_t* freq, const int64_t* per,
                      const uint64_t* count, const uint64_t* added, const uint64_t* taken,
                      const int64_t* elapsed, uint8_t* status, uint64_t* remaining,
                      uint64_t* have_bits, uint64_t* reply_added, uint64_t* reply_taken,
-                     int64_t* reply_elapsed) {
+                     int64_t* reply_elapsed, int64_t* reply_created) {
   LocalRepo* repo = (LocalRepo*)r;
   Bucket remote;
   for (uint32_t i = 0; i < n; ++i) {
@@ -507,10 +521,11 @@ void orc_apply_mixed(void* r, const uint8_t* kind, const uint8_t* names, const u
       up.name.assign(name);
       up.added = b2f(added[i]); up.taken = b2f(taken[i]); up.elapsed = elapsed[i];
       bool merged;
-      repo->upsert_bucket(up, now[i], &merged);
+      const Bucket* got = repo->upsert_bucket(up, now[i], &merged);
       status[i] = merged ? ST_MERGED : (ST_UPSERT_INSERTED | ST_CREATED);
       if (remaining) remaining[i] = 0;
       if (have_bits) have_bits[i] = 0;
+      put_reply(got, i, reply_added, reply_taken, reply_elapsed, reply_created);
       continue;
     }
     bool existed;
@@ -521,15 +536,14 @@ void orc_apply_mixed(void* r, const uint8_t* kind, const uint8_t* names, const u
       st = t.ok ? ST_TAKE_OK : ST_TAKE_DENIED;
       if (remaining) remaining[i] = t.remaining;
       if (have_bits) have_bits[i] = f2b(t.have);
+      put_reply(b, i, reply_added, reply_taken, reply_elapsed, reply_created);
     } else {
       remote.added = b2f(added[i]); remote.taken = b2f(taken[i]); remote.elapsed = elapsed[i];
       if (!is_zero(remote)) { merge(*b, remote); st = ST_MERGED; }
-      else if (existed && !is_zero(*b)) {
-        st = ST_INCAST_REPLY;
-        if (reply_added) reply_added[i] = f2b(b->added);
-        if (reply_taken) reply_taken[i] = f2b(b->taken);
-        if (reply_elapsed) reply_elapsed[i] = b->elapsed;
-      } else st = ST_INCAST_NOREPLY;
+      else {
+        st = existed && !is_zero(*b) ? ST_INCAST_REPLY : ST_INCAST_NOREPLY;
+        put_reply(b, i, reply_added, reply_taken, reply_elapsed, reply_created);
+      }
       if (remaining) remaining[i] = 0;
       if (have_bits) have_bits[i] = 0;
     }
@@ -716,7 +730,70 @@ double orc_bench_mixed(void* r, const uint8_t* kind, const uint8_t* names, const
                        const int64_t* elapsed, uint8_t* status, uint64_t* remaining) {
   auto t0 = std::chrono::steady_clock::now();
   orc_apply_mixed(r, kind, names, offs, n, now, freq, per, count, added, taken, elapsed, status,
-                  remaining, nullptr, nullptr, nullptr, nullptr);
+                  remaining, nullptr, nullptr, nullptr, nullptr, nullptr);
+  auto t1 = std::chrono::steady_clock::now();
+  return std::chrono::duration<double>(t1 - t0).count();
+}
+
+// Times the ordered mixed stream on `threads` workers the way concurrent Go
+// handlers run it: every op takes the global map lock (GetBucket,
+// repo.go:189-211) and its bucket's mutex (bucket.go:186-225, 240-263);
+// per-bucket order is the stream's, because each bucket's ops are given to
+// one worker (by a hash of the name, assigned before the timed region) and
+// that worker runs them in stream order.  Returns seconds.
+double orc_bench_mixed_mt(void* r, const uint8_t* kind, const uint8_t* names, const uint32_t* offs,
+                          uint32_t n, const int64_t* now, const int64_t* freq, const int64_t* per,
+                          const uint64_t* count, const uint64_t* added, const uint64_t* taken,
+                          const int64_t* elapsed, uint8_t* status, uint64_t* remaining,
+                          int threads) {
+  LocalRepo* repo = (LocalRepo*)r;
+  if (threads < 1) threads = 1;
+  std::vector<std::vector<uint32_t>> part(threads);
+  for (uint32_t i = 0; i < n; ++i) {
+    std::string_view name((const char*)names + offs[i], offs[i + 1] - offs[i]);
+    part[std::hash<std::string_view>{}(name) % (size_t)threads].push_back(i);
+  }
+  std::vector<std::thread> th;
+  std::atomic<int> ready{0};
+  std::atomic<bool> go{false};
+  auto worker = [&](int t) {
+    Bucket remote;
+    ready.fetch_add(1);
+    while (!go.load(std::memory_order_acquire)) {}
+    for (uint32_t i : part[t]) {
+      std::string_view name((const char*)names + offs[i], offs[i + 1] - offs[i]);
+      if (kind[i] == 2) {
+        Bucket up;
+        up.name.assign(name);
+        up.added = b2f(added[i]); up.taken = b2f(taken[i]); up.elapsed = elapsed[i];
+        bool merged;
+        repo->upsert_bucket(up, now[i], &merged);
+        status[i] = merged ? ST_MERGED : (ST_UPSERT_INSERTED | ST_CREATED);
+        continue;
+      }
+      bool existed;
+      Bucket* b = repo->get_bucket(name, now[i], &existed);
+      uint8_t st;
+      if (kind[i] == 0) {
+        TakeOut o = take(*b, now[i], Rate{freq[i], per[i]}, count[i]);
+        st = o.ok ? ST_TAKE_OK : ST_TAKE_DENIED;
+        remaining[i] = o.remaining;
+      } else {
+        {
+          std::unique_lock<std::shared_mutex> l(remote.mu);
+          remote.added = b2f(added[i]); remote.taken = b2f(taken[i]); remote.elapsed = elapsed[i];
+        }
+        if (!is_zero(remote)) { merge(*b, remote); st = ST_MERGED; }
+        else st = existed && !is_zero(*b) ? ST_INCAST_REPLY : ST_INCAST_NOREPLY;
+      }
+      status[i] = st | (existed ? 0 : ST_CREATED);
+    }
+  };
+  for (int t = 0; t < threads; ++t) th.emplace_back(worker, t);
+  while (ready.load() < threads) {}
+  auto t0 = std::chrono::steady_clock::now();
+  go.store(true, std::memory_order_release);
+  for (auto& x : th) x.join();
   auto t1 = std::chrono::steady_clock::now();
   return std::chrono::duration<double>(t1 - t0).count();
 }

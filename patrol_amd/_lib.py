@@ -24,7 +24,8 @@ EXPORTS = [
     "phip_ring_open", "phip_ring_close", "phip_ring_acquire", "phip_ring_submit",
     "phip_ring_receive", "phip_udp_recv_batch", "phip_incast_replies", "phip_udp_send_batch",
     "phip_batcher_open", "phip_batcher_close", "phip_batcher_take", "phip_batcher_api_take",
-    "phip_batcher_stats", "phip_group_unique_id", "phip_group_open_all", "phip_group_open_rank",
+    "phip_batcher_stats", "phip_batcher_take_reply", "phip_batcher_api_take_reply",
+    "phip_table_stats", "phip_group_unique_id", "phip_group_open_all", "phip_group_open_rank",
     "phip_group_close", "phip_group_last_error", "phip_group_world", "phip_group_local",
     "phip_group_handle", "phip_group_receive", "phip_group_anti_entropy",
 ]
@@ -40,13 +41,16 @@ OP_TAKE, OP_RECEIVE, OP_UPSERT = 0, 1, 2
 DEVICE_PTRS = 0x1
 CFG_NO_GROW = 0x1
 CFG_NO_SMALL = 0x2
+CFG_FIXED_SEED = 0x4
 ROUTE_COMBINE = 0x2
+GROUP_RCCL_SELF = 0x4
+PACKET_SIZE = 256
 
 
 class phip_config(C.Structure):
     _fields_ = [("device", C.c_int32), ("log2_slots", C.c_uint32), ("arena_bytes", C.c_uint64),
                 ("max_load_pct", C.c_uint32), ("debug_tag_bits", C.c_uint32),
-                ("flags", C.c_uint32), ("reserved", C.c_uint32)]
+                ("flags", C.c_uint32), ("reserved", C.c_uint32), ("hash_seed", C.c_uint64)]
 
 
 class phip_state(C.Structure):
@@ -69,6 +73,12 @@ class phip_ops(C.Structure):
 
 class phip_batcher_config(C.Structure):
     _fields_ = [("window_us", C.c_uint32), ("max_batch", C.c_uint32)]
+
+
+class phip_take_reply(C.Structure):
+    _fields_ = [("remaining", C.c_uint64), ("ok", C.c_uint8), ("created", C.c_uint8),
+                ("datagram_len", C.c_uint16), ("reserved", C.c_uint32), ("seq", C.c_uint64),
+                ("state", phip_state), ("datagram", C.c_uint8 * 256)]
 
 
 class phip_results(C.Structure):
@@ -153,6 +163,12 @@ def load(path: str = LIB_PATH):
     L.phip_batcher_api_take.argtypes = [vp, C.c_char_p, u32, C.c_char_p, u32, C.c_char_p, u32,
                                         i64, C.c_char_p, C.POINTER(u32)]
     L.phip_batcher_stats.argtypes = [vp, C.POINTER(u64), C.c_int]
+    L.phip_batcher_take_reply.argtypes = [vp, C.c_char_p, u32, i64, i64, i64, u64,
+                                          C.POINTER(phip_take_reply)]
+    L.phip_batcher_api_take_reply.argtypes = [vp, C.c_char_p, u32, C.c_char_p, u32, C.c_char_p,
+                                              u32, i64, C.c_char_p, C.POINTER(u32),
+                                              C.POINTER(phip_take_reply)]
+    L.phip_table_stats.argtypes = [vp, C.POINTER(u64), C.c_int]
     L.phip_group_unique_id.argtypes = [C.c_char_p]
     L.phip_group_open_all.argtypes = [C.POINTER(phip_config), C.POINTER(C.c_int32), u32,
                                       C.POINTER(vp)]

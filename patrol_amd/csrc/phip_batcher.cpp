@@ -40,6 +40,7 @@ struct Req {
   uint64_t remaining = 0;
   uint64_t seq = 0;
   uint8_t status = 0;
+  phip_state post{};            // the bucket right after this Take (phip_results.reply)
   int rc = 0;
   bool done = false;
   std::condition_variable cv;   // its caller waits here (woken alone, not with every waiter)
@@ -58,6 +59,8 @@ struct phip_batcher {
   std::vector<Req*> pending;
   Clock::time_point first_arrival;
   bool stop = false;
+  uint32_t waiters = 0;                // callers inside submit_and_wait (under mu)
+  std::condition_variable cv_idle;     // close() waits here for waiters == 0
   std::thread th;
   // stats
   uint64_t batches = 0, requests = 0, max_seen = 0, gpu_ns = 0, errors = 0;
@@ -67,6 +70,7 @@ struct phip_batcher {
   std::vector<uint32_t> offs;
   std::vector<int64_t> now, freq, per;
   std::vector<uint64_t> count, remaining;
+  std::vector<phip_state> post;
 
   void run();
   void dispatch(std::vector<Req*>& batch);
@@ -77,7 +81,7 @@ void phip_batcher::dispatch(std::vector<Req*>& batch) {
   kind.assign(n, PHIP_OP_TAKE);
   offs.resize(n + 1);
   now.resize(n); freq.resize(n); per.resize(n); count.resize(n);
-  status.assign(n, 0); remaining.assign(n, 0);
+  status.assign(n, 0); remaining.assign(n, 0); post.assign(n, phip_state{});
   size_t nb = 0;
   for (uint32_t i = 0; i < n; ++i) nb += batch[i]->len;
   names.resize(nb + 8);
@@ -102,6 +106,7 @@ void phip_batcher::dispatch(std::vector<Req*>& batch) {
   phip_results res{};
   res.status = status.data();
   res.remaining = remaining.data();
+  res.reply = post.data();   // each Take's post state: its broadcast, in the same launch
   const auto t0 = Clock::now();
   const int rc = phip_apply_mixed(h, &ops, &res, 0);
   gpu_ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now() - t0).count();
@@ -109,6 +114,7 @@ void phip_batcher::dispatch(std::vector<Req*>& batch) {
     batch[i]->rc = rc;
     batch[i]->status = status[i];
     batch[i]->remaining = remaining[i];
+    batch[i]->post = post[i];
   }
   if (rc) ++errors;
 }
@@ -154,15 +160,46 @@ void phip_batcher::run() {
 
 namespace {
 
+// The caller counts itself in `waiters` for as long as it touches the
+// batcher: close() deletes the batcher only once every woken caller has left
+// (a caller woken by the last batch may not yet have re-acquired mu when the
+// dispatcher exits).
 int submit_and_wait(phip_batcher* b, Req* r) {
   std::unique_lock<std::mutex> l(b->mu);
   if (b->stop) return PHIP_ERR_INVALID;
+  ++b->waiters;
   if (b->pending.empty()) b->first_arrival = Clock::now();
   r->seq = b->arrivals++;
   b->pending.push_back(r);
   if (b->pending.size() == 1 || b->pending.size() >= b->max_batch) b->cv_submit.notify_one();
   r->cv.wait(l, [&] { return r->done; });
+  if (--b->waiters == 0 && b->stop) b->cv_idle.notify_all();
   return r->rc;
+}
+
+// Take request -> its Req, the fields of phip_take_reply filled from it.
+int run_take(phip_batcher* b, const uint8_t* name, uint32_t len, int64_t now, int64_t freq,
+             int64_t per, uint64_t count, Req* r) {
+  if (!b || (!name && len)) return PHIP_ERR_INVALID;
+  if (len > PHIP_MAX_NAME_LEN) return PHIP_ERR_NAME_TOO_LARGE;
+  r->name = name;
+  r->len = len;
+  r->now = now;
+  r->freq = freq;
+  r->per = per;
+  r->count = count;
+  return submit_and_wait(b, r);
+}
+
+void fill_reply(const Req& r, phip_take_reply* out) {
+  out->remaining = r.remaining;
+  out->ok = (r.status & 0x7F) == PHIP_ST_TAKE_OK;
+  out->created = (r.status & PHIP_ST_CREATED) != 0;
+  out->reserved = 0;
+  out->seq = r.seq;
+  out->state = r.post;
+  const int sz = phip_marshal(r.len ? r.name : (const uint8_t*)"", r.len, &r.post, out->datagram);
+  out->datagram_len = sz > 0 ? (uint16_t)sz : 0;
 }
 
 }  // namespace
@@ -196,22 +233,18 @@ void phip_batcher_close(phip_batcher* b) {
   }
   b->cv_submit.notify_all();
   if (b->th.joinable()) b->th.join();
+  {
+    std::unique_lock<std::mutex> l(b->mu);
+    b->cv_idle.wait(l, [&] { return b->waiters == 0; });
+  }
   delete b;
 }
 
 int phip_batcher_take(phip_batcher* b, const uint8_t* name, uint32_t len, int64_t now,
                       int64_t freq, int64_t per, uint64_t count, uint64_t* remaining,
                       uint8_t* ok, uint64_t* seq) {
-  if (!b || (!name && len)) return PHIP_ERR_INVALID;
-  if (len > PHIP_MAX_NAME_LEN) return PHIP_ERR_NAME_TOO_LARGE;
   Req r;
-  r.name = name;
-  r.len = len;
-  r.now = now;
-  r.freq = freq;
-  r.per = per;
-  r.count = count;
-  const int rc = submit_and_wait(b, &r);
+  const int rc = run_take(b, name, len, now, freq, per, count, &r);
   if (rc) return rc;
   if (remaining) *remaining = r.remaining;
   if (ok) *ok = (r.status & 0x7F) == PHIP_ST_TAKE_OK;
@@ -237,6 +270,37 @@ int phip_batcher_api_take(phip_batcher* b, const uint8_t* name, uint32_t len, co
   std::memcpy(body, s.data(), s.size());
   *body_len = (uint32_t)s.size();
   return ok ? 200 : 429;
+}
+
+int phip_batcher_take_reply(phip_batcher* b, const uint8_t* name, uint32_t len, int64_t now,
+                            int64_t freq, int64_t per, uint64_t count, phip_take_reply* out) {
+  if (!out) return PHIP_ERR_INVALID;
+  Req r;
+  const int rc = run_take(b, name, len, now, freq, per, count, &r);
+  if (rc) return rc;
+  fill_reply(r, out);
+  return PHIP_OK;
+}
+
+int phip_batcher_api_take_reply(phip_batcher* b, const uint8_t* name, uint32_t len,
+                                const char* rate, uint32_t rate_len, const char* count,
+                                uint32_t count_len, int64_t now, char* body, uint32_t* body_len,
+                                phip_take_reply* out) {
+  if (!b || !body || !body_len || !out) return PHIP_ERR_INVALID;
+  std::memset(out, 0, sizeof *out);
+  int64_t freq, per;
+  uint64_t n;
+  const int pre = phip_host::api_prepare(name, len, rate, rate_len, count, count_len, &freq,
+                                         &per, &n, body, body_len);
+  if (pre) return pre;                                    // 400: name too large, nothing sent
+  Req r;
+  const int rc = run_take(b, len ? name : (const uint8_t*)"", len, now, freq, per, n, &r);
+  if (rc < 0) return rc;
+  fill_reply(r, out);
+  const std::string s = std::to_string(r.remaining);      // api.go:84-85
+  std::memcpy(body, s.data(), s.size());
+  *body_len = (uint32_t)s.size();
+  return out->ok ? 200 : 429;
 }
 
 int phip_batcher_stats(phip_batcher* b, uint64_t* out, int max) {

@@ -9,6 +9,9 @@
 //                 -> k_fold_thread / k_fold_wave / k_fold_block (stream2)
 // Everything runs on the handle's own HIP stream; host synchronisation only
 // reads back small counters (miss count, segment count) between stages.
+#include <sys/random.h>
+
+#include <chrono>
 #include <cstdlib>
 #include <cstring>
 #include <hip/hip_runtime.h>
@@ -57,7 +60,8 @@ enum BufId {
   B_SLOT, B_IDX, B_SSLOT, B_SIDX, B_USLOT, B_SCNT, B_SSTART, B_LONG, B_HUGE, B_TEMP, B_DUMP,
   B_OPS, B_HOFF, B_HOP, B_HVAL, B_RPOS, B_RST, B_RUNN, B_SEGEX, B_WOFF, B_SUMS, B_WRUN,
   B_WING, B_SEGXF, B_FOLDDBG, B_SMALL, B_HUGE2, B_LONG2,
-  B_STATES, B_NAME1, B_HOT, B_ROUTE, B_EXPORT, B_MSHARD, B_MSCNT, B_DEDUP, B_DSET, B_COUNT_
+  B_STATES, B_NAME1, B_HOT, B_ROUTE, B_EXPORT, B_MSHARD, B_MSCNT, B_DEDUP, B_DSET, B_TSTATS,
+  B_COUNT_
 };
 
 struct DevBuf {
@@ -102,6 +106,7 @@ struct phip_handle {
   u32* ctr_host = nullptr;   // pinned mirror
   u64 n_buckets = 0;
   u64 tag_mask = ~0ull;
+  u64 seed = 0;              // placement seed (Table::home, seeded_mix)
   DevBuf buf[B_COUNT_];
   bool timing = false;
   bool timing_accumulate = false;   // phip_set_timing(h, 2): keep every call's timings
@@ -155,6 +160,7 @@ inline Table table(phip_handle* h) {
   t.arena = h->arena;
   t.L = h->L;
   t.tag_mask = h->tag_mask;
+  t.seed = h->seed;
   return t;
 }
 
@@ -1138,6 +1144,14 @@ int receive_decoded(phip_handle* h, Src src, const uint64_t* a, const uint64_t* 
   return finish_receive(h, src, a, t, e, n, fd, nmiss, now, ow);
 }
 
+// Whether an op's phip_results.reply entry is written (step_sop): Takes,
+// Upserts and incast requests carry the bucket's state right after the op.
+inline bool has_reply_state(u8 status, u8 kind) {
+  const u8 st = status & 0x7F;
+  return kind == PHIP_OP_TAKE || kind == PHIP_OP_UPSERT || st == PHIP_ST_INCAST_REPLY ||
+         st == PHIP_ST_INCAST_NOREPLY;
+}
+
 // A host-pointer batch of at most kSmallMax ops through k_small_mixed: one
 // pinned copy in, one launch, one pinned copy out (the large path takes a
 // dozen launches and several host round trips, ~0.2 ms whatever the size).
@@ -1231,7 +1245,8 @@ int small_mixed(phip_handle* h, const phip_ops* ops, const phip_results* res, bo
   if (r.remaining) std::memcpy(r.remaining, pout + o_rem, 8 * n);
   if (r.have) std::memcpy(r.have, pout + o_have, 8 * n);
   if (r.reply) {
-    // an op's reply is defined only for INCAST_REPLY statuses; copy those
+    // reply states are defined for Takes, Upserts and incasts (step_sop);
+    // copy those, leaving the caller's other entries as they were
     const phip_state* src_r = (const phip_state*)(pout + o_reply);
     std::vector<u8> st;
     const u8* stp = r.status;
@@ -1241,7 +1256,7 @@ int small_mixed(phip_handle* h, const phip_ops* ops, const phip_results* res, bo
       stp = st.data();
     }
     for (u32 i = 0; i < n; ++i)
-      if ((stp[i] & 0x7F) == PHIP_ST_INCAST_REPLY) r.reply[i] = src_r[i];
+      if (has_reply_state(stp[i], ops->kind ? ops->kind[i] : (u8)PHIP_OP_RECEIVE)) r.reply[i] = src_r[i];
   }
   *done = true;
   return PHIP_OK;
@@ -1347,6 +1362,13 @@ int phip_open(const phip_config* cfg, phip_handle** out) {
   h->small = !(cfg->flags & PHIP_CFG_NO_SMALL);
   h->arena_cap = cfg->arena_bytes ? cfg->arena_bytes : (1ull << 20);
   if (cfg->debug_tag_bits && cfg->debug_tag_bits < 64) h->tag_mask = (1ull << cfg->debug_tag_bits) - 1;
+  if (cfg->flags & PHIP_CFG_FIXED_SEED) {
+    h->seed = cfg->hash_seed;
+  } else if (getrandom(&h->seed, sizeof h->seed, 0) != (ssize_t)sizeof h->seed) {
+    // no entropy source: a seed from the clock and the handle's address
+    h->seed = seeded_mix((u64)std::chrono::steady_clock::now().time_since_epoch().count(),
+                         (u64)(uintptr_t)h);
+  }
   auto fail = [&](hipError_t e) {
     phip_close(h);
     (void)e;
@@ -1533,6 +1555,7 @@ int phip_snapshot(phip_handle* h, uint8_t* out, uint64_t cap) {
   hd.n_buckets = h->n_buckets;
   hd.arena_used = used;
   hd.rec_bytes = sizeof(Rec);
+  hd.reserved[0] = h->seed;   // the records lie where this seed placed them
   std::memcpy(out, &hd, sizeof hd);
   u8* p = out + sizeof hd;
   HIPCHK(h, hipMemcpyAsync(p, h->recs, h->cap * sizeof(Rec), hipMemcpyDeviceToHost, h->stream));
@@ -1588,6 +1611,7 @@ int phip_restore(phip_handle* h, const uint8_t* in, uint64_t len) {
   HIPCHK(h, hipMemcpyAsync(h->arena_cursor, &hd.arena_used, sizeof(u64), hipMemcpyHostToDevice, h->stream));
   HIPCHK(h, hipStreamSynchronize(h->stream));
   h->n_buckets = hd.n_buckets;
+  h->seed = hd.reserved[0];   // the image's placement
   return PHIP_OK;
 }
 
@@ -2252,6 +2276,25 @@ int phip_set_stream(phip_handle* h, void* stream) {
   HIPCHK(h, hipStreamSynchronize(h->stream));
   h->stream = stream ? (hipStream_t)stream : h->own_stream;
   return PHIP_OK;
+}
+
+int phip_table_stats(phip_handle* h, uint64_t* out, int max) {
+  if (!h || !out) return PHIP_ERR_INVALID;
+  std::lock_guard<std::mutex> g(h->mu);
+  if (int rc0 = begin_call(h)) return rc0;
+  u64* d;
+  int rc;
+  if ((rc = ensure(h, B_TSTATS, 2, &d))) return rc;
+  HIPCHK(h, hipMemsetAsync(d, 0, 2 * sizeof(u64), h->stream));
+  k_table_stats<<<grid_for(h->cap), kBlock, 0, h->stream>>>(table(h), h->cap, d);
+  HIPCHK(h, hipGetLastError());
+  u64 r[2] = {0, 0};
+  HIPCHK(h, hipMemcpyAsync(r, d, sizeof r, hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  const u64 v[4] = {h->n_buckets, h->cap, r[0], r[1]};
+  int k = 0;
+  for (; k < max && k < 4; ++k) out[k] = v[k];
+  return k;
 }
 
 int phip_last_stats(phip_handle* h, uint64_t* out, int max) {

@@ -185,6 +185,30 @@ int for_members(phip_group* g, F f) {
   return PHIP_OK;
 }
 
+// The exchange plan of one member, shared by the RCCL and the shared-device
+// paths: with hs = the member's split sizes [send counts | send name bytes |
+// recv counts | recv name bytes] (W entries each), peer p's entry gives
+//   send side: where the member's packed segment for owner p lies in its
+//              owner-major send buffers (so messages / sb name bytes in) and
+//              its size (sc, sbytes);
+//   recv side: where the segment source p sends this member lands in the
+//              receive buffers (ro / rb: sources in rank order) and its size
+//              (rc, rbytes).
+struct Seg {
+  u64 so, sb, sc, sbytes;
+  u64 ro, rb, rc, rbytes;
+};
+void segment_plan(const u64* hs, u32 W, std::vector<Seg>* plan) {
+  plan->resize(W);
+  u64 so = 0, sb = 0, ro = 0, rb = 0;
+  for (u32 p = 0; p < W; ++p) {
+    Seg& g = (*plan)[p];
+    g.so = so; g.sb = sb; g.sc = hs[p]; g.sbytes = hs[W + p];
+    g.ro = ro; g.rb = rb; g.rc = hs[2 * W + p]; g.rbytes = hs[3 * W + p];
+    so += g.sc; sb += g.sbytes; ro += g.rc; rb += g.rbytes;
+  }
+}
+
 // One member's owner-routed Receive.
 // The owner's merge of n received messages (lengths, packed names, states):
 // name offsets by an inclusive scan of the lengths, then phip_receive_soa
@@ -216,6 +240,20 @@ int member_receive(phip_group* g, Member& mb, const phip_msgs& in, int64_t now, 
   const u32 n = in.n;
   GHIP(mb, hipSetDevice(mb.device));
   hipStream_t st = (hipStream_t)phip_host::handle_stream(mb.h);
+  // PHIP_GROUP_RCCL_SELF: the member's own segment goes through RCCL too (a
+  // send/recv pair to itself), so that the per-peer exchange below runs at
+  // world 1, on one GPU, with the plan the multi-GPU group uses
+  const bool rccl_self = (flags & PHIP_GROUP_RCCL_SELF) && !g->shared;
+  if (W == 1 && !rccl_self) {
+    // One owner: every message is this member's, so there is nothing to
+    // pack or exchange; the batch is merged as it came (the sender-side
+    // combine is subsumed by the fast path's hot directory).
+    if (sent) *sent = n;
+    if (merged) *merged = n;
+    if (n == 0) return PHIP_OK;
+    GPHIP(mb, phip_receive_soa(mb.h, &in, now, nullptr, PHIP_DEVICE_PTRS));
+    return PHIP_OK;
+  }
   // 1. pack by owner (device; phip_route_pack returns when the sizes are written)
   size_t in_bytes = 0;
   if (n) {
@@ -263,12 +301,6 @@ int member_receive(phip_group* g, Member& mb, const phip_msgs& in, int64_t now, 
                 (unsigned long long)n_recv, (unsigned long long)b_recv);
   if (sent) *sent = n_send;
   if (merged) *merged = n_recv;
-  if (W == 1) {   // the whole batch stays here: merge straight from the packed buffers
-    if (n_recv == 0) return PHIP_OK;
-    return merge_received(mb, st, (const u32*)mb.s_lens.p, (const uint8_t*)mb.s_names.p,
-                          (const u64*)mb.s_a.p, (const u64*)mb.s_t.p, (const int64_t*)mb.s_e.p, n_recv,
-                          now);
-  }
   GHIP(mb, mb.r_names.ensure(b_recv + 64));
   GHIP(mb, mb.r_lens.ensure(n_recv * 4 + 4));
   GHIP(mb, mb.r_offs.ensure(n_recv * 4 + 8));
@@ -277,26 +309,35 @@ int member_receive(phip_group* g, Member& mb, const phip_msgs& in, int64_t now, 
   GHIP(mb, mb.r_e.ensure(n_recv * 8 + 8));
   // 3. the segments: one send and one receive per peer and column; this
   // member's own segment is a device copy (no RCCL round trip through its
-  // buffers)
+  // buffers) unless rccl_self
+  std::vector<Seg> plan;
+  segment_plan(hs, W, &plan);
+  // one segment from a source's packed buffers (src: its send side) into
+  // this member's receive buffers (dst: its receive side)
+  auto copy_seg = [&](const Member& src, const Seg& s_, const Seg& d_) -> int {
+    GHIP(mb, hipMemcpyAsync((u32*)mb.r_lens.p + d_.ro, (const u32*)src.s_lens.p + s_.so, d_.rc * 4,
+                            hipMemcpyDeviceToDevice, st));
+    GHIP(mb, hipMemcpyAsync((uint8_t*)mb.r_names.p + d_.rb, (const uint8_t*)src.s_names.p + s_.sb,
+                            d_.rbytes, hipMemcpyDeviceToDevice, st));
+    GHIP(mb, hipMemcpyAsync((u64*)mb.r_a.p + d_.ro, (const u64*)src.s_a.p + s_.so, d_.rc * 8,
+                            hipMemcpyDeviceToDevice, st));
+    GHIP(mb, hipMemcpyAsync((u64*)mb.r_t.p + d_.ro, (const u64*)src.s_t.p + s_.so, d_.rc * 8,
+                            hipMemcpyDeviceToDevice, st));
+    GHIP(mb, hipMemcpyAsync((int64_t*)mb.r_e.p + d_.ro, (const int64_t*)src.s_e.p + s_.so,
+                            d_.rc * 8, hipMemcpyDeviceToDevice, st));
+    return PHIP_OK;
+  };
   if (g->shared) {   // each segment copied from its source member's packed buffers
-    u64 ro = 0, rb = 0;
+    std::vector<Seg> splan;
     for (u32 p = 0; p < W; ++p) {
       const Member& src = g->m[p];
-      const u64* ps = src.host_sizes;
-      u64 so = 0, sb = 0;   // the source's segment for this member
-      for (u32 o = 0; o < mb.rank; ++o) { so += ps[o]; sb += ps[W + o]; }
-      const u64 rc = hs[2 * W + p], rbytes = hs[3 * W + p];
-      GHIP(mb, hipMemcpyAsync((u32*)mb.r_lens.p + ro, (const u32*)src.s_lens.p + so, rc * 4,
-                              hipMemcpyDeviceToDevice, st));
-      GHIP(mb, hipMemcpyAsync((uint8_t*)mb.r_names.p + rb, (const uint8_t*)src.s_names.p + sb, rbytes,
-                              hipMemcpyDeviceToDevice, st));
-      GHIP(mb, hipMemcpyAsync((u64*)mb.r_a.p + ro, (const u64*)src.s_a.p + so, rc * 8,
-                              hipMemcpyDeviceToDevice, st));
-      GHIP(mb, hipMemcpyAsync((u64*)mb.r_t.p + ro, (const u64*)src.s_t.p + so, rc * 8,
-                              hipMemcpyDeviceToDevice, st));
-      GHIP(mb, hipMemcpyAsync((int64_t*)mb.r_e.p + ro, (const int64_t*)src.s_e.p + so, rc * 8,
-                              hipMemcpyDeviceToDevice, st));
-      ro += rc; rb += rbytes;
+      segment_plan(src.host_sizes, W, &splan);   // the source's send side
+      const Seg& s_ = splan[mb.rank];
+      if (s_.sc != plan[p].rc || s_.sbytes != plan[p].rbytes)
+        return fail(mb, PHIP_ERR_INVALID, "internal: member %u sends %llu/%llu, %u expects %llu/%llu",
+                    p, (unsigned long long)s_.sc, (unsigned long long)s_.sbytes, mb.rank,
+                    (unsigned long long)plan[p].rc, (unsigned long long)plan[p].rbytes);
+      if (int rc = copy_seg(src, s_, plan[p])) return rc;
     }
     // every member copied what it needs before any packs again (the next
     // call's route_pack overwrites the send buffers)
@@ -308,35 +349,27 @@ int member_receive(phip_group* g, Member& mb, const phip_msgs& in, int64_t now, 
                           n_recv, now);
   }
   void* tm = phip_host::timing_begin(mb.h, "rccl_exchange");
+  // the own segment's size must be what this member packed for itself
+  if (plan[mb.rank].sc != plan[mb.rank].rc || plan[mb.rank].sbytes != plan[mb.rank].rbytes)
+    return fail(mb, PHIP_ERR_INVALID, "internal: own segment %llu/%llu vs %llu/%llu",
+                (unsigned long long)plan[mb.rank].sc, (unsigned long long)plan[mb.rank].sbytes,
+                (unsigned long long)plan[mb.rank].rc, (unsigned long long)plan[mb.rank].rbytes);
+  if (!rccl_self)
+    if (int rc = copy_seg(mb, plan[mb.rank], plan[mb.rank])) return rc;
   GNCCL(mb, ncclGroupStart());
-  u64 so = 0, sb = 0, ro = 0, rb = 0;
   for (u32 p = 0; p < W; ++p) {
-    const u64 sc = hs[p], sbytes = hs[W + p], rc = hs[2 * W + p], rbytes = hs[3 * W + p];
-    if (p == mb.rank) {
-      GHIP(mb, hipMemcpyAsync((u32*)mb.r_lens.p + ro, (u32*)mb.s_lens.p + so, sc * 4,
-                              hipMemcpyDeviceToDevice, st));
-      GHIP(mb, hipMemcpyAsync((uint8_t*)mb.r_names.p + rb, (uint8_t*)mb.s_names.p + sb, sbytes,
-                              hipMemcpyDeviceToDevice, st));
-      GHIP(mb, hipMemcpyAsync((u64*)mb.r_a.p + ro, (u64*)mb.s_a.p + so, sc * 8,
-                              hipMemcpyDeviceToDevice, st));
-      GHIP(mb, hipMemcpyAsync((u64*)mb.r_t.p + ro, (u64*)mb.s_t.p + so, sc * 8,
-                              hipMemcpyDeviceToDevice, st));
-      GHIP(mb, hipMemcpyAsync((u64*)mb.r_e.p + ro, (u64*)mb.s_e.p + so, sc * 8,
-                              hipMemcpyDeviceToDevice, st));
-      so += sc; sb += sbytes; ro += rc; rb += rbytes;
-      continue;
-    }
-    GNCCL(mb, ncclSend((u32*)mb.s_lens.p + so, sc, ncclUint32, p, mb.comm, st));
-    GNCCL(mb, ncclRecv((u32*)mb.r_lens.p + ro, rc, ncclUint32, p, mb.comm, st));
-    GNCCL(mb, ncclSend((uint8_t*)mb.s_names.p + sb, sbytes, ncclUint8, p, mb.comm, st));
-    GNCCL(mb, ncclRecv((uint8_t*)mb.r_names.p + rb, rbytes, ncclUint8, p, mb.comm, st));
-    GNCCL(mb, ncclSend((u64*)mb.s_a.p + so, sc, ncclUint64, p, mb.comm, st));
-    GNCCL(mb, ncclRecv((u64*)mb.r_a.p + ro, rc, ncclUint64, p, mb.comm, st));
-    GNCCL(mb, ncclSend((u64*)mb.s_t.p + so, sc, ncclUint64, p, mb.comm, st));
-    GNCCL(mb, ncclRecv((u64*)mb.r_t.p + ro, rc, ncclUint64, p, mb.comm, st));
-    GNCCL(mb, ncclSend((u64*)mb.s_e.p + so, sc, ncclUint64, p, mb.comm, st));
-    GNCCL(mb, ncclRecv((u64*)mb.r_e.p + ro, rc, ncclUint64, p, mb.comm, st));
-    so += sc; sb += sbytes; ro += rc; rb += rbytes;
+    if (p == mb.rank && !rccl_self) continue;
+    const Seg& x = plan[p];
+    GNCCL(mb, ncclSend((u32*)mb.s_lens.p + x.so, x.sc, ncclUint32, p, mb.comm, st));
+    GNCCL(mb, ncclRecv((u32*)mb.r_lens.p + x.ro, x.rc, ncclUint32, p, mb.comm, st));
+    GNCCL(mb, ncclSend((uint8_t*)mb.s_names.p + x.sb, x.sbytes, ncclUint8, p, mb.comm, st));
+    GNCCL(mb, ncclRecv((uint8_t*)mb.r_names.p + x.rb, x.rbytes, ncclUint8, p, mb.comm, st));
+    GNCCL(mb, ncclSend((u64*)mb.s_a.p + x.so, x.sc, ncclUint64, p, mb.comm, st));
+    GNCCL(mb, ncclRecv((u64*)mb.r_a.p + x.ro, x.rc, ncclUint64, p, mb.comm, st));
+    GNCCL(mb, ncclSend((u64*)mb.s_t.p + x.so, x.sc, ncclUint64, p, mb.comm, st));
+    GNCCL(mb, ncclRecv((u64*)mb.r_t.p + x.ro, x.rc, ncclUint64, p, mb.comm, st));
+    GNCCL(mb, ncclSend((u64*)mb.s_e.p + x.so, x.sc, ncclUint64, p, mb.comm, st));
+    GNCCL(mb, ncclRecv((u64*)mb.r_e.p + x.ro, x.rc, ncclUint64, p, mb.comm, st));
   }
   GNCCL(mb, ncclGroupEnd());
   phip_host::timing_end(mb.h, tm);

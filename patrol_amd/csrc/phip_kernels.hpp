@@ -253,6 +253,21 @@ __device__ inline bool name_equal(const Rec& r, const Name& nm, const u8* src, c
 
 enum ProbeResult : int { kFound = 0, kMiss = 1, kPending = 2, kFull = 3 };
 
+// Seeded placement mix of a tag: murmur3's 64-bit finaliser of tag ^ seed
+// (a bijection whose every output bit depends on every input bit), so that
+// names crafted to share a home under one seed scatter under another.  The
+// seed is per handle (phip_config.hash_seed / the OS), as Go's map seeds its
+// hash per process (repo.go:175).
+__host__ __device__ inline u64 seeded_mix(u64 tag, u64 seed) {
+  u64 x = tag ^ seed;
+  x ^= x >> 33;
+  x *= 0xff51afd7ed558ccdull;
+  x ^= x >> 33;
+  x *= 0xc4ceb9fe1a85ec53ull;
+  x ^= x >> 33;
+  return x;
+}
+
 // The device table, passed to kernels by value.
 struct Table {
   Rec* recs;
@@ -260,10 +275,9 @@ struct Table {
   const u8* arena;
   u32 L;
   u64 tag_mask;   // all ones; narrower only in collision tests (phip_config.debug_tag_bits)
+  u64 seed;       // placement seed (seeded_mix)
   __device__ inline u64 tag(u64 h) const { return tag_of(h & tag_mask); }
-  __device__ inline u32 home(u64 tag) const {
-    return (u32)((tag * 0x9E3779B97F4A7C15ull) >> (64 - L));
-  }
+  __device__ inline u32 home(u64 tag) const { return (u32)(seeded_mix(tag, seed) >> (64 - L)); }
   __device__ inline u32 mask() const { return (u32)((1ull << L) - 1); }
 };
 
@@ -1053,7 +1067,7 @@ __global__ __launch_bounds__(kBlock) void k_dedupe(Src src, u32 n, const u32* __
     load_name_wide<false>(src.blob, off, len, nm);
     const u64 tag = T.tag(nm.h);
     const u64 mask = (1ull << setbits) - 1;
-    u64 h = (tag * 0x9E3779B97F4A7C15ull) >> (64 - setbits);
+    u64 h = seeded_mix(tag, T.seed) >> (64 - setbits);
     keep = true;   // no free entry found (cannot happen at <= 50% load): keep it
     for (u64 k = 0; k <= mask; ++k, h = (h + 1) & mask) {
       u64 v = __hip_atomic_load(&set[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1275,6 +1289,28 @@ __global__ __launch_bounds__(kBlock) void k_rehash(const Rec* __restrict__ old,
   T.aux[d] = old_aux[s];
 }
 
+// Placement quality (phip_table_stats): every bucket's probe distance from
+// its home slot; out[0] the longest (atomicMax), out[1] the sum.
+__global__ __launch_bounds__(kBlock) void k_table_stats(Table T, u64 cap, u64* out) {
+  const u64 s = (u64)blockIdx.x * kBlock + threadIdx.x;
+  u64 d = 0;
+  if (s < cap) {
+    const u64 tag = T.recs[s].tag;
+    if (tag) d = ((u32)s - T.home(tag)) & T.mask();
+  }
+  // a wave's maximum and sum first: one atomic pair per wave
+  u64 mx = d, sm = d;
+  for (int o = 32; o > 0; o >>= 1) {
+    const u64 x = __shfl_down(mx, o), y = __shfl_down(sm, o);
+    mx = x > mx ? x : mx;
+    sm += y;
+  }
+  if (__lane_id() == 0 && sm) {
+    atomicMax(&out[0], mx);
+    atomicAdd(&out[1], sm);
+  }
+}
+
 // --------------------------------------------------------------- decode --
 // UnmarshalBinary (bucket.go:71-91) for a batch of raw datagrams: big-endian
 // fields, name length byte, io.ErrShortBuffer when < 25 bytes or the name is
@@ -1391,7 +1427,7 @@ struct FState {
 
 struct OpOut {
   u8 st;
-  bool has_reply;
+  bool has_reply;   // the op has a reply state: the bucket right after it
   u64 rem, have;
 };
 
@@ -1404,27 +1440,36 @@ __device__ inline bool step_sop(const SOp& op, const FState& S, FState& S2, OpOu
   u8 cflag = 0;
   if (!S.existed) { S2.c = op.now; S2.existed = true; cflag = 0x80; }   // repo.go:208
   if (kOut) { out.has_reply = false; out.rem = 0; out.have = 0; }
+  // Reply states (phip_results.reply): the bucket right after the op for a
+  // Take (what UpsertBucket then broadcasts, api.go:74, repo.go:123-127), an
+  // Upsert (repo.go:123-127 broadcasts the upserted bucket) and an incast
+  // request (unchanged by it: the unicast payload of repo.go:86-90, and the
+  // find-or-create result GetBucket returns); none for a merged replica.
   if (op.kind == PHIP_OP_TAKE) {
     TakeResult r = take_step(S2.a, S2.t, S2.e, S2.c, op.now, (i64)op.x, as_f64(op.y), as_f64(op.z));
     if (kOut) {
       out.st = (r.ok ? PHIP_ST_TAKE_OK : PHIP_ST_TAKE_DENIED) | cflag;
       out.rem = r.remaining; out.have = r.have_bits;
+      out.has_reply = true;
     }
   } else {
     const u64 ab = op.x, tb = op.y;
     const i64 eb = (i64)op.z;
     if (op.kind == PHIP_OP_UPSERT && !S.existed) {               // repo.go:225-230
       S2.a = as_f64(ab); S2.t = as_f64(tb); S2.e = eb;
-      if (kOut) out.st = PHIP_ST_UPSERT_INSERTED | cflag;
+      if (kOut) { out.st = PHIP_ST_UPSERT_INSERTED | cflag; out.has_reply = true; }
     } else if (op.kind == PHIP_OP_RECEIVE && state_is_zero(ab, tb, eb)) {   // repo.go:86-90
       if (kOut) {
         bool reply = S.existed && !state_is_zero(as_bits(S.a), as_bits(S.t), S.e);
         out.st = (reply ? PHIP_ST_INCAST_REPLY : PHIP_ST_INCAST_NOREPLY) | cflag;
-        out.has_reply = reply;
+        out.has_reply = true;
       }
     } else {                                                      // bucket.go:240-263
       go_merge(S2.a, S2.t, S2.e, as_f64(ab), as_f64(tb), eb);
-      if (kOut) out.st = PHIP_ST_MERGED | cflag;
+      if (kOut) {
+        out.st = PHIP_ST_MERGED | cflag;
+        out.has_reply = op.kind == PHIP_OP_UPSERT;
+      }
     }
   }
   return !S.existed || as_bits(S2.a) != as_bits(S.a) || as_bits(S2.t) != as_bits(S.t) ||
@@ -1438,7 +1483,7 @@ __device__ inline bool apply_sop(const SOp& op, const FState& S, FState& S2) {
   return step_sop<false>(op, S, S2, unused);
 }
 
-// S is the state the op saw (an incast reply carries it, repo.go:86-90).
+// S is the bucket's state right after the op (its reply state, step_sop).
 __device__ inline void write_out(const OutView& o, u32 i, const OpOut& r, const FState& S) {
   if (o.status) o.status[i] = r.st;
   if (o.remaining) o.remaining[i] = r.rem;
@@ -1538,7 +1583,7 @@ __global__ __launch_bounds__(kBlock) void k_fold_thread(
     SOp nx = load_sop(ops, v1);
     OpOut o;
     eval_sop(op, S, S2, o);
-    write_out_m<kOut>(ow, op.idx, o, S);
+    write_out_m<kOut>(ow, op.idx, o, S2);
     S = S2;
     op = nx;
     v1 = v2;
@@ -1595,7 +1640,7 @@ __global__ __launch_bounds__(64) void k_fold_wave(
   // counts loads and stores in one counter) never waits for the stores
   // issued after them.  Window 0 starts with placeholder stores to its own
   // outputs, rewritten with its results.
-  // (Incast replies, rare, are stored where their op retires.)
+  // (Reply states, when asked for, are stored where their op retires.)
   constexpr u32 kDefer = kOut & ~kOutReply;
   const FState none{};
   OpOut po{};
@@ -1618,7 +1663,7 @@ __global__ __launch_bounds__(64) void k_fold_wave(
       if (active && lane <= p) {
         mo = o;
         if constexpr ((kOut & kOutReply) != 0) {
-          if (o.has_reply) write_out_m<kOutReply>(ow, op.idx, o, S);
+          if (o.has_reply) write_out_m<kOutReply>(ow, op.idx, o, S2);
         }
       }
       if (p >= 64) break;
@@ -1809,7 +1854,7 @@ __global__ __launch_bounds__(kSmallMax) void k_small_mixed(NamesOffs src, OpView
           const SOp op = make_sop(sop[o], sval[o]);
           OpOut out;
           eval_sop(op, S, S2, out);
-          write_out(ow, op.idx, out, S);
+          write_out(ow, op.idx, out, S2);
           S = S2;
         }
         store_state(rec, S);
@@ -1835,7 +1880,7 @@ __global__ __launch_bounds__(kSmallMax) void k_small_mixed(NamesOffs src, OpView
         if (active) ch = eval_sop(op, S, S2, out);
         const u64 m = __ballot(ch);
         const u32 p = m ? (u32)(__ffsll((long long)m) - 1) : 64u;
-        if (active && lane <= p) write_out(ow, op.idx, out, S);
+        if (active && lane <= p) write_out(ow, op.idx, out, S2);
         if (p >= 64) break;
         S = lane_state(S2, p);
         c = p + 1;
@@ -2761,7 +2806,7 @@ __global__ __launch_bounds__(kBlock) void k_huge_outputs(
     const SOp sop = make_sop(op[k], val[k]);
     FState S2;
     eval_sop(sop, S, S2, o[k]);
-    seen[k] = S;
+    seen[k] = S2;   // the reply state: the bucket right after the op
     if (j0 + k < p1) gj = gmax(gj, merge_contrib(op[k], val[k]));
   }
 #pragma unroll

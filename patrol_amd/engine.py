@@ -22,7 +22,8 @@ from typing import Iterable, Sequence
 import numpy as np
 
 from . import _lib
-from ._lib import (DEVICE_PTRS, phip_config, phip_msgs, phip_ops, phip_results, phip_state)
+from ._lib import (DEVICE_PTRS, phip_config, phip_msgs, phip_ops, phip_results, phip_state,
+                   phip_take_reply)
 
 
 class PatrolHipError(RuntimeError):
@@ -83,10 +84,16 @@ class GPURepo:
 
     def __init__(self, device: int = 0, log2_slots: int = 20, arena_bytes: int = 1 << 24,
                  max_load_pct: int = 90, debug_tag_bits: int = 0, grow: bool = True,
-                 small: bool = True):
+                 small: bool = True, hash_seed: int | None = None):
+        """hash_seed: None = a random placement seed per handle (the default,
+        as Go's map seeds its hash per process); an int pins it
+        (PHIP_CFG_FIXED_SEED; 0 = the unseeded placement)."""
         self.L = _lib.load()
         flags = (0 if grow else _lib.CFG_NO_GROW) | (0 if small else _lib.CFG_NO_SMALL)
-        cfg = phip_config(device, log2_slots, arena_bytes, max_load_pct, debug_tag_bits, flags, 0)
+        if hash_seed is not None:
+            flags |= _lib.CFG_FIXED_SEED
+        cfg = phip_config(device, log2_slots, arena_bytes, max_load_pct, debug_tag_bits, flags, 0,
+                          (hash_seed or 0) & (2**64 - 1))
         h = C.c_void_p()
         rc = self.L.phip_open(C.byref(cfg), C.byref(h))
         if rc != 0:
@@ -158,6 +165,14 @@ class GPURepo:
         out = (C.c_uint64 * 4)()
         k = self.L.phip_last_stats(self.h, out, 4)
         return tuple(int(out[i]) for i in range(k))
+
+    def table_stats(self):
+        """dict(buckets, slots, max_probe, sum_probe): probe distances of the
+        buckets from their home slots (phip_table_stats)."""
+        out = (C.c_uint64 * 4)()
+        k = self._check(self.L.phip_table_stats(self.h, out, 4))
+        keys = ("buckets", "slots", "max_probe", "sum_probe")
+        return {keys[i]: int(out[i]) for i in range(k)}
 
     def timings(self, max_entries: int = 1 << 14):
         names = (C.c_char_p * max_entries)()
@@ -402,7 +417,7 @@ class GPUGroup:
     def open_all(cls, devices, log2_slots: int = 20, arena_bytes: int = 1 << 24,
                  max_load_pct: int = 90):
         L = _lib.load()
-        cfg = phip_config(0, log2_slots, arena_bytes, max_load_pct, 0, 0, 0)
+        cfg = phip_config(0, log2_slots, arena_bytes, max_load_pct, 0, 0, 0, 0)
         devs = (C.c_int32 * len(devices))(*devices)
         g = C.c_void_p()
         rc = L.phip_group_open_all(C.byref(cfg), devs, len(devices), C.byref(g))
@@ -428,17 +443,20 @@ class GPUGroup:
         if rc != 0:
             raise PatrolHipError(rc, self.L.phip_group_last_error(self.g).decode(errors="replace"))
 
-    def receive(self, batches, now: int, combine: bool = True):
+    def receive(self, batches, now: int, combine: bool = True, rccl_self: bool = False):
         """batches: one (names uint8, name_offs int32[n+1], added, taken, elapsed)
-        tuple of CUDA tensors per local member -> (sent, merged) lists."""
+        tuple of CUDA tensors per local member -> (sent, merged) lists.
+        rccl_self (PHIP_GROUP_RCCL_SELF, testing): every segment, the
+        member's own included, travels through ncclSend/ncclRecv."""
         k = len(batches)
         msgs = (phip_msgs * k)()
         for i, (names, offs, a, t, e) in enumerate(batches):
             msgs[i] = phip_msgs(offs.numel() - 1, 0, _ptr(names), _ptr(offs), _ptr(a), _ptr(t),
                                 _ptr(e))
         sent, merged = (C.c_uint64 * k)(), (C.c_uint64 * k)()
-        self._check(self.L.phip_group_receive(self.g, msgs, int(now), sent, merged,
-                                              DEVICE_PTRS | (_lib.ROUTE_COMBINE if combine else 0)))
+        flags = DEVICE_PTRS | (_lib.ROUTE_COMBINE if combine else 0) | \
+            (_lib.GROUP_RCCL_SELF if rccl_self else 0)
+        self._check(self.L.phip_group_receive(self.g, msgs, int(now), sent, merged, flags))
         return [int(x) for x in sent], [int(x) for x in merged]
 
     def anti_entropy(self, replicas):
@@ -505,6 +523,36 @@ class TakeBatcher:
         if code < 0:
             raise PatrolHipError(code, "phip_batcher_api_take failed")
         return code, body.raw[:bl.value].decode()
+
+    @staticmethod
+    def _reply(r):
+        st = r.state
+        return dict(remaining=int(r.remaining), ok=bool(r.ok), created=bool(r.created),
+                    seq=int(r.seq), state=BucketState(st.added, st.taken, st.elapsed, st.created),
+                    datagram=bytes(r.datagram[:r.datagram_len]))
+
+    def take_reply(self, name: bytes, now: int, freq: int, per: int, count: int):
+        """A Take with everything the handler replicates (phip_batcher_take_reply):
+        dict(remaining, ok, created, seq, state, datagram)."""
+        r = phip_take_reply()
+        rc = self.L.phip_batcher_take_reply(self.b, name, len(name), int(now), int(freq), int(per),
+                                            int(count), C.byref(r))
+        if rc != 0:
+            raise PatrolHipError(rc, "phip_batcher_take_reply failed")
+        return self._reply(r)
+
+    def api_take_reply(self, name: bytes, rate: bytes, count: bytes, now: int):
+        """API.takeBucket plus its replication (phip_batcher_api_take_reply):
+        (HTTP status, body, reply dict)."""
+        body = C.create_string_buffer(64)
+        bl = C.c_uint32()
+        r = phip_take_reply()
+        code = self.L.phip_batcher_api_take_reply(self.b, name, len(name), rate, len(rate), count,
+                                                  len(count), int(now), body, C.byref(bl),
+                                                  C.byref(r))
+        if code < 0:
+            raise PatrolHipError(code, "phip_batcher_api_take_reply failed")
+        return code, body.raw[:bl.value].decode(), self._reply(r)
 
     def stats(self):
         """dict(batches, requests, max_batch, gpu_ns, errors)."""

@@ -36,14 +36,42 @@ def test_exports_match_header():
     L = _lib.load()
     for name in declared:
         assert hasattr(L, name)
-    assert L.phip_abi_version() == 2
+    assert L.phip_abi_version() == 3
 
 
 def test_config_struct_layout():
     """phip_config as the header lays it out (a cgo binding mirrors it)."""
     import ctypes as C
-    assert C.sizeof(_lib.phip_config) == 32
+    assert C.sizeof(_lib.phip_config) == 40
     assert _lib.phip_config.flags.offset == 24
+    assert _lib.phip_config.hash_seed.offset == 32
+    # phip_take_reply: remaining, ok, created, datagram_len, reserved, seq, state, datagram
+    assert C.sizeof(_lib.phip_take_reply) == 8 + 8 + 8 + 32 + 256
+    assert _lib.phip_take_reply.state.offset == 24
+    assert _lib.phip_take_reply.datagram.offset == 56
+
+
+def test_seeded_mix_host_copy():
+    """The placement mix (phip_kernels.hpp seeded_mix: murmur3 fmix64 of
+    tag ^ seed) is a bijection that spreads tags differing in one bit."""
+    M = (1 << 64) - 1
+
+    def mix(t, s):
+        x = t ^ s
+        x ^= x >> 33
+        x = (x * 0xff51afd7ed558ccd) & M
+        x ^= x >> 33
+        x = (x * 0xc4ceb9fe1a85ec53) & M
+        x ^= x >> 33
+        return x
+    import random
+    rng = random.Random(3)
+    tags = [rng.getrandbits(64) for _ in range(2000)]
+    seed = rng.getrandbits(64)
+    assert len({mix(t, seed) for t in tags}) == len(tags)
+    # one flipped input bit flips about half of the output bits
+    flips = [bin(mix(t, seed) ^ mix(t ^ (1 << (k % 64)), seed)).count("1") for k, t in enumerate(tags)]
+    assert 28 < sum(flips) / len(flips) < 36
 
 
 def test_library_is_gfx950_code_object():

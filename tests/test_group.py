@@ -38,11 +38,15 @@ def _dump(repo):
     return {k: (v.added, v.taken, v.elapsed, v.created) for k, v in repo.dump().items()}
 
 
-@pytest.mark.parametrize("mode", ["all", "rank"])
-def test_group_receive_vs_oracle(pa, mode):
+@pytest.mark.parametrize("mode,rccl_self", [("all", False), ("rank", False), ("all", True),
+                                             ("rank", True)])
+def test_group_receive_vs_oracle(pa, mode, rccl_self):
     """Two owner-routed batches (the second large enough for the sender-side
     combine) merged through phip_group_receive equal the oracle's Receive of
-    the same messages."""
+    the same messages.  rccl_self (PHIP_GROUP_RCCL_SELF): the member's own
+    segment travels through grouped ncclSend/ncclRecv to itself, so the
+    per-peer exchange of the multi-GPU group (segment plan, counts, dtypes,
+    offsets) runs on this one GPU."""
     dev = torch.device("cuda", 0)
     rng = np.random.default_rng(61)
     if mode == "all":
@@ -56,9 +60,11 @@ def test_group_receive_vs_oracle(pa, mode):
     for k, n in enumerate((5000, 1 << 21)):
         names, a, t, e, dv = _batch(rng, n, 20000, dev)
         torch.cuda.synchronize()
-        sent, merged = g.receive([dv], _gen.T0 + k, combine=True)
+        sent, merged = g.receive([dv], _gen.T0 + k, combine=True, rccl_self=rccl_self)
         assert sent == merged and 0 < merged[0] <= n
-        if n >= 1 << 20:
+        if not rccl_self:
+            assert merged[0] == n         # one owner: merged as it came, no pack
+        elif n >= 1 << 20:
             assert merged[0] < n          # hot names were combined at the sender
         o.receive_soa(names, a, t, e, _gen.T0 + k)
     got = _dump(repo)
@@ -90,7 +96,7 @@ def test_group_anti_entropy_equals_torch_restatement(pa):
     g.close()
 
 
-@pytest.mark.parametrize("world,dirty", [(2, 0.0), (3, 0.0), (3, 0.05)])
+@pytest.mark.parametrize("world,dirty", [(2, 0.0), (2, 0.05), (3, 0.0), (3, 0.05)])
 def test_shared_device_group_receive_vs_oracle(pa, world, dirty):
     """A group of `world` shards on one GPU (phip_group_open_all with the
     device listed `world` times): the multi-member exchange (split sizes,

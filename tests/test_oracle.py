@@ -242,3 +242,35 @@ def test_fnv1a():
     assert O.fnv1a64(b"a") == 0xAF63DC4C8601EC8C
     for s in [b"foo", b"b123", b"x" * 231]:
         assert O.fnv1a64(s) == G.fnv1a64(s)
+
+
+def test_bench_mixed_mt_matches_serial_stream_order():
+    """The CPU baseline's multi-threaded mixed stream (orc_bench_mixed_mt:
+    each bucket's ops on one worker in stream order) gives exactly the
+    single-threaded stream's statuses, remaining and table."""
+    import numpy as np
+    from oracle import oracle as O
+    from tests import _gen
+    rng = np.random.default_rng(12)
+    n, K = 20000, 500
+    ids = _gen.zipf_ids(rng, n, K)
+    names = _gen.key_names(ids)
+    blob, offs = O._names_blob(names)
+    kind = rng.choice(np.array([0, 1, 2], np.uint8), n, p=[0.5, 0.4, 0.1])
+    now = _gen.T0 + np.arange(n, dtype=np.int64) * 1000
+    freq = np.full(n, 100, np.int64)
+    per = np.full(n, 10**9, np.int64)
+    cnt = np.ones(n, np.uint64)
+    a, t, e = _gen.dirty_states(rng, n, 0.1)
+    outs = []
+    for th in (1, 7):
+        r = O.Repo()
+        st = np.zeros(n, np.uint8)
+        rm = np.zeros(n, np.uint64)
+        f = r.L.orc_bench_mixed if th == 1 else r.L.orc_bench_mixed_mt
+        extra = () if th == 1 else (th,)
+        f(r.h, kind, blob, offs, n, now, freq, per, cnt, a, t, e, st, rm, *extra)
+        outs.append((st, np.where(kind == 0, rm, 0), r.dump()))
+    assert np.array_equal(outs[0][0], outs[1][0])
+    assert np.array_equal(outs[0][1], outs[1][1])
+    assert outs[0][2] == outs[1][2]
