@@ -527,9 +527,10 @@ def run_routed(args, torch, dist, dev, local, rank, world):
         "messages_per_step_total": n, "messages_per_step_per_gpu": m, "buckets_total": K,
         "merged_per_step_total": float(sm[1]), "merged_per_step_max_gpu": float(mx[1]),
         "buckets_max_gpu": int(mx[2]), "slots_per_gpu": 1 << L, "sender_combine": True,
-        "step": ("phip_group_receive (C ABI: phip_route_pack with sender-side combine, RCCL "
-                 "all-to-all of the split sizes, grouped send/recv per column, phip_receive_soa "
-                 "on the owner)" if group is not None else
+        "step": ("phip_group_receive (C ABI: at one GPU every message is owned locally and is "
+                 "merged as it came, phip_receive_soa; at N GPUs phip_route_pack with "
+                 "sender-side combine, RCCL all-to-all of the split sizes, grouped send/recv "
+                 "per column, phip_receive_soa on the owner)" if group is not None else
                  "phip_route_pack + torch.distributed all-to-all per column + phip_receive_soa"),
     }
 

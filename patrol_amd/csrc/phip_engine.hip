@@ -281,9 +281,17 @@ int grow_table(phip_handle* h, u32 newL) {
     (void)hipFree(nrecs);
     return set_err(h, PHIP_ERR_FULL, "table growth to 2^%u slots: device memory", newL);
   }
-  HIPCHK(h, hipMemsetAsync(nrecs, 0, ncap * sizeof(Rec), h->stream));
-  HIPCHK(h, hipMemsetAsync(naux, 0, ncap * sizeof(u32), h->stream));
-  HIPCHK(h, hipMemsetAsync(h->ctr + 8, 0, sizeof(u32), h->stream));
+  // from here on an error frees the new table (the old one stays live)
+  auto drop_new = [&](int rc) {
+    (void)hipStreamSynchronize(h->stream);
+    (void)hipFree(nrecs);
+    (void)hipFree(naux);
+    return rc;
+  };
+  if (hipMemsetAsync(nrecs, 0, ncap * sizeof(Rec), h->stream) != hipSuccess ||
+      hipMemsetAsync(naux, 0, ncap * sizeof(u32), h->stream) != hipSuccess ||
+      hipMemsetAsync(h->ctr + 8, 0, sizeof(u32), h->stream) != hipSuccess)
+    return drop_new(set_err(h, PHIP_ERR_HIP, "table growth: clearing the new table failed"));
   Table nt = table(h);
   nt.recs = nrecs;
   nt.aux = naux;
@@ -292,10 +300,11 @@ int grow_table(phip_handle* h, u32 newL) {
     Launch l(h, "k_rehash");
     k_rehash<<<grid_for(h->cap), kBlock, 0, h->stream>>>(h->recs, h->aux, h->cap, nt, h->ctr);
   }
-  HIPCHK(h, hipGetLastError());
+  if (hipGetLastError() != hipSuccess)
+    return drop_new(set_err(h, PHIP_ERR_HIP, "k_rehash launch failed"));
   int rc;
-  if ((rc = read_ctr(h))) return rc;   // synchronises: the old table is no longer read
-  if (h->ctr_host[8]) return set_err(h, PHIP_ERR_INVALID, "internal: rehash probe wrapped");
+  if ((rc = read_ctr(h))) return drop_new(rc);   // synchronises: the old table is no longer read
+  if (h->ctr_host[8]) return drop_new(set_err(h, PHIP_ERR_INVALID, "internal: rehash probe wrapped"));
   HIPCHK(h, hipFree(h->recs));
   HIPCHK(h, hipFree(h->aux));
   h->recs = nrecs;
@@ -367,13 +376,29 @@ int reserve(phip_handle* h, Src src, const u32* list, u32 nlist, u64 bound, bool
 // once done).  Every claimed slot is published before an error returns, so a
 // failing round leaves no claimed-but-unnamed slot behind.
 template <class Src>
+int dedupe_names(phip_handle* h, Src src, const u32* list, u32 n, u32** out, u32* nout);
+
+// `distinct`: the list holds each name once (a k_dedupe output); otherwise a
+// name may be listed many times (a fast batch's misses), and a list whose
+// length alone would pass the load limit is bounded by its distinct names
+// first, so that one new hot name does not grow (or, without growth, fill)
+// the table for the thousands of messages naming it.
+template <class Src>
 int insert_names(phip_handle* h, Src src, u32* list, u32 nlist, const int64_t* now_arr, i64 now0,
-                 u32* n_claimed, bool* grew = nullptr) {
+                 u32* n_claimed, bool* grew = nullptr, bool distinct = false) {
   u32 *cslot, *cmsg, *retry, *cur = list;
   int rc;
   *n_claimed = 0;
   bool g = false;
-  if ((rc = reserve(h, src, list, nlist, nlist, &g))) return rc;
+  u64 bound = nlist;
+  if (!distinct && nlist > 1 && h->n_buckets + nlist > h->max_load) {
+    u32 *dd, nd = 0;
+    if ((rc = dedupe_names(h, src, list, nlist, &dd, &nd))) return rc;
+    // names that share a 64-bit tag count once there: with full tags that is
+    // a birthday rarity; narrowed test tags keep the list's length
+    if (h->tag_mask == ~0ull) bound = nd;
+  }
+  if ((rc = reserve(h, src, list, nlist, bound, &g))) return rc;
   if (grew) *grew = g;
   if ((rc = ensure(h, B_CSLOT, nlist, &cslot)) || (rc = ensure(h, B_CMSG, nlist, &cmsg)) ||
       (rc = ensure(h, B_RETRY, nlist, &retry)))
@@ -645,7 +670,7 @@ int finish_many_misses(phip_handle* h, Src src, const uint64_t* a, const uint64_
   if ((rc = dedupe_names(h, src, miss, nmiss, &dedup, &nd))) return rc;
   // 2. create them (aux = ~0 and the NEW flag on every claimed slot)
   u32 n_claimed = 0;
-  if ((rc = insert_names(h, src, dedup, nd, nullptr, now, &n_claimed))) return rc;
+  if ((rc = insert_names(h, src, dedup, nd, nullptr, now, &n_claimed, nullptr, true))) return rc;
   // 3. creator tracking over the first pass's misses (every message of a new
   //    bucket is among them), before the second pass reuses B_MISS
   if (status) {
@@ -771,7 +796,7 @@ int resolve_all(phip_handle* h, Src src, u32 n, const int64_t* now_arr, i64 now0
     // dropped for a shared tag miss again and take the general rounds below.
     u32 *dedup, nd = 0;
     if ((rc = dedupe_names(h, src, miss, nmiss, &dedup, &nd)) ||
-        (rc = insert_names(h, src, dedup, nd, now_arr, now0, n_claimed, &grew)))
+        (rc = insert_names(h, src, dedup, nd, now_arr, now0, n_claimed, &grew, true)))
       return rc;
     Sharded r2;
     if ((rc = sharded(h, B_MSHARD, grid_for(nmiss), kBlock, &r2))) return rc;

@@ -708,6 +708,31 @@ def test_table_full_refused_without_growth(pa, path):
     assert_same_dump(gpu_dump(g), o.dump())
 
 
+def test_near_full_table_one_new_hot_name_fits(pa):
+    """PHIP_CFG_NO_GROW, a table a few buckets below its load limit, and a
+    fast batch whose 60000 messages all name one new bucket:
+    the insert step bounds its reservation by the batch's distinct missing
+    names (one), so the batch is applied instead of refused, exactly."""
+    rng = np.random.default_rng(21)
+    g = pa.GPURepo(log2_slots=16, max_load_pct=90, grow=False)     # 58982 buckets allowed
+    o = O.Repo()
+    K = 58900
+    names = _gen.key_names(range(K))
+    z = np.zeros(K, np.uint64)
+    g.seed(names, z, z, np.zeros(K, np.int64), np.full(K, _gen.T0, np.int64))
+    o.seed(names, z, z, np.zeros(K, np.int64), np.full(K, _gen.T0, np.int64))
+    n = 60000
+    hot = [b"one-new-hot-bucket"] * n
+    for i in rng.integers(0, n, 500):
+        hot[i] = names[int(i) % K]                 # some existing buckets too
+    a, t, e = _gen.clean_states(rng, n)
+    out = g.receive_soa(hot, a, t, e, _gen.T0 + SEC)
+    st, _, _, _ = o.receive_soa(hot, a, t, e, _gen.T0 + SEC)
+    assert np.array_equal(out["status"], st)
+    assert len(g) == K + 1
+    assert_same_dump(gpu_dump(g), o.dump())
+
+
 @pytest.mark.parametrize("tag_bits", [0, 12])
 def test_table_grows_vs_oracle(pa, tag_bits):
     """Go's map never refuses a bucket (repo.go:204-207): a 2^10-slot table
