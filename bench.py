@@ -62,7 +62,10 @@ def parse():
     p.add_argument("--seed", type=int, default=1234)
     p.add_argument("--no-combine", action="store_true",
                    help="c4: no sender-side combine of hot names (PHIP_ROUTE_COMBINE)")
-    p.add_argument("--workload", default="c2", choices=["c1", "c2", "c3", "c4", "c5"],
+    p.add_argument("--route-world", type=int, default=8,
+                   help="route: the number of owners phip_route_pack packs for (the per-rank "
+                        "pack of an N-GPU group, timed on this one GPU)")
+    p.add_argument("--workload", default="c2", choices=["c1", "c2", "c3", "c4", "c5", "route"],
                    help="c2: batched Receive merges (headline); c1: the reference's CPU case "
                         "(1M messages into 100k buckets, the whole of it timed on the CPU "
                         "restatement beside the GPU); c3: mixed Take+Merge stream")
@@ -426,6 +429,44 @@ def run_c4(args, torch, dev, repo, rank, world, K, gen):
     return n, step, owned, merged
 
 
+def run_route(args, torch, dev, repo, K, gen):
+    """The sender's half of C4 at N GPUs, on one: every step packs this
+    rank's batch by owner for --route-world owners (phip_route_pack with the
+    sender-side combine: owner hash, combine of the sampled hot names, stable
+    owner-major pack), into preallocated send buffers.  No exchange: the
+    step is the pack kernels only (bench c4 at N GPUs adds the RCCL
+    exchange and the owner's merge)."""
+    import ctypes as C
+    from patrol_amd import _lib
+    from patrol_amd.engine import phip_msgs
+    n, W = args.messages, args.route_world
+    ids = zipf_ids(torch, gen, n, K, args.zipf, dev)
+    blob, offs = names_for_ids(torch, ids)
+    del ids
+    batches = [replica_states(torch, gen, n, j, dev) for j in range(args.warmup + args.steps)]
+    s_names = torch.empty(blob.numel(), dtype=torch.uint8, device=dev)
+    s_lens = torch.empty(n, dtype=torch.int32, device=dev)
+    s_a, s_t, s_e = (torch.empty(n, dtype=torch.int64, device=dev) for _ in range(3))
+    cnt = torch.zeros(W, dtype=torch.int64, device=dev)
+    nb = torch.zeros(W, dtype=torch.int64, device=dev)
+    L = _lib.load()
+    sent = []
+    torch.cuda.synchronize()
+
+    def step(j):
+        a, t, e = batches[j]
+        m = phip_msgs(n, 0, blob.data_ptr(), offs.data_ptr(), a.data_ptr(), t.data_ptr(),
+                      e.data_ptr())
+        rc = L.phip_route_pack(repo.h, C.byref(m), W, s_names.data_ptr(), s_lens.data_ptr(),
+                               s_a.data_ptr(), s_t.data_ptr(), s_e.data_ptr(), cnt.data_ptr(),
+                               nb.data_ptr(), _lib.DEVICE_PTRS | _lib.ROUTE_COMBINE)
+        if rc != 0:
+            raise RuntimeError(f"phip_route_pack: {rc}")
+        if j == 0:   # a warmup step (its read-back synchronises; keep it out of the timing)
+            sent.append(int(cnt.sum()))
+    return n, step, sent
+
+
 def dist_module():
     import torch.distributed as dist
     return dist
@@ -655,6 +696,9 @@ def main():
     elif args.workload == "c5":
         n, step, c5_check = run_c5(args, torch, dev, repo, rank, world, gen)
         ids = None
+    elif args.workload == "route":
+        n, step, route_sent = run_route(args, torch, dev, repo, K, gen)
+        ids = None
     else:
         ids = zipf_ids(torch, gen, n, K, args.zipf, dev)
         blob, offs = names_for_ids(torch, ids + base, args.name_len)
@@ -801,6 +845,17 @@ def main():
         extra["messages_merged_per_step_rank0"] = float(np.mean(c4_merged))
         if "rccl_exchange" in kms:   # the grouped send/recv of the packed segments
             extra["exchange_ms"] = kms["rccl_exchange"]
+    elif args.workload == "route":
+        # the pack's algorithmic bytes: read the message (offset 4 + name +
+        # 24), write it owner-major (length 4 + name + 24); names ~7 B
+        bpo = 2 * (4 + 24 + 7)
+        dom_name = "k_route_count+k_route_scatter"
+        dom_ms = kms.get("k_route_count", float("nan")) + kms.get("k_route_scatter", float("nan"))
+        unit, metric = "messages/s", METRIC + " [owner-routing pack, messages packed/sec]"
+        workload = (f"owner-routing pack: {n} messages (Zipf({args.zipf}) over {K} buckets) packed by "
+                    f"owner for {args.route_world} owners with the sender-side combine")
+        extra["route_world"] = args.route_world
+        extra["messages_sent_after_combine"] = route_sent[0] if route_sent else None
     elif args.workload == "c3":
         # Take 89 B (op 24 + state read 32 + write 24 + result 9), Merge 88 B.
         bpo = 88.5
