@@ -263,17 +263,17 @@ def host_cpu():
     return {"host_nproc": os.cpu_count(), "host_affinity_cpus": affinity, "host_cpu_model": model}
 
 
-def pmc_traffic(key, workload):
+def pmc_traffic(key, workload, kernel):
     """HBM bytes per launch of the dominant kernel from the committed PMC
-    summary (profiles/pmc_summary.json, produced by tools/pmc_summary.py):
+    summary (profiles/pmc_summary.json, produced by tools/pmc_workloads.py):
     one entry per workload key (c1..c5), used when it was measured on the
-    same workload description."""
+    same workload description and the same dominant kernel(s)."""
     path = os.path.join(ROOT, "profiles", "pmc_summary.json")
     try:
         with open(path) as f:
             d = json.load(f)
         d = d.get(key, d) if "kernel" not in d else d
-        if d.get("workload") == workload:
+        if d.get("workload") == workload and d.get("kernel") == kernel:
             return d.get("hbm_bytes_per_step")
     except (OSError, ValueError, AttributeError):
         pass
@@ -581,7 +581,8 @@ def run_c5(args, torch, dev, repo, rank, world, gen):
     (E-encoded state planes, patrol_amd.shard).  A round = fresh local writes
     (a random fraction of each replica's buckets grows) followed by one
     anti-entropy pass: k_ae_local_max, RCCL all-reduce(MAX) of the [3, B]
-    join over all GPUs, k_ae_apply.  One round converges (max is idempotent);
+    join over all GPUs, k_ae_apply (one GPU: the fused k_ae_join, nothing to
+    exchange).  One round converges (max is idempotent);
     the loop models new writes between rounds.  A unit is one replica-bucket
     brought to the cluster-wide join."""
     from patrol_amd import shard
@@ -814,9 +815,15 @@ def main():
         # writes only the fields the join changed, data-dependent and not
         # counted (profiles/r02_c5_kernels.json has the measured writes)
         R, B = args.replicas, args.buckets
-        bpo = (2 * R + 2) * 24 / R
-        dom_name = "k_ae_local_max+k_ae_apply"
-        dom_ms = kms.get("k_ae_local_max", float("nan")) + kms.get("k_ae_apply", float("nan"))
+        if "k_ae_join" in kms:
+            # one GPU: the fused join (phip_ae_join) reads each replica's 24
+            # bytes once and writes only what the join raised
+            bpo = 24.0
+            dom_name, dom_ms = "k_ae_join", kms["k_ae_join"]
+        else:
+            bpo = (2 * R + 2) * 24 / R
+            dom_name = "k_ae_local_max+k_ae_apply"
+            dom_ms = kms.get("k_ae_local_max", float("nan")) + kms.get("k_ae_apply", float("nan"))
         unit, metric = "merges/s", METRIC + " [C5: anti-entropy replica-bucket joins/sec]"
         workload = (f"C5 anti-entropy: {R} replicas/GPU x {B} buckets, {args.writes:g} of buckets "
                     f"written per replica per round, all-reduce(max) over {world} GPU(s)")
@@ -887,7 +894,7 @@ def main():
     # messages, so its algorithmic bytes count those
     n_roof = float(np.mean(c4_merged)) if args.workload == "c4" else n
     achieved = bpo * n_roof / (dom_ms / 1e3) / 1e9
-    traffic = pmc_traffic(args.workload if not c1 else "c1", workload)
+    traffic = pmc_traffic(args.workload if not c1 else "c1", workload, dom_name)
     out = {
         "metric": metric,
         "value": total / el,

@@ -456,6 +456,11 @@ int phip_ae_local_max(phip_handle* h, const int64_t* replicas, uint32_t nrep, ui
                       int64_t* out, uint32_t flags);
 int phip_ae_apply(phip_handle* h, int64_t* replicas, uint32_t nrep, uint64_t nbuckets,
                   const int64_t* joined, uint32_t flags);
+/* The join of one GPU's replicas with no exchange: phip_ae_local_max then
+ * phip_ae_apply in one pass (each field read once, written only where the
+ * join raises it).  What phip_group_anti_entropy runs in a world of one. */
+int phip_ae_join(phip_handle* h, int64_t* replicas, uint32_t nrep, uint64_t nbuckets,
+                 uint32_t flags);
 
 /* ---- shard group: owner routing and anti-entropy over RCCL ----
  * A group is the set of GPUs the buckets are hash-sharded over (owner =

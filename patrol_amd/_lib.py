@@ -19,7 +19,7 @@ EXPORTS = [
     "phip_capacity", "phip_seed", "phip_get", "phip_dump", "phip_receive_datagrams",
     "phip_receive_soa", "phip_upsert_soa", "phip_apply_mixed", "phip_take", "phip_parse_rate",
     "phip_marshal", "phip_api_take", "phip_last_timings", "phip_set_timing", "phip_last_stats", "phip_hash_names",
-    "phip_ae_local_max", "phip_ae_apply", "phip_set_stream", "phip_route_pack",
+    "phip_ae_local_max", "phip_ae_apply", "phip_ae_join", "phip_set_stream", "phip_route_pack",
     "phip_export_datagrams", "phip_snapshot_bytes", "phip_snapshot", "phip_restore",
     "phip_ring_open", "phip_ring_close", "phip_ring_acquire", "phip_ring_submit",
     "phip_ring_receive", "phip_udp_recv_batch", "phip_incast_replies", "phip_udp_send_batch",
@@ -144,6 +144,7 @@ def load(path: str = LIB_PATH):
     L.phip_last_stats.restype = C.c_int
     L.phip_ae_local_max.argtypes = [vp, vp, u32, u64, vp, u32]
     L.phip_ae_apply.argtypes = [vp, vp, u32, u64, vp, u32]
+    L.phip_ae_join.argtypes = [vp, vp, u32, u64, u32]
     L.phip_set_stream.argtypes = [vp, vp]
     L.phip_route_pack.argtypes = [vp, C.POINTER(phip_msgs), u32, vp, vp, vp, vp, vp, vp, vp, u32]
     L.phip_ring_open.argtypes = [vp, u32, u32, u64, C.POINTER(vp)]

@@ -2258,6 +2258,23 @@ int phip_ae_apply(phip_handle* h, int64_t* replicas, uint32_t nrep, uint64_t nbu
   return PHIP_OK;
 }
 
+int phip_ae_join(phip_handle* h, int64_t* replicas, uint32_t nrep, uint64_t nbuckets,
+                 uint32_t flags) {
+  if (!h || !(flags & PHIP_DEVICE_PTRS) || (nbuckets && !replicas) || nrep == 0)
+    return PHIP_ERR_INVALID;
+  std::lock_guard<std::mutex> g(h->mu);
+  if (int rc0 = begin_call(h)) return rc0;
+  if (nbuckets == 0) return PHIP_OK;
+  {
+    Launch l(h, "k_ae_join");
+    k_ae_join<<<dim3(grid_for((nbuckets + 1) / 2), 3), kBlock, 0, h->stream>>>(replicas, nrep,
+                                                                                nbuckets);
+  }
+  HIPCHK(h, hipGetLastError());
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  return PHIP_OK;
+}
+
 int phip_last_timings(phip_handle* h, const char** names, float* ms, int max) {
   if (!h) return 0;
   std::lock_guard<std::mutex> g(h->mu);

@@ -386,6 +386,10 @@ __global__ void k_max_into(int64_t* __restrict__ dst, const int64_t* __restrict_
 
 int member_anti_entropy(phip_group* g, Member& mb, int64_t* reps, uint32_t nrep, uint64_t B) {
   GHIP(mb, hipSetDevice(mb.device));
+  if (g->world == 1) {   // nothing to exchange: the fused local join
+    GPHIP(mb, phip_ae_join(mb.h, reps, nrep, B, PHIP_DEVICE_PTRS));
+    return PHIP_OK;
+  }
   hipStream_t st = (hipStream_t)phip_host::handle_stream(mb.h);
   GHIP(mb, mb.ae.ensure((size_t)3 * B * 8 * (g->shared ? 2 : 1)));
   int64_t* j = (int64_t*)mb.ae.p;

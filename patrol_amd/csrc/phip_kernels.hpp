@@ -3095,19 +3095,10 @@ __global__ __launch_bounds__(kRouteBlock) void k_route_count(
       if (hidx[u] >= 0) hit[hidx[u]] = 1;
     }
 #pragma unroll
-    for (u32 u = 0; u < kRU; ++u) {   // one LDS update per (wave, owner), not per message
-      const bool plain = valid[u] && hidx[u] < 0;
-      u64 rest = __ballot(plain);
-      while (rest) {
-        const u32 leader = __ffsll((long long)rest) - 1;
-        const u32 ob = __shfl(o[u], leader);
-        const bool mine = plain && o[u] == ob;
-        const u64 m = __ballot(mine);
-        u32 v = mine ? len[u] : 0;
-#pragma unroll
-        for (u32 d = 32; d; d >>= 1) v += __shfl_xor(v, d);
-        if (lane == leader) { wc[wave][ob] += (u32)__popcll(m); wb[wave][ob] += v; }
-        rest &= ~m;
+    for (u32 u = 0; u < kRU; ++u) {   // the wave's own row: LDS atomics, no cross-lane loop
+      if (valid[u] && hidx[u] < 0) {
+        atomicAdd(&wc[wave][o[u]], 1u);
+        atomicAdd(&wb[wave][o[u]], len[u]);
       }
     }
   }
@@ -3157,6 +3148,64 @@ __device__ inline void route_place(bool take, u32 o, u32 len, u32* run, u32* run
     const u32 tot = __shfl(sc, 63);
     if (lane == leader) { run[ob] = base + __popcll(m); runb[ob] = bbase + tot; }
     rest &= ~m;
+  }
+}
+
+// Inclusive wave sum scan with DPP moves (VALU only; the row_shr /
+// row_bcast pattern of wave_incl_max).  All 64 lanes must be active.
+template <int Ctrl, int RowMask = 0xF>
+__device__ inline u32 dpp_u32(u32 v) {
+  return (u32)__builtin_amdgcn_update_dpp(0, (int)v, Ctrl, RowMask, 0xF, true);
+}
+__device__ inline u32 wave_incl_sum(u32 x) {
+  x += dpp_u32<0x111>(x);
+  x += dpp_u32<0x112>(x);
+  x += dpp_u32<0x114>(x);
+  x += dpp_u32<0x118>(x);
+  x += dpp_u32<0x142, 0xA>(x);
+  x += dpp_u32<0x143, 0xC>(x);
+  return x;
+}
+
+// route_place for world <= 4 * NC (and 2 * NB == 4 * NC) and names of <= 255
+// bytes: every owner's running count and byte total packed in fields of a
+// few registers (8-bit counts, four owners a register; 16-bit byte sums, two
+// a register: a wave's 64 names fit), one DPP scan per register instead of
+// a ballot round and an LDS shuffle scan per owner present.  A lane's place
+// is its owner's base plus its inclusive field minus itself; the owner's
+// last lane advances the base.  Same result as route_place.
+template <u32 NC, u32 NB>
+__device__ inline void route_place_packed(bool take, u32 o, u32 len, u32* run, u32* runb, u32& dst,
+                                          u32& dby) {
+  u32 c[NC], b[NB];
+#pragma unroll
+  for (u32 r = 0; r < NC; ++r) c[r] = (take && (o >> 2) == r) ? 1u << (8 * (o & 3)) : 0u;
+#pragma unroll
+  for (u32 r = 0; r < NB; ++r) b[r] = (take && (o >> 1) == r) ? len << (16 * (o & 1)) : 0u;
+#pragma unroll
+  for (u32 r = 0; r < NC; ++r) c[r] = wave_incl_sum(c[r]);
+#pragma unroll
+  for (u32 r = 0; r < NB; ++r) b[r] = wave_incl_sum(b[r]);
+  u32 ci = 0, ct = 0, bi = 0, bt = 0;
+#pragma unroll
+  for (u32 r = 0; r < NC; ++r) {
+    const u32 tot = (u32)__builtin_amdgcn_readlane((int)c[r], 63);
+    if ((o >> 2) == r) { ci = c[r]; ct = tot; }
+  }
+#pragma unroll
+  for (u32 r = 0; r < NB; ++r) {
+    const u32 tot = (u32)__builtin_amdgcn_readlane((int)b[r], 63);
+    if ((o >> 1) == r) { bi = b[r]; bt = tot; }
+  }
+  ci = (ci >> (8 * (o & 3))) & 0xFFu;
+  ct = (ct >> (8 * (o & 3))) & 0xFFu;
+  bi = (bi >> (16 * (o & 1))) & 0xFFFFu;
+  bt = (bt >> (16 * (o & 1))) & 0xFFFFu;
+  if (take) {
+    const u32 base = run[o], bbase = runb[o];
+    dst = base + ci - 1;
+    dby = bbase + bi - len;
+    if (ci == ct) { run[o] = base + ct; runb[o] = bbase + bt; }
   }
 }
 
@@ -3216,7 +3265,13 @@ __global__ __launch_bounds__(kRouteBlock) void k_route_scatter(
         hit[j] = 1;
       }
       u32 dst = 0, dby = 0;
-      route_place(plain, c[u], plain ? len[u] : 0u, run[wave], runb[wave], dst, dby);
+      const u32 pl = plain ? len[u] : 0u;
+      if (world <= 8 && !__ballot(pl > 255))
+        route_place_packed<2, 4>(plain, c[u], pl, run[wave], runb[wave], dst, dby);
+      else if (world <= 16 && !__ballot(pl > 255))
+        route_place_packed<4, 8>(plain, c[u], pl, run[wave], runb[wave], dst, dby);
+      else
+        route_place(plain, c[u], pl, run[wave], runb[wave], dst, dby);
       if (!plain) continue;
       out_lens[dst] = len[u];
       out_a[dst] = va[u];
@@ -3329,6 +3384,73 @@ __global__ __launch_bounds__(kBlock) void k_ae_apply(int64_t* __restrict__ rep, 
     } else {
       if (mv > own) p[r * stride] = mv;
     }
+  }
+}
+
+// k_ae_join: the one-GPU join (phip_ae_join; the group's world-1 round).
+// local_max and apply fused: each lane reads its two buckets' R values once,
+// keeps them in registers (R <= kAeRegs; a larger R re-reads them), and
+// writes back only those below the join, so a round costs one read of the planes plus
+// the changed fields instead of two reads and the [3, B] join's round trip.
+constexpr u32 kAeRegs = 16;
+// One field of one bucket pair (buckets 2q, 2q+1) of every replica: 16-byte
+// loads, the values kept in registers for the write-back test.
+template <bool kPair>
+__device__ inline void ae_join_pair(int64_t* __restrict__ p, u32 R, u64 stride, u64 bias,
+                                    bool nanf) {
+  u64x2 v[kAeRegs];
+  u64x2 best = {0, 0};
+  auto ld2 = [&](u32 r) -> u64x2 {
+    // plain loads: the lines stay in L2 for the write-back of a changed
+    // field (non-temporal loads: 1.10 vs 0.75-0.84 ms at 8 x 2^24)
+    const int64_t* q = p + r * stride;
+    if constexpr (kPair) return *reinterpret_cast<const u64x2*>(q);
+    else return u64x2{(u64)*q, 0};
+  };
+  auto acc = [&](u64x2 e) {
+    e ^= bias;
+    u64x2 c = e;
+    if (nanf) {
+      c.x = c.x >= kNanBase ? 0 : c.x;
+      c.y = c.y >= kNanBase ? 0 : c.y;
+    }
+    best.x = c.x > best.x ? c.x : best.x;
+    best.y = c.y > best.y ? c.y : best.y;
+    return e;
+  };
+#pragma unroll
+  for (u32 r = 0; r < kAeRegs; ++r)
+    if (r < R) v[r] = acc(ld2(r));
+  for (u32 r = kAeRegs; r < R; ++r) (void)acc(ld2(r));
+  auto put = [&](u32 r, u64x2 own) {
+    int64_t* q = p + r * stride;
+    if (best.x > own.x) q[0] = (int64_t)(best.x ^ bias);
+    if (kPair && best.y > own.y) q[1] = (int64_t)(best.y ^ bias);
+  };
+#pragma unroll
+  for (u32 r = 0; r < kAeRegs; ++r)
+    if (r < R) put(r, v[r]);
+  for (u32 r = kAeRegs; r < R; ++r) {
+    const int64_t* q = p + r * stride;
+    put(r, u64x2{(u64)q[0] ^ bias, kPair ? (u64)q[1] ^ bias : 0});
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_ae_join(int64_t* __restrict__ rep, u32 R, u64 B) {
+  const u64 i = 2 * ((u64)blockIdx.x * kBlock + threadIdx.x);
+  const u32 f = blockIdx.y;
+  if (i >= B) return;
+  // the join in the unsigned E order (float planes: NaN never wins; elapsed
+  // is signed, so it is biased by 2^63 into the same order)
+  const u64 bias = f < 2 ? 0 : kSign;
+  int64_t* p = rep + (u64)f * B + i;
+  // pairs need 16-byte alignment: rep aligned, B even (every plane start
+  // aligned) and i even
+  if (i + 1 < B && !(B & 1) && !(reinterpret_cast<uintptr_t>(rep) & 15)) {
+    ae_join_pair<true>(p, R, 3 * B, bias, f < 2);
+  } else {
+    ae_join_pair<false>(p, R, 3 * B, bias, f < 2);
+    if (i + 1 < B) ae_join_pair<false>(p + 1, R, 3 * B, bias, f < 2);
   }
 }
 

@@ -288,10 +288,47 @@ def test_anti_entropy_native_gpu_equals_go_merge_and_torch():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world", [1, 3, 8, 64])
-def test_route_pack_is_stable_owner_partition(world):
+@pytest.mark.parametrize("R,B", [(1, 1031), (6, 1031), (6, 1032), (16, 1032), (21, 1031),
+                                 (21, 1032)])
+def test_ae_join_equals_local_max_apply(R, B):
+    """phip_ae_join (k_ae_join: the one-GPU round, fused) on cuda:0 equals
+    the torch restatement and the two-kernel path, for R held in registers
+    and R above kAeRegs (16) that re-reads, odd B (one bucket per load) and
+    even B (16-byte pairs); special floats (NaN sticking, +-Inf, -0.0),
+    INT64_MIN/MAX elapsed."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import patrol_amd
+    from patrol_amd import _lib
+    reps = _replicas(R, R, B)
+    x = torch.zeros((R, 3, B), dtype=torch.int64)
+    for k, (a, t, e) in enumerate(reps):
+        x[k, 0] = shard.e_encode(torch.tensor([to_i64(v) for v in a]))
+        x[k, 1] = shard.e_encode(torch.tensor([to_i64(v) for v in t]))
+        x[k, 2] = torch.tensor(e)
+    x[:, 2, :5] = torch.tensor([-(1 << 63), (1 << 63) - 1, 0, -1, -(1 << 63)])
+    x[:, 2, 5] = -(1 << 63)          # every replica at INT64_MIN: unchanged
+    want = shard.anti_entropy(x.clone())
+    repo = patrol_amd.GPURepo(device=0, log2_slots=10)
+    xd = x.cuda()
+    x2 = x.cuda()
+    torch.cuda.synchronize()
+    assert _lib.load().phip_ae_join(repo.h, xd.data_ptr(), R, B, _lib.DEVICE_PTRS) == 0
+    shard.anti_entropy_native(x2, repo)
+    assert torch.equal(xd.cpu(), want)
+    assert torch.equal(x2.cpu(), want)
+    assert _lib.load().phip_ae_join(repo.h, xd.data_ptr(), R, B, 0) == -1   # PHIP_ERR_INVALID
+    repo.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,huge", [(1, False), (3, False), (8, False), (8, True), (16, False),
+                                        (16, True), (64, False)])
+def test_route_pack_is_stable_owner_partition(world, huge):
     """phip_route_pack on cuda:0: owner-major, per-owner original order,
-    names/lengths/states moved intact, per-owner counts and byte totals."""
+    names/lengths/states moved intact, per-owner counts and byte totals.
+    World <= 16 places by packed DPP scans, larger worlds (and waves holding
+    a name over 255 bytes: `huge`) by the per-owner ballot rounds."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     import ctypes as C
@@ -303,6 +340,8 @@ def test_route_pack_is_stable_owner_partition(world):
     ids = rng.integers(0, 50_000, n)
     names = [(b"b%d" % i) if i % 7 else (b"a-long-bucket-name-%d-%s" % (i, b"x" * (i % 40)))
              for i in ids]
+    if huge:
+        names = [nm + b"y" * 300 if k % 5003 == 0 else nm for k, nm in enumerate(names)]
     blob_np, offs_np = names_blob(names)
     a = rng.integers(0, 1 << 62, n).astype(np.int64)
     t = rng.integers(0, 1 << 62, n).astype(np.int64)
