@@ -60,7 +60,7 @@ enum BufId {
   B_SLOT, B_IDX, B_SSLOT, B_SIDX, B_USLOT, B_SCNT, B_SSTART, B_LONG, B_HUGE, B_TEMP, B_DUMP,
   B_OPS, B_HOFF, B_HOP, B_HVAL, B_RPOS, B_RST, B_RUNN, B_SEGEX, B_WOFF, B_SUMS, B_WRUN,
   B_WING, B_SEGXF, B_FOLDDBG, B_SMALL, B_HUGE2, B_LONG2,
-  B_STATES, B_NAME1, B_HOT, B_ROUTE, B_EXPORT, B_MSHARD, B_MSCNT, B_DEDUP, B_DSET, B_TSTATS,
+  B_STATES, B_NAME1, B_HOT, B_ROUTE, B_EXPORT, B_MSHARD, B_MSCNT, B_DEDUP, B_DSET, B_TSTATS, B_SEGT,
   B_COUNT_
 };
 
@@ -87,6 +87,7 @@ struct phip_handle {
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   hipEvent_t ev_fork3 = nullptr, ev_join3 = nullptr;
   hipEvent_t ev_gather = nullptr, ev_gather3 = nullptr;   // huge-segment gathers done
+  hipEvent_t ev_pack = nullptr;   // ordered path: op records packed (stream2)
   std::mutex mu;
   std::string err;
   u32 L = 0;
@@ -771,7 +772,7 @@ int join_hot(phip_handle* h, const HotHdr* hot) {
 
 template <class Src>
 int resolve_all(phip_handle* h, Src src, u32 n, const int64_t* now_arr, i64 now0, u32** slot_out,
-                u32* n_claimed) {
+                u32* n_claimed, SortVals sv = SortVals{nullptr, 0, nullptr}) {
   u32 *slot, *miss;
   int rc;
   Sharded rsh;
@@ -782,7 +783,7 @@ int resolve_all(phip_handle* h, Src src, u32 n, const int64_t* now_arr, i64 now0
   {
     Launch l(h, "k_resolve");
     k_resolve<Src><<<grid_for(n), kBlock, 0, h->stream>>>(src, n, nullptr, table(h), slot, rsh,
-                                                           h->ctr);
+                                                           h->ctr, sv);
   }
   HIPCHK(h, hipGetLastError());
   u32 nmiss = 0;
@@ -803,7 +804,7 @@ int resolve_all(phip_handle* h, Src src, u32 n, const int64_t* now_arr, i64 now0
     {
       Launch l(h, "k_resolve_miss");
       k_resolve<Src><<<grid_for(nmiss), kBlock, 0, h->stream>>>(src, nmiss, miss, table(h), slot,
-                                                                 r2, h->ctr);
+                                                                 r2, h->ctr, SortVals{});
     }
     HIPCHK(h, hipGetLastError());
     if ((rc = pack_sharded(h, r2, 2, miss, &nmiss))) return rc;
@@ -817,7 +818,7 @@ int resolve_all(phip_handle* h, Src src, u32 n, const int64_t* now_arr, i64 now0
     if (!grew) {
       Launch l(h, "k_resolve_miss");
       k_resolve<Src><<<grid_for(nmiss), kBlock, 0, h->stream>>>(src, nmiss, miss, table(h), slot,
-                                                                 Sharded{}, h->ctr);
+                                                                 Sharded{}, h->ctr, SortVals{});
       HIPCHK(h, hipGetLastError());
     }
   }
@@ -825,7 +826,7 @@ int resolve_all(phip_handle* h, Src src, u32 n, const int64_t* now_arr, i64 now0
     // The table was rehashed: every op's slot is looked up again.
     Launch l(h, "k_resolve");
     k_resolve<Src><<<grid_for(n), kBlock, 0, h->stream>>>(src, n, nullptr, table(h), slot,
-                                                           Sharded{}, h->ctr);
+                                                           Sharded{}, h->ctr, SortVals{});
     HIPCHK(h, hipGetLastError());
   }
   *slot_out = slot;
@@ -840,9 +841,6 @@ int ordered(phip_handle* h, Src src, u32 n, const OpView& ov, const OutView& ow)
   if (n > kMaxOrderedOps)
     return set_err(h, PHIP_ERR_INVALID, "ordered batch of %u ops exceeds 2^30", n);
   int rc;
-  u32* slot;
-  u32 n_claimed = 0;
-  if ((rc = resolve_all(h, src, n, ov.now, ov.now0, &slot, &n_claimed))) return rc;
   u32 *idx, *sslot, *sidx, *uslot, *scnt, *sstart, *lng, *huge;
   if ((rc = ensure(h, B_IDX, n, &idx)) || (rc = ensure(h, B_SSLOT, n, &sslot)) ||
       (rc = ensure(h, B_SIDX, n, &sidx)) || (rc = ensure(h, B_USLOT, n, &uslot)) ||
@@ -851,54 +849,113 @@ int ordered(phip_handle* h, Src src, u32 n, const OpView& ov, const OutView& ow)
     return rc;
   OpRec* opr;
   if ((rc = ensure(h, B_OPS, n, &opr))) return rc;
-  {
-    Launch l(h, "k_pack_ops");
-    k_pack_ops<<<grid_for(n), kBlock, 0, h->stream>>>(ov, n, opr, idx);
-  }
+  // The op records are read by the folds only: k_pack_ops runs on stream2
+  // beside the resolve, the sort and the segmentation (independent streams of
+  // the batch's columns; the resolve is bound by probe latency), and the main
+  // stream joins it before the first fold, or on any error return (PackJoin).
+  struct PackJoin {
+    phip_handle* h;
+    bool armed = true;
+    int join() {
+      armed = false;
+      return hipStreamWaitEvent(h->stream, h->ev_pack, 0) == hipSuccess
+                 ? PHIP_OK
+                 : set_err(h, PHIP_ERR_HIP, "hipStreamWaitEvent (op records)");
+    }
+    ~PackJoin() { if (armed) (void)hipStreamWaitEvent(h->stream, h->ev_pack, 0); }
+  } pack_join{h};
+  auto fork_pack = [&]() -> int {
+    HIPCHK(h, hipEventRecord(h->ev_fork, h->stream));
+    HIPCHK(h, hipStreamWaitEvent(h->stream2, h->ev_fork, 0));
+    {
+      Launch l(h, "k_pack_ops", h->stream2);
+      k_pack_ops<<<grid_for(n), kBlock, 0, h->stream2>>>(ov, n, opr, nullptr);
+    }
+    HIPCHK(h, hipGetLastError());
+    HIPCHK(h, hipEventRecord(h->ev_pack, h->stream2));
+    return PHIP_OK;
+  };
+  // (PHIP_PACK_AFTER=1: the pack starts after the resolve, beside the sort; A/B)
+  static const bool pack_after = getenv("PHIP_PACK_AFTER") != nullptr;
+  if (!pack_after && (rc = fork_pack())) return rc;
+  u32* slot;
+  u32 n_claimed = 0;
+  if ((rc = resolve_all(h, src, n, ov.now, ov.now0, &slot, &n_claimed,
+                        SortVals{ov.kind, ov.kind0, idx})))
+    return rc;
+  if (pack_after && (rc = fork_pack())) return rc;
   // Stable radix sort of (slot, seq) pairs: per-bucket arrival order kept.
   size_t tb = 0;
   HIPCHK(h, rocprim::radix_sort_pairs<SlotSortConfig>(nullptr, tb, slot, sslot, idx, sidx, n, 0u, h->L,
                                                        h->stream));
-  size_t tb2 = 0;
-  HIPCHK(h, rocprim::run_length_encode(nullptr, tb2, sslot, n, uslot, scnt, h->ctr + 6, h->stream));
-  size_t tb3 = 0;
-  HIPCHK(h, rocprim::exclusive_scan(nullptr, tb3, scnt, sstart, 0u, (size_t)n, rocprim::plus<u32>(),
-                                    h->stream));
+  // segmentation buffers and scan temp sized before the sort is enqueued (a
+  // larger B_TEMP must not replace the one the sort is using)
+  static const bool seg_rle = getenv("PHIP_SEG_RLE") != nullptr;
+  const u32 ntiles = (u32)(((u64)n + kSegTile - 1) / kSegTile);
+  u32 *segt = nullptr, *segb = nullptr;
+  size_t tbs = 0;
+  if (!seg_rle) {
+    if ((rc = ensure(h, B_SEGT, 2 * ((size_t)ntiles + 1), &segt))) return rc;
+    segb = segt + ntiles + 1;
+    HIPCHK(h, rocprim::exclusive_scan(nullptr, tbs, segt, segb, 0u, (size_t)ntiles + 1,
+                                      rocprim::plus<u32>(), h->stream));
+  }
   u8* temp;
-  if ((rc = ensure(h, B_TEMP, std::max(tb, std::max(tb2, tb3)), &temp))) return rc;
+  if ((rc = ensure(h, B_TEMP, std::max(tb, tbs), &temp))) return rc;
   {
     Launch l(h, "radix_sort_pairs");
     HIPCHK(h, rocprim::radix_sort_pairs<SlotSortConfig>(temp, tb, slot, sslot, idx, sidx, n, 0u,
                                                          h->L, h->stream));
   }
-  {
-    Launch l(h, "run_length_encode");
-    HIPCHK(h, rocprim::run_length_encode(temp, tb2, sslot, n, uslot, scnt, h->ctr + 6, h->stream));
-  }
-  if ((rc = read_ctr(h))) return rc;
-  u32 nseg = h->ctr_host[6];
-  {
-    Launch l(h, "exclusive_scan");
-    HIPCHK(h, rocprim::exclusive_scan(temp, tb3, scnt, sstart, 0u, (size_t)nseg, rocprim::plus<u32>(),
+  u32 nseg = 0;
+  // (PHIP_SEG_RLE=1: run_length_encode + scan + selects, for A/B timing)
+  if (!seg_rle) {
+    Launch l(h, "segments");
+    k_seg_count<<<ntiles, 256, 0, h->stream>>>(sslot, n, segt, h->ctr);
+    HIPCHK(h, rocprim::exclusive_scan(temp, tbs, segt, segb, 0u, (size_t)ntiles + 1,
+                                      rocprim::plus<u32>(), h->stream));
+    k_seg_write<<<ntiles, 256, 0, h->stream>>>(sslot, n, segb, uslot, sstart);
+    k_seg_finish<<<std::max(1u, std::min<u32>(ntiles, (u32)h->ncu * 4)), 256, 0, h->stream>>>(
+        segb, ntiles, sstart, n, scnt, lng, huge, h->ctr);
+    HIPCHK(h, hipGetLastError());
+    if ((rc = read_ctr(h))) return rc;
+    nseg = h->ctr_host[kCtrSegs];
+  } else {
+    size_t tb2 = 0, tb3 = 0;
+    HIPCHK(h, rocprim::run_length_encode(nullptr, tb2, sslot, n, uslot, scnt, h->ctr + 6, h->stream));
+    HIPCHK(h, rocprim::exclusive_scan(nullptr, tb3, scnt, sstart, 0u, (size_t)n, rocprim::plus<u32>(),
                                       h->stream));
+    if ((rc = ensure(h, B_TEMP, std::max(tb2, tb3), &temp))) return rc;
+    {
+      Launch l(h, "run_length_encode");
+      HIPCHK(h, rocprim::run_length_encode(temp, tb2, sslot, n, uslot, scnt, h->ctr + 6, h->stream));
+    }
+    if ((rc = read_ctr(h))) return rc;
+    nseg = h->ctr_host[6];
+    {
+      Launch l(h, "exclusive_scan");
+      HIPCHK(h, rocprim::exclusive_scan(temp, tb3, scnt, sstart, 0u, (size_t)nseg,
+                                        rocprim::plus<u32>(), h->stream));
+    }
+    {
+      // long / huge segment lists (order-preserving compaction, no atomics)
+      Launch l(h, "select_segments");
+      size_t tb4 = 0, tb5 = 0;
+      rocprim::counting_iterator<u32> segs(0u);
+      HIPCHK(h, rocprim::select(nullptr, tb4, segs, lng, h->ctr + 6, (size_t)nseg, LongSeg{scnt},
+                                h->stream));
+      HIPCHK(h, rocprim::select(nullptr, tb5, segs, huge, h->ctr + 9, (size_t)nseg, HugeSeg{scnt},
+                                h->stream));
+      if ((rc = ensure(h, B_TEMP, std::max(tb4, tb5), &temp))) return rc;
+      HIPCHK(h, rocprim::select(temp, tb4, segs, lng, h->ctr + 6, (size_t)nseg, LongSeg{scnt},
+                                h->stream));
+      HIPCHK(h, rocprim::select(temp, tb5, segs, huge, h->ctr + 9, (size_t)nseg, HugeSeg{scnt},
+                                h->stream));
+    }
+    if ((rc = read_ctr(h))) return rc;
   }
-  {
-    // long / huge segment lists (order-preserving compaction, no atomics)
-    Launch l(h, "select_segments");
-    size_t tb4 = 0, tb5 = 0;
-    rocprim::counting_iterator<u32> segs(0u);
-    HIPCHK(h, rocprim::select(nullptr, tb4, segs, lng, h->ctr + 6, (size_t)nseg, LongSeg{scnt},
-                              h->stream));
-    HIPCHK(h, rocprim::select(nullptr, tb5, segs, huge, h->ctr + 9, (size_t)nseg, HugeSeg{scnt},
-                              h->stream));
-    if ((rc = ensure(h, B_TEMP, std::max(tb4, tb5), &temp))) return rc;
-    HIPCHK(h, rocprim::select(temp, tb4, segs, lng, h->ctr + 6, (size_t)nseg, LongSeg{scnt},
-                              h->stream));
-    HIPCHK(h, rocprim::select(temp, tb5, segs, huge, h->ctr + 9, (size_t)nseg, HugeSeg{scnt},
-                              h->stream));
-  }
-  if ((rc = read_ctr(h))) return rc;
   u32 nlong = h->ctr_host[6], nhuge = h->ctr_host[9];
+  if ((rc = pack_join.join())) return rc;
   // Different segments touch different slots, so the folds may overlap: the
   // hot-bucket workgroups run on stream2 beside the wave and thread folds.
   if (nhuge) {
@@ -950,6 +1007,8 @@ int ordered(phip_handle* h, Src src, u32 n, const OpView& ov, const OutView& ow)
     u64* fold_dbg = nullptr;
     if (fold_stats && (rc = ensure(h, B_FOLDDBG, (size_t)nhuge * 16, &fold_dbg))) return rc;
     auto kb = variant == 1 ? k_fold_block<1> : k_fold_block<0>;
+    // (PHIP_FOLD_NOPRIO=1: the block folds at normal issue priority, A/B)
+    static const u32 fold_prio = getenv("PHIP_FOLD_NOPRIO") ? 0u : 1u;
     // gather / outputs: window-striding grids of 8 workgroups per CU (the
     // window count is known on the device only)
     const unsigned hgrid = (unsigned)std::min<size_t>(nwin_max, (size_t)h->ncu * 8);
@@ -974,7 +1033,7 @@ int ordered(phip_handle* h, Src src, u32 n, const OpView& ov, const OutView& ow)
         Launch l(h, nf, st);
         kb<<<h1 - h0, kFoldThreads, 0, st>>>(hl, h1, uslot, hoff, scnt, hval, hop, h->recs, rpos,
                                              rst, runn, segex, segxf, woff, sums, wrun, wing,
-                                             fold_dbg, h0);
+                                             fold_dbg, h0, fold_prio);
       }
       HIPCHK(h, hipGetLastError());
       {
@@ -1407,8 +1466,15 @@ int phip_open(const phip_config* cfg, phip_handle** out) {
   if ((e = hipStreamCreateWithFlags(&h->own_stream, hipStreamNonBlocking)) != hipSuccess)
     return fail(e);
   h->stream = h->own_stream;
-  if ((e = hipStreamCreateWithFlags(&h->stream2, hipStreamNonBlocking)) != hipSuccess) return fail(e);
-  if ((e = hipStreamCreateWithFlags(&h->stream3, hipStreamNonBlocking)) != hipSuccess) return fail(e);
+  // (PHIP_STREAM_PRIO=1: stream2/stream3 at the device's greatest priority, A/B)
+  int prio_lo = 0, prio_hi = 0;
+  if (getenv("PHIP_STREAM_PRIO") &&
+      (e = hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi)) != hipSuccess)
+    return fail(e);
+  if ((e = hipStreamCreateWithPriority(&h->stream2, hipStreamNonBlocking, prio_hi)) != hipSuccess)
+    return fail(e);
+  if ((e = hipStreamCreateWithPriority(&h->stream3, hipStreamNonBlocking, prio_hi)) != hipSuccess)
+    return fail(e);
   if ((e = hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming)) != hipSuccess) return fail(e);
   if ((e = hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming)) != hipSuccess) return fail(e);
   if ((e = hipEventCreateWithFlags(&h->ev_fork3, hipEventDisableTiming)) != hipSuccess) return fail(e);
@@ -1416,6 +1482,7 @@ int phip_open(const phip_config* cfg, phip_handle** out) {
   if ((e = hipEventCreateWithFlags(&h->ev_gather, hipEventDisableTiming)) != hipSuccess) return fail(e);
   if ((e = hipEventCreateWithFlags(&h->ev_gather3, hipEventDisableTiming)) != hipSuccess)
     return fail(e);
+  if ((e = hipEventCreateWithFlags(&h->ev_pack, hipEventDisableTiming)) != hipSuccess) return fail(e);
   if ((e = hipMalloc(&h->recs, h->cap * sizeof(Rec))) != hipSuccess) return fail(e);
   if ((e = hipMalloc(&h->aux, h->cap * sizeof(u32))) != hipSuccess) return fail(e);
   if ((e = hipMalloc(&h->arena, h->arena_cap + 64)) != hipSuccess) return fail(e);
@@ -1459,6 +1526,7 @@ void phip_close(phip_handle* h) {
   if (h->ev_join3) (void)hipEventDestroy(h->ev_join3);
   if (h->ev_gather) (void)hipEventDestroy(h->ev_gather);
   if (h->ev_gather3) (void)hipEventDestroy(h->ev_gather3);
+  if (h->ev_pack) (void)hipEventDestroy(h->ev_pack);
   if (h->stream2) (void)hipStreamDestroy(h->stream2);
   if (h->stream3) (void)hipStreamDestroy(h->stream3);
   if (h->own_stream) {

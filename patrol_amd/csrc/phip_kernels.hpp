@@ -1127,16 +1127,25 @@ __global__ void k_mark_created(Src src, u32 n, const u32* __restrict__ list, Tab
 }
 
 // -------------------------------------------------------------- resolve --
+// The ordered path's sort values (op index | kind << kOpIdxBits), written by
+// the first full resolve (val == nullptr: none).
+struct SortVals {
+  const u8* kind; u32 kind0;
+  u32* val;
+};
+constexpr u32 kSortValKindShift = 30;
+
 // Name -> slot for every op (ordered path, seed, get).  Misses appended.
 template <class Src>
 __global__ __launch_bounds__(kBlock) void k_resolve(Src src, u32 n, const u32* __restrict__ list,
                                                     Table T, u32* __restrict__ slot_out, Sharded miss,
-                                                    u32* ctr) {
+                                                    u32* ctr, SortVals sv) {
   u32 tid = blockIdx.x * blockDim.x + threadIdx.x;
   bool missed = false;
   u32 i = 0;
   if (tid < n) {
     i = list ? list[tid] : tid;
+    if (sv.val) sv.val[i] = i | ((u32)(sv.kind ? sv.kind[i] : sv.kind0) << kSortValKindShift);
     u64 off; u32 len;
     src.get(i, off, len);
     Name nm;
@@ -1371,6 +1380,7 @@ struct alignas(32) OpRec {
   u64 x, y, z;
 };
 constexpr u32 kOpIdxBits = 30;
+static_assert(kOpIdxBits == kSortValKindShift, "k_resolve's sort values");
 constexpr u32 kOpIdxMask = (1u << kOpIdxBits) - 1;
 constexpr u32 kMaxOrderedOps = 1u << kOpIdxBits;
 
@@ -1416,7 +1426,7 @@ __global__ __launch_bounds__(kBlock) void k_pack_ops(OpView ov, u32 n, OpRec* __
   ulonglong2* q = reinterpret_cast<ulonglong2*>(ops + i);
   q[0] = ulonglong2{(u64)r.now, r.x};
   q[1] = ulonglong2{r.y, r.z};
-  val[i] = i | (kind << kOpIdxBits);
+  if (val) val[i] = i | (kind << kOpIdxBits);
 }
 
 struct FState {
@@ -1545,7 +1555,7 @@ constexpr u32 kLongSeg = 32;        // longer segments: one wave each (k_fold_wa
 constexpr u32 kHugeSeg = PHIP_HUGE_SEG;   // longer still: one workgroup each (k_fold_block)
 // The largest huge segments (at most this many) fold on a stream of their own.
 #ifndef PHIP_HUGE_FIRST
-#define PHIP_HUGE_FIRST 4
+#define PHIP_HUGE_FIRST 8
 #endif
 constexpr u32 kHugeFirstMax = 16;
 static_assert(PHIP_HUGE_FIRST <= kHugeFirstMax, "PHIP_HUGE_FIRST");
@@ -2580,10 +2590,14 @@ __global__ __launch_bounds__(kFoldThreads) void k_fold_block(
     u32* __restrict__ run_pos, RunState* __restrict__ run_st, u32* __restrict__ run_n,
     u8* __restrict__ seg_existed, u32* __restrict__ seg_exact_from,
     const u64* __restrict__ woff, const WinSum* __restrict__ sums, u32* __restrict__ win_run,
-    GMax* __restrict__ win_g, u64* __restrict__ dbg, u32 h_begin) {
+    GMax* __restrict__ win_g, u64* __restrict__ dbg, u32 h_begin, u32 prio) {
   __shared__ FoldShared sh;
   const u32 hs = h_begin + blockIdx.x;   // segments [h_begin, nhuge) of the list
   if (hs >= nhuge) return;
+  // A hot segment's fold is one sequential chain of dependent rounds beside
+  // the bandwidth-bound wave and thread folds: its waves take the SIMD's
+  // issue priority.
+  if (prio) __builtin_amdgcn_s_setprio(3);
   const u64 t_begin = wall_clock64();
   u32 n_folded = 0;
   const u32 g = huge_list[hs];
@@ -2834,6 +2848,123 @@ struct BigLongSeg {
   const u32* cnt;
   __device__ bool operator()(u32 g) const { return cnt[g] > kBigLongSeg; }
 };
+
+// Per-bucket segments of the sorted ops in three passes over the sorted slots
+// (run_length_encode + exclusive_scan + two selects before: 0.31 ms and a
+// host round trip on C3): k_seg_count counts the segment heads of every tile
+// of kSegTile sorted ops, a scan of the tile counts places them, k_seg_write
+// writes each head's slot and start, and k_seg_finish derives the counts and
+// appends the long (ctr[6]) and huge (ctr[9]) segments; ctr[15] = segments.
+// The long / huge lists come out in no particular order: every segment is
+// folded on its own, so the order only schedules.
+constexpr u32 kSegTile = 4096;
+constexpr u32 kSegPer = kSegTile / 256;
+constexpr u32 kCtrSegs = 15;
+
+__device__ inline bool seg_head(const u32* __restrict__ key, u64 k) {
+  return k == 0 || key[k] != key[k - 1];
+}
+
+__global__ __launch_bounds__(256) void k_seg_count(const u32* __restrict__ key, u32 n,
+                                                   u32* __restrict__ tile_cnt, u32* ctr) {
+  __shared__ u32 part[4];
+  const u32 wave = threadIdx.x / 64, lane = threadIdx.x & 63;
+  const u64 k0 = (u64)blockIdx.x * kSegTile;
+  u32 c = 0;
+#pragma unroll 4
+  for (u32 r = 0; r < kSegPer; ++r) {
+    const u64 k = k0 + r * 256 + threadIdx.x;
+    c += (u32)__popcll(__ballot(k < n && seg_head(key, k)));
+  }
+  if (lane == 0) part[wave] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    tile_cnt[blockIdx.x] = part[0] + part[1] + part[2] + part[3];
+    if (blockIdx.x == 0) { ctr[6] = 0; ctr[9] = 0; tile_cnt[gridDim.x] = 0; }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_seg_write(const u32* __restrict__ key, u32 n,
+                                                   const u32* __restrict__ tile_base,
+                                                   u32* __restrict__ uslot, u32* __restrict__ sstart) {
+  __shared__ u32 wtot[kSegPer][4];
+  const u32 wave = threadIdx.x / 64, lane = threadIdx.x & 63;
+  const u64 k0 = (u64)blockIdx.x * kSegTile;
+  bool hd[kSegPer];
+  u32 rank[kSegPer];
+#pragma unroll
+  for (u32 r = 0; r < kSegPer; ++r) {
+    const u64 k = k0 + r * 256 + threadIdx.x;
+    hd[r] = k < n && seg_head(key, k);
+    const u64 m = __ballot(hd[r]);
+    rank[r] = (u32)__popcll(m & ((1ull << lane) - 1));
+    if (lane == 0) wtot[r][wave] = (u32)__popcll(m);
+  }
+  __syncthreads();
+  u32 base = tile_base[blockIdx.x];
+#pragma unroll
+  for (u32 r = 0; r < kSegPer; ++r) {
+    u32 pre = 0;
+    for (u32 w = 0; w < wave; ++w) pre += wtot[r][w];
+    const u64 k = k0 + r * 256 + threadIdx.x;
+    if (hd[r]) {
+      const u32 j = base + pre + rank[r];
+      uslot[j] = key[k];
+      sstart[j] = (u32)k;
+    }
+    base += wtot[r][0] + wtot[r][1] + wtot[r][2] + wtot[r][3];
+  }
+}
+
+// Each workgroup takes a contiguous range of the segments (their number is on
+// the device only) and appends its long / huge ones through LDS lists, with
+// one global atomic per list and flush: a wave-level atomic on ctr[6] per
+// 64 segments serialised ~10^5 same-address atomics (0.41 ms on C3).
+constexpr u32 kSegListCap = 1024;
+__device__ inline void seg_flush(u32* lst, u32& cnt, u32* gcnt, u32* out, u32* base_sh) {
+  __syncthreads();
+  const u32 c = cnt;
+  if (threadIdx.x == 0) *base_sh = c ? atomicAdd(gcnt, c) : 0u;
+  __syncthreads();
+  const u32 b = *base_sh;
+  for (u32 k = threadIdx.x; k < c; k += 256) out[b + k] = lst[k];
+  __syncthreads();
+  if (threadIdx.x == 0) cnt = 0;
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(256) void k_seg_finish(const u32* __restrict__ tile_base, u32 ntiles,
+                                                    const u32* __restrict__ sstart, u32 n,
+                                                    u32* __restrict__ scnt, u32* __restrict__ lng,
+                                                    u32* __restrict__ huge, u32* ctr) {
+  __shared__ u32 llist[kSegListCap], hlist[kSegListCap];
+  __shared__ u32 lcnt, hcnt, base_sh;
+  const u32 nseg = tile_base[ntiles];
+  if (blockIdx.x == 0 && threadIdx.x == 0) ctr[kCtrSegs] = nseg;
+  if (threadIdx.x == 0) { lcnt = 0; hcnt = 0; }
+  const u32 per = (nseg + gridDim.x - 1) / gridDim.x;
+  const u32 g0 = min(nseg, blockIdx.x * per), g1 = min(nseg, g0 + per);
+  __syncthreads();
+  for (u32 j0 = g0; j0 < g1; j0 += 256) {
+    const u32 j = j0 + threadIdx.x;
+    u32 c = 0;
+    if (j < g1) {
+      c = (j + 1 < nseg ? sstart[j + 1] : n) - sstart[j];
+      scnt[j] = c;
+    }
+    const bool lo = c > kLongSeg && c <= kHugeSeg, hu = c > kHugeSeg;
+    if (lo) llist[atomicAdd(&lcnt, 1u)] = j;
+    if (hu) hlist[atomicAdd(&hcnt, 1u)] = j;
+    __syncthreads();
+    const u32 lc = lcnt, hc = hcnt;   // the same in every thread: read between barriers
+    __syncthreads();
+    // room for the next 256 in both lists
+    if (lc > kSegListCap - 256) seg_flush(llist, lcnt, &ctr[6], lng, &base_sh);
+    if (hc > kSegListCap - 256) seg_flush(hlist, hcnt, &ctr[9], huge, &base_sh);
+  }
+  seg_flush(llist, lcnt, &ctr[6], lng, &base_sh);
+  seg_flush(hlist, hcnt, &ctr[9], huge, &base_sh);
+}
 
 // Sorted-slot segments from run-length output (counts -> starts is a scan).
 __global__ void k_seg_mark(const u32* __restrict__ sorted_slot, u32 n, u32* head) {
