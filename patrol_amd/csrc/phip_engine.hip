@@ -60,7 +60,7 @@ enum BufId {
   B_SLOT, B_IDX, B_SSLOT, B_SIDX, B_USLOT, B_SCNT, B_SSTART, B_LONG, B_HUGE, B_TEMP, B_DUMP,
   B_OPS, B_HOFF, B_HOP, B_HVAL, B_RPOS, B_RST, B_RUNN, B_SEGEX, B_WOFF, B_SUMS, B_WRUN,
   B_WING, B_SEGXF, B_FOLDDBG, B_SMALL, B_HUGE2, B_LONG2,
-  B_STATES, B_NAME1, B_HOT, B_ROUTE, B_EXPORT, B_MSHARD, B_MSCNT, B_DEDUP, B_DSET, B_TSTATS, B_SEGT,
+  B_STATES, B_NAME1, B_HOT, B_ROUTE, B_EXPORT, B_MSHARD, B_MSCNT, B_DEDUP, B_DSET, B_TSTATS, B_SEGT, B_FUSE,
   B_COUNT_
 };
 
@@ -595,13 +595,38 @@ int fast_apply(phip_handle* h, In in, HotSrc hsrc, u32 n, u8* status, u32* first
   if (with_hot) HIPCHK(h, hipEventRecord(h->ev_fork, h->stream));
   if (with_hot && hot_first && (rc = fork_hot(h, hsrc, n, &hot, &hot_dir))) return rc;
   if (status) HIPCHK(h, hipMemsetAsync(status, PHIP_ST_MERGED, n, h->stream));
+  // A large decoded batch is classified in the fast kernel past its first
+  // fc.pre segments (FuseCls, phip_kernels.hpp); k_classify takes those
+  // beside the hot-directory chain.  Experimental: on with PHIP_FUSE_CLS=1
+  // (DESIGN.md §4, round 3).  (PHIP_NO_FUSE_CLS=1: k_classify over the
+  // whole batch first, for A/B; PHIP_CLS_PRE: segments classified before.)
+  FuseCls fc{};
+  u32 ncls = n;
+  if constexpr (In::kSoa) {
+    // (read per batch, so a test can switch it within one process)
+    const bool no_fuse = !getenv("PHIP_FUSE_CLS") || getenv("PHIP_NO_FUSE_CLS") != nullptr;
+    const u32 pre_env = getenv("PHIP_CLS_PRE") ? (u32)atoi(getenv("PHIP_CLS_PRE")) : 2u;
+    const u32 pre = std::max(1u, std::min(pre_env, kClsSegs));
+    if (!no_fuse && pre < kClsSegs && n >= kFuseClsMin &&
+        (((uintptr_t)in.ma | (uintptr_t)in.mt) & 15) == 0) {
+      const u32 nunits = (n + kClsUnit - 1) / kClsUnit;
+      const u32 seg_units =
+          ((nunits + kClsSegs - 1) / kClsSegs + kClsGroup - 1) / kClsGroup * kClsGroup;
+      const size_t words = (size_t)nunits + (nunits + kClsGroup - 1) / kClsGroup;
+      u32* fb;
+      if ((rc = ensure(h, B_FUSE, words, &fb))) return rc;
+      HIPCHK(h, hipMemsetAsync(fb, 0, words * sizeof(u32), h->stream));
+      fc = FuseCls{fb, seg_units, nunits, pre, 1};
+      ncls = (u32)std::min<u64>(n, (u64)pre * seg_units * kClsUnit);
+    }
+  }
   {
     Launch l(h, "k_classify");
     bool done = false;
     if constexpr (In::kSoa) {
       if ((((uintptr_t)in.ma | (uintptr_t)in.mt) & 15) == 0) {
-        k_classify_soa2<<<grid_for((n + 1) / 2), kBlock, 0, h->stream>>>(in.ma, in.mt, in.me, n,
-                                                                          h->ctr);
+        k_classify_soa2<<<grid_for((ncls + 1) / 2), kBlock, 0, h->stream>>>(in.ma, in.mt, in.me,
+                                                                             ncls, h->ctr);
         done = true;
       }
     }
@@ -615,7 +640,7 @@ int fast_apply(phip_handle* h, In in, HotSrc hsrc, u32 n, u8* status, u32* first
   {
     Launch l(h, "k_receive_fast");
     k_receive_fast<In><<<fast_grid(h, n), kFastBlock, 0, h->stream>>>(
-        in, n, table(h), msh, h->ctr, hot, hot_dir);
+        in, n, table(h), msh, h->ctr, hot, hot_dir, fc);
   }
   HIPCHK(h, hipGetLastError());
   if ((rc = pack_sharded(h, msh, 2, miss, nmiss))) return rc;
@@ -2207,10 +2232,11 @@ int phip_route_pack(phip_handle* h, const phip_msgs* m, uint32_t world, uint8_t*
     HIPCHK(h, hipStreamSynchronize(h->stream));
     return PHIP_OK;
   }
-  // One wave per tile of `span` messages, eight per workgroup, four
-  // workgroups per CU.
+  // One wave per tile of `span` messages, eight per workgroup.
+  // 12 workgroups per CU: k_route_count holds 4 per CU, k_route_scatter 3,
+  // so both grids run in whole rounds (no tail round of a quarter of the chip)
   const u32 nblk = (u32)std::max<u64>(1, std::min<u64>((n + kRouteBlock - 1) / kRouteBlock,
-                                                       (u64)h->ncu * 4));
+                                                       (u64)h->ncu * 12));
   const u32 ntile = nblk * kRouteWaves;
   const u32 span = (u32)(((u64)n + ntile - 1) / ntile + 63) & ~63u;
   const size_t cells = (size_t)world * ntile;

@@ -491,7 +491,7 @@ constexpr u32 kRouteHotMax = 512;
 static_assert(kHotLds * 2 >= kRouteHotMax * 3 && kHotLds * 2 >= kHotMax * 3, "LDS lookup load");
 constexpr u32 kHotCntBits = 18;       // sample count table: 2^18 (slot+1, count) pairs
 constexpr u32 kHotSampleMax = 1u << 17;   // samples per batch (half the count table)
-constexpr u32 kHotSamplePerBlock = 1024;
+constexpr u32 kHotSamplePerBlock = 256;   // one sample a thread: 512 workgroups (the chain runs beside segment 0's classification)
 constexpr u32 kHotHist = 4096;        // histogram bins of sample counts
 constexpr u32 kHotMinCount = 8;       // sample hits for a bucket to qualify
 // Smaller batches skip the directory.  2^16, not larger: a skewed batch of a
@@ -849,10 +849,170 @@ __device__ inline bool tail_match(const u64 (&htail)[kHotTailWords][kHotMax], u3
   return eq;
 }
 
+// ------------------------------------------ classification in the fast pass --
+// A large decoded batch is classified inside k_receive_fast instead of by a
+// whole-batch k_classify in front of it (0.25 ms of the 2.15 ms C2 step).
+// The batch is cut into kClsSegs segments of units of kClsUnit messages;
+// k_classify covers segment 0 before the kernel, beside the hot-directory
+// chain.  A wave entering segment s applies nothing there before every unit
+// of segments <= s is classified (the clean prefix is only known then): the
+// units of segment s+1 are classified ahead, one unit per wave that draws a
+// ticket on entering segment s, and a wave that finds a unit of a segment it
+// needs unclassified claims it and classifies it itself (a unit claimed by
+// another wave is being classified by a running wave: waiting for it cannot
+// deadlock, whatever part of the grid is resident).  A unit's dirty index is
+// recorded (atomicMin) before the unit is marked done (release); a wave reads
+// the first dirty index after it has seen its segments done (acquire).
+constexpr u32 kClsUnit = 4096;
+constexpr u32 kClsSegs = 8;
+constexpr u32 kClsFree = 0, kClsClaimed = 1, kClsDone = 2;
+constexpr u32 kFuseClsMin = 1u << 22;   // smaller batches: k_classify over the whole batch
+constexpr u32 kClsGroup = 64;   // units per done counter (a segment is whole groups)
+struct FuseCls {
+  // one buffer, zeroed per batch (one pointer: the fast kernel is short of
+  // scalar registers): a flag per unit, then a done counter per group of
+  // kClsGroup units (at most kClsGroup-way contention on one address: a
+  // counter per segment took thousands of same-address atomics a segment)
+  u32* base;
+  u32 seg_units;    // units per segment (a multiple of kClsGroup)
+  u32 nunits;
+  u32 pre;          // segments [0, pre) classified by k_classify before the kernel
+  u32 on;           // 0: k_classify covered the whole batch
+  __device__ u32* flag() const { return base; }
+  __device__ u32* gdone() const { return base + nunits; }
+};
+
+__device__ inline u32 cls_seg_units(const FuseCls& fc, u32 s) {
+  const u32 u0 = s * fc.seg_units;
+  return u0 >= fc.nunits ? 0u : min(fc.seg_units, fc.nunits - u0);
+}
+
+// Unit u of a decoded batch, by one wave: k_classify_soa2's pass (two
+// messages a lane, 16-byte loads), four steps of 128 messages in flight.
+template <class In>
+__device__ inline void cls_unit(const In& in, u32 u, u32 n, u32* ctr) {
+  if constexpr (In::kSoa) {
+    const u32 lane = __lane_id();
+    const u32 ub = u * kClsUnit;
+    for (u32 k = 0; k < kClsUnit; k += 4 * 128) {
+      u64x2 a[4], t[4];
+#pragma unroll
+      for (u32 r = 0; r < 4; ++r) {
+        const u32 i = min(ub + k + r * 128 + 2 * lane, (n - 1) & ~1u);
+        a[r] = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(in.ma + i));
+        t[r] = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(in.mt + i));
+      }
+#pragma unroll
+      for (u32 r = 0; r < 4; ++r) {
+        const u32 i = ub + k + r * 128 + 2 * lane;
+        bool d0 = false, d1 = false;
+        if (i + 1 < n) {
+          const bool z0 = is_zero_bits(a[r].x) && is_zero_bits(t[r].x);
+          const bool z1 = is_zero_bits(a[r].y) && is_zero_bits(t[r].y);
+          d0 = (z0 && in.me[i] == 0) || a[r].x == kSign || t[r].x == kSign;
+          d1 = (z1 && in.me[i + 1] == 0) || a[r].y == kSign || t[r].y == kSign;
+        } else if (i < n) {
+          d0 = in.dirty(i, ctr);
+        }
+        note_dirty(d0 || d1, d0 ? i : i + 1, ctr);
+      }
+    }
+  }
+}
+
+// Cross-workgroup signalling in the fast kernel uses atomic read-modify-
+// writes only (relaxed, device scope: performed where every XCD sees them).
+// Acquire loads and release stores at agent scope write back / invalidate the
+// XCD's L2 on gfx950, which, issued by thousands of waves, cost the merge its
+// cache (a first version: k_receive_fast 1.87 -> 11.5 ms).  Ordering comes
+// from completion instead: a unit's dirty minima are complete (s_waitcnt)
+// before its done mark is issued, and a reader issues its read of the first
+// dirty index only after its read of the done marks has returned.
+__device__ inline u32 rmw_read(u32* p) {
+  return __hip_atomic_fetch_or(p, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ inline u32 wave_rmw_read(u32* p) {
+  u32 v = 0;
+  if (__lane_id() == 0) v = rmw_read(p);
+  return (u32)__builtin_amdgcn_readfirstlane((int)v);
+}
+
+// Classify unit u if it is free (claimed here), else wait until the wave that
+// claimed it is done.  Wave-uniform.
+template <class In>
+__device__ inline void cls_claim(const In& in, const FuseCls& fc, u32 u, u32 n, u32* ctr) {
+  u32 f = wave_rmw_read(&fc.flag()[u]);
+  if (f == kClsDone) return;
+  if (f == kClsFree) {
+    u32 old = 0;
+    if (__lane_id() == 0) old = atomicCAS(&fc.flag()[u], kClsFree, kClsClaimed);
+    old = (u32)__builtin_amdgcn_readfirstlane((int)old);
+    if (old == kClsFree) {
+      cls_unit(in, u, n, ctr);
+      // the unit's atomicMin (if any) complete before the done mark
+      __builtin_amdgcn_s_waitcnt(0);
+      __asm__ __volatile__("" ::: "memory");
+      if (__lane_id() == 0) {
+        (void)__hip_atomic_exchange(&fc.flag()[u], kClsDone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        atomicAdd(&fc.gdone()[u / kClsGroup], 1u);
+      }
+      return;
+    }
+  }
+  while (wave_rmw_read(&fc.flag()[u]) != kClsDone) __builtin_amdgcn_s_sleep(4);
+}
+
+// Every unit of segment s classified.  The classify-ahead assignment has
+// claimed them (normally done by now): lane k reads group k's done counter
+// (a segment is at most 64 groups for kClsSegs = 8 and 2^30 messages... and
+// more groups take more rounds); after a while help, 64 flags at a time (a
+// unit no wave claimed is classified here, one being classified is waited
+// for).  Wave-uniform.
+constexpr u32 kClsSpin = 64;
+template <class In>
+__device__ inline void cls_segment(const In& in, const FuseCls& fc, u32 s, u32 n, u32* ctr) {
+  const u32 cnt = cls_seg_units(fc, s);
+  if (!cnt) return;
+  const u32 u0 = s * fc.seg_units;
+  const u32 g0 = u0 / kClsGroup, ng = (cnt + kClsGroup - 1) / kClsGroup;
+  for (u32 spin = 0;; ++spin) {
+    bool all = true;
+    for (u32 k0 = 0; k0 < ng; k0 += 64) {
+      const u32 k = k0 + __lane_id();
+      const u32 want = k < ng ? min(kClsGroup, cnt - k * kClsGroup) : 0u;
+      const u32 got = k < ng ? rmw_read(&fc.gdone()[g0 + k]) : 0u;
+      all &= __ballot(got < want) == 0;
+    }
+    if (all) return;
+    if (spin >= kClsSpin) break;
+    __builtin_amdgcn_s_sleep(8);
+  }
+  for (u32 k0 = 0; k0 < cnt; k0 += 64) {
+    const u32 k = k0 + __lane_id();
+    const u32 f = k < cnt ? rmw_read(&fc.flag()[u0 + k]) : kClsDone;
+    u64 m = __ballot(f != kClsDone);
+    while (m) {
+      const u32 q = (u32)__ffsll((long long)m) - 1;
+      cls_claim(in, fc, u0 + k0 + q, n, ctr);
+      m &= m - 1;
+    }
+  }
+}
+
+// Classify-ahead on entering segment s: the units of segment s+1 are dealt to
+// the grid's waves by wave index (no shared ticket counter).
+template <class In>
+__device__ inline void cls_ahead(const In& in, const FuseCls& fc, u32 s, u32 n, u32* ctr, u32 wid,
+                                 u32 nwaves) {
+  if (s + 1 >= kClsSegs) return;
+  const u32 cnt = cls_seg_units(fc, s + 1);
+  for (u32 k = wid; k < cnt; k += nwaves) cls_claim(in, fc, (s + 1) * fc.seg_units + k, n, ctr);
+}
+
 template <class In>
 __global__ __launch_bounds__(kFastBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_receive_fast(
     In in, u32 n, Table T, Sharded miss, u32* ctr,
-    const HotHdr* __restrict__ hot, const HotEntry* __restrict__ hot_dir) {
+    const HotHdr* __restrict__ hot, const HotEntry* __restrict__ hot_dir, FuseCls fc) {
   __shared__ u32 hslot[kHotLds];        // directory index + 1 (0 = empty)
   __shared__ u64 htag[kHotMax], hw0[kHotMax], hw1[kHotMax], hw2[kHotMax];
   __shared__ u32 hrec[kHotMax], haoff[kHotMax];
@@ -860,11 +1020,16 @@ __global__ __launch_bounds__(kFastBlock) __attribute__((amdgpu_waves_per_eu(8, 8
   __shared__ u64 hmax[3][kHotMax];      // per-workgroup maxima (elapsed biased by 2^63)
   __shared__ u32 hhits;
 
-  // Gate (k_classify ran before): only the clean prefix is applied, the
-  // messages before the first dirty one (ctr[kCtrDirty]) and before the first
-  // malformed datagram (ctr[5]); none: ~0.
+  // Gate (k_classify ran before, over segment 0 only when fc.on): only the
+  // clean prefix is applied, the messages before the first dirty one
+  // (ctr[kCtrDirty]) and before the first malformed datagram (ctr[5]); none:
+  // ~0.  With fc.on, `lim` falls further as the segments are classified.
+  const u32 n_in = n;
   n = min(n, min(ctr[5], ctr[kCtrDirty]));
   if (n == 0) return;
+  u32 lim = n;
+  const u32 seg_chunks = fc.seg_units * (kClsUnit / 64);
+  u32 vseg = fc.pre - 1;   // segments <= vseg are classified
   const u32 nh = hot ? min(hot->n, kHotMax) : 0u;
   for (u32 j = threadIdx.x; j < kHotLds; j += kFastBlock) hslot[j] = 0;
   for (u32 j = threadIdx.x; j < kHotMax; j += kFastBlock) {
@@ -892,12 +1057,27 @@ __global__ __launch_bounds__(kFastBlock) __attribute__((amdgpu_waves_per_eu(8, 8
   // arrive meanwhile.
   // wave-uniform (in SGPRs): the chunk index, its shard of the miss list
   u32 chunk = blockIdx.x * kWaves + __builtin_amdgcn_readfirstlane(threadIdx.x / 64);
+  const u32 wid = chunk;   // the wave's index in the grid
+  if constexpr (In::kSoa)
+    if (fc.on) cls_ahead(in, fc, vseg, n_in, ctr, wid, cstride);   // the first segment k_classify left
   typename In::Pre pre{};
   if (chunk < nchunks) pre = in.pre(min(chunk * 64 + lane, n - 1));
   for (; chunk < nchunks; chunk += cstride) {
+    if (In::kSoa && fc.on) {
+      const u32 sg = chunk / seg_chunks;
+      if (sg > vseg) {
+        for (u32 x = vseg + 1; x <= sg; ++x) {
+          cls_ahead(in, fc, x, n_in, ctr, wid, cstride);
+          cls_segment(in, fc, x, n_in, ctr);
+        }
+        vseg = sg;
+        lim = min(lim, wave_rmw_read(&ctr[kCtrDirty]));
+      }
+      if (chunk * 64 >= lim) break;   // past the first dirty message
+    }
     const u32 tid = chunk * 64 + lane;
-    const bool valid = tid < n;
-    const u32 i = valid ? tid : n - 1;
+    const bool valid = tid < lim;
+    const u32 i = tid < n ? tid : n - 1;
     // round 2: the name words and replica fields
     u64 off, w0, w1, w2, ra, rt;
     u32 len;
@@ -3041,6 +3221,10 @@ constexpr u16 kRouteHot = 0x8000;   // route code: combined into hot entry (low 
 #define PHIP_ROUTE_UNROLL 2
 #endif
 constexpr u32 kRU = PHIP_ROUTE_UNROLL;   // chunks of 64 messages per wave step
+#ifndef PHIP_ROUTE_COUNT_UNROLL
+#define PHIP_ROUTE_COUNT_UNROLL 2
+#endif
+constexpr u32 kRUC = PHIP_ROUTE_COUNT_UNROLL;   // k_route_count's (it holds less per message)
 
 __device__ inline u32 owner_of_hash(u64 h, u32 world) {
   return (u32)(((h >> 32) * (u64)world) >> 32);
@@ -3115,11 +3299,20 @@ __global__ void k_route_dir_build(const u32* __restrict__ ckeys, const u32* __re
   dir[idx] = RouteHot{nm.h, nm.w0, nm.w1, owner_of_hash(nm.h, world), 0};
 }
 
-struct RouteLds {   // the hot directory in LDS, open-addressed by name hash
-  u32 slot[kHotLds];   // entry + 1 (0 = empty)
+// The hot directory in LDS, open-addressed by name hash at a quarter load:
+// each slot holds the entry + 1 (low 16 bits) and 16 bits of the hash, so a
+// probe is one LDS read and a name that is not hot (most of a batch) ends
+// after ~1.2 slots (k_route_count probed a half-full table of bare indices,
+// two LDS reads a step, the wave waiting for its longest chain).
+constexpr u32 kRouteLds = 2048;
+static_assert(kRouteLds >= 4 * kRouteHotMax && kRouteHotMax < 0xFFFF, "route directory load");
+struct RouteLds {
+  u32 slot[kRouteLds];   // (hash >> 48) << 16 | (entry + 1); 0 = empty
   u64 h[kRouteHotMax], w0[kRouteHotMax], w1[kRouteHotMax];
   u32 owner[kRouteHotMax];
 };
+
+__device__ inline u32 route_home(u64 h) { return (u32)(h ^ (h >> 29)) & (kRouteLds - 1); }
 
 // Entries used by this launch: none without a directory or on a dirty batch.
 __device__ inline u32 route_hot_n(const HotHdr* hot, const u32* ctr) {
@@ -3127,21 +3320,25 @@ __device__ inline u32 route_hot_n(const HotHdr* hot, const u32* ctr) {
 }
 
 __device__ inline void route_lds_load(RouteLds& L, const RouteHot* dir, u32 nh) {
-  for (u32 j = threadIdx.x; j < kHotLds; j += kRouteBlock) L.slot[j] = 0;
+  for (u32 j = threadIdx.x; j < kRouteLds; j += kRouteBlock) L.slot[j] = 0;
   __syncthreads();
   for (u32 j = threadIdx.x; j < nh; j += kRouteBlock) {
     const RouteHot d = dir[j];
     L.h[j] = d.h; L.w0[j] = d.w0; L.w1[j] = d.w1; L.owner[j] = d.owner;
-    u32 hs = hot_home(d.h);
-    while (atomicCAS(&L.slot[hs], 0u, j + 1) != 0) hs = (hs + 1) & (kHotLds - 1);
+    const u32 v = (u32)(d.h >> 48) << 16 | (j + 1);
+    u32 hs = route_home(d.h);
+    while (atomicCAS(&L.slot[hs], 0u, v) != 0) hs = (hs + 1) & (kRouteLds - 1);
   }
 }
 
 __device__ inline int route_hot_find(const RouteLds& L, const Name& nm) {
-  for (u32 hs = hot_home(nm.h);; hs = (hs + 1) & (kHotLds - 1)) {
-    const u32 e = L.slot[hs];
-    if (!e) return -1;
-    if (L.h[e - 1] == nm.h && L.w0[e - 1] == nm.w0 && L.w1[e - 1] == nm.w1) return (int)e - 1;
+  const u32 tag = (u32)(nm.h >> 48);
+  for (u32 hs = route_home(nm.h);; hs = (hs + 1) & (kRouteLds - 1)) {
+    const u32 v = L.slot[hs];
+    if (!v) return -1;
+    const u32 e = v & 0xFFFFu;
+    if ((v >> 16) == tag && L.h[e - 1] == nm.h && L.w0[e - 1] == nm.w0 && L.w1[e - 1] == nm.w1)
+      return (int)e - 1;
   }
 }
 
@@ -3195,23 +3392,23 @@ __global__ __launch_bounds__(kRouteBlock) void k_route_count(
   const u32 wave = threadIdx.x / 64, lane = threadIdx.x & 63;
   const u32 tile = blockIdx.x * kRouteWaves + wave;
   const u64 t0 = (u64)tile * span, t1 = min((u64)n, t0 + span);
-  // kRU chunks of 64 per step, their loads issued together (the loads of one
+  // kRUC chunks of 64 per step, their loads issued together (the loads of one
   // message depend on each other; those of different chunks do not)
-  for (u64 b0 = t0; b0 < t1; b0 += 64 * kRU) {
-    u32 o[kRU], len[kRU];
-    int hidx[kRU];
-    bool valid[kRU];
-    u64 off[kRU], w0[kRU], w1[kRU], w2[kRU];
+  for (u64 b0 = t0; b0 < t1; b0 += 64 * kRUC) {
+    u32 o[kRUC], len[kRUC];
+    int hidx[kRUC];
+    bool valid[kRUC];
+    u64 off[kRUC], w0[kRUC], w1[kRUC], w2[kRUC];
 #pragma unroll
-    for (u32 u = 0; u < kRU; ++u) {
+    for (u32 u = 0; u < kRUC; ++u) {
       const u64 i = b0 + u * 64 + lane;
       valid[u] = i < t1;
       src.template get<true>((u32)(valid[u] ? i : t0), off[u], len[u]);
     }
 #pragma unroll
-    for (u32 u = 0; u < kRU; ++u) load_words3<true>(src.blob, off[u], len[u], w0[u], w1[u], w2[u]);
+    for (u32 u = 0; u < kRUC; ++u) load_words3<true>(src.blob, off[u], len[u], w0[u], w1[u], w2[u]);
 #pragma unroll
-    for (u32 u = 0; u < kRU; ++u) {
+    for (u32 u = 0; u < kRUC; ++u) {
       const u64 i = b0 + u * 64 + lane;
       Name nm;
       if (len[u] <= kShortName) short_name(w0[u], w1[u], w2[u], off[u], len[u], nm);
@@ -3226,7 +3423,7 @@ __global__ __launch_bounds__(kRouteBlock) void k_route_count(
       if (hidx[u] >= 0) hit[hidx[u]] = 1;
     }
 #pragma unroll
-    for (u32 u = 0; u < kRU; ++u) {   // the wave's own row: LDS atomics, no cross-lane loop
+    for (u32 u = 0; u < kRUC; ++u) {   // the wave's own row: LDS atomics, no cross-lane loop
       if (valid[u] && hidx[u] < 0) {
         atomicAdd(&wc[wave][o[u]], 1u);
         atomicAdd(&wb[wave][o[u]], len[u]);
@@ -3340,8 +3537,84 @@ __device__ inline void route_place_packed(bool take, u32 o, u32 len, u32* run, u
   }
 }
 
+// Short names (<= 16 bytes) reach out_names as whole dwords.  A chunk's
+// names are staged by owner in the wave's LDS buffer at the byte alignment
+// they have in out_names, and the dwords the chunk completes are stored with
+// one dword store each (byte stores of 64 lanes scattered over 8 owners made
+// the scatter L2-request bound).  Per owner (lane o < world):
+//   t0   the owner's first byte of this run of the tile (bytes before it in
+//        its first dword belong to the tile before: stored one by one)
+//   pend the dword holding the run's end, not yet complete: carried to the
+//        next chunk, stored byte by byte at the end of the tile
+// A chunk with a longer name takes the byte path (route_names_bytes) after a
+// flush, and the next chunk starts a new run.
+constexpr u32 kStageWords = (64 * 16) / 4 + 2 * kRouteMaxWorld;
+
+__device__ inline void route_store_bytes(u8* out, u32 from, u32 to, u32 word_start, u32 word) {
+  for (u32 x = from; x < to; ++x) out[x] = (u8)(word >> (8 * (x - word_start)));
+}
+
+// Flush of the carried partial dwords (lane o: owner o's run ends at `be`).
+__device__ inline void route_flush_pend(u8* out, u32 world, u32 be, u32 t0, u32 pend) {
+  const u32 lane = __lane_id();
+  if (lane < world && (be & 3)) {
+    const u32 ws = be & ~3u;
+    route_store_bytes(out, max(ws, t0), be, ws, pend);
+  }
+}
+
+// The staged path for one chunk.  All 64 lanes active.  bo / be: lane o's
+// owner run [bo, be) in out_names for this chunk; plain lanes carry a name of
+// len <= 16 bytes (n0, n1) for owner o at byte dby.
+__device__ inline void route_names_staged(u8* __restrict__ out, u32* stg, u32 world, bool plain, u32 o,
+                                          u32 len, u32 dby, u64 n0, u64 n1, u32 bo, u32 be, u32 t0,
+                                          u32& pend) {
+  const u32 lane = __lane_id();
+  const u32 so = be - bo, lead = bo & 3u;
+  const u32 dcnt = (lane < world && so) ? (lead + so + 3) >> 2 : 0u;
+  const u32 pstart = wave_incl_sum(dcnt) - dcnt;   // dwords, exclusive over owners
+  const u32 total = (u32)__builtin_amdgcn_readlane((int)(pstart + dcnt), 63);
+  if (dcnt && lead) stg[pstart] = pend;   // the run's first dword: bytes before bo
+  const u32 oo = o & 63u;
+  const u32 ps_o = (u32)__shfl((int)pstart, (int)oo), bo_o = (u32)__shfl((int)bo, (int)oo);
+  if (plain) {
+    u8* sb = reinterpret_cast<u8*>(stg);
+    const u32 p = ps_o * 4 + (bo_o & 3u) + (dby - bo_o);
+#pragma unroll
+    for (u32 k = 0; k < 16; ++k)
+      if (k < len) sb[p + k] = (u8)((k < 8 ? n0 >> (8 * k) : n1 >> (8 * (k - 8))) & 0xFFu);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  u32* outw = reinterpret_cast<u32*>(out);
+  for (u32 tb = 0; tb < total; tb += 64) {   // uniform: every lane takes part in the shuffles
+    const u32 t = tb + lane;
+    // owner of staged dword t: the last owner with a run whose dwords start at or before t
+    u32 w = 0;
+    for (u32 x = 0; x < world; ++x) {
+      const u32 sx = (u32)__builtin_amdgcn_readlane((int)pstart, (int)x);
+      const u32 dx = (u32)__builtin_amdgcn_readlane((int)dcnt, (int)x);
+      if (dx && sx <= t) w = x;
+    }
+    const u32 bw = (u32)__shfl((int)bo, (int)w), ew = (u32)__shfl((int)be, (int)w);
+    const u32 tw = (u32)__shfl((int)t0, (int)w), sw = (u32)__shfl((int)pstart, (int)w);
+    const u32 gdw = (bw >> 2) + (t - sw);
+    const u32 word = stg[min(t, total - 1)];
+    if (t < total && 4 * gdw + 4 <= ew) {   // complete
+      if (4 * gdw >= tw) outw[gdw] = word;
+      else route_store_bytes(out, tw, 4 * gdw + 4, 4 * gdw, word);   // the tile's first dword
+    }
+  }
+  // the carried dword: lane o keeps the one holding its run's end
+  if (dcnt && (be & 3u)) pend = stg[pstart + dcnt - 1];
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();   // stg is rewritten by the next chunk
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 template <class Src>
-__global__ __launch_bounds__(kRouteBlock) void k_route_scatter(
+__global__ __launch_bounds__(kRouteBlock) __attribute__((amdgpu_waves_per_eu(6, 6))) void k_route_scatter(
     Src src, const uint64_t* __restrict__ a, const uint64_t* __restrict__ t,
     const int64_t* __restrict__ e, u32 n, u32 span, u32 world, u32 ntile,
     const HotHdr* __restrict__ hot, const RouteHot* __restrict__ dir, const u32* __restrict__ ctr,
@@ -3352,6 +3625,7 @@ __global__ __launch_bounds__(kRouteBlock) void k_route_scatter(
   __shared__ u32 run[kRouteWaves][kRouteMaxWorld], runb[kRouteWaves][kRouteMaxWorld];
   __shared__ u64 hmax[3][kRouteHotMax];
   __shared__ u32 hit[kRouteHotMax];
+  __shared__ u32 nstage[kRouteWaves][kStageWords];
   const u32 nh = route_hot_n(hot, ctr);
   const u32 wave = threadIdx.x / 64, lane = threadIdx.x & 63;
   const u32 tile = blockIdx.x * kRouteWaves + wave;
@@ -3365,6 +3639,9 @@ __global__ __launch_bounds__(kRouteBlock) void k_route_scatter(
   route_lds_load(L, dir, nh);
   __syncthreads();
   const u64 t0 = (u64)tile * span, t1 = min((u64)n, t0 + span);
+  u32* stg = nstage[wave];
+  // per owner lane: the run's start in this tile and the carried dword
+  u32 rt0 = lane < world ? runb[wave][lane] : 0u, pend = 0;
   for (u64 b0 = t0; b0 < t1; b0 += 64 * kRU) {
     u32 c[kRU], len[kRU];
     u64 off[kRU], va[kRU], vt[kRU], w0[kRU], w1[kRU], w2[kRU];
@@ -3395,6 +3672,7 @@ __global__ __launch_bounds__(kRouteBlock) void k_route_scatter(
         if (ee > hmax[2][j]) atomicMax(&hmax[2][j], ee);
         hit[j] = 1;
       }
+      const u32 bo = lane < world ? runb[wave][lane] : 0u;   // owner runs before this chunk
       u32 dst = 0, dby = 0;
       const u32 pl = plain ? len[u] : 0u;
       if (world <= 8 && !__ballot(pl > 255))
@@ -3403,23 +3681,35 @@ __global__ __launch_bounds__(kRouteBlock) void k_route_scatter(
         route_place_packed<4, 8>(plain, c[u], pl, run[wave], runb[wave], dst, dby);
       else
         route_place(plain, c[u], pl, run[wave], runb[wave], dst, dby);
-      if (!plain) continue;
-      out_lens[dst] = len[u];
-      out_a[dst] = va[u];
-      out_t[dst] = vt[u];
-      out_e[dst] = ve[u];
-      if (len[u] <= 16) {   // bytes from the words already in registers
-        const u32 sh = (u32)(off[u] & 7) * 8;
-        const u64 n0 = sh ? (w0[u] >> sh) | (w1[u] << (64 - sh)) : w0[u];
-        const u64 n1 = sh ? (w1[u] >> sh) | (w2[u] << (64 - sh)) : w1[u];
+      const u32 be = lane < world ? runb[wave][lane] : 0u;
+      if (plain) {
+        out_lens[dst] = len[u];
+        out_a[dst] = va[u];
+        out_t[dst] = vt[u];
+        out_e[dst] = ve[u];
+      }
+      const u32 sh = (u32)(off[u] & 7) * 8;
+      const u64 n0 = sh ? (w0[u] >> sh) | (w1[u] << (64 - sh)) : w0[u];
+      const u64 n1 = sh ? (w1[u] >> sh) | (w2[u] << (64 - sh)) : w1[u];
+      if (!__ballot(plain && len[u] > 16)) {
+        route_names_staged(out_names, stg, world, plain, c[u], len[u], dby, n0, n1, bo, be, rt0, pend);
+      } else {   // a longer name: flush, bytes, and a new run from here
+        route_flush_pend(out_names, world, bo, rt0, pend);
+        if (plain) {
+          if (len[u] <= 16) {
 #pragma unroll
-        for (u32 k = 0; k < 16; ++k)
-          if (k < len[u]) out_names[dby + k] = (u8)((k < 8 ? n0 >> (8 * k) : n1 >> (8 * (k - 8))) & 0xFFu);
-      } else {
-        for (u32 k = 0; k < len[u]; ++k) out_names[dby + k] = src.blob[off[u] + k];
+            for (u32 k = 0; k < 16; ++k)
+              if (k < len[u]) out_names[dby + k] = (u8)((k < 8 ? n0 >> (8 * k) : n1 >> (8 * (k - 8))) & 0xFFu);
+          } else {
+            for (u32 k = 0; k < len[u]; ++k) out_names[dby + k] = src.blob[off[u] + k];
+          }
+        }
+        rt0 = be;
+        pend = 0;
       }
     }
   }
+  route_flush_pend(out_names, world, lane < world ? runb[wave][lane] : 0u, rt0, pend);
   __syncthreads();
   if (wave != kRouteWaves - 1 || !nh) return;
   // The workgroup's combined messages, in directory order, after this tile.

@@ -94,6 +94,62 @@ def test_c2_full_size_vs_oracle(env):
     repo.close()
 
 
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("first", [None, 3_000_000, 5_500_000, 9_000_001, 16_000_000])
+def test_receive_fused_classification_vs_oracle(env, first, monkeypatch):
+    """A 2^24-message batch: k_classify covers its first two of eight
+    segments, k_receive_fast classifies the rest as it goes (FuseCls).  The
+    first incast / -0.0 sits in a pre-classified segment, in a fused one, in
+    the last one, or nowhere; more follow it.  Statuses (merged on the fast
+    path before it, ordered from it on, incast replies) and the table equal
+    the oracle's."""
+    torch, bench, pa = env
+    monkeypatch.setenv("PHIP_FUSE_CLS", "1")
+    dev = torch.device("cuda", 0)
+    K, n, L = 1_000_000, 1 << 24, 21
+    s = torch.cuda.Stream(dev)
+    with torch.cuda.stream(s):
+        gen = torch.Generator(device=dev).manual_seed(77 + (first or 0))
+        repo, o = _seeded(torch, bench, pa, dev, K, L, s)
+        ids = bench.zipf_ids(torch, gen, n, K, 1.1, dev)
+        blob, offs = bench.names_for_ids(torch, ids)
+        del ids
+        a, t, e = bench.replica_states(torch, gen, n, 0, dev)
+        if first is not None:
+            rng = np.random.default_rng(first)
+            later = np.sort(rng.integers(first + 1, n, 30))
+            neg0 = -(1 << 63)                                            # -0.0's bits
+            if first % 2:
+                a[first] = neg0
+            else:
+                a[first] = 0; t[first] = 0; e[first] = 0                  # incast
+            for k, j in enumerate(later.tolist()):
+                if k % 2:
+                    t[j] = neg0
+                else:
+                    a[j] = 0; t[j] = 0; e[j] = 0
+        status = torch.empty(n, dtype=torch.uint8, device=dev)
+        torch.cuda.synchronize()
+        repo.receive_soa(blob, a, t, e, T0, name_offs=offs, n=n, status=status, device=True)
+        torch.cuda.synchronize()
+        g_st = status.cpu().numpy()
+        blob_h, offs_h = blob.cpu().numpy(), offs.cpu().numpy().view(np.uint32)
+        a_h, t_h, e_h = (x.cpu().numpy() for x in (a, t, e))
+    del blob, offs, a, t, e, status
+    torch.cuda.empty_cache()
+    o_st = np.zeros(n, np.uint8)
+    o.L.orc_receive_soa(o.h, blob_h, offs_h, n, a_h.view(np.uint64), t_h.view(np.uint64), e_h, T0,
+                        o_st, np.empty(n, np.uint64), np.empty(n, np.uint64), np.empty(n, np.int64))
+    bad = np.flatnonzero(g_st != o_st)
+    assert bad.size == 0, (bad[:5], g_st[bad[:5]], o_st[bad[:5]])
+    if first is not None:
+        assert (o_st[:first] == 1).all()
+        if first % 2 == 0:   # an incast is not merged (a -0.0 replica is)
+            assert (o_st[first] & 0x7F) != 1
+    _check_table(repo, o)
+    repo.close()
+
+
 @pytest.mark.timeout(900)
 @pytest.mark.parametrize("clock", ["below", "ahead"])
 def test_c3_full_size_vs_oracle(env, clock):

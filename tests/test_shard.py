@@ -323,12 +323,16 @@ def test_ae_join_equals_local_max_apply(R, B):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("world,huge", [(1, False), (3, False), (8, False), (8, True), (16, False),
-                                        (16, True), (64, False)])
+                                        (16, True), (64, False), (1, "short"), (3, "short"),
+                                        (8, "short"), (64, "short"), (8, "sparse")])
 def test_route_pack_is_stable_owner_partition(world, huge):
     """phip_route_pack on cuda:0: owner-major, per-owner original order,
     names/lengths/states moved intact, per-owner counts and byte totals.
     World <= 16 places by packed DPP scans, larger worlds (and waves holding
-    a name over 255 bytes: `huge`) by the per-owner ballot rounds."""
+    a name over 255 bytes: `huge`) by the per-owner ballot rounds.  "short":
+    every name of 1-16 bytes (all at every byte alignment), so every chunk
+    takes the LDS-staged dword path; "sparse": a long name in one message of
+    5000, so staged chunks and byte-path chunks alternate within a tile."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     import ctypes as C
@@ -338,9 +342,14 @@ def test_route_pack_is_stable_owner_partition(world, huge):
     rng = np.random.default_rng(world)
     n = 200_003
     ids = rng.integers(0, 50_000, n)
-    names = [(b"b%d" % i) if i % 7 else (b"a-long-bucket-name-%d-%s" % (i, b"x" * (i % 40)))
-             for i in ids]
-    if huge:
+    if huge == "short":
+        names = [(b"%x" % i)[: 1 + k % 16].ljust(1 + k % 16, b"z") for k, i in enumerate(ids)]
+    elif huge == "sparse":
+        names = [(b"b%d" % i) if k % 5000 else (b"a-long-bucket-name-%d" % i) for k, i in enumerate(ids)]
+    else:
+        names = [(b"b%d" % i) if i % 7 else (b"a-long-bucket-name-%d-%s" % (i, b"x" * (i % 40)))
+                 for i in ids]
+    if huge is True:
         names = [nm + b"y" * 300 if k % 5003 == 0 else nm for k, nm in enumerate(names)]
     blob_np, offs_np = names_blob(names)
     a = rng.integers(0, 1 << 62, n).astype(np.int64)
