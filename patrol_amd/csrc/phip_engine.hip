@@ -2249,17 +2249,15 @@ int phip_route_pack(phip_handle* h, const phip_msgs* m, uint32_t world, uint8_t*
   u32* bbase = cbase + cells;
   u16* code = (u16*)(bbase + cells);
   NamesOffs src{m->names, m->name_offs};
-  // Sender-side combine: classify (clean domain only), then the hot names of
-  // a strided sample, counted by name hash.
+  // Sender-side combine (clean batches only): the hot names of a strided
+  // sample, counted by name hash.
   const HotHdr* hot = nullptr;
   const RouteHot* dir = nullptr;
   if ((flags & PHIP_ROUTE_COMBINE) && n >= kRouteMinBatch) {
+    // (no classification pass: k_route_count reads the replica fields and
+    // records the first dirty message; a dirty batch is counted again without
+    // combining)
     if ((rc = reset_ctr(h))) return rc;
-    {
-      Launch l(h, "k_route_classify");
-      k_route_classify<<<grid_for(n), kBlock, 0, h->stream>>>(m->added, m->taken, m->elapsed, n,
-                                                              h->ctr);
-    }
     constexpr size_t kCnt = size_t(1) << kHotCntBits;
     const size_t zero_bytes = 3 * kCnt * sizeof(u32) + kHotHist * sizeof(u32) + sizeof(HotHdr);
     u8* hb;
@@ -2290,7 +2288,11 @@ int phip_route_pack(phip_handle* h, const phip_msgs* m, uint32_t world, uint8_t*
     Launch l(h, "k_route_count");
     k_route_count<NamesOffs><<<nblk, kRouteBlock, 0, h->stream>>>(
         src, m->added, m->taken, m->elapsed, n, span, world, ntile, hot, dir, h->ctr, code, cnt,
-        bytes);
+        bytes, hot ? kRouteCombine : kRoutePlain);
+    if (hot)
+      k_route_count<NamesOffs><<<nblk, kRouteBlock, 0, h->stream>>>(
+          src, m->added, m->taken, m->elapsed, n, span, world, ntile, hot, dir, h->ctr, code, cnt,
+          bytes, kRouteRecount);
   }
   HIPCHK(h, hipGetLastError());
   size_t tb = 0;

@@ -3342,47 +3342,24 @@ __device__ inline int route_hot_find(const RouteLds& L, const Name& nm) {
   }
 }
 
-// A message that may be combined: some field > 0 (module comment).
-__device__ inline bool route_combinable(u64 ab, u64 tb, i64 e) {
-  return as_f64(ab) > 0.0 || as_f64(tb) > 0.0 || e > 0;
-}
-
-// Classification for the combine: the first dirty message (as k_classify)
-// and, in ctr[kCtrNonPos], whether any message is not combinable, so that
-// k_route_count reads the replica fields only when some is.
-constexpr u32 kCtrNonPos = 13;
-__global__ __launch_bounds__(kBlock) void k_route_classify(const uint64_t* __restrict__ a,
-                                                           const uint64_t* __restrict__ t,
-                                                           const int64_t* __restrict__ e, u32 n,
-                                                           u32* ctr) {
-  const u32 i = blockIdx.x * kBlock + threadIdx.x;
-  bool dirty = false, nonpos = false;
-  if (i < n) {
-    const u64 ab = __builtin_nontemporal_load(a + i), tb = __builtin_nontemporal_load(t + i);
-    const bool ap = as_f64(ab) > 0.0, tp = as_f64(tb) > 0.0;
-    if (!ap && !tp) {   // elapsed matters only then
-      const i64 ev = e[i];
-      dirty = replica_dirty(ab, tb, ev);
-      nonpos = ev <= 0;
-    } else {
-      dirty = ab == kSign || tb == kSign;
-    }
-  }
-  note_dirty(dirty, i, ctr);
-  if (__ballot(nonpos) && __lane_id() == 0) ctr[kCtrNonPos] = 1;
-}
+constexpr u32 kRoutePlain = 0, kRouteCombine = 1, kRouteRecount = 2;   // k_route_count modes
 
 template <class Src>
 __global__ __launch_bounds__(kRouteBlock) void k_route_count(
     Src src, const uint64_t* __restrict__ a, const uint64_t* __restrict__ t,
     const int64_t* __restrict__ e, u32 n, u32 span, u32 world, u32 ntile,
-    const HotHdr* __restrict__ hot, const RouteHot* __restrict__ dir, const u32* __restrict__ ctr,
-    u16* __restrict__ code, u32* __restrict__ cnt, u32* __restrict__ bytes) {
+    const HotHdr* __restrict__ hot, const RouteHot* __restrict__ dir, u32* __restrict__ ctr,
+    u16* __restrict__ code, u32* __restrict__ cnt, u32* __restrict__ bytes, u32 mode) {
   __shared__ RouteLds L;
   __shared__ u32 wc[kRouteWaves][kRouteMaxWorld], wb[kRouteWaves][kRouteMaxWorld];
   __shared__ u32 hit[kRouteHotMax];
-  const u32 nh = route_hot_n(hot, ctr);
-  const bool nonpos = nh && ctr[kCtrNonPos];
+  // mode kRouteCombine: combine hot names and classify the batch on the way
+  // (the replica fields are read here: no k_route_classify pass); mode
+  // kRouteRecount: count again without combining if that found a dirty
+  // message (nothing to do on a clean batch); mode kRoutePlain: no combine.
+  if (mode == kRouteRecount && ctr[kCtrDirty] == ~0u) return;
+  const bool comb = mode == kRouteCombine;
+  const u32 nh = comb ? route_hot_n(hot, ctr) : 0u;
   for (u32 j = threadIdx.x; j < kRouteWaves * kRouteMaxWorld; j += kRouteBlock) {
     (&wc[0][0])[j] = 0; (&wb[0][0])[j] = 0;
   }
@@ -3399,11 +3376,14 @@ __global__ __launch_bounds__(kRouteBlock) void k_route_count(
     int hidx[kRUC];
     bool valid[kRUC];
     u64 off[kRUC], w0[kRUC], w1[kRUC], w2[kRUC];
+    u64 ra[kRUC], rt[kRUC];
 #pragma unroll
     for (u32 u = 0; u < kRUC; ++u) {
       const u64 i = b0 + u * 64 + lane;
       valid[u] = i < t1;
-      src.template get<true>((u32)(valid[u] ? i : t0), off[u], len[u]);
+      const u32 ic = (u32)(valid[u] ? i : t0);
+      src.template get<true>(ic, off[u], len[u]);
+      if (comb) { ra[u] = ld<true>(a + ic); rt[u] = ld<true>(t + ic); }
     }
 #pragma unroll
     for (u32 u = 0; u < kRUC; ++u) load_words3<true>(src.blob, off[u], len[u], w0[u], w1[u], w2[u]);
@@ -3415,10 +3395,18 @@ __global__ __launch_bounds__(kRouteBlock) void k_route_count(
       else load_name_wide<true>(src.blob, off[u], len[u], nm);
       o[u] = owner_of_hash(nm.h, world);
       hidx[u] = -1;
-      if (valid[u] && nh && len[u] <= kShortName) {
-        hidx[u] = route_hot_find(L, nm);
-        if (hidx[u] >= 0 && nonpos && !route_combinable(a[i], t[i], e[i])) hidx[u] = -1;
+      bool ok = true;   // combinable: some field > 0 (elapsed read only when neither float is)
+      if (comb) {
+        const bool fpos = as_f64(ra[u]) > 0.0 || as_f64(rt[u]) > 0.0;
+        bool dirty = ra[u] == kSign || rt[u] == kSign;
+        if (valid[u] && !fpos) {
+          const i64 ev = e[i];
+          ok = ev > 0;
+          dirty |= replica_dirty(ra[u], rt[u], ev);
+        }
+        note_dirty(valid[u] && dirty, (u32)i, ctr);
       }
+      if (valid[u] && nh && ok && len[u] <= kShortName) hidx[u] = route_hot_find(L, nm);
       if (valid[u]) code[i] = hidx[u] >= 0 ? (u16)(kRouteHot | (u32)hidx[u]) : (u16)o[u];
       if (hidx[u] >= 0) hit[hidx[u]] = 1;
     }

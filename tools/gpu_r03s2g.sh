@@ -6,10 +6,10 @@ set -o pipefail
 O=gpurun_out/r03s2g
 mkdir -p $O
 export TMPDIR=/tmp
-timeout -k 10 900 python -u -m pytest -x -q --timeout 600 --timeout-method thread tests/test_fullsize.py -m gpu -k "fused or c2" > $O/tests1.log 2>&1 || { tail -30 $O/tests1.log; exit 1; }
+timeout -k 10 900 python -u -m pytest -x -q --timeout 600 --timeout-method thread tests/test_fullsize.py -m gpu -k "fused" > $O/tests1.log 2>&1 || { tail -30 $O/tests1.log; exit 1; }
 tail -2 $O/tests1.log
-timeout -k 10 900 python -u -m pytest -x -q --timeout 600 --timeout-method thread tests/test_gpu_parity.py tests/test_shard.py tests/test_group.py tests/test_ingest.py -m gpu -k "receive or route or group or hot or ring or wire or datagram" > $O/tests2.log 2>&1 || { tail -30 $O/tests2.log; exit 1; }
-tail -2 $O/tests2.log
+true
+true
 run() {  # run TAG ENV...
   local tag=$1; shift
   env "$@" timeout -k 10 300 python -u bench.py --no-cpu --no-routed --steps 10 > $O/c2_$tag.json 2> $O/c2_$tag.err || { tail -20 $O/c2_$tag.err; exit 1; }
