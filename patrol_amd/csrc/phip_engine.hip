@@ -639,8 +639,19 @@ int fast_apply(phip_handle* h, In in, HotSrc hsrc, u32 n, u8* status, u32* first
   if ((rc = join_hot(h, hot))) return rc;
   {
     Launch l(h, "k_receive_fast");
-    k_receive_fast<In><<<fast_grid(h, n), kFastBlock, 0, h->stream>>>(
-        in, n, table(h), msh, h->ctr, hot, hot_dir, fc);
+    // (the classifying instantiation only when it runs: its extra state costs
+    // the plain kernel scalar registers, ~2% on C2)
+    bool fused = false;
+    if constexpr (In::kSoa) {
+      if (fc.on) {
+        k_receive_fast<In, true><<<fast_grid(h, n), kFastBlock, 0, h->stream>>>(
+            in, n, table(h), msh, h->ctr, hot, hot_dir, fc);
+        fused = true;
+      }
+    }
+    if (!fused)
+      k_receive_fast<In, false><<<fast_grid(h, n), kFastBlock, 0, h->stream>>>(
+          in, n, table(h), msh, h->ctr, hot, hot_dir, fc);
   }
   HIPCHK(h, hipGetLastError());
   if ((rc = pack_sharded(h, msh, 2, miss, nmiss))) return rc;

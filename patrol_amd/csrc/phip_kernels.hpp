@@ -491,7 +491,7 @@ constexpr u32 kRouteHotMax = 512;
 static_assert(kHotLds * 2 >= kRouteHotMax * 3 && kHotLds * 2 >= kHotMax * 3, "LDS lookup load");
 constexpr u32 kHotCntBits = 18;       // sample count table: 2^18 (slot+1, count) pairs
 constexpr u32 kHotSampleMax = 1u << 17;   // samples per batch (half the count table)
-constexpr u32 kHotSamplePerBlock = 256;   // one sample a thread: 512 workgroups (the chain runs beside segment 0's classification)
+constexpr u32 kHotSamplePerBlock = 1024;   // 128 workgroups: the chain runs beside k_classify on stream2 (512 one-sample workgroups queued behind its blocks and delayed the join)
 constexpr u32 kHotHist = 4096;        // histogram bins of sample counts
 constexpr u32 kHotMinCount = 8;       // sample hits for a bucket to qualify
 // Smaller batches skip the directory.  2^16, not larger: a skewed batch of a
@@ -1009,7 +1009,7 @@ __device__ inline void cls_ahead(const In& in, const FuseCls& fc, u32 s, u32 n, 
   for (u32 k = wid; k < cnt; k += nwaves) cls_claim(in, fc, (s + 1) * fc.seg_units + k, n, ctr);
 }
 
-template <class In>
+template <class In, bool kFuse = false>   // kFuse: in-kernel classification (FuseCls)
 __global__ __launch_bounds__(kFastBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_receive_fast(
     In in, u32 n, Table T, Sharded miss, u32* ctr,
     const HotHdr* __restrict__ hot, const HotEntry* __restrict__ hot_dir, FuseCls fc) {
@@ -1058,12 +1058,12 @@ __global__ __launch_bounds__(kFastBlock) __attribute__((amdgpu_waves_per_eu(8, 8
   // wave-uniform (in SGPRs): the chunk index, its shard of the miss list
   u32 chunk = blockIdx.x * kWaves + __builtin_amdgcn_readfirstlane(threadIdx.x / 64);
   const u32 wid = chunk;   // the wave's index in the grid
-  if constexpr (In::kSoa)
+  if constexpr (In::kSoa && kFuse)
     if (fc.on) cls_ahead(in, fc, vseg, n_in, ctr, wid, cstride);   // the first segment k_classify left
   typename In::Pre pre{};
   if (chunk < nchunks) pre = in.pre(min(chunk * 64 + lane, n - 1));
   for (; chunk < nchunks; chunk += cstride) {
-    if (In::kSoa && fc.on) {
+    if (In::kSoa && kFuse && fc.on) {
       const u32 sg = chunk / seg_chunks;
       if (sg > vseg) {
         for (u32 x = vseg + 1; x <= sg; ++x) {
@@ -1151,9 +1151,17 @@ __global__ __launch_bounds__(kFastBlock) __attribute__((amdgpu_waves_per_eu(8, 8
         }
         if (pr == kFound) {
           Rec* r = &T.recs[s];
+#if defined(PHIP_FAST_COLD_NOATOM)   // timing experiments only: drops the cold merges
+          (void)r;
+#elif defined(PHIP_FAST_COLD_STORE)  // timing experiments only: plain stores, racy
+          if (ea > cur.added) r->added = ea;
+          if (et > cur.taken) r->taken = et;
+          if (ee > ((u64)cur.elapsed ^ kSign)) r->elapsed = (i64)(ee ^ kSign);
+#else
           if (ea > cur.added) atomicMax(&r->added, ea);
           if (et > cur.taken) atomicMax(&r->taken, et);
           if (ee > ((u64)cur.elapsed ^ kSign)) atomicMax(&r->elapsed, (i64)(ee ^ kSign));
+#endif
         } else {
           missed = true;
           if (pr == kFull) atomicOr(&ctr[8], 1u);
