@@ -992,9 +992,6 @@ int ordered(phip_handle* h, Src src, u32 n, const OpView& ov, const OutView& ow)
   }
   u32 nlong = h->ctr_host[6], nhuge = h->ctr_host[9];
   if ((rc = pack_join.join())) return rc;
-  static const u32 tsplit =
-      getenv("PHIP_THREAD_SPLIT") ? std::min(100, std::max(0, atoi(getenv("PHIP_THREAD_SPLIT")))) : 0;
-  const u32 nseg_s2 = nhuge ? (u32)((u64)nseg * tsplit / 100) : 0u;
   // Different segments touch different slots, so the folds may overlap: the
   // hot-bucket workgroups run on stream2 beside the wave and thread folds.
   if (nhuge) {
@@ -1089,18 +1086,6 @@ int ordered(phip_handle* h, Src src, u32 n, const OpView& ov, const OutView& ow)
     if ((rc = chain(0, hsplit, h->stream2, h->ev_gather, "k_gather_huge", "k_fold_block",
                     "k_huge_outputs")))
       return rc;
-    // (PHIP_THREAD_SPLIT=P, A/B: the thread folds of the first P% of the
-    // segments on stream2 after its huge outputs, the rest on the main
-    // stream after the wave folds; different segments, different slots)
-    if (nseg_s2) {
-      Launch l(h, "k_fold_thread2", h->stream2);
-#define PHIP_FOLD_THREAD2(M)                                                                  \
-  k_fold_thread<M><<<grid_for(nseg_s2), kBlock, 0, h->stream2>>>(uslot, sstart, scnt, nseg_s2, \
-                                                                 sidx, opr, h->recs, ow)
-      PHIP_OUT_DISPATCH(out_mask(ow), PHIP_FOLD_THREAD2);
-#undef PHIP_FOLD_THREAD2
-      HIPCHK(h, hipGetLastError());
-    }
     if (split) {
       if ((rc = chain(hsplit, nhuge, h->stream3, h->ev_gather3, "k_gather_huge2", "k_fold_block2",
                       "k_huge_outputs2")))
@@ -1152,16 +1137,12 @@ int ordered(phip_handle* h, Src src, u32 n, const OpView& ov, const OutView& ow)
   }
   {
     Launch l(h, "k_fold_thread");
-    const u32 nrest = nseg - nseg_s2;
-    if (nrest) {
-#define PHIP_FOLD_THREAD(M)                                                                    \
-  k_fold_thread<M><<<grid_for(nrest), kBlock, 0, h->stream>>>(uslot + nseg_s2, sstart + nseg_s2, \
-                                                              scnt + nseg_s2, nrest, sidx, opr,  \
-                                                              h->recs, ow)
-      PHIP_OUT_DISPATCH(out_mask(ow), PHIP_FOLD_THREAD);
+#define PHIP_FOLD_THREAD(M)                                                            \
+  k_fold_thread<M><<<grid_for(nseg), kBlock, 0, h->stream>>>(uslot, sstart, scnt, nseg, sidx, \
+                                                             opr, h->recs, ow)
+    PHIP_OUT_DISPATCH(out_mask(ow), PHIP_FOLD_THREAD);
 #undef PHIP_FOLD_THREAD
-      HIPCHK(h, hipGetLastError());
-    }
+    HIPCHK(h, hipGetLastError());
   }
   if (nhuge) {
     HIPCHK(h, hipEventRecord(h->ev_join, h->stream2));
