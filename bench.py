@@ -45,6 +45,8 @@ T0 = 1_700_000_000_000_000_000
 BYTES_PER_MERGE = 88     # msg 32 + slot key 8 + state read 24 + state write 24
 HBM_PEAK_GBS = 8000.0    # MI355X_MICROARCH.md chip-level parameters (spec)
 DOMINANT = "k_receive_fast"
+CPU_REPS = 5                 # median of 5 runs per thread count
+CPU_SLOW_SAMPLE = 2_000_000  # messages per run at 1 and nproc (> 16) threads
 
 
 def parse():
@@ -94,6 +96,13 @@ def parse():
                    help="c2: pad every bucket name to this many bytes (e.g. 32: the arena path)")
     p.add_argument("--no-routed", action="store_true",
                    help="c2: skip the owner_routed (strong-scaling) object")
+    p.add_argument("--no-c4", action="store_true", help="c2: skip the c4 object")
+    p.add_argument("--no-ae", action="store_true", help="c2: skip the anti_entropy object")
+    p.add_argument("--c4-keys", type=int, default=125_000_000,
+                   help="c4 object: buckets per GPU (SURVEY C4: 1B over 8 GPUs)")
+    p.add_argument("--c4-messages", type=int, default=100_000_000,
+                   help="c4 object: messages per GPU per step")
+    p.add_argument("--c4-log2-slots", type=int, default=28)
     p.add_argument("--route-path", default="c", choices=["c", "torch"],
                    help="owner routing / anti-entropy through the C shard group (phip_group_*, "
                         "RCCL inside libpatrolhip) or the torch.distributed glue; the gloo "
@@ -222,27 +231,41 @@ def cpu_baseline(args, K, ids_host):
     ids = ids_host[:n]
     blob, offs = names_for_ids(torch, ids, args.name_len)
     g = torch.Generator().manual_seed(args.seed + 99)
-    a, t, e = replica_states(torch, g, n, 0, "cpu")
     blob_np, offs_np = blob.numpy(), offs.numpy().astype(np.uint32)
-    a_np, t_np, e_np = a.numpy().view(np.uint64), t.numpy().view(np.uint64), e.numpy()
+    counts = cpu_thread_counts(args)
+    repo = seeded()
     runs = {}
-    for th in cpu_thread_counts(args):
-        # one goroutine (the reference's Receive loop, repo.go:54) gets a
-        # smaller sample: it runs at a few M merges/s
-        m = n if th > 1 else min(n, 2_000_000)
-        repo = seeded()
-        secs = L.orc_bench_receive(repo.h, blob_np, offs_np, m, a_np, t_np, e_np, T0, th)
-        del repo
-        runs[th] = dict(value=m / secs, messages=m)
-    top = max(runs)
-    return dict(value=runs[top]["value"], unit="merges/s", cores=top, kind="port", **host_cpu(),
-                sample=f"{n} of the step-0 messages (Zipf {args.zipf} over {K} buckets) into a "
-                       f"{K}-bucket Go-structured map, {top} threads (nproc); 1 thread: "
-                       f"{runs[min(runs)]['messages']} messages",
-                by_threads={str(k): v["value"] for k, v in sorted(runs.items())},
-                single_thread=dict(value=runs[min(runs)]["value"],
-                                   sample=f"{runs[min(runs)]['messages']} messages, 1 thread (the "
-                                          "reference's single Receive goroutine)"))
+    shift = 0
+    for th in counts:
+        # a bounded sample per run: 16 threads merge ~5-8 M/s, but one
+        # goroutine (the reference's Receive loop, repo.go:54) and the
+        # lock-bound nproc case ~0.5-3 M/s
+        m = n if 1 < th <= 16 else min(n, CPU_SLOW_SAMPLE)
+        vals = []
+        for _ in range(CPU_REPS):
+            # every run applies states above the previous run's, so each is a
+            # first application (every touched bucket grows), as on the GPU
+            a, t, e = replica_states(torch, g, m, shift, "cpu")
+            shift += 1
+            secs = L.orc_bench_receive(repo.h, blob_np, offs_np, m, a.numpy().view(np.uint64),
+                                       t.numpy().view(np.uint64), e.numpy(), T0, th)
+            vals.append(m / secs)
+        runs[th] = dict(median=float(np.median(vals)), min=float(min(vals)),
+                        max=float(max(vals)), runs=CPU_REPS, messages=m)
+    del repo
+    top, one = max(runs), min(runs)
+    return dict(value=runs[top]["median"], unit="merges/s", cores=top, kind="port", **host_cpu(),
+                what="Go-semantics C++ restatement (oracle/patrol_oracle.cc: LocalRepo's "
+                     "RWMutex map + per-bucket mutex, ReplicatedRepo.Receive's loop body)",
+                sample=f"the first {runs[top]['messages']} step-0 messages (Zipf {args.zipf} over "
+                       f"{K} buckets) into a {K}-bucket map, {top} threads (nproc); median of "
+                       f"{CPU_REPS} runs, each run's states above the last",
+                by_threads={str(k): v for k, v in sorted(runs.items())},
+                single_thread=dict(value=runs[one]["median"], min=runs[one]["min"],
+                                   max=runs[one]["max"],
+                                   sample=f"{runs[one]['messages']} messages, 1 thread (the "
+                                          f"reference's single Receive goroutine), median of "
+                                          f"{CPU_REPS}"))
 
 
 def host_cpu():
@@ -263,21 +286,27 @@ def host_cpu():
     return {"host_nproc": os.cpu_count(), "host_affinity_cpus": affinity, "host_cpu_model": model}
 
 
-def pmc_traffic(key, workload, kernel):
+def pmc_traffic(key, workload, kernel, build):
     """HBM bytes per launch of the dominant kernel from the committed PMC
     summary (profiles/pmc_summary.json, produced by tools/pmc_workloads.py):
-    one entry per workload key (c1..c5), used when it was measured on the
-    same workload description and the same dominant kernel(s)."""
+    one entry per workload key (c1..c5), used only when it was measured on
+    the same workload description, the same dominant kernel(s) and the same
+    library build (phip_build_id, a hash of the sources) as this run.
+    Returns (bytes or None, the entry's source or why it was not used)."""
     path = os.path.join(ROOT, "profiles", "pmc_summary.json")
     try:
         with open(path) as f:
-            d = json.load(f)
-        d = d.get(key, d) if "kernel" not in d else d
-        if d.get("workload") == workload and d.get("kernel") == kernel:
-            return d.get("hbm_bytes_per_step")
+            d = json.load(f).get(key)
     except (OSError, ValueError, AttributeError):
-        pass
-    return None
+        return None, "no profiles/pmc_summary.json"
+    if not d:
+        return None, f"no PMC entry for {key}"
+    if d.get("workload") != workload or d.get("kernel") != kernel:
+        return None, f"PMC entry for {key} measured another workload or kernel"
+    if d.get("build_id") != build:
+        return None, (f"PMC entry for {key} is from build {d.get('build_id')}, this run is "
+                      f"build {build}")
+    return d.get("hbm_bytes_per_step"), d.get("source")
 
 
 def datagrams(torch, blob, offs, a, t, e):
@@ -361,27 +390,41 @@ def run_c3(args, torch, dev, repo, rank, K, base, gen):
         sb_np, so_np = sb.numpy(), so.numpy().astype(np.uint32)
         now, a, t, e = steps[args.warmup]
         cols = [x[:m].cpu().numpy() for x in (kind, now, freq, per, cnt, a, t, e)]
+        orepo = O.Repo()
+        L.orc_repo_seed(orepo.h, kb_np, ko_np, K, z, z, np.zeros(K, np.int64),
+                        np.full(K, T0, np.int64))
         runs = {}
+        rep = 0
         for th in cpu_thread_counts(args):
-            orepo = O.Repo()
-            L.orc_repo_seed(orepo.h, kb_np, ko_np, K, z, z, np.zeros(K, np.int64),
-                            np.full(K, T0, np.int64))
-            st = np.zeros(m, np.uint8)
-            rm = np.zeros(m, np.uint64)
+            mm = m if 1 < th <= 16 else min(m, CPU_SLOW_SAMPLE // 2)
+            st = np.zeros(mm, np.uint8)
+            rm = np.zeros(mm, np.uint64)
             f = L.orc_bench_mixed if th == 1 else L.orc_bench_mixed_mt
             extra = () if th == 1 else (th,)
-            secs = f(orepo.h, cols[0], sb_np, so_np, m, cols[1], cols[2], cols[3],
-                     cols[4].view(np.uint64), cols[5].view(np.uint64), cols[6].view(np.uint64),
-                     cols[7], st, rm, *extra)
-            del orepo
-            runs[th] = m / secs
-        top = max(runs)
-        return dict(value=runs[top], unit="ops/s", cores=top, kind="port", **host_cpu(),
-                    sample=f"first {m} ops of the timed stream (Zipf {args.zipf} over {K} "
-                           f"buckets) through the Go-structured restatement, {top} threads "
-                           "(nproc; each bucket's ops on one worker, in stream order)",
+            vals = []
+            for _ in range(CPU_REPS):
+                # each run one second of clock later than the last (Takes refill)
+                nw = cols[1][:mm] + rep * 10**9
+                rep += 1
+                secs = f(orepo.h, cols[0], sb_np, so_np, mm, nw, cols[2], cols[3],
+                         cols[4].view(np.uint64), cols[5].view(np.uint64), cols[6].view(np.uint64),
+                         cols[7], st, rm, *extra)
+                vals.append(mm / secs)
+            runs[th] = dict(median=float(np.median(vals)), min=float(min(vals)),
+                            max=float(max(vals)), runs=CPU_REPS, ops=mm)
+        del orepo
+        top, one = max(runs), min(runs)
+        return dict(value=runs[top]["median"], unit="ops/s", cores=top, kind="port", **host_cpu(),
+                    what="Go-semantics C++ restatement (oracle/patrol_oracle.cc)",
+                    sample=f"first {runs[top]['ops']} ops of the timed stream (Zipf {args.zipf} "
+                           f"over {K} buckets), {top} threads (nproc; each bucket's ops on one "
+                           f"worker, in stream order); median of {CPU_REPS} runs, each run's "
+                           "clock 1 s after the last",
                     by_threads={str(k): v for k, v in sorted(runs.items())},
-                    single_thread=dict(value=runs[min(runs)], sample=f"the same {m} ops, 1 thread"))
+                    single_thread=dict(value=runs[one]["median"], min=runs[one]["min"],
+                                       max=runs[one]["max"],
+                                       sample=f"{runs[one]['ops']} ops, 1 thread, median of "
+                                              f"{CPU_REPS}"))
     return n, step, cpu
 
 
@@ -486,8 +529,9 @@ def open_group(args, dist, repo, rank, world):
     return patrol_amd.GPUGroup.open_rank(repo, obj[0], world, rank)
 
 
-ROUTED_LIMIT_S = 300   # the owner-routed leg's watchdog (main())
-ROUTED_TIMEOUT_EXIT = 3   # exit status when the watchdog fired
+LEG_LIMIT_S = 300   # each extra leg's watchdog (main())
+LEG_TIMEOUT_EXIT = 3   # exit status when a watchdog fired
+LEG_FAILED_EXIT = 4    # exit status when a leg raised or its in-run parity check failed
 
 
 def run_routed(args, torch, dist, dev, local, rank, world):
@@ -573,6 +617,300 @@ def run_routed(args, torch, dist, dev, local, rank, world):
                  "sender-side combine, RCCL all-to-all of the split sizes, grouped send/recv "
                  "per column, phip_receive_soa on the owner)" if group is not None else
                  "phip_route_pack + torch.distributed all-to-all per column + phip_receive_soa"),
+    }
+
+
+def _coll(dist, args, torch, x, op="max"):
+    """all_reduce (max / sum) of a device tensor; the gloo rehearsal backend
+    reduces a host copy.  Checker plumbing only (never on a timed path)."""
+    red = dist.ReduceOp.MAX if op == "max" else dist.ReduceOp.SUM
+    if args.dist_backend == "nccl":
+        dist.all_reduce(x, op=red)
+        return x
+    h = x.cpu()
+    dist.all_reduce(h, op=red)
+    return h.to(x.device)
+
+
+def _all_gather(dist, args, torch, x):
+    """all_gather of equal-shaped device tensors -> [world, *x.shape]."""
+    world = dist.get_world_size()
+    src = x if args.dist_backend == "nccl" else x.cpu()
+    out = [torch.empty_like(src) for _ in range(world)]
+    dist.all_gather(out, src)
+    return torch.stack(out).to(x.device)
+
+
+def _timed_steps(dist, torch, dev, args, warmup, steps, step):
+    """warmup untimed, then `steps` timed between barrier + synchronize on both
+    sides; the max over ranks of the elapsed seconds."""
+    for j in range(warmup):
+        step(j)
+    torch.cuda.synchronize()
+    dist.barrier()
+    t0 = time.perf_counter()
+    for j in range(warmup, warmup + steps):
+        step(j)
+    torch.cuda.synchronize()
+    dist.barrier()
+    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+    return float(_coll(dist, args, torch, el, "max").item())
+
+
+def zipf_mult(K):
+    """zipf_ids' rank -> id multiplier (a unit mod K)."""
+    mult = 2654435761 % K or 1
+    while np.gcd(mult, K) != 1:
+        mult += 1
+    return mult
+
+
+C4_CHUNK = 1 << 27   # seeding: bucket ids named and hashed per chunk
+
+
+def run_c4_leg(args, torch, dist, dev, local, rank, world):
+    """The `c4` object (BASELINE configs[3]): 125M buckets per
+    GPU (2^28 slots; 1B buckets at N = 8) hash-sharded by name, every rank
+    drawing 100M messages per step Zipf(1.1) over ALL buckets, and every step
+    one phip_group_receive: phip_route_pack with the sender-side combine,
+    the exchange of the split sizes and the grouped per-peer send/recv over
+    RCCL, and the owner's phip_receive_soa (repo.go:54-92 sharded).  At one
+    GPU the exchange runs as a send/recv pair to the member itself
+    (PHIP_GROUP_RCCL_SELF), so the line measures the same routed pipeline at
+    every N.  Weak scaling: value = all ranks' messages per step x steps /
+    max-over-ranks time.
+
+    `verified` (in-run parity): a sample of 2^16 uniform bucket ids plus the
+    512 hottest Zipf ranks, identical on every rank.  The expectation is an
+    independent max-reduce of every message every rank generated for those
+    ids over all the steps it applied (torch scatter_reduce amax, then an
+    all-reduce MAX over ranks: the states are clean-domain positive floats
+    and the table starts at zero, so Bucket.Merge, bucket.go:240-263, is the
+    field-wise max).  Each owner reads its sampled buckets back through the
+    C ABI (phip_export_datagrams, MarshalBinary words); the reads are summed
+    over ranks (exactly one owner per id) and must equal the expectation,
+    every sampled id found exactly once."""
+    import patrol_amd
+    from patrol_amd import shard
+    K, n, L = args.c4_keys, args.c4_messages, args.c4_log2_slots
+    rehearsal = args.dist_backend != "nccl"
+    if rehearsal:   # gloo moves every column through host memory: a smaller batch
+        n = min(n, 10_000_000)
+    KT = K * world
+    warm, steps = max(1, min(args.warmup, 2)), max(1, min(args.steps, 10))
+    gen = torch.Generator(device=dev).manual_seed(args.seed + 101 + 7919 * rank)
+    repo = patrol_amd.GPURepo(device=local, log2_slots=L, arena_bytes=1 << 20)
+    repo.use_torch_stream()
+    t_setup = time.perf_counter()
+    owned = 0
+    for c0 in range(0, KT, C4_CHUNK):
+        keys = torch.arange(c0, min(KT, c0 + C4_CHUNK), dtype=torch.int64, device=dev)
+        if world > 1:
+            kb, ko = names_for_ids(torch, keys)
+            keys = keys[shard.owner_of(shard.hash_names(kb, ko, repo), world) == rank]
+            del kb, ko
+        kb, ko = names_for_ids(torch, keys)
+        st = torch.zeros((keys.numel(), 4), dtype=torch.int64, device=dev)
+        st[:, 3] = T0
+        torch.cuda.synchronize()
+        repo.seed_device(kb, ko, st, keys.numel())
+        owned += keys.numel()
+        del keys, kb, ko, st
+    assert len(repo) == owned
+    ids = zipf_ids(torch, gen, n, KT, args.zipf, dev)
+    blob, offs = names_for_ids(torch, ids)
+    batches = [replica_states(torch, gen, n, j, dev) for j in range(warm + steps)]
+    torch.cuda.synchronize()
+    group = open_group(args, dist, repo, rank, world)
+    merged = []
+
+    def step(j):
+        a, t, e = batches[j]
+        if group is not None:
+            _, got = group.receive([(blob, offs, a, t, e)], T0 + j, combine=True,
+                                   rccl_self=world == 1)
+            k = got[0]
+        else:
+            rb, ro, ra, rt, re = shard.route_messages_native(blob, offs, a, t, e, repo,
+                                                             combine=True)
+            k = ro.numel() - 1
+            if k:
+                repo.receive_soa(rb, ra, rt, re, T0 + j, name_offs=ro, n=k, device=True)
+        merged.append(k)
+    t_setup = time.perf_counter() - t_setup
+    el = _timed_steps(dist, torch, dev, args, warm, steps, step)
+
+    # ---- in-run parity on a sample (outside the timed region)
+    vg = torch.Generator(device=dev).manual_seed(args.seed + 555)   # the same on every rank
+    hot = (torch.arange(512, dtype=torch.int64, device=dev) * zipf_mult(KT)) % KT
+    samp = torch.unique(torch.cat([torch.randint(0, KT, (1 << 16,), device=dev, generator=vg),
+                                   hot]))
+    S = samp.numel()
+    pos = torch.searchsorted(samp, ids).clamp_(max=S - 1)
+    hit = samp[pos] == ids
+    pos = pos[hit]
+    want = torch.zeros((3, S), dtype=torch.int64, device=dev)
+    for a, t, e in batches:
+        for f, x in enumerate((a, t, e)):
+            want[f].scatter_reduce_(0, pos, x[hit], reduce="amax", include_self=True)
+    want = _coll(dist, args, torch, want, "max")
+    sb, so = names_for_ids(torch, samp)
+    mine = shard.owner_of(shard.hash_names(sb, so, repo), world) == rank
+    idx = torch.nonzero(mine).flatten()
+    got = torch.zeros((4, S), dtype=torch.int64, device=dev)
+    if idx.numel():
+        mb, mo = names_for_ids(torch, samp[idx])
+        ga, gt, ge, found = repo.export_states_device(mb, mo, idx.numel())
+        got[0, idx], got[1, idx], got[2, idx] = ga, gt, ge
+        got[3, idx] = found.to(torch.int64)
+    got = _coll(dist, args, torch, got, "sum")
+    found_once = bool((got[3] == 1).all())
+    bad = int((got[:3] != want).any(0).sum())
+    verified = found_once and bad == 0
+    tt = torch.tensor([float(np.mean(merged[warm:])), float(owned)], dtype=torch.float64,
+                      device=dev)
+    sm = _coll(dist, args, torch, tt.clone(), "sum")
+    mx = _coll(dist, args, torch, tt.clone(), "max")
+    if group is not None:
+        group.close()
+    repo.close()
+    del batches, blob, offs, ids
+    return {
+        "metric": "bucket-state merges/sec, owner-routed C4 (messages routed by owner and merged)",
+        "value": world * n * steps / el, "unit": "merges/s", "scaling": "weak", "n_gpus": world,
+        "steps": steps, "warmup": warm, "ms_per_step": el / steps * 1e3,
+        "workload": (f"C4: {K} buckets per GPU ({KT} total, 2^{L} slots per GPU) hash-sharded by "
+                     f"name; {n} messages per GPU per step Zipf({args.zipf}) over all buckets"),
+        "buckets_total": int(sm[1]), "buckets_max_gpu": int(mx[1]),
+        "messages_per_step_per_gpu": n, "merged_per_step_total": float(sm[0]),
+        "merged_per_step_max_gpu": float(mx[0]), "sender_combine": True,
+        "step": ("phip_group_receive: phip_route_pack (owner partition + sender-side combine), "
+                 "RCCL all-to-all of the split sizes, grouped ncclSend/ncclRecv per peer and "
+                 "column, phip_receive_soa on the owner" +
+                 ("; one GPU: the segment goes to the member itself through ncclSend/ncclRecv "
+                  "(PHIP_GROUP_RCCL_SELF)" if world == 1 and group is not None else "")
+                 if group is not None else
+                 "gloo rehearsal: phip_route_pack + torch.distributed all-to-all per column + "
+                 "phip_receive_soa"),
+        "rehearsal": rehearsal,
+        "setup_s": t_setup,
+        "verified": verified,
+        "verify": {"sampled_buckets": S, "found_exactly_once": found_once, "mismatched": bad,
+                   "reference": "independent per-id max-reduce of every rank's messages over all "
+                                "applied steps (torch scatter_reduce amax + all-reduce MAX)"},
+    }
+
+
+def run_ae_leg(args, torch, dist, dev, local, rank, world):
+    """The `anti_entropy` object (BASELINE configs[4]): R = 8
+    simulated replicas per GPU of 2^24 buckets each (64 replicas at N = 8).
+    A round = fresh local writes to 1% of every replica's buckets, then one
+    phip_group_anti_entropy: the local join, RCCL all-reduce(MAX) of the
+    [3, B] E-coded join over all GPUs, and the apply (one GPU: the fused
+    k_ae_join, nothing to exchange).  value = replica-buckets brought to the
+    cluster-wide join per second over all ranks.
+
+    `verified`: one more round after the timed ones.  Right before its
+    anti-entropy call a sample of 4096 buckets is read from every replica
+    of every rank (all-gather).  Go's Bucket.Merge (bucket.go:240-263) of
+    all of them, for these clean-domain states (positive floats, no NaN or
+    -0.0: the merge is the float max, elapsed the int max), is computed in
+    float64 by torch; afterwards every replica of every rank must hold
+    exactly those bits, and every replica must equal replica 0 on every
+    bucket with one checksum across ranks (converged)."""
+    from patrol_amd import shard
+    import patrol_amd
+    R, B = args.replicas, args.buckets
+    warm, steps = max(1, min(args.warmup, 2)), max(1, min(args.steps, 10))
+    gen = torch.Generator(device=dev).manual_seed(args.seed + 202 + 7919 * rank)
+    repo = patrol_amd.GPURepo(device=local, log2_slots=10)
+    repo.use_torch_stream()
+    taken = torch.randint(0, 10**6, (R, B), device=dev, generator=gen).to(torch.float64)
+    added = taken + torch.rand((R, B), dtype=torch.float64, device=dev, generator=gen) * 100.0
+    reps = torch.empty((R, 3, B), dtype=torch.int64, device=dev)
+    reps[:, 0] = shard.e_encode(added.view(torch.int64))
+    reps[:, 1] = shard.e_encode(taken.view(torch.int64))
+    reps[:, 2] = torch.randint(0, 1 << 40, (R, B), device=dev, generator=gen, dtype=torch.int64)
+    del taken, added
+    nw = max(1, int(B * args.writes))
+    rounds = []
+    for j in range(warm + steps + 1):
+        idx = torch.randint(0, B, (R, nw), device=dev, generator=gen) + \
+            torch.arange(R, device=dev).unsqueeze(1) * (3 * B)
+        rounds.append((idx.flatten(), torch.randint(1, 8, (R * nw,), device=dev, generator=gen),
+                       torch.randint(1, 10**6, (R * nw,), device=dev, generator=gen)))
+    flat = reps.view(-1)
+    torch.cuda.synchronize()
+    group = open_group(args, dist, repo, rank, world)
+
+    def writes(j):
+        idx, dt, de = rounds[j]
+        flat.index_add_(0, idx + B, dt)    # a local Take: taken grows by a few ulps
+        flat.index_add_(0, idx + 2 * B, de)
+
+    def exchange():
+        if group is not None:
+            group.anti_entropy([reps])
+        else:
+            shard.anti_entropy_native(reps, repo)
+
+    def step(j):
+        writes(j)
+        exchange()
+    el = _timed_steps(dist, torch, dev, args, warm, steps, step)
+
+    # ---- the verification round
+    writes(warm + steps)
+    vg = torch.Generator(device=dev).manual_seed(args.seed + 777)   # the same on every rank
+    samp = torch.randint(0, B, (4096,), device=dev, generator=vg)
+    before = _all_gather(dist, args, torch, reps[:, :, samp].contiguous())   # [W, R, 3, S]
+    torch.cuda.synchronize()
+    exchange()
+    torch.cuda.synchronize()
+    before = before.reshape(world * R, 3, -1)
+    fa = shard.e_decode(before[:, 0]).view(torch.float64).max(0).values
+    ft = shard.e_decode(before[:, 1]).view(torch.float64).max(0).values
+    fe = before[:, 2].max(0).values
+    after = reps[:, :, samp]
+    go = (bool((shard.e_decode(after[:, 0]) == fa.view(torch.int64)).all()) and
+          bool((shard.e_decode(after[:, 1]) == ft.view(torch.int64)).all()) and
+          bool((after[:, 2] == fe).all()))
+    conv = torch.tensor([int(bool((reps == reps[0:1]).all())), 0, 0], dtype=torch.int64,
+                        device=dev)
+    conv[1] = reps[0].sum(dtype=torch.int64)
+    conv[2] = -conv[1]
+    lo_hi = _coll(dist, args, torch, conv.clone(), "max")
+    cnt = _coll(dist, args, torch, conv[:1].clone(), "sum")
+    converged = int(cnt.item()) == world and int(lo_hi[1]) == -int(lo_hi[2])
+    go_all = _coll(dist, args, torch, torch.tensor([int(go)], dtype=torch.int64, device=dev), "sum")
+    go_ok = int(go_all.item()) == world
+    if group is not None:
+        group.close()
+    repo.close()
+    del reps, rounds
+    # the fused one-GPU join reads 24 B per replica-bucket; at N GPUs the
+    # local max reads R*24 + writes 24, the apply reads 24 + R*24 per bucket
+    bpo = 24.0 if world == 1 else (2 * R + 2) * 24 / R
+    step_s = el / steps
+    return {
+        "metric": "anti-entropy replica-bucket joins/sec (C5: all-reduce(max) over xGMI)",
+        "value": world * R * B * steps / el, "unit": "joins/s", "scaling": "weak",
+        "n_gpus": world, "steps": steps, "warmup": warm, "ms_per_step": step_s * 1e3,
+        "workload": (f"C5: {R} replicas/GPU ({R * world} total) x {B} buckets, {args.writes:g} of "
+                     "the buckets written per replica per round, one anti-entropy pass per round"),
+        "replicas_total": R * world, "allreduce_bytes": 3 * 8 * B,
+        "local_GBps": bpo * R * B / step_s / 1e9,
+        "step": ("phip_group_anti_entropy: " +
+                 ("fused local join k_ae_join (one GPU: nothing to exchange)" if world == 1 else
+                  "k_ae_local_max, ncclAllReduce(int64, MAX), k_ae_apply")
+                 if group is not None else
+                 "gloo rehearsal: phip_ae_local_max + torch all_reduce(MAX) + phip_ae_apply"),
+        "rehearsal": args.dist_backend != "nccl",
+        "verified": converged and go_ok, "converged": converged,
+        "verify": {"sampled_buckets": 4096, "replicas_checked": R * world, "go_merge_equal": go_ok,
+                   "reference": "float64 max of every replica's decoded added/taken and int max of "
+                                "elapsed, gathered from all ranks before the round (Go Merge of "
+                                "clean-domain states)"},
     }
 
 
@@ -894,7 +1232,8 @@ def main():
     # messages, so its algorithmic bytes count those
     n_roof = float(np.mean(c4_merged)) if args.workload == "c4" else n
     achieved = bpo * n_roof / (dom_ms / 1e3) / 1e9
-    traffic = pmc_traffic(args.workload if not c1 else "c1", workload, dom_name)
+    build = patrol_amd.build_id()
+    traffic, traffic_src = pmc_traffic(args.workload if not c1 else "c1", workload, dom_name, build)
     out = {
         "metric": metric,
         "value": total / el,
@@ -915,10 +1254,12 @@ def main():
                    "dist_backend": args.dist_backend if dist.is_initialized() else None},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "traffic_source": traffic_src,
                      "kernel": dom_name, "kernel_ms_per_step": dom_ms,
                      "launches_per_step": launches.get(dom_name, args.steps) / args.steps,
                      "algorithmic_bytes_per_step": bpo * n_roof},
         "kernels_ms": kms,
+        "build_id": build,
     }
     out["config"].update(extra)
     if rank == 0 and world == 1 and not args.no_cpu and args.workload == "c2":
@@ -939,37 +1280,51 @@ def main():
         repo._group.close()
     repo.close()
     if routed:
-        # the C2 batches are freed first: the owner-routed line has its own
+        # the C2 batches are freed first: every extra leg has its own
         del step
         if args.workload == "c2":
             del batches, blob, offs, ids
-        torch.cuda.synchronize()
-        torch.cuda.empty_cache()
-        # The routed leg is an extra object in the line: an error or a hang
-        # there (one rank failing inside a collective leaves the others
-        # waiting) must not cost the headline.  A watchdog on every rank
-        # prints the line without it and ends the process.
+        legs = [("owner_routed", run_routed)]
+        if not args.no_c4:
+            legs.append(("c4", run_c4_leg))
+        if not args.no_ae:
+            legs.append(("anti_entropy", run_ae_leg))
+        # Each extra leg is an object in the line: an error or a hang there
+        # (one rank failing inside a collective leaves the others waiting)
+        # must not cost the headline.  A watchdog on every rank prints the
+        # line without it and ends the process with a non-zero status.
         import threading
+        failed = False
+        for key, fn in legs:
+            torch.cuda.synchronize()
+            torch.cuda.empty_cache()
 
-        def give_up():
-            # the line still carries the headline, but the exit status says
-            # the routed leg hung (a driver or CI must be able to tell)
-            if rank == 0:
-                out["owner_routed"] = {"error": f"timed out after {ROUTED_LIMIT_S} s"}
-                print(json.dumps(out), file=json_out, flush=True)
-            os._exit(ROUTED_TIMEOUT_EXIT)
-        dog = threading.Timer(ROUTED_LIMIT_S, give_up)
-        dog.daemon = True
-        dog.start()
-        try:
-            out["owner_routed"] = run_routed(args, torch, dist, dev, local, rank, world)
-        except Exception as ex:
-            out["owner_routed"] = {"error": repr(ex)}
-        dog.cancel()
+            def give_up(key=key):
+                # the line still carries the headline, but the exit status says
+                # the leg hung (a driver or CI must be able to tell)
+                if rank == 0:
+                    out[key] = {"error": f"timed out after {LEG_LIMIT_S} s"}
+                    print(json.dumps(out), file=json_out, flush=True)
+                os._exit(LEG_TIMEOUT_EXIT)
+            dog = threading.Timer(LEG_LIMIT_S, give_up)
+            dog.daemon = True
+            dog.start()
+            try:
+                out[key] = fn(args, torch, dist, dev, local, rank, world)
+                if out[key].get("verified") is False:
+                    failed = True
+            except Exception as ex:
+                out[key] = {"error": repr(ex)}
+                failed = True
+            dog.cancel()
+        if failed:
+            print("bench.py: an extra leg failed or did not verify", file=sys.stderr)
     if rank == 0:
         print(json.dumps(out), file=json_out, flush=True)
     if dist.is_initialized():
         dist.destroy_process_group()
+    if routed and failed:
+        sys.exit(LEG_FAILED_EXIT)
 
 
 if __name__ == "__main__":

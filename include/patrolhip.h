@@ -103,6 +103,9 @@ enum {
                                      of a device copy, and a world-1 group exchanges through
                                      RCCL instead of merging its send buffers in place, so the
                                      per-peer RCCL exchange runs on a single GPU */
+#define PHIP_GROUP_SMALL_CHUNKS 0x8u /* phip_group_receive (testing): pipeline the exchange in
+                                        chunks of 4096 messages instead of 2^24, so that small
+                                        batches run many pack / exchange rounds */
 
 /* phip_config.flags */
 #define PHIP_CFG_NO_GROW 0x1u   /* refuse (PHIP_ERR_FULL / PHIP_ERR_ARENA) instead of growing */
@@ -198,12 +201,16 @@ typedef struct phip_results {
                                         unchanged by it: the unicast payload of an
                                         INCAST_REPLY (repo.go:86-90), and what
                                         GetBucket found or created (repo.go:189-211).
-                                  Not written for a merged replica (PHIP_ST_MERGED of
-                                  a RECEIVE op).                                    */
+                                  A merged replica (PHIP_ST_MERGED of a RECEIVE op)
+                                  has no reply state: its entry is all zeros.       */
 } phip_results;
 
 /* ---- lifecycle ---- */
 int phip_abi_version(void);
+/* 16 hex digits naming the library's sources (a hash of csrc/, this header
+ * and the Makefile taken when the library was built): counter profiles and
+ * bench lines record it, so a measurement can be tied to the code that ran. */
+const char* phip_build_id(void);
 int phip_open(const phip_config* cfg, phip_handle** out);
 void phip_close(phip_handle* h);
 const char* phip_last_error(const phip_handle* h);
@@ -498,10 +505,18 @@ phip_handle* phip_group_handle(phip_group* g, uint32_t i);
  * by owner (phip_route_pack; PHIP_ROUTE_COMBINE max-combines a clean batch's
  * hot names at the sender), the members exchange the packed segments (one
  * all-to-all of the split sizes, then grouped send/recv per column), and
- * every owner merges what it received, sources in rank order, each in its
- * order (phip_receive_soa, `now` for buckets it creates).  sent[i] /
+ * every owner merges what it received (phip_receive_soa, `now` for buckets
+ * it creates).  The pack and the exchange are pipelined by chunks of 2^24
+ * messages (the pack of chunk k+1 runs while chunk k travels); an owner
+ * receives chunk by chunk, sources in rank order within a chunk, every
+ * source's messages in their order (as peers' datagrams interleave in
+ * Patrol: per-bucket order from one source is kept).  Every member runs the
+ * longest batch's number of rounds (a shorter batch sends empty chunks).  sent[i] /
  * merged[i] (optional) receive the messages member i sent after the combine
- * and merged. */
+ * and merged.  A world of one (without PHIP_GROUP_RCCL_SELF) has nothing to
+ * route: the batch is merged as it came, PHIP_ROUTE_COMBINE is ignored (the
+ * fast path's hot directory does what the combine would) and sent / merged
+ * are the batch's raw message count. */
 int phip_group_receive(phip_group* g, const phip_msgs* batches, int64_t now, uint64_t* sent,
                        uint64_t* merged, uint32_t flags);
 /* Anti-entropy round over simulated replicas (BASELINE configs[4]):

@@ -5,7 +5,7 @@ include/patrolhip.h).  This package holds its sources (csrc/), the in-tree
 build (Makefile -> libpatrolhip.so) and a thin Python binding used by tests
 and bench.py.
 """
-from ._lib import EXPORTS, LIB_PATH, load  # noqa: F401
+from ._lib import EXPORTS, LIB_PATH, build_id, load  # noqa: F401
 from .engine import (BucketState, GPUGroup, GPURepo, PatrolHipError, Ring, TakeBatcher,  # noqa: F401
                      incast_replies, marshal, names_blob, parse_rate, udp_recv_batch,
                      udp_send_batch)

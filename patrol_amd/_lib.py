@@ -15,7 +15,7 @@ LIB_PATH = os.environ.get("PATROLHIP_LIB") or os.path.join(HERE, "libpatrolhip.s
 
 # Every symbol include/patrolhip.h declares (tests/test_abi.py checks both ways).
 EXPORTS = [
-    "phip_abi_version", "phip_open", "phip_close", "phip_last_error", "phip_flush", "phip_len",
+    "phip_abi_version", "phip_build_id", "phip_open", "phip_close", "phip_last_error", "phip_flush", "phip_len",
     "phip_capacity", "phip_seed", "phip_get", "phip_dump", "phip_receive_datagrams",
     "phip_receive_soa", "phip_upsert_soa", "phip_apply_mixed", "phip_take", "phip_parse_rate",
     "phip_marshal", "phip_api_take", "phip_last_timings", "phip_set_timing", "phip_last_stats", "phip_hash_names",
@@ -44,7 +44,9 @@ CFG_NO_SMALL = 0x2
 CFG_FIXED_SEED = 0x4
 ROUTE_COMBINE = 0x2
 GROUP_RCCL_SELF = 0x4
+GROUP_SMALL_CHUNKS = 0x8
 PACKET_SIZE = 256
+BUCKET_FIXED_SIZE = 25   # PHIP_BUCKET_FIXED_SIZE: added, taken, elapsed, name length
 
 
 class phip_config(C.Structure):
@@ -89,6 +91,11 @@ class phip_results(C.Structure):
 _lib = None
 
 
+def build_id() -> str:
+    """phip_build_id() of the loaded library (a hash of its sources)."""
+    return load().phip_build_id().decode()
+
+
 def load(path: str = LIB_PATH):
     """Load libpatrolhip.so (raises OSError if it was not built)."""
     global _lib
@@ -108,6 +115,7 @@ def load(path: str = LIB_PATH):
     L = C.CDLL(path)
     vp, u32, u64, i64 = C.c_void_p, C.c_uint32, C.c_uint64, C.c_int64
     L.phip_abi_version.restype = C.c_int
+    L.phip_build_id.restype = C.c_char_p
     L.phip_open.argtypes = [C.POINTER(phip_config), C.POINTER(vp)]
     L.phip_close.argtypes = [vp]
     L.phip_close.restype = None

@@ -60,7 +60,7 @@ enum BufId {
   B_SLOT, B_IDX, B_SSLOT, B_SIDX, B_USLOT, B_SCNT, B_SSTART, B_LONG, B_HUGE, B_TEMP, B_DUMP,
   B_OPS, B_HOFF, B_HOP, B_HVAL, B_RPOS, B_RST, B_RUNN, B_SEGEX, B_WOFF, B_SUMS, B_WRUN,
   B_WING, B_SEGXF, B_FOLDDBG, B_SMALL, B_HUGE2, B_LONG2,
-  B_STATES, B_NAME1, B_HOT, B_ROUTE, B_EXPORT, B_MSHARD, B_MSCNT, B_DEDUP, B_DSET, B_TSTATS, B_SEGT, B_FUSE,
+  B_STATES, B_NAME1, B_HOT, B_ROUTE, B_EXPORT, B_MSHARD, B_MSCNT, B_DEDUP, B_DSET, B_TSTATS, B_SEGT, B_RHOT,
   B_COUNT_
 };
 
@@ -392,14 +392,24 @@ int insert_names(phip_handle* h, Src src, u32* list, u32 nlist, const int64_t* n
   *n_claimed = 0;
   bool g = false;
   u64 bound = nlist;
+  // the names whose long-name arena bytes reserve() counts: the list, or its
+  // distinct names once they are known (one new long hot name listed by
+  // 65535 misses needs its bytes once)
+  const u32* blist = list;
+  u32 nb = nlist;
   if (!distinct && nlist > 1 && h->n_buckets + nlist > h->max_load) {
     u32 *dd, nd = 0;
     if ((rc = dedupe_names(h, src, list, nlist, &dd, &nd))) return rc;
     // names that share a 64-bit tag count once there: with full tags that is
-    // a birthday rarity; narrowed test tags keep the list's length
-    if (h->tag_mask == ~0ull) bound = nd;
+    // a birthday rarity; narrowed test tags keep the list's length (and the
+    // bytes of every listed name)
+    if (h->tag_mask == ~0ull) {
+      bound = nd;
+      blist = dd;
+      nb = nd;
+    }
   }
-  if ((rc = reserve(h, src, list, nlist, bound, &g))) return rc;
+  if ((rc = reserve(h, src, blist, nb, bound, &g))) return rc;
   if (grew) *grew = g;
   if ((rc = ensure(h, B_CSLOT, nlist, &cslot)) || (rc = ensure(h, B_CMSG, nlist, &cmsg)) ||
       (rc = ensure(h, B_RETRY, nlist, &retry)))
@@ -595,38 +605,13 @@ int fast_apply(phip_handle* h, In in, HotSrc hsrc, u32 n, u8* status, u32* first
   if (with_hot) HIPCHK(h, hipEventRecord(h->ev_fork, h->stream));
   if (with_hot && hot_first && (rc = fork_hot(h, hsrc, n, &hot, &hot_dir))) return rc;
   if (status) HIPCHK(h, hipMemsetAsync(status, PHIP_ST_MERGED, n, h->stream));
-  // A large decoded batch is classified in the fast kernel past its first
-  // fc.pre segments (FuseCls, phip_kernels.hpp); k_classify takes those
-  // beside the hot-directory chain.  Experimental: on with PHIP_FUSE_CLS=1
-  // (DESIGN.md §4, round 3).  (PHIP_NO_FUSE_CLS=1: k_classify over the
-  // whole batch first, for A/B; PHIP_CLS_PRE: segments classified before.)
-  FuseCls fc{};
-  u32 ncls = n;
-  if constexpr (In::kSoa) {
-    // (read per batch, so a test can switch it within one process)
-    const bool no_fuse = !getenv("PHIP_FUSE_CLS") || getenv("PHIP_NO_FUSE_CLS") != nullptr;
-    const u32 pre_env = getenv("PHIP_CLS_PRE") ? (u32)atoi(getenv("PHIP_CLS_PRE")) : 2u;
-    const u32 pre = std::max(1u, std::min(pre_env, kClsSegs));
-    if (!no_fuse && pre < kClsSegs && n >= kFuseClsMin &&
-        (((uintptr_t)in.ma | (uintptr_t)in.mt) & 15) == 0) {
-      const u32 nunits = (n + kClsUnit - 1) / kClsUnit;
-      const u32 seg_units =
-          ((nunits + kClsSegs - 1) / kClsSegs + kClsGroup - 1) / kClsGroup * kClsGroup;
-      const size_t words = (size_t)nunits + (nunits + kClsGroup - 1) / kClsGroup;
-      u32* fb;
-      if ((rc = ensure(h, B_FUSE, words, &fb))) return rc;
-      HIPCHK(h, hipMemsetAsync(fb, 0, words * sizeof(u32), h->stream));
-      fc = FuseCls{fb, seg_units, nunits, pre, 1};
-      ncls = (u32)std::min<u64>(n, (u64)pre * seg_units * kClsUnit);
-    }
-  }
   {
     Launch l(h, "k_classify");
     bool done = false;
     if constexpr (In::kSoa) {
       if ((((uintptr_t)in.ma | (uintptr_t)in.mt) & 15) == 0) {
-        k_classify_soa2<<<grid_for((ncls + 1) / 2), kBlock, 0, h->stream>>>(in.ma, in.mt, in.me,
-                                                                             ncls, h->ctr);
+        k_classify_soa2<<<grid_for((n + 1) / 2), kBlock, 0, h->stream>>>(in.ma, in.mt, in.me, n,
+                                                                          h->ctr);
         done = true;
       }
     }
@@ -639,19 +624,8 @@ int fast_apply(phip_handle* h, In in, HotSrc hsrc, u32 n, u8* status, u32* first
   if ((rc = join_hot(h, hot))) return rc;
   {
     Launch l(h, "k_receive_fast");
-    // (the classifying instantiation only when it runs: its extra state costs
-    // the plain kernel scalar registers, ~2% on C2)
-    bool fused = false;
-    if constexpr (In::kSoa) {
-      if (fc.on) {
-        k_receive_fast<In, true><<<fast_grid(h, n), kFastBlock, 0, h->stream>>>(
-            in, n, table(h), msh, h->ctr, hot, hot_dir, fc);
-        fused = true;
-      }
-    }
-    if (!fused)
-      k_receive_fast<In, false><<<fast_grid(h, n), kFastBlock, 0, h->stream>>>(
-          in, n, table(h), msh, h->ctr, hot, hot_dir, fc);
+    k_receive_fast<In><<<fast_grid(h, n), kFastBlock, 0, h->stream>>>(in, 0, n, table(h), msh,
+                                                                      h->ctr, hot, hot_dir);
   }
   HIPCHK(h, hipGetLastError());
   if ((rc = pack_sharded(h, msh, 2, miss, nmiss))) return rc;
@@ -911,31 +885,25 @@ int ordered(phip_handle* h, Src src, u32 n, const OpView& ov, const OutView& ow)
     HIPCHK(h, hipEventRecord(h->ev_pack, h->stream2));
     return PHIP_OK;
   };
-  // (PHIP_PACK_AFTER=1: the pack starts after the resolve, beside the sort; A/B)
-  static const bool pack_after = getenv("PHIP_PACK_AFTER") != nullptr;
-  if (!pack_after && (rc = fork_pack())) return rc;
+  if ((rc = fork_pack())) return rc;
   u32* slot;
   u32 n_claimed = 0;
   if ((rc = resolve_all(h, src, n, ov.now, ov.now0, &slot, &n_claimed,
                         SortVals{ov.kind, ov.kind0, idx})))
     return rc;
-  if (pack_after && (rc = fork_pack())) return rc;
   // Stable radix sort of (slot, seq) pairs: per-bucket arrival order kept.
   size_t tb = 0;
   HIPCHK(h, rocprim::radix_sort_pairs<SlotSortConfig>(nullptr, tb, slot, sslot, idx, sidx, n, 0u, h->L,
                                                        h->stream));
   // segmentation buffers and scan temp sized before the sort is enqueued (a
   // larger B_TEMP must not replace the one the sort is using)
-  static const bool seg_rle = getenv("PHIP_SEG_RLE") != nullptr;
   const u32 ntiles = (u32)(((u64)n + kSegTile - 1) / kSegTile);
   u32 *segt = nullptr, *segb = nullptr;
   size_t tbs = 0;
-  if (!seg_rle) {
-    if ((rc = ensure(h, B_SEGT, 2 * ((size_t)ntiles + 1), &segt))) return rc;
-    segb = segt + ntiles + 1;
-    HIPCHK(h, rocprim::exclusive_scan(nullptr, tbs, segt, segb, 0u, (size_t)ntiles + 1,
-                                      rocprim::plus<u32>(), h->stream));
-  }
+  if ((rc = ensure(h, B_SEGT, 2 * ((size_t)ntiles + 1), &segt))) return rc;
+  segb = segt + ntiles + 1;
+  HIPCHK(h, rocprim::exclusive_scan(nullptr, tbs, segt, segb, 0u, (size_t)ntiles + 1,
+                                    rocprim::plus<u32>(), h->stream));
   u8* temp;
   if ((rc = ensure(h, B_TEMP, std::max(tb, tbs), &temp))) return rc;
   {
@@ -944,8 +912,7 @@ int ordered(phip_handle* h, Src src, u32 n, const OpView& ov, const OutView& ow)
                                                          h->L, h->stream));
   }
   u32 nseg = 0;
-  // (PHIP_SEG_RLE=1: run_length_encode + scan + selects, for A/B timing)
-  if (!seg_rle) {
+  {
     Launch l(h, "segments");
     k_seg_count<<<ntiles, 256, 0, h->stream>>>(sslot, n, segt, h->ctr);
     HIPCHK(h, rocprim::exclusive_scan(temp, tbs, segt, segb, 0u, (size_t)ntiles + 1,
@@ -956,39 +923,6 @@ int ordered(phip_handle* h, Src src, u32 n, const OpView& ov, const OutView& ow)
     HIPCHK(h, hipGetLastError());
     if ((rc = read_ctr(h))) return rc;
     nseg = h->ctr_host[kCtrSegs];
-  } else {
-    size_t tb2 = 0, tb3 = 0;
-    HIPCHK(h, rocprim::run_length_encode(nullptr, tb2, sslot, n, uslot, scnt, h->ctr + 6, h->stream));
-    HIPCHK(h, rocprim::exclusive_scan(nullptr, tb3, scnt, sstart, 0u, (size_t)n, rocprim::plus<u32>(),
-                                      h->stream));
-    if ((rc = ensure(h, B_TEMP, std::max(tb2, tb3), &temp))) return rc;
-    {
-      Launch l(h, "run_length_encode");
-      HIPCHK(h, rocprim::run_length_encode(temp, tb2, sslot, n, uslot, scnt, h->ctr + 6, h->stream));
-    }
-    if ((rc = read_ctr(h))) return rc;
-    nseg = h->ctr_host[6];
-    {
-      Launch l(h, "exclusive_scan");
-      HIPCHK(h, rocprim::exclusive_scan(temp, tb3, scnt, sstart, 0u, (size_t)nseg,
-                                        rocprim::plus<u32>(), h->stream));
-    }
-    {
-      // long / huge segment lists (order-preserving compaction, no atomics)
-      Launch l(h, "select_segments");
-      size_t tb4 = 0, tb5 = 0;
-      rocprim::counting_iterator<u32> segs(0u);
-      HIPCHK(h, rocprim::select(nullptr, tb4, segs, lng, h->ctr + 6, (size_t)nseg, LongSeg{scnt},
-                                h->stream));
-      HIPCHK(h, rocprim::select(nullptr, tb5, segs, huge, h->ctr + 9, (size_t)nseg, HugeSeg{scnt},
-                                h->stream));
-      if ((rc = ensure(h, B_TEMP, std::max(tb4, tb5), &temp))) return rc;
-      HIPCHK(h, rocprim::select(temp, tb4, segs, lng, h->ctr + 6, (size_t)nseg, LongSeg{scnt},
-                                h->stream));
-      HIPCHK(h, rocprim::select(temp, tb5, segs, huge, h->ctr + 9, (size_t)nseg, HugeSeg{scnt},
-                                h->stream));
-    }
-    if ((rc = read_ctr(h))) return rc;
   }
   u32 nlong = h->ctr_host[6], nhuge = h->ctr_host[9];
   if ((rc = pack_join.join())) return rc;
@@ -1017,9 +951,7 @@ int ordered(phip_handle* h, Src src, u32 n, const OpView& ov, const OutView& ow)
     // the same chain on stream3, beside the wave and thread folds on the
     // main stream: the largest segments' folds are the longest sequential
     // chains, so they start as soon as their own (smaller) gather is done.
-    static const u32 first_env =
-        getenv("PHIP_HUGE_FIRST") ? (u32)atoi(getenv("PHIP_HUGE_FIRST")) : PHIP_HUGE_FIRST;
-    const u32 kFirst = std::min<u32>(first_env, kHugeFirstMax);
+    const u32 kFirst = std::min<u32>(PHIP_HUGE_FIRST, kHugeFirstMax);
     const bool split = kFirst > 0 && nhuge > kFirst;
     const u32 hsplit = split ? kFirst : nhuge;
     u32* hl = huge;
@@ -1036,15 +968,13 @@ int ordered(phip_handle* h, Src src, u32 n, const OpView& ov, const OutView& ow)
       HIPCHK(h, hipEventRecord(h->ev_fork3, h->stream2));
       HIPCHK(h, hipStreamWaitEvent(h->stream3, h->ev_fork3, 0));
     }
-    static const int variant = getenv("PHIP_FOLD_VARIANT") ? atoi(getenv("PHIP_FOLD_VARIANT")) : 0;
-    // PHIP_FOLD_STATS=1 (diagnostics): per hot segment, ops / windows /
-    // windows folded / rounds / bursts / ops walked / runs / cycles, to stderr
-    static const bool fold_stats = getenv("PHIP_FOLD_STATS") != nullptr;
+    // A diagnostics build (tools/build_variants.sh "stats:-DPHIP_FOLD_STATS")
+    // prints per hot segment ops / windows / windows folded / rounds / bursts
+    // / ops walked / runs / cycles to stderr.
     u64* fold_dbg = nullptr;
-    if (fold_stats && (rc = ensure(h, B_FOLDDBG, (size_t)nhuge * 16, &fold_dbg))) return rc;
-    auto kb = variant == 1 ? k_fold_block<1> : k_fold_block<0>;
-    // (PHIP_FOLD_NOPRIO=1: the block folds at normal issue priority, A/B)
-    static const u32 fold_prio = getenv("PHIP_FOLD_NOPRIO") ? 0u : 1u;
+#ifdef PHIP_FOLD_STATS
+    if ((rc = ensure(h, B_FOLDDBG, (size_t)nhuge * 16, &fold_dbg))) return rc;
+#endif
     // gather / outputs: window-striding grids of 8 workgroups per CU (the
     // window count is known on the device only)
     const unsigned hgrid = (unsigned)std::min<size_t>(nwin_max, (size_t)h->ncu * 8);
@@ -1052,7 +982,6 @@ int ordered(phip_handle* h, Src src, u32 n, const OpView& ov, const OutView& ow)
     // main stream's wave and thread folds wait for the gathers (ev): the
     // gathers alone, then the latency-bound block folds beside those
     // bandwidth-bound folds, is the shorter schedule.
-    static const bool gather_first = !getenv("PHIP_C3_GATHER_BESIDE");
     auto chain = [&](u32 h0, u32 h1, hipStream_t st, hipEvent_t ev, const char* ng,
                      const char* nf, const char* no) -> int {
       {
@@ -1061,15 +990,13 @@ int ordered(phip_handle* h, Src src, u32 n, const OpView& ov, const OutView& ow)
                                                  hval, sums, h0);
       }
       HIPCHK(h, hipGetLastError());
-      if (gather_first) {
-        HIPCHK(h, hipEventRecord(ev, st));
-        HIPCHK(h, hipStreamWaitEvent(h->stream, ev, 0));
-      }
+      HIPCHK(h, hipEventRecord(ev, st));
+      HIPCHK(h, hipStreamWaitEvent(h->stream, ev, 0));
       {
         Launch l(h, nf, st);
-        kb<<<h1 - h0, kFoldThreads, 0, st>>>(hl, h1, uslot, hoff, scnt, hval, hop, h->recs, rpos,
-                                             rst, runn, segex, segxf, woff, sums, wrun, wing,
-                                             fold_dbg, h0, fold_prio);
+        k_fold_block<<<h1 - h0, kFoldThreads, 0, st>>>(hl, h1, uslot, hoff, scnt, hval, hop,
+                                                       h->recs, rpos, rst, runn, segex, segxf,
+                                                       woff, sums, wrun, wing, fold_dbg, h0);
       }
       HIPCHK(h, hipGetLastError());
       {
@@ -1115,8 +1042,7 @@ int ordered(phip_handle* h, Src src, u32 n, const OpView& ov, const OutView& ow)
   if (nlong) {
     // the long segments over kBigLongSeg ops first (their sequential chains
     // are the longest), then the rest
-    static const bool big_first = !getenv("PHIP_LONG_SLOT_ORDER");
-    if (big_first && nlong > 1) {
+    if (nlong > 1) {
       u32* lng2;
       if ((rc = ensure(h, B_LONG2, nlong, &lng2))) return rc;
       size_t tb7 = 0;
@@ -1196,6 +1122,9 @@ int outputs(phip_handle* h, const phip_results* res, u32 n, bool dev, OutView* o
       (rc = out_buf(h, B_HAVE, r.have, n, dev, &ow->have)) ||
       (rc = out_buf(h, B_REPLY, r.reply, n, dev, &ow->reply)))
     return rc;
+  // an entry with no reply state (a merged replica) reads as zeros, on every
+  // path (the staged buffer would otherwise hand back an earlier call's data)
+  if (ow->reply) HIPCHK(h, hipMemsetAsync(ow->reply, 0, (size_t)n * sizeof(phip_state), h->stream));
   return PHIP_OK;
 }
 
@@ -1366,7 +1295,7 @@ int small_mixed(phip_handle* h, const phip_ops* ops, const phip_results* res, bo
   if (r.have) std::memcpy(r.have, pout + o_have, 8 * n);
   if (r.reply) {
     // reply states are defined for Takes, Upserts and incasts (step_sop);
-    // copy those, leaving the caller's other entries as they were
+    // the other entries read as zeros, as on the large path (outputs())
     const phip_state* src_r = (const phip_state*)(pout + o_reply);
     std::vector<u8> st;
     const u8* stp = r.status;
@@ -1376,7 +1305,8 @@ int small_mixed(phip_handle* h, const phip_ops* ops, const phip_results* res, bo
       stp = st.data();
     }
     for (u32 i = 0; i < n; ++i)
-      if (has_reply_state(stp[i], ops->kind ? ops->kind[i] : (u8)PHIP_OP_RECEIVE)) r.reply[i] = src_r[i];
+      r.reply[i] = has_reply_state(stp[i], ops->kind ? ops->kind[i] : (u8)PHIP_OP_RECEIVE)
+                       ? src_r[i] : phip_state{};
   }
   *done = true;
   return PHIP_OK;
@@ -1460,10 +1390,146 @@ int small_datagrams(phip_handle* h, const uint8_t* bytes, const uint64_t* offs, 
 }
 }  // namespace
 
+// ------------------------------------------------------- owner routing ----
+// The pack of phip_route_pack (and of phip_group_receive's chunks), queued on
+// stream `st` without a host synchronisation.
+// One wave per tile of `span` messages, eight per workgroup.  12 workgroups
+// per CU: k_route_count holds 4 per CU, k_route_scatter 3, so both grids run
+// in whole rounds (no tail round of a quarter of the chip).
+struct RoutePlan {
+  u32 nblk, ntile, span;
+  size_t cells;
+};
+static RoutePlan route_plan(const phip_handle* h, u32 n, u32 world) {
+  RoutePlan p;
+  p.nblk = (u32)std::max<u64>(1, std::min<u64>((n + kRouteBlock - 1) / kRouteBlock, (u64)h->ncu * 12));
+  p.ntile = p.nblk * kRouteWaves;
+  p.span = (u32)(((u64)n + p.ntile - 1) / p.ntile + 63) & ~63u;
+  p.cells = (size_t)world * p.ntile;
+  return p;
+}
+
+// Scratch of a pack of up to n messages (B_ROUTE: the per-(owner, tile)
+// cells, the route codes, its own counters) and the scans' temporary
+// storage (B_TEMP), sized before anything is queued: the packs of a
+// pipelined exchange reuse them in stream order, never reallocated midway.
+static int route_scratch(phip_handle* h, u32 n, u32 world, u8** base, u32** pctr, size_t* scan_bytes,
+                  u8** temp) {
+  const RoutePlan p = route_plan(h, n, world);
+  // cells | codes | the pack's own counter block (16-byte aligned)
+  const size_t ctr_off = (4 * p.cells * sizeof(u32) + 2 * (size_t)n + 15) & ~(size_t)15;
+  int rc;
+  if ((rc = ensure(h, B_ROUTE, ctr_off + kCtrWords * sizeof(u32), base))) return rc;
+  *pctr = (u32*)(*base + ctr_off);
+  size_t tb = 0;
+  HIPCHK(h, rocprim::exclusive_scan(nullptr, tb, (u32*)nullptr, (u32*)nullptr, 0u, p.cells,
+                                    rocprim::plus<u32>(), h->stream));
+  *scan_bytes = tb;
+  return ensure(h, B_TEMP, tb, temp);
+}
+
+// Sender-side combine: the hot names of a strided sample of the
+// whole batch, counted by name hash (the buckets live on other ranks, so
+// there is no slot to count), as a directory for every pack of the batch.
+static int route_dir_on(phip_handle* h, hipStream_t st, const phip_msgs& m, u32 world, const void** out) {
+  *out = nullptr;
+  const u32 n = m.n;
+  if (n < kRouteMinBatch) return PHIP_OK;
+  constexpr size_t kCnt = size_t(1) << kHotCntBits;
+  const size_t zero_bytes = 3 * kCnt * sizeof(u32) + kHotHist * sizeof(u32) + sizeof(HotHdr);
+  u8* hb;
+  int rc;
+  if ((rc = ensure(h, B_RHOT, zero_bytes + kRouteHotMax * sizeof(RouteHot), &hb))) return rc;
+  u32* ckeys = (u32*)hb;
+  u32* ccnt = ckeys + kCnt;
+  u32* cidx = ccnt + kCnt;
+  u32* hist = cidx + kCnt;
+  HotHdr* hdr = (HotHdr*)(hist + kHotHist);
+  RouteHot* d = (RouteHot*)(hdr + 1);
+  HIPCHK(h, hipMemsetAsync(hb, 0, zero_bytes, st));
+  const u32 stride = std::max<u32>(64, (n + kHotSampleMax - 1) / kHotSampleMax);
+  const u32 nsample = (n + stride - 1) / stride;
+  NamesOffs src{m.names, m.name_offs};
+  {
+    Launch l(h, "k_route_sample", st);
+    k_route_sample<NamesOffs><<<grid_for(nsample, kHotSamplePerBlock), 256, 0, st>>>(
+        src, n, stride, nsample, ckeys, ccnt, cidx);
+    k_hot_hist<<<grid_for(kCnt), kBlock, 0, st>>>(ccnt, hist);
+    k_hot_select<<<1, 256, 0, st>>>(hist, hdr, kRouteHotMax);
+    k_route_dir_build<NamesOffs><<<grid_for(kCnt), kBlock, 0, st>>>(ckeys, ccnt, cidx, hdr, src,
+                                                                     world, d);
+  }
+  HIPCHK(h, hipGetLastError());
+  *out = hdr;
+  return PHIP_OK;
+}
+
+// Stable owner partition of m's messages into owner-major send buffers, the
+// per-owner totals into counts / nbytes (device).  With a directory (dir) a
+// clean batch's hot names are max-combined (k_route_count classifies the
+// batch on the way; a dirty one is counted again without combining).
+static int route_pack_on(phip_handle* h, hipStream_t st, const phip_msgs& m, u32 world, const void* dir,
+                  uint8_t* send_names, uint32_t* send_lens, uint64_t* send_added,
+                  uint64_t* send_taken, int64_t* send_elapsed, uint64_t* counts,
+                  uint64_t* nbytes) {
+  const u32 n = m.n;
+  if (n == 0) {
+    HIPCHK(h, hipMemsetAsync(counts, 0, world * sizeof(uint64_t), st));
+    HIPCHK(h, hipMemsetAsync(nbytes, 0, world * sizeof(uint64_t), st));
+    return PHIP_OK;
+  }
+  const RoutePlan p = route_plan(h, n, world);
+  u8 *base, *temp;
+  u32* pctr;
+  size_t tb;
+  int rc;
+  if ((rc = route_scratch(h, n, world, &base, &pctr, &tb, &temp))) return rc;
+  u32* cnt = (u32*)base;
+  u32* bytes = cnt + p.cells;
+  u32* cbase = bytes + p.cells;
+  u32* bbase = cbase + p.cells;
+  u16* code = (u16*)(bbase + p.cells);
+  const HotHdr* hot = (const HotHdr*)dir;
+  const RouteHot* rdir = hot ? (const RouteHot*)(hot + 1) : nullptr;
+  NamesOffs src{m.names, m.name_offs};
+  k_batch_reset<<<1, kShards, 0, st>>>(pctr, nullptr);
+  {
+    Launch l(h, "k_route_count", st);
+    k_route_count<NamesOffs><<<p.nblk, kRouteBlock, 0, st>>>(
+        src, m.added, m.taken, m.elapsed, n, p.span, world, p.ntile, hot, rdir, pctr, code, cnt,
+        bytes, hot ? kRouteCombine : kRoutePlain);
+    if (hot)
+      k_route_count<NamesOffs><<<p.nblk, kRouteBlock, 0, st>>>(
+          src, m.added, m.taken, m.elapsed, n, p.span, world, p.ntile, hot, rdir, pctr, code, cnt,
+          bytes, kRouteRecount);
+  }
+  HIPCHK(h, hipGetLastError());
+  {
+    Launch l(h, "route_scan", st);
+    HIPCHK(h, rocprim::exclusive_scan(temp, tb, cnt, cbase, 0u, p.cells, rocprim::plus<u32>(), st));
+    HIPCHK(h, rocprim::exclusive_scan(temp, tb, bytes, bbase, 0u, p.cells, rocprim::plus<u32>(), st));
+  }
+  {
+    Launch l(h, "k_route_scatter", st);
+    k_route_scatter<NamesOffs><<<p.nblk, kRouteBlock, 0, st>>>(
+        src, m.added, m.taken, m.elapsed, n, p.span, world, p.ntile, hot, rdir, pctr, code, cbase,
+        bbase, send_names, send_lens, send_added, send_taken, send_elapsed);
+  }
+  k_route_totals<<<1, kRouteMaxWorld, 0, st>>>(cnt, bytes, cbase, bbase, p.ntile, world, counts,
+                                               nbytes);
+  HIPCHK(h, hipGetLastError());
+  return PHIP_OK;
+}
+
 // ===================================================================== ABI
 extern "C" {
 
 int phip_abi_version(void) { return PHIP_ABI_VERSION; }
+
+#ifndef PHIP_BUILD_ID
+#error "PHIP_BUILD_ID is set by patrol_amd/Makefile (a hash of the sources)"
+#endif
+const char* phip_build_id(void) { return PHIP_BUILD_ID; }
 
 int phip_open(const phip_config* cfg, phip_handle** out) {
   if (!cfg || !out) return PHIP_ERR_INVALID;
@@ -1502,15 +1568,8 @@ int phip_open(const phip_config* cfg, phip_handle** out) {
   if ((e = hipStreamCreateWithFlags(&h->own_stream, hipStreamNonBlocking)) != hipSuccess)
     return fail(e);
   h->stream = h->own_stream;
-  // (PHIP_STREAM_PRIO=1: stream2/stream3 at the device's greatest priority, A/B)
-  int prio_lo = 0, prio_hi = 0;
-  if (getenv("PHIP_STREAM_PRIO") &&
-      (e = hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi)) != hipSuccess)
-    return fail(e);
-  if ((e = hipStreamCreateWithPriority(&h->stream2, hipStreamNonBlocking, prio_hi)) != hipSuccess)
-    return fail(e);
-  if ((e = hipStreamCreateWithPriority(&h->stream3, hipStreamNonBlocking, prio_hi)) != hipSuccess)
-    return fail(e);
+  if ((e = hipStreamCreateWithFlags(&h->stream2, hipStreamNonBlocking)) != hipSuccess) return fail(e);
+  if ((e = hipStreamCreateWithFlags(&h->stream3, hipStreamNonBlocking)) != hipSuccess) return fail(e);
   if ((e = hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming)) != hipSuccess) return fail(e);
   if ((e = hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming)) != hipSuccess) return fail(e);
   if ((e = hipEventCreateWithFlags(&h->ev_fork3, hipEventDisableTiming)) != hipSuccess) return fail(e);
@@ -2237,96 +2296,12 @@ int phip_route_pack(phip_handle* h, const phip_msgs* m, uint32_t world, uint8_t*
     return PHIP_ERR_INVALID;
   std::lock_guard<std::mutex> g(h->mu);
   if (int rc0 = begin_call(h)) return rc0;
-  if (n == 0) {
-    HIPCHK(h, hipMemsetAsync(counts, 0, world * sizeof(uint64_t), h->stream));
-    HIPCHK(h, hipMemsetAsync(name_bytes, 0, world * sizeof(uint64_t), h->stream));
-    HIPCHK(h, hipStreamSynchronize(h->stream));
-    return PHIP_OK;
-  }
-  // One wave per tile of `span` messages, eight per workgroup.
-  // 12 workgroups per CU: k_route_count holds 4 per CU, k_route_scatter 3,
-  // so both grids run in whole rounds (no tail round of a quarter of the chip)
-  const u32 nblk = (u32)std::max<u64>(1, std::min<u64>((n + kRouteBlock - 1) / kRouteBlock,
-                                                       (u64)h->ncu * 12));
-  const u32 ntile = nblk * kRouteWaves;
-  const u32 span = (u32)(((u64)n + ntile - 1) / ntile + 63) & ~63u;
-  const size_t cells = (size_t)world * ntile;
-  u8* base;
   int rc;
-  if ((rc = ensure(h, B_ROUTE, 2 * (size_t)n + 4 * cells * sizeof(u32) + 64, &base))) return rc;
-  u32* cnt = (u32*)base;
-  u32* bytes = cnt + cells;
-  u32* cbase = bytes + cells;
-  u32* bbase = cbase + cells;
-  u16* code = (u16*)(bbase + cells);
-  NamesOffs src{m->names, m->name_offs};
-  // Sender-side combine (clean batches only): the hot names of a strided
-  // sample, counted by name hash.
-  const HotHdr* hot = nullptr;
-  const RouteHot* dir = nullptr;
-  if ((flags & PHIP_ROUTE_COMBINE) && n >= kRouteMinBatch) {
-    // (no classification pass: k_route_count reads the replica fields and
-    // records the first dirty message; a dirty batch is counted again without
-    // combining)
-    if ((rc = reset_ctr(h))) return rc;
-    constexpr size_t kCnt = size_t(1) << kHotCntBits;
-    const size_t zero_bytes = 3 * kCnt * sizeof(u32) + kHotHist * sizeof(u32) + sizeof(HotHdr);
-    u8* hb;
-    if ((rc = ensure(h, B_HOT, zero_bytes + kRouteHotMax * sizeof(RouteHot), &hb))) return rc;
-    u32* ckeys = (u32*)hb;
-    u32* ccnt = ckeys + kCnt;
-    u32* cidx = ccnt + kCnt;
-    u32* hist = cidx + kCnt;
-    HotHdr* hdr = (HotHdr*)(hist + kHotHist);
-    RouteHot* d = (RouteHot*)(hdr + 1);
-    HIPCHK(h, hipMemsetAsync(hb, 0, zero_bytes, h->stream));
-    const u32 stride = std::max<u32>(64, (n + kHotSampleMax - 1) / kHotSampleMax);
-    const u32 nsample = (n + stride - 1) / stride;
-    {
-      Launch l(h, "k_route_sample");
-      k_route_sample<NamesOffs><<<grid_for(nsample, kHotSamplePerBlock), 256, 0, h->stream>>>(
-          src, n, stride, nsample, ckeys, ccnt, cidx);
-      k_hot_hist<<<grid_for(kCnt), kBlock, 0, h->stream>>>(ccnt, hist);
-      k_hot_select<<<1, 256, 0, h->stream>>>(hist, hdr, kRouteHotMax);
-      k_route_dir_build<NamesOffs><<<grid_for(kCnt), kBlock, 0, h->stream>>>(ckeys, ccnt, cidx, hdr,
-                                                                             src, world, d);
-    }
-    HIPCHK(h, hipGetLastError());
-    hot = hdr;
-    dir = d;
-  }
-  {
-    Launch l(h, "k_route_count");
-    k_route_count<NamesOffs><<<nblk, kRouteBlock, 0, h->stream>>>(
-        src, m->added, m->taken, m->elapsed, n, span, world, ntile, hot, dir, h->ctr, code, cnt,
-        bytes, hot ? kRouteCombine : kRoutePlain);
-    if (hot)
-      k_route_count<NamesOffs><<<nblk, kRouteBlock, 0, h->stream>>>(
-          src, m->added, m->taken, m->elapsed, n, span, world, ntile, hot, dir, h->ctr, code, cnt,
-          bytes, kRouteRecount);
-  }
-  HIPCHK(h, hipGetLastError());
-  size_t tb = 0;
-  HIPCHK(h, rocprim::exclusive_scan(nullptr, tb, cnt, cbase, 0u, cells, rocprim::plus<u32>(),
-                                    h->stream));
-  u8* temp;
-  if ((rc = ensure(h, B_TEMP, tb, &temp))) return rc;
-  {
-    Launch l(h, "route_scan");
-    HIPCHK(h, rocprim::exclusive_scan(temp, tb, cnt, cbase, 0u, cells, rocprim::plus<u32>(),
-                                      h->stream));
-    HIPCHK(h, rocprim::exclusive_scan(temp, tb, bytes, bbase, 0u, cells, rocprim::plus<u32>(),
-                                      h->stream));
-  }
-  {
-    Launch l(h, "k_route_scatter");
-    k_route_scatter<NamesOffs><<<nblk, kRouteBlock, 0, h->stream>>>(
-        src, m->added, m->taken, m->elapsed, n, span, world, ntile, hot, dir, h->ctr, code, cbase,
-        bbase, send_names, send_lens, send_added, send_taken, send_elapsed);
-  }
-  k_route_totals<<<1, kRouteMaxWorld, 0, h->stream>>>(cnt, bytes, cbase, bbase, ntile, world, counts,
-                                                     name_bytes);
-  HIPCHK(h, hipGetLastError());
+  const void* dir = nullptr;
+  if ((flags & PHIP_ROUTE_COMBINE) && (rc = route_dir_on(h, h->stream, *m, world, &dir))) return rc;
+  if ((rc = route_pack_on(h, h->stream, *m, world, dir, send_names, send_lens, send_added,
+                          send_taken, send_elapsed, counts, name_bytes)))
+    return rc;
   HIPCHK(h, hipStreamSynchronize(h->stream));
   return PHIP_OK;
 }
@@ -2459,11 +2434,24 @@ int phip_last_stats(phip_handle* h, uint64_t* out, int max) {
 
 namespace phip_host {
 void* handle_stream(phip_handle* h) { return h ? (void*)h->stream : nullptr; }
+int route_dir(phip_handle* h, void* stream, const phip_msgs* m, uint32_t world, const void** dir) {
+  std::lock_guard<std::mutex> g(h->mu);
+  HIPCHK(h, hipSetDevice(h->device));
+  return route_dir_on(h, (hipStream_t)stream, *m, world, dir);
+}
+int route_pack(phip_handle* h, void* stream, const phip_msgs* m, uint32_t world, const void* dir,
+               uint8_t* names, uint32_t* lens, uint64_t* a, uint64_t* t, int64_t* e,
+               uint64_t* counts, uint64_t* nbytes) {
+  std::lock_guard<std::mutex> g(h->mu);
+  HIPCHK(h, hipSetDevice(h->device));
+  return route_pack_on(h, (hipStream_t)stream, *m, world, dir, names, lens, a, t, e, counts, nbytes);
+}
+const char* last_error(phip_handle* h) { return h ? h->err.c_str() : ""; }
 int handle_device(const phip_handle* h) { return h ? h->device : -1; }
-void* timing_begin(phip_handle* h, const char* name) {
+void* timing_begin(phip_handle* h, const char* name, void* stream) {
   if (!h) return nullptr;
   std::lock_guard<std::mutex> g(h->mu);
-  return h->timing ? new Launch(h, name) : nullptr;
+  return h->timing ? new Launch(h, name, (hipStream_t)stream) : nullptr;
 }
 void timing_end(phip_handle* h, void* token) {
   if (!h || !token) return;

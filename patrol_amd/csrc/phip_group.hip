@@ -5,10 +5,15 @@
 // messages that arrive anywhere are routed to their owner, and simulated
 // replicas converge by an all-reduce(max).
 //
-// Per member and call, one host thread: it binds its GPU, queues the member's
-// kernels and RCCL calls on the member handle's stream, and synchronises only
-// to read the split sizes of the exchange.  With one process per GPU the
-// calling thread is the member's thread.
+// Per member and call, one host thread: it binds its GPU and queues the
+// member's work on three streams, synchronising only to read the split sizes
+// of each chunk's exchange.  With one process per GPU the calling thread is
+// the member's thread.
+//
+// Owner-routed Receive is pipelined by chunks of kChunk messages: the pack of
+// chunk k+1 (pack stream) runs while chunk k travels (exchange stream: the
+// split sizes, then the grouped per-peer send/recv), over two send sets; the
+// owner merges everything it received once, on the handle's stream.
 //
 // Members sharing one GPU (phip_group_open_all with a device listed more
 // than once: several shards' tables on one device, e.g. to rehearse an
@@ -57,11 +62,49 @@ struct Buf {
     if (e == hipSuccess) cap = want;
     return e;
   }
+  // Grow to `bytes`, keeping the first `used` bytes (copied on stream s).
+  hipError_t grow_keep(size_t bytes, size_t used, hipStream_t s) {
+    if (cap >= bytes) return hipSuccess;
+    const size_t want = std::max(bytes, cap * 2) + 64;
+    void* np = nullptr;
+    hipError_t e = hipMalloc(&np, want);
+    if (e != hipSuccess) return e;
+    if (p && used) {
+      if ((e = hipMemcpyAsync(np, p, used, hipMemcpyDeviceToDevice, s)) != hipSuccess ||
+          (e = hipStreamSynchronize(s)) != hipSuccess) {
+        (void)hipFree(np);
+        return e;
+      }
+    }
+    if (p) (void)hipFree(p);
+    p = np;
+    cap = want;
+    return hipSuccess;
+  }
   void release() {
     if (p) (void)hipFree(p);
     p = nullptr;
     cap = 0;
   }
+};
+
+// Messages per pipelined chunk.  A chunk's name bytes are bounded by
+// kChunk x 231 (PHIP_MAX_NAME_LEN), so the send sets are sized from the
+// batch's message count alone (no host read of its name offsets): 3.9 GB of
+// name space per set at full size, laid out for 288 GB of HBM.
+constexpr uint32_t kChunk = 1u << 24;
+constexpr uint32_t kSmallChunk = 1u << 12;   // PHIP_GROUP_SMALL_CHUNKS
+
+// One chunk's send buffers (owner-major, phip_route_pack's layout) and its
+// split sizes.  sizes (device) and host (pinned) hold [6 * world] u64:
+//   send counts | send name bytes | send chunk totals | recv counts | recv name bytes | recv chunk totals
+// (the chunk totals: every member's chunk count K, so that all members run
+// the same number of exchange rounds).
+struct SendSet {
+  Buf names, lens, a, t, e, sizes;
+  uint64_t* host = nullptr;
+  hipEvent_t ev_pack = nullptr, ev_sz = nullptr, ev_x = nullptr;
+  bool x_pending = false;   // ev_x recorded for an exchange reading this set
 };
 
 struct Member {
@@ -70,10 +113,14 @@ struct Member {
   int device = 0;
   u32 rank = 0;
   ncclComm_t comm = nullptr;
-  // send side (phip_route_pack's owner-major buffers), receive side
-  Buf s_names, s_lens, s_a, s_t, s_e, r_names, r_lens, r_offs, r_a, r_t, r_e;
-  Buf sizes, scan_tmp, ae;
-  u64* host_sizes = nullptr;   // pinned [4 * world]: send counts, send bytes, recv counts, recv bytes
+  hipStream_t sp = nullptr, sx = nullptr;   // pack stream, exchange stream
+  hipEvent_t ev_done = nullptr;             // the call's last exchange
+  SendSet set[2];
+  // receive side: every chunk's segments, chunk-major, sources in rank order
+  Buf r_names, r_lens, r_offs, r_a, r_t, r_e;
+  Buf scan_tmp, ae;
+  u64* host_k = nullptr;       // pinned [world]: this member's chunk count, to every peer
+  u64 k_local = 0;             // (shared-device groups read each other's)
   std::string err;
 };
 
@@ -185,15 +232,15 @@ int for_members(phip_group* g, F f) {
   return PHIP_OK;
 }
 
-// The exchange plan of one member, shared by the RCCL and the shared-device
-// paths: with hs = the member's split sizes [send counts | send name bytes |
-// recv counts | recv name bytes] (W entries each), peer p's entry gives
+// The exchange plan of one chunk of one member, shared by the RCCL and the
+// shared-device paths: with hs = the chunk's split sizes (SendSet::host),
+// peer p's entry gives
 //   send side: where the member's packed segment for owner p lies in its
 //              owner-major send buffers (so messages / sb name bytes in) and
 //              its size (sc, sbytes);
 //   recv side: where the segment source p sends this member lands in the
-//              receive buffers (ro / rb: sources in rank order) and its size
-//              (rc, rbytes).
+//              chunk's part of the receive buffers (ro / rb: sources in rank
+//              order) and its size (rc, rbytes).
 struct Seg {
   u64 so, sb, sc, sbytes;
   u64 ro, rb, rc, rbytes;
@@ -204,19 +251,32 @@ void segment_plan(const u64* hs, u32 W, std::vector<Seg>* plan) {
   for (u32 p = 0; p < W; ++p) {
     Seg& g = (*plan)[p];
     g.so = so; g.sb = sb; g.sc = hs[p]; g.sbytes = hs[W + p];
-    g.ro = ro; g.rb = rb; g.rc = hs[2 * W + p]; g.rbytes = hs[3 * W + p];
+    g.ro = ro; g.rb = rb; g.rc = hs[3 * W + p]; g.rbytes = hs[4 * W + p];
     so += g.sc; sb += g.sbytes; ro += g.rc; rb += g.rbytes;
   }
 }
 
-// One member's owner-routed Receive.
+// The send side of one segment only (where a source's segment for owner p
+// lies in its send set): what a shared-device peer reads of another
+// member's sizes (their receive side is that member's own to write).
+Seg send_seg(const u64* hs, u32 W, u32 p) {
+  Seg g{};
+  for (u32 q = 0; q < p; ++q) {
+    g.so += hs[q];
+    g.sb += hs[W + q];
+  }
+  g.sc = hs[p];
+  g.sbytes = hs[W + p];
+  return g;
+}
+
 // The owner's merge of n received messages (lengths, packed names, states):
 // name offsets by an inclusive scan of the lengths, then phip_receive_soa
-// (sources in rank order, each in its order).
-int merge_received(Member& mb, hipStream_t st, const u32* lens, const uint8_t* names, const u64* a,
-                   const u64* t, const int64_t* e, u64 n, int64_t now) {
+// (chunks in order; in each, sources in rank order, each in its order).
+int merge_received(Member& mb, hipStream_t st, u64 n, int64_t now) {
   GHIP(mb, mb.r_offs.ensure(n * 4 + 8));
   u32* offs = (u32*)mb.r_offs.p;
+  const u32* lens = (const u32*)mb.r_lens.p;
   GHIP(mb, hipMemsetAsync(offs, 0, sizeof(u32), st));
   size_t tb = 0;
   GHIP(mb, rocprim::inclusive_scan(nullptr, tb, lens, offs + 1, (size_t)n, rocprim::plus<u32>(), st));
@@ -225,12 +285,56 @@ int merge_received(Member& mb, hipStream_t st, const u32* lens, const uint8_t* n
                                    rocprim::plus<u32>(), st));
   phip_msgs rm{};
   rm.n = (u32)n;
-  rm.names = names;
+  rm.names = (const uint8_t*)mb.r_names.p;
   rm.name_offs = offs;
-  rm.added = a;
-  rm.taken = t;
-  rm.elapsed = e;
+  rm.added = (const u64*)mb.r_a.p;
+  rm.taken = (const u64*)mb.r_t.p;
+  rm.elapsed = (const int64_t*)mb.r_e.p;
   GPHIP(mb, phip_receive_soa(mb.h, &rm, now, nullptr, PHIP_DEVICE_PTRS));
+  return PHIP_OK;
+}
+
+// Chunk k of a batch: messages [k * chunk, ...) (empty past the batch).
+phip_msgs chunk_of(const phip_msgs& in, u64 chunk, u64 k) {
+  phip_msgs c = in;
+  const u64 lo = k * chunk;
+  c.n = lo < in.n ? (u32)std::min<u64>(chunk, in.n - lo) : 0u;
+  if (c.n) {
+    c.name_offs = in.name_offs + lo;   // absolute offsets into the same blob
+    c.added = in.added + lo;
+    c.taken = in.taken + lo;
+    c.elapsed = in.elapsed + lo;
+  }
+  return c;
+}
+
+// Room in the receive buffers for `n` more messages and `nb` more name bytes
+// after the `msgs` / `bytes` already received (kept, on the exchange stream).
+int recv_room(Member& mb, u64 msgs, u64 bytes, u64 n, u64 nb) {
+  GHIP(mb, mb.r_lens.grow_keep((msgs + n) * 4 + 4, msgs * 4, mb.sx));
+  GHIP(mb, mb.r_a.grow_keep((msgs + n) * 8 + 8, msgs * 8, mb.sx));
+  GHIP(mb, mb.r_t.grow_keep((msgs + n) * 8 + 8, msgs * 8, mb.sx));
+  GHIP(mb, mb.r_e.grow_keep((msgs + n) * 8 + 8, msgs * 8, mb.sx));
+  GHIP(mb, mb.r_names.grow_keep(bytes + nb + 64, bytes, mb.sx));
+  return PHIP_OK;
+}
+
+// One segment from a source's send set (src) into this member's receive
+// buffers at chunk base (m0, b0), on stream st.
+int copy_seg(Member& mb, const SendSet& src, const Seg& s_, const Seg& d_, u64 m0, u64 b0,
+             hipStream_t st) {
+  if (!d_.rc) return PHIP_OK;
+  GHIP(mb, hipMemcpyAsync((u32*)mb.r_lens.p + m0 + d_.ro, (const u32*)src.lens.p + s_.so, d_.rc * 4,
+                          hipMemcpyDeviceToDevice, st));
+  if (d_.rbytes)
+    GHIP(mb, hipMemcpyAsync((uint8_t*)mb.r_names.p + b0 + d_.rb, (const uint8_t*)src.names.p + s_.sb,
+                            d_.rbytes, hipMemcpyDeviceToDevice, st));
+  GHIP(mb, hipMemcpyAsync((u64*)mb.r_a.p + m0 + d_.ro, (const u64*)src.a.p + s_.so, d_.rc * 8,
+                          hipMemcpyDeviceToDevice, st));
+  GHIP(mb, hipMemcpyAsync((u64*)mb.r_t.p + m0 + d_.ro, (const u64*)src.t.p + s_.so, d_.rc * 8,
+                          hipMemcpyDeviceToDevice, st));
+  GHIP(mb, hipMemcpyAsync((int64_t*)mb.r_e.p + m0 + d_.ro, (const int64_t*)src.e.p + s_.so,
+                          d_.rc * 8, hipMemcpyDeviceToDevice, st));
   return PHIP_OK;
 }
 
@@ -254,129 +358,167 @@ int member_receive(phip_group* g, Member& mb, const phip_msgs& in, int64_t now, 
     GPHIP(mb, phip_receive_soa(mb.h, &in, now, nullptr, PHIP_DEVICE_PTRS));
     return PHIP_OK;
   }
-  // 1. pack by owner (device; phip_route_pack returns when the sizes are written)
-  size_t in_bytes = 0;
-  if (n) {
-    u32 last = 0;
-    GHIP(mb, hipMemcpyAsync(&last, in.name_offs + n, sizeof last, hipMemcpyDeviceToHost, st));
-    GHIP(mb, hipStreamSynchronize(st));
-    in_bytes = last;
+  // The batch's producers are on the handle's stream: both pipeline streams
+  // start behind it.
+  GHIP(mb, hipEventRecord(mb.ev_done, st));
+  GHIP(mb, hipStreamWaitEvent(mb.sp, mb.ev_done, 0));
+  GHIP(mb, hipStreamWaitEvent(mb.sx, mb.ev_done, 0));
+  // (PHIP_GROUP_SMALL_CHUNKS, testing: many rounds on small batches)
+  const u64 chunk = (flags & PHIP_GROUP_SMALL_CHUNKS) ? kSmallChunk : kChunk;
+  const u64 k_local = ((u64)n + chunk - 1) / chunk;
+  mb.k_local = k_local;
+  for (u32 p = 0; p < W; ++p) mb.host_k[p] = k_local;
+  const u64 cmax = std::max<u64>(1, std::min<u64>(n, chunk));
+  for (SendSet& ss : mb.set) {
+    GHIP(mb, ss.names.ensure(cmax * PHIP_MAX_NAME_LEN + 64));
+    GHIP(mb, ss.lens.ensure(cmax * 4 + 4));
+    GHIP(mb, ss.a.ensure(cmax * 8 + 8));
+    GHIP(mb, ss.t.ensure(cmax * 8 + 8));
+    GHIP(mb, ss.e.ensure(cmax * 8 + 8));
+    GHIP(mb, ss.sizes.ensure((size_t)6 * W * 8));
+    ss.x_pending = false;
   }
-  GHIP(mb, mb.s_names.ensure(in_bytes + 64));
-  GHIP(mb, mb.s_lens.ensure((size_t)n * 4 + 4));
-  GHIP(mb, mb.s_a.ensure((size_t)n * 8 + 8));
-  GHIP(mb, mb.s_t.ensure((size_t)n * 8 + 8));
-  GHIP(mb, mb.s_e.ensure((size_t)n * 8 + 8));
-  GHIP(mb, mb.sizes.ensure((size_t)4 * W * 8));
-  u64* sz = (u64*)mb.sizes.p;   // [send counts | send bytes | recv counts | recv bytes]
-  GPHIP(mb, phip_route_pack(mb.h, &in, W, (uint8_t*)mb.s_names.p, (uint32_t*)mb.s_lens.p,
-                            (uint64_t*)mb.s_a.p, (uint64_t*)mb.s_t.p, (int64_t*)mb.s_e.p, sz,
-                            sz + W, PHIP_DEVICE_PTRS | (flags & PHIP_ROUTE_COMBINE)));
-  // 2. split sizes: every member learns what each source sends it
-  if (g->shared) {
-    GHIP(mb, hipMemcpyAsync(mb.host_sizes, sz, 2 * W * sizeof(u64), hipMemcpyDeviceToHost, st));
-    GHIP(mb, hipStreamSynchronize(st));
-    if (!g->bar.wait()) return fail(mb, PHIP_ERR_INVALID, "another member failed");
-    for (u32 p = 0; p < W; ++p) {   // what member p packed for this one
-      mb.host_sizes[2 * W + p] = g->m[p].host_sizes[mb.rank];
-      mb.host_sizes[3 * W + p] = g->m[p].host_sizes[W + mb.rank];
-    }
-  } else {
-    GNCCL(mb, ncclGroupStart());
-    GNCCL(mb, ncclAllToAll(sz, sz + 2 * W, 1, ncclUint64, mb.comm, st));
-    GNCCL(mb, ncclAllToAll(sz + W, sz + 3 * W, 1, ncclUint64, mb.comm, st));
-    GNCCL(mb, ncclGroupEnd());
-    GHIP(mb, hipMemcpyAsync(mb.host_sizes, sz, 4 * W * sizeof(u64), hipMemcpyDeviceToHost, st));
-    GHIP(mb, hipStreamSynchronize(st));
-  }
-  const u64* hs = mb.host_sizes;
-  u64 n_send = 0, n_recv = 0, b_recv = 0;
-  for (u32 p = 0; p < W; ++p) {
-    n_send += hs[p];
-    n_recv += hs[2 * W + p];
-    b_recv += hs[3 * W + p];
-  }
-  if (n_recv > 0xFFFFFFFFull || b_recv > 0xFFFFFFFFull)
-    return fail(mb, PHIP_ERR_INVALID, "routed batch of %llu messages / %llu name bytes exceeds 2^32",
-                (unsigned long long)n_recv, (unsigned long long)b_recv);
-  if (sent) *sent = n_send;
-  if (merged) *merged = n_recv;
-  GHIP(mb, mb.r_names.ensure(b_recv + 64));
-  GHIP(mb, mb.r_lens.ensure(n_recv * 4 + 4));
-  GHIP(mb, mb.r_offs.ensure(n_recv * 4 + 8));
-  GHIP(mb, mb.r_a.ensure(n_recv * 8 + 8));
-  GHIP(mb, mb.r_t.ensure(n_recv * 8 + 8));
-  GHIP(mb, mb.r_e.ensure(n_recv * 8 + 8));
-  // 3. the segments: one send and one receive per peer and column; this
-  // member's own segment is a device copy (no RCCL round trip through its
-  // buffers) unless rccl_self
-  std::vector<Seg> plan;
-  segment_plan(hs, W, &plan);
-  // one segment from a source's packed buffers (src: its send side) into
-  // this member's receive buffers (dst: its receive side)
-  auto copy_seg = [&](const Member& src, const Seg& s_, const Seg& d_) -> int {
-    GHIP(mb, hipMemcpyAsync((u32*)mb.r_lens.p + d_.ro, (const u32*)src.s_lens.p + s_.so, d_.rc * 4,
-                            hipMemcpyDeviceToDevice, st));
-    GHIP(mb, hipMemcpyAsync((uint8_t*)mb.r_names.p + d_.rb, (const uint8_t*)src.s_names.p + s_.sb,
-                            d_.rbytes, hipMemcpyDeviceToDevice, st));
-    GHIP(mb, hipMemcpyAsync((u64*)mb.r_a.p + d_.ro, (const u64*)src.s_a.p + s_.so, d_.rc * 8,
-                            hipMemcpyDeviceToDevice, st));
-    GHIP(mb, hipMemcpyAsync((u64*)mb.r_t.p + d_.ro, (const u64*)src.s_t.p + s_.so, d_.rc * 8,
-                            hipMemcpyDeviceToDevice, st));
-    GHIP(mb, hipMemcpyAsync((int64_t*)mb.r_e.p + d_.ro, (const int64_t*)src.s_e.p + s_.so,
-                            d_.rc * 8, hipMemcpyDeviceToDevice, st));
+  // 1. the combine's directory, from a sample of the whole batch
+  const void* dir = nullptr;
+  if ((flags & PHIP_ROUTE_COMBINE) && n &&
+      phip_host::route_dir(mb.h, mb.sp, &in, W, &dir) != PHIP_OK)
+    return fail(mb, PHIP_ERR_HIP, "route directory: %s", phip_host::last_error(mb.h));
+  // 2. pack chunk k into set k & 1 (pack stream), once no exchange reads it
+  auto pack = [&](u64 k) -> int {
+    SendSet& ss = mb.set[k & 1];
+    if (ss.x_pending) GHIP(mb, hipStreamWaitEvent(mb.sp, ss.ev_x, 0));
+    const phip_msgs c = chunk_of(in, chunk, k);
+    u64* sz = (u64*)ss.sizes.p;
+    if (phip_host::route_pack(mb.h, mb.sp, &c, W, dir, (uint8_t*)ss.names.p, (uint32_t*)ss.lens.p,
+                              (uint64_t*)ss.a.p, (uint64_t*)ss.t.p, (int64_t*)ss.e.p, sz, sz + W) !=
+        PHIP_OK)
+      return fail(mb, PHIP_ERR_HIP, "route pack: %s", phip_host::last_error(mb.h));
+    GHIP(mb, hipMemcpyAsync(sz + 2 * W, mb.host_k, W * 8, hipMemcpyHostToDevice, mb.sp));
+    GHIP(mb, hipEventRecord(ss.ev_pack, mb.sp));
     return PHIP_OK;
   };
-  if (g->shared) {   // each segment copied from its source member's packed buffers
-    std::vector<Seg> splan;
-    for (u32 p = 0; p < W; ++p) {
-      const Member& src = g->m[p];
-      segment_plan(src.host_sizes, W, &splan);   // the source's send side
-      const Seg& s_ = splan[mb.rank];
-      if (s_.sc != plan[p].rc || s_.sbytes != plan[p].rbytes)
-        return fail(mb, PHIP_ERR_INVALID, "internal: member %u sends %llu/%llu, %u expects %llu/%llu",
-                    p, (unsigned long long)s_.sc, (unsigned long long)s_.sbytes, mb.rank,
-                    (unsigned long long)plan[p].rc, (unsigned long long)plan[p].rbytes);
-      if (int rc = copy_seg(src, s_, plan[p])) return rc;
+  // 3. chunk k's split sizes: every member learns what each source sends it
+  //    (RCCL; shared-device groups read each other's after a barrier)
+  auto sizes = [&](u64 k) -> int {
+    SendSet& ss = mb.set[k & 1];
+    u64* sz = (u64*)ss.sizes.p;
+    GHIP(mb, hipStreamWaitEvent(mb.sx, ss.ev_pack, 0));
+    if (!g->shared) {
+      GNCCL(mb, ncclGroupStart());
+      GNCCL(mb, ncclAllToAll(sz, sz + 3 * W, 1, ncclUint64, mb.comm, mb.sx));
+      GNCCL(mb, ncclAllToAll(sz + W, sz + 4 * W, 1, ncclUint64, mb.comm, mb.sx));
+      GNCCL(mb, ncclAllToAll(sz + 2 * W, sz + 5 * W, 1, ncclUint64, mb.comm, mb.sx));
+      GNCCL(mb, ncclGroupEnd());
     }
-    // every member copied what it needs before any packs again (the next
-    // call's route_pack overwrites the send buffers)
-    GHIP(mb, hipStreamSynchronize(st));
-    if (!g->bar.wait()) return fail(mb, PHIP_ERR_INVALID, "another member failed");
-    if (n_recv == 0) return PHIP_OK;
-    return merge_received(mb, st, (const u32*)mb.r_lens.p, (const uint8_t*)mb.r_names.p,
-                          (const u64*)mb.r_a.p, (const u64*)mb.r_t.p, (const int64_t*)mb.r_e.p,
-                          n_recv, now);
+    GHIP(mb, hipMemcpyAsync(ss.host, sz, 6 * W * sizeof(u64), hipMemcpyDeviceToHost, mb.sx));
+    GHIP(mb, hipEventRecord(ss.ev_sz, mb.sx));
+    return PHIP_OK;
+  };
+  int rc;
+  if ((rc = pack(0)) || (rc = sizes(0))) return rc;
+  if (k_local > 1 && (rc = pack(1))) return rc;
+  u64 K = 1, n_send = 0, recv_msgs = 0, recv_bytes = 0;
+  u64 packed = k_local > 1 ? 2 : 1;   // chunks whose pack is queued
+  std::vector<Seg> plan;
+  void* tm = phip_host::timing_begin(mb.h, "rccl_exchange", mb.sx);
+  for (u64 k = 0; k < K; ++k) {
+    SendSet& ss = mb.set[k & 1];
+    GHIP(mb, hipEventSynchronize(ss.ev_sz));
+    u64* hs = ss.host;
+    if (g->shared) {   // what member p packed for this one, after every member packed chunk k
+      if (!g->bar.wait()) return fail(mb, PHIP_ERR_INVALID, "another member failed");
+      for (u32 p = 0; p < W; ++p) {
+        const SendSet& ps = g->m[p].set[k & 1];
+        hs[3 * W + p] = ps.host[mb.rank];
+        hs[4 * W + p] = ps.host[W + mb.rank];
+        hs[5 * W + p] = g->m[p].k_local;
+      }
+    }
+    if (k == 0) {   // every member runs max(K) rounds (a shorter batch sends empty chunks)
+      for (u32 p = 0; p < W; ++p) K = std::max<u64>(K, hs[5 * W + p]);
+      K = std::max<u64>(K, 1);
+    }
+    segment_plan(hs, W, &plan);
+    u64 c_send = 0, c_recv = 0, b_recv = 0;
+    for (u32 p = 0; p < W; ++p) {
+      c_send += plan[p].sc;
+      c_recv += plan[p].rc;
+      b_recv += plan[p].rbytes;
+    }
+    if (recv_msgs + c_recv > 0xFFFFFFFFull || recv_bytes + b_recv > 0xFFFFFFFFull)
+      return fail(mb, PHIP_ERR_INVALID, "routed batch of %llu messages / %llu name bytes exceeds 2^32",
+                  (unsigned long long)(recv_msgs + c_recv), (unsigned long long)(recv_bytes + b_recv));
+    if ((rc = recv_room(mb, recv_msgs, recv_bytes, c_recv, b_recv))) return rc;
+    // 4. the segments: one send and one receive per peer and column; this
+    //    member's own segment is a device copy unless rccl_self
+    if (g->shared) {
+      for (u32 p = 0; p < W; ++p) {
+        const Member& src = g->m[p];
+        const Seg s_ = send_seg(src.set[k & 1].host, W, mb.rank);   // the source's send side
+        if (s_.sc != plan[p].rc || s_.sbytes != plan[p].rbytes)
+          return fail(mb, PHIP_ERR_INVALID, "internal: member %u sends %llu/%llu, %u expects %llu/%llu",
+                      p, (unsigned long long)s_.sc, (unsigned long long)s_.sbytes, mb.rank,
+                      (unsigned long long)plan[p].rc, (unsigned long long)plan[p].rbytes);
+        if ((rc = copy_seg(mb, src.set[k & 1], s_, plan[p], recv_msgs, recv_bytes, mb.sx))) return rc;
+      }
+    } else {
+      const Seg& own = plan[mb.rank];
+      if (own.sc != own.rc || own.sbytes != own.rbytes)
+        return fail(mb, PHIP_ERR_INVALID, "internal: own segment %llu/%llu vs %llu/%llu",
+                    (unsigned long long)own.sc, (unsigned long long)own.sbytes,
+                    (unsigned long long)own.rc, (unsigned long long)own.rbytes);
+      if (!rccl_self && (rc = copy_seg(mb, ss, own, own, recv_msgs, recv_bytes, mb.sx))) return rc;
+      GNCCL(mb, ncclGroupStart());
+      for (u32 p = 0; p < W; ++p) {
+        if (p == mb.rank && !rccl_self) continue;
+        const Seg& x = plan[p];
+        const u64 mo = recv_msgs + x.ro, bo = recv_bytes + x.rb;
+        GNCCL(mb, ncclSend((u32*)ss.lens.p + x.so, x.sc, ncclUint32, p, mb.comm, mb.sx));
+        GNCCL(mb, ncclRecv((u32*)mb.r_lens.p + mo, x.rc, ncclUint32, p, mb.comm, mb.sx));
+        GNCCL(mb, ncclSend((uint8_t*)ss.names.p + x.sb, x.sbytes, ncclUint8, p, mb.comm, mb.sx));
+        GNCCL(mb, ncclRecv((uint8_t*)mb.r_names.p + bo, x.rbytes, ncclUint8, p, mb.comm, mb.sx));
+        GNCCL(mb, ncclSend((u64*)ss.a.p + x.so, x.sc, ncclUint64, p, mb.comm, mb.sx));
+        GNCCL(mb, ncclRecv((u64*)mb.r_a.p + mo, x.rc, ncclUint64, p, mb.comm, mb.sx));
+        GNCCL(mb, ncclSend((u64*)ss.t.p + x.so, x.sc, ncclUint64, p, mb.comm, mb.sx));
+        GNCCL(mb, ncclRecv((u64*)mb.r_t.p + mo, x.rc, ncclUint64, p, mb.comm, mb.sx));
+        GNCCL(mb, ncclSend((u64*)ss.e.p + x.so, x.sc, ncclUint64, p, mb.comm, mb.sx));
+        GNCCL(mb, ncclRecv((int64_t*)mb.r_e.p + mo, x.rc, ncclUint64, p, mb.comm, mb.sx));
+      }
+      GNCCL(mb, ncclGroupEnd());
+    }
+    GHIP(mb, hipEventRecord(ss.ev_x, mb.sx));
+    ss.x_pending = true;
+    n_send += c_send;
+    recv_msgs += c_recv;
+    recv_bytes += b_recv;
+    if (g->shared) {
+      // every member has copied chunk k out of every set k & 1 before any
+      // packs chunk k + 2 into it
+      GHIP(mb, hipEventSynchronize(ss.ev_x));
+      if (!g->bar.wait()) return fail(mb, PHIP_ERR_INVALID, "another member failed");
+    }
+    // 5. next: chunk k+1's sizes behind chunk k's exchange (RCCL keeps one
+    //    order per communicator), chunk k+2's pack into the set just sent
+    if (k + 1 < K) {
+      if (packed < k + 2) {   // a chunk past this member's batch: an empty pack
+        if ((rc = pack(k + 1))) return rc;
+        packed = k + 2;
+      }
+      if ((rc = sizes(k + 1))) return rc;
+      if (k + 2 < K && packed < k + 3) {
+        if ((rc = pack(k + 2))) return rc;
+        packed = k + 3;
+      }
+    }
   }
-  void* tm = phip_host::timing_begin(mb.h, "rccl_exchange");
-  // the own segment's size must be what this member packed for itself
-  if (plan[mb.rank].sc != plan[mb.rank].rc || plan[mb.rank].sbytes != plan[mb.rank].rbytes)
-    return fail(mb, PHIP_ERR_INVALID, "internal: own segment %llu/%llu vs %llu/%llu",
-                (unsigned long long)plan[mb.rank].sc, (unsigned long long)plan[mb.rank].sbytes,
-                (unsigned long long)plan[mb.rank].rc, (unsigned long long)plan[mb.rank].rbytes);
-  if (!rccl_self)
-    if (int rc = copy_seg(mb, plan[mb.rank], plan[mb.rank])) return rc;
-  GNCCL(mb, ncclGroupStart());
-  for (u32 p = 0; p < W; ++p) {
-    if (p == mb.rank && !rccl_self) continue;
-    const Seg& x = plan[p];
-    GNCCL(mb, ncclSend((u32*)mb.s_lens.p + x.so, x.sc, ncclUint32, p, mb.comm, st));
-    GNCCL(mb, ncclRecv((u32*)mb.r_lens.p + x.ro, x.rc, ncclUint32, p, mb.comm, st));
-    GNCCL(mb, ncclSend((uint8_t*)mb.s_names.p + x.sb, x.sbytes, ncclUint8, p, mb.comm, st));
-    GNCCL(mb, ncclRecv((uint8_t*)mb.r_names.p + x.rb, x.rbytes, ncclUint8, p, mb.comm, st));
-    GNCCL(mb, ncclSend((u64*)mb.s_a.p + x.so, x.sc, ncclUint64, p, mb.comm, st));
-    GNCCL(mb, ncclRecv((u64*)mb.r_a.p + x.ro, x.rc, ncclUint64, p, mb.comm, st));
-    GNCCL(mb, ncclSend((u64*)mb.s_t.p + x.so, x.sc, ncclUint64, p, mb.comm, st));
-    GNCCL(mb, ncclRecv((u64*)mb.r_t.p + x.ro, x.rc, ncclUint64, p, mb.comm, st));
-    GNCCL(mb, ncclSend((u64*)mb.s_e.p + x.so, x.sc, ncclUint64, p, mb.comm, st));
-    GNCCL(mb, ncclRecv((u64*)mb.r_e.p + x.ro, x.rc, ncclUint64, p, mb.comm, st));
-  }
-  GNCCL(mb, ncclGroupEnd());
   phip_host::timing_end(mb.h, tm);
-  if (n_recv == 0) return PHIP_OK;
-  return merge_received(mb, st, (const u32*)mb.r_lens.p, (const uint8_t*)mb.r_names.p,
-                        (const u64*)mb.r_a.p, (const u64*)mb.r_t.p, (const int64_t*)mb.r_e.p, n_recv,
-                        now);
+  if (sent) *sent = n_send;
+  if (merged) *merged = recv_msgs;
+  // 6. the owner's merge, on the handle's stream behind the last exchange
+  GHIP(mb, hipEventRecord(mb.ev_done, mb.sx));
+  GHIP(mb, hipStreamWaitEvent(st, mb.ev_done, 0));
+  if (recv_msgs == 0) return PHIP_OK;
+  return merge_received(mb, st, recv_msgs, now);
 }
 
 __global__ void k_max_into(int64_t* __restrict__ dst, const int64_t* __restrict__ src, u64 n) {
@@ -419,21 +561,43 @@ void destroy(phip_group* g) {
   for (auto& mb : g->m) {
     (void)hipSetDevice(mb.device);
     if (mb.h) (void)phip_flush(mb.h);
+    if (mb.sp) (void)hipStreamSynchronize(mb.sp);
+    if (mb.sx) (void)hipStreamSynchronize(mb.sx);
     if (mb.comm) (void)ncclCommDestroy(mb.comm);
-    for (Buf* b : {&mb.s_names, &mb.s_lens, &mb.s_a, &mb.s_t, &mb.s_e, &mb.r_names, &mb.r_lens,
-                   &mb.r_offs, &mb.r_a, &mb.r_t, &mb.r_e, &mb.sizes, &mb.scan_tmp, &mb.ae})
+    for (SendSet& ss : mb.set) {
+      for (Buf* b : {&ss.names, &ss.lens, &ss.a, &ss.t, &ss.e, &ss.sizes}) b->release();
+      if (ss.host) (void)hipHostFree(ss.host);
+      for (hipEvent_t ev : {ss.ev_pack, ss.ev_sz, ss.ev_x})
+        if (ev) (void)hipEventDestroy(ev);
+    }
+    for (Buf* b : {&mb.r_names, &mb.r_lens, &mb.r_offs, &mb.r_a, &mb.r_t, &mb.r_e, &mb.scan_tmp,
+                   &mb.ae})
       b->release();
-    if (mb.host_sizes) (void)hipHostFree(mb.host_sizes);
+    if (mb.host_k) (void)hipHostFree(mb.host_k);
+    if (mb.ev_done) (void)hipEventDestroy(mb.ev_done);
+    if (mb.sp) (void)hipStreamDestroy(mb.sp);
+    if (mb.sx) (void)hipStreamDestroy(mb.sx);
     if (mb.own && mb.h) phip_close(mb.h);
   }
   delete g;
 }
 
-int alloc_host_sizes(phip_group* g) {
+// Per member: the pipeline's two streams, the send sets' pinned size mirrors
+// and events.
+int alloc_member_state(phip_group* g) {
   for (auto& mb : g->m) {
     if (hipSetDevice(mb.device) != hipSuccess ||
-        hipHostMalloc(&mb.host_sizes, 4 * (size_t)g->world * sizeof(u64), 0) != hipSuccess)
+        hipStreamCreateWithFlags(&mb.sp, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&mb.sx, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&mb.ev_done, hipEventDisableTiming) != hipSuccess ||
+        hipHostMalloc(&mb.host_k, (size_t)g->world * sizeof(u64), 0) != hipSuccess)
       return PHIP_ERR_HIP;
+    for (SendSet& ss : mb.set)
+      if (hipHostMalloc(&ss.host, 6 * (size_t)g->world * sizeof(u64), 0) != hipSuccess ||
+          hipEventCreateWithFlags(&ss.ev_pack, hipEventDisableTiming) != hipSuccess ||
+          hipEventCreateWithFlags(&ss.ev_sz, hipEventDisableTiming) != hipSuccess ||
+          hipEventCreateWithFlags(&ss.ev_x, hipEventDisableTiming) != hipSuccess)
+        return PHIP_ERR_HIP;
   }
   return PHIP_OK;
 }
@@ -489,7 +653,7 @@ int phip_group_open_all(const phip_config* cfg, const int32_t* devices, uint32_t
     }
     for (u32 i = 0; i < n; ++i) g->m[i].comm = comms[i];
   }
-  if (int rc = alloc_host_sizes(g)) {
+  if (int rc = alloc_member_state(g)) {
     destroy(g);
     return rc;
   }
@@ -516,7 +680,7 @@ int phip_group_open_rank(phip_handle* h, const uint8_t* id, uint32_t nranks, uin
     destroy(g);
     return PHIP_ERR_RCCL;
   }
-  if (int rc = alloc_host_sizes(g)) {
+  if (int rc = alloc_member_state(g)) {
     destroy(g);
     return rc;
   }

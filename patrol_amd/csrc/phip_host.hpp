@@ -2,7 +2,7 @@
 #pragma once
 #include <cstdint>
 
-struct phip_handle;
+#include "patrolhip.h"
 
 namespace phip_host {
 
@@ -11,11 +11,28 @@ namespace phip_host {
 void* handle_stream(phip_handle* h);
 int handle_device(const phip_handle* h);
 
-// A timed region on the handle's stream (HIP events, like the engine's own
-// kernels; nothing when timing is off): the group's RCCL calls show up in
-// phip_last_timings under `name`.  timing_end takes what timing_begin gave.
-void* timing_begin(phip_handle* h, const char* name);
+// A timed region on `stream` (the handle's when null; HIP events, like the
+// engine's own kernels; nothing when timing is off): the group's RCCL calls
+// show up in phip_last_timings under `name`.  timing_end takes what
+// timing_begin gave.
+void* timing_begin(phip_handle* h, const char* name, void* stream = nullptr);
 void timing_end(phip_handle* h, void* token);
+
+// Owner routing as phip_route_pack does it, queued on `stream` (a hipStream_t
+// of the handle's device) with no host synchronisation: the pipelined
+// exchange of phip_group_receive packs chunk k+1 while chunk k travels.
+//   route_dir:  the sender-side combine's hot-name directory, from a strided
+//               sample of the whole batch m (nullptr below kRouteMinBatch);
+//   route_pack: the stable owner partition of m (one chunk) into owner-major
+//               send buffers, with the per-owner totals in counts / nbytes
+//               (device), combining with `dir` when it is not null.
+// The scratch they use is the handle's, reused in stream order: every pack
+// of one call must be queued on the same stream, none larger than the first.
+int route_dir(phip_handle* h, void* stream, const phip_msgs* m, uint32_t world, const void** dir);
+int route_pack(phip_handle* h, void* stream, const phip_msgs* m, uint32_t world, const void* dir,
+               uint8_t* names, uint32_t* lens, uint64_t* a, uint64_t* t, int64_t* e,
+               uint64_t* counts, uint64_t* nbytes);
+const char* last_error(phip_handle* h);
 
 // The request parsing of API.takeBucket (api.go:55-65): the name-length check
 // (returns 400 with ErrNameTooLarge's text as the body), ParseRate with its

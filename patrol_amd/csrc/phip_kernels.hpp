@@ -15,15 +15,10 @@ constexpr int kBlock = 256;
 
 // Streaming loads, optionally non-temporal (read-once batch data should not
 // push hot slot records out of the XCD's L2).
-// (PHIP_PLAIN_STREAM: every streaming load plain, for A/B timing only.)
 template <bool NT, class T>
 __device__ inline T ld(const T* p) {
-#ifndef PHIP_PLAIN_STREAM
   if constexpr (NT) return __builtin_nontemporal_load(p);
   else return *p;
-#else
-  return *p;
-#endif
 }
 
 __device__ inline u64 load_be64(const u8* p) {
@@ -302,18 +297,9 @@ __device__ inline Rec load_rec(const Rec* p) {
 // are left 0.  Enough to find and merge a name of <= kShortName bytes.
 __device__ inline Rec load_rec48(const Rec* p) {
   const uint4* q = reinterpret_cast<const uint4*>(p);
-#ifndef PHIP_NT_REC   // (A/B timing only: non-temporal record loads)
+  // (plain loads: the kernel lives on L2 / Infinity Cache retention of warm
+  // records; non-temporal record loads made it 65% slower)
   uint4 a = q[0], b = q[1], c = q[2];
-#else
-  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-  const u32x4* v = reinterpret_cast<const u32x4*>(p);
-  const u32x4 va = __builtin_nontemporal_load(v), vb = __builtin_nontemporal_load(v + 1),
-              vc = __builtin_nontemporal_load(v + 2);
-  uint4 a, b, c;
-  a.x = va.x; a.y = va.y; a.z = va.z; a.w = va.w;
-  b.x = vb.x; b.y = vb.y; b.z = vb.z; b.w = vb.w;
-  c.x = vc.x; c.y = vc.y; c.z = vc.z; c.w = vc.w;
-#endif
   Rec r;
   r.tag = ((u64)a.y << 32) | a.x;
   r.added = ((u64)a.w << 32) | a.z;
@@ -417,7 +403,6 @@ __device__ inline void short_name(u64 w0, u64 w1, u64 w2, u64 off, u32 len, Name
   b1 = len > 8 ? (b1 & ((1ull << (8 * (len - 8))) - 1)) : 0;
   u32 lo = (u32)kFnvOffset, hi = (u32)(kFnvOffset >> 32);
   const u32 q[4] = {(u32)b0, (u32)(b0 >> 32), (u32)b1, (u32)(b1 >> 32)};
-#ifndef PHIP_FNV_FULL
   // A wave whose names all fit in 8 bytes (most of a batch of short names)
   // hashes 8 bytes, not 14 (a wave-uniform branch on one ballot).
   if (__builtin_amdgcn_ballot_w64(len > 8) == 0) {
@@ -425,7 +410,6 @@ __device__ inline void short_name(u64 w0, u64 w1, u64 w2, u64 off, u32 len, Name
     for (u32 k = 0; k < 8; ++k)
       if (k < len) fnv_step32(lo, hi, (q[k >> 2] >> (8 * (k & 3))) & 0xFFu);
   } else
-#endif
   {
 #pragma unroll
     for (u32 k = 0; k < kShortName; ++k)
@@ -657,9 +641,6 @@ __global__ void k_hot_build(const u32* __restrict__ ckeys, const u32* __restrict
 #ifndef PHIP_FAST_PER_CU
 #define PHIP_FAST_PER_CU 4
 #endif
-#ifndef PHIP_FAST_PIPE
-#define PHIP_FAST_PIPE 1
-#endif
 constexpr u32 kFastBlock = PHIP_FAST_BLOCK;
 constexpr u32 kFastPerCU = PHIP_FAST_PER_CU;   // resident workgroups per CU (LDS-bound)
 
@@ -699,11 +680,7 @@ struct SoaIn {   // decoded messages (phip_receive_soa / decoded datagrams)
     if constexpr (kOffs) { off = p.a; len = p.b - p.a; }
     else { off = p.off; len = p.len; }
     ra = ld<true>(ma + i); rt = ld<true>(mt + i); re = ld<true>(me + i);
-#ifndef PHIP_NT_NAMES
     load_words3<false>(src.blob, off, len, w0, w1, w2);
-#else   // A/B timing only
-    load_words3<true>(src.blob, off, len, w0, w1, w2);
-#endif
   }
   // Classification (elapsed matters only when both floats are zero, so it is
   // read only then: a third of the pass's bytes on a clean batch).
@@ -801,13 +778,8 @@ __global__ __launch_bounds__(kBlock) void k_classify_soa2(const uint64_t* __rest
   bool d = false;
   u32 at = i0;
   if (i0 + 1 < n) {
-#ifndef PHIP_PLAIN_CLASSIFY   // (A/B timing only: plain loads)
     const u64x2 a = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(ma + i0));
     const u64x2 t = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(mt + i0));
-#else
-    const u64x2 a = *reinterpret_cast<const u64x2*>(ma + i0);
-    const u64x2 t = *reinterpret_cast<const u64x2*>(mt + i0);
-#endif
     const bool z0 = is_zero_bits(a.x) && is_zero_bits(t.x);
     const bool z1 = is_zero_bits(a.y) && is_zero_bits(t.y);
     const bool d0 = (z0 && me[i0] == 0) || a.x == kSign || t.x == kSign;
@@ -849,170 +821,12 @@ __device__ inline bool tail_match(const u64 (&htail)[kHotTailWords][kHotMax], u3
   return eq;
 }
 
-// ------------------------------------------ classification in the fast pass --
-// A large decoded batch is classified inside k_receive_fast instead of by a
-// whole-batch k_classify in front of it (0.25 ms of the 2.15 ms C2 step).
-// The batch is cut into kClsSegs segments of units of kClsUnit messages;
-// k_classify covers segment 0 before the kernel, beside the hot-directory
-// chain.  A wave entering segment s applies nothing there before every unit
-// of segments <= s is classified (the clean prefix is only known then): the
-// units of segment s+1 are classified ahead, one unit per wave that draws a
-// ticket on entering segment s, and a wave that finds a unit of a segment it
-// needs unclassified claims it and classifies it itself (a unit claimed by
-// another wave is being classified by a running wave: waiting for it cannot
-// deadlock, whatever part of the grid is resident).  A unit's dirty index is
-// recorded (atomicMin) before the unit is marked done (release); a wave reads
-// the first dirty index after it has seen its segments done (acquire).
-constexpr u32 kClsUnit = 4096;
-constexpr u32 kClsSegs = 8;
-constexpr u32 kClsFree = 0, kClsClaimed = 1, kClsDone = 2;
-constexpr u32 kFuseClsMin = 1u << 22;   // smaller batches: k_classify over the whole batch
-constexpr u32 kClsGroup = 64;   // units per done counter (a segment is whole groups)
-struct FuseCls {
-  // one buffer, zeroed per batch (one pointer: the fast kernel is short of
-  // scalar registers): a flag per unit, then a done counter per group of
-  // kClsGroup units (at most kClsGroup-way contention on one address: a
-  // counter per segment took thousands of same-address atomics a segment)
-  u32* base;
-  u32 seg_units;    // units per segment (a multiple of kClsGroup)
-  u32 nunits;
-  u32 pre;          // segments [0, pre) classified by k_classify before the kernel
-  u32 on;           // 0: k_classify covered the whole batch
-  __device__ u32* flag() const { return base; }
-  __device__ u32* gdone() const { return base + nunits; }
-};
-
-__device__ inline u32 cls_seg_units(const FuseCls& fc, u32 s) {
-  const u32 u0 = s * fc.seg_units;
-  return u0 >= fc.nunits ? 0u : min(fc.seg_units, fc.nunits - u0);
-}
-
-// Unit u of a decoded batch, by one wave: k_classify_soa2's pass (two
-// messages a lane, 16-byte loads), four steps of 128 messages in flight.
+// Messages [lo, n) of the batch (lo a multiple of 64: a segment of a batch
+// classified segment by segment, or 0).
 template <class In>
-__device__ inline void cls_unit(const In& in, u32 u, u32 n, u32* ctr) {
-  if constexpr (In::kSoa) {
-    const u32 lane = __lane_id();
-    const u32 ub = u * kClsUnit;
-    for (u32 k = 0; k < kClsUnit; k += 4 * 128) {
-      u64x2 a[4], t[4];
-#pragma unroll
-      for (u32 r = 0; r < 4; ++r) {
-        const u32 i = min(ub + k + r * 128 + 2 * lane, (n - 1) & ~1u);
-        a[r] = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(in.ma + i));
-        t[r] = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(in.mt + i));
-      }
-#pragma unroll
-      for (u32 r = 0; r < 4; ++r) {
-        const u32 i = ub + k + r * 128 + 2 * lane;
-        bool d0 = false, d1 = false;
-        if (i + 1 < n) {
-          const bool z0 = is_zero_bits(a[r].x) && is_zero_bits(t[r].x);
-          const bool z1 = is_zero_bits(a[r].y) && is_zero_bits(t[r].y);
-          d0 = (z0 && in.me[i] == 0) || a[r].x == kSign || t[r].x == kSign;
-          d1 = (z1 && in.me[i + 1] == 0) || a[r].y == kSign || t[r].y == kSign;
-        } else if (i < n) {
-          d0 = in.dirty(i, ctr);
-        }
-        note_dirty(d0 || d1, d0 ? i : i + 1, ctr);
-      }
-    }
-  }
-}
-
-// Cross-workgroup signalling in the fast kernel uses atomic read-modify-
-// writes only (relaxed, device scope: performed where every XCD sees them).
-// Acquire loads and release stores at agent scope write back / invalidate the
-// XCD's L2 on gfx950, which, issued by thousands of waves, cost the merge its
-// cache (a first version: k_receive_fast 1.87 -> 11.5 ms).  Ordering comes
-// from completion instead: a unit's dirty minima are complete (s_waitcnt)
-// before its done mark is issued, and a reader issues its read of the first
-// dirty index only after its read of the done marks has returned.
-__device__ inline u32 rmw_read(u32* p) {
-  return __hip_atomic_fetch_or(p, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ inline u32 wave_rmw_read(u32* p) {
-  u32 v = 0;
-  if (__lane_id() == 0) v = rmw_read(p);
-  return (u32)__builtin_amdgcn_readfirstlane((int)v);
-}
-
-// Classify unit u if it is free (claimed here), else wait until the wave that
-// claimed it is done.  Wave-uniform.
-template <class In>
-__device__ inline void cls_claim(const In& in, const FuseCls& fc, u32 u, u32 n, u32* ctr) {
-  u32 f = wave_rmw_read(&fc.flag()[u]);
-  if (f == kClsDone) return;
-  if (f == kClsFree) {
-    u32 old = 0;
-    if (__lane_id() == 0) old = atomicCAS(&fc.flag()[u], kClsFree, kClsClaimed);
-    old = (u32)__builtin_amdgcn_readfirstlane((int)old);
-    if (old == kClsFree) {
-      cls_unit(in, u, n, ctr);
-      // the unit's atomicMin (if any) complete before the done mark
-      __builtin_amdgcn_s_waitcnt(0);
-      __asm__ __volatile__("" ::: "memory");
-      if (__lane_id() == 0) {
-        (void)__hip_atomic_exchange(&fc.flag()[u], kClsDone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        atomicAdd(&fc.gdone()[u / kClsGroup], 1u);
-      }
-      return;
-    }
-  }
-  while (wave_rmw_read(&fc.flag()[u]) != kClsDone) __builtin_amdgcn_s_sleep(4);
-}
-
-// Every unit of segment s classified.  The classify-ahead assignment has
-// claimed them (normally done by now): lane k reads group k's done counter
-// (a segment is at most 64 groups for kClsSegs = 8 and 2^30 messages... and
-// more groups take more rounds); after a while help, 64 flags at a time (a
-// unit no wave claimed is classified here, one being classified is waited
-// for).  Wave-uniform.
-constexpr u32 kClsSpin = 64;
-template <class In>
-__device__ inline void cls_segment(const In& in, const FuseCls& fc, u32 s, u32 n, u32* ctr) {
-  const u32 cnt = cls_seg_units(fc, s);
-  if (!cnt) return;
-  const u32 u0 = s * fc.seg_units;
-  const u32 g0 = u0 / kClsGroup, ng = (cnt + kClsGroup - 1) / kClsGroup;
-  for (u32 spin = 0;; ++spin) {
-    bool all = true;
-    for (u32 k0 = 0; k0 < ng; k0 += 64) {
-      const u32 k = k0 + __lane_id();
-      const u32 want = k < ng ? min(kClsGroup, cnt - k * kClsGroup) : 0u;
-      const u32 got = k < ng ? rmw_read(&fc.gdone()[g0 + k]) : 0u;
-      all &= __ballot(got < want) == 0;
-    }
-    if (all) return;
-    if (spin >= kClsSpin) break;
-    __builtin_amdgcn_s_sleep(8);
-  }
-  for (u32 k0 = 0; k0 < cnt; k0 += 64) {
-    const u32 k = k0 + __lane_id();
-    const u32 f = k < cnt ? rmw_read(&fc.flag()[u0 + k]) : kClsDone;
-    u64 m = __ballot(f != kClsDone);
-    while (m) {
-      const u32 q = (u32)__ffsll((long long)m) - 1;
-      cls_claim(in, fc, u0 + k0 + q, n, ctr);
-      m &= m - 1;
-    }
-  }
-}
-
-// Classify-ahead on entering segment s: the units of segment s+1 are dealt to
-// the grid's waves by wave index (no shared ticket counter).
-template <class In>
-__device__ inline void cls_ahead(const In& in, const FuseCls& fc, u32 s, u32 n, u32* ctr, u32 wid,
-                                 u32 nwaves) {
-  if (s + 1 >= kClsSegs) return;
-  const u32 cnt = cls_seg_units(fc, s + 1);
-  for (u32 k = wid; k < cnt; k += nwaves) cls_claim(in, fc, (s + 1) * fc.seg_units + k, n, ctr);
-}
-
-template <class In, bool kFuse = false>   // kFuse: in-kernel classification (FuseCls)
 __global__ __launch_bounds__(kFastBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_receive_fast(
-    In in, u32 n, Table T, Sharded miss, u32* ctr,
-    const HotHdr* __restrict__ hot, const HotEntry* __restrict__ hot_dir, FuseCls fc) {
+    In in, u32 lo, u32 n, Table T, Sharded miss, u32* ctr,
+    const HotHdr* __restrict__ hot, const HotEntry* __restrict__ hot_dir) {
   __shared__ u32 hslot[kHotLds];        // directory index + 1 (0 = empty)
   __shared__ u64 htag[kHotMax], hw0[kHotMax], hw1[kHotMax], hw2[kHotMax];
   __shared__ u32 hrec[kHotMax], haoff[kHotMax];
@@ -1020,16 +834,12 @@ __global__ __launch_bounds__(kFastBlock) __attribute__((amdgpu_waves_per_eu(8, 8
   __shared__ u64 hmax[3][kHotMax];      // per-workgroup maxima (elapsed biased by 2^63)
   __shared__ u32 hhits;
 
-  // Gate (k_classify ran before, over segment 0 only when fc.on): only the
-  // clean prefix is applied, the messages before the first dirty one
+  // Gate (k_classify ran before, over every message up to n): only the clean
+  // prefix is applied, the messages before the first dirty one
   // (ctr[kCtrDirty]) and before the first malformed datagram (ctr[5]); none:
-  // ~0.  With fc.on, `lim` falls further as the segments are classified.
-  const u32 n_in = n;
+  // ~0.
   n = min(n, min(ctr[5], ctr[kCtrDirty]));
-  if (n == 0) return;
-  u32 lim = n;
-  const u32 seg_chunks = fc.seg_units * (kClsUnit / 64);
-  u32 vseg = fc.pre - 1;   // segments <= vseg are classified
+  if (n <= lo) return;
   const u32 nh = hot ? min(hot->n, kHotMax) : 0u;
   for (u32 j = threadIdx.x; j < kHotLds; j += kFastBlock) hslot[j] = 0;
   for (u32 j = threadIdx.x; j < kHotMax; j += kFastBlock) {
@@ -1056,38 +866,19 @@ __global__ __launch_bounds__(kFastBlock) __attribute__((amdgpu_waves_per_eu(8, 8
   // chain is then name words -> home slot, and the next chunk's offsets
   // arrive meanwhile.
   // wave-uniform (in SGPRs): the chunk index, its shard of the miss list
-  u32 chunk = blockIdx.x * kWaves + __builtin_amdgcn_readfirstlane(threadIdx.x / 64);
-  const u32 wid = chunk;   // the wave's index in the grid
-  if constexpr (In::kSoa && kFuse)
-    if (fc.on) cls_ahead(in, fc, vseg, n_in, ctr, wid, cstride);   // the first segment k_classify left
+  u32 chunk = lo / 64 + blockIdx.x * kWaves + __builtin_amdgcn_readfirstlane(threadIdx.x / 64);
   typename In::Pre pre{};
   if (chunk < nchunks) pre = in.pre(min(chunk * 64 + lane, n - 1));
   for (; chunk < nchunks; chunk += cstride) {
-    if (In::kSoa && kFuse && fc.on) {
-      const u32 sg = chunk / seg_chunks;
-      if (sg > vseg) {
-        for (u32 x = vseg + 1; x <= sg; ++x) {
-          cls_ahead(in, fc, x, n_in, ctr, wid, cstride);
-          cls_segment(in, fc, x, n_in, ctr);
-        }
-        vseg = sg;
-        lim = min(lim, wave_rmw_read(&ctr[kCtrDirty]));
-      }
-      if (chunk * 64 >= lim) break;   // past the first dirty message
-    }
     const u32 tid = chunk * 64 + lane;
-    const bool valid = tid < lim;
+    const bool valid = tid < n;
     const u32 i = tid < n ? tid : n - 1;
     // round 2: the name words and replica fields
     u64 off, w0, w1, w2, ra, rt;
     u32 len;
     i64 re;
-#if PHIP_FAST_PIPE
     in.load(i, pre, off, len, w0, w1, w2, ra, rt, re);
     if (chunk + cstride < nchunks) pre = in.pre(min((chunk + cstride) * 64 + lane, n - 1));
-#else
-    in.load(i, in.pre(i), off, len, w0, w1, w2, ra, rt, re);
-#endif
     Name nm;
     short_name(w0, w1, w2, off, len, nm);
     const bool shortname = len <= kShortName;
@@ -1151,17 +942,9 @@ __global__ __launch_bounds__(kFastBlock) __attribute__((amdgpu_waves_per_eu(8, 8
         }
         if (pr == kFound) {
           Rec* r = &T.recs[s];
-#if defined(PHIP_FAST_COLD_NOATOM)   // timing experiments only: drops the cold merges
-          (void)r;
-#elif defined(PHIP_FAST_COLD_STORE)  // timing experiments only: plain stores, racy
-          if (ea > cur.added) r->added = ea;
-          if (et > cur.taken) r->taken = et;
-          if (ee > ((u64)cur.elapsed ^ kSign)) r->elapsed = (i64)(ee ^ kSign);
-#else
           if (ea > cur.added) atomicMax(&r->added, ea);
           if (et > cur.taken) atomicMax(&r->taken, et);
           if (ee > ((u64)cur.elapsed ^ kSign)) atomicMax(&r->elapsed, (i64)(ee ^ kSign));
-#endif
         } else {
           missed = true;
           if (pr == kFull) atomicOr(&ctr[8], 1u);
@@ -1178,9 +961,6 @@ __global__ __launch_bounds__(kFastBlock) __attribute__((amdgpu_waves_per_eu(8, 8
   }
 
   // Directory flush: the workgroup's maxima, skipping fields already beaten.
-#ifdef PHIP_FAST_NOFLUSH   // timing experiments only (drops the hot buckets' merges)
-  return;
-#endif
   for (u32 j = threadIdx.x; j < nh; j += kFastBlock) {
     const u64 xa = hmax[0][j], xt = hmax[1][j], xe = hmax[2][j];
     if (!(xa | xt | xe)) continue;
@@ -2506,14 +2286,13 @@ __device__ inline u32 block_min(u32 m, FoldShared& sh, u32& round, u32 tid) {
 }
 
 // Exact fold of a staged window: every change of the state is a run.
-template <int V>
 __device__ inline void fold_window(u32 pos, u32 lim, FState& S, u32& round, FoldShared& sh, u32* rp,
                                    RunState* rs, u32 tid) {
   const u32 lane = tid & 63, wv = tid >> 6;
   u32 cur = 0;
   while (cur < lim) {
     u32 my_first = 0xFFFFFFFFu;
-    if constexpr (!(V & 1)) {
+    {
 #pragma unroll 1
       for (u32 k = 0; k < kFoldPer; ++k) {
         const u32 w = k * kFoldThreads + tid;
@@ -2668,7 +2447,6 @@ __device__ inline GMax pick(const GMax (&g)[kFoldPer], u32 k) {
 // change that lowers a field ends the identity: the run it starts is exact
 // (sh.exact_from) and the rest of the window is applied one op at a time,
 // every change a run.  R and G are updated in place.
-template <int V>
 __device__ inline void fold_window_absorb(u32 pos, u32 lim, FState& R, GMax& G, u32& round,
                                           FoldShared& sh, u32* rp, RunState* rs, u32 tid) {
   const u32 lane = tid & 63, wv = tid >> 6;
@@ -2679,7 +2457,7 @@ __device__ inline void fold_window_absorb(u32 pos, u32 lim, FState& R, GMax& G, 
   u32 cur = 0;
   while (cur < lim) {
     u32 my_first = 0xFFFFFFFFu;
-    if constexpr (!(V & 1)) {
+    {
 #pragma unroll 1
       for (u32 k = 0; k < kFoldPer; ++k) {
         const u32 idx = k * kFoldThreads + tid;
@@ -2770,7 +2548,6 @@ __device__ inline void fold_window_absorb(u32 pos, u32 lim, FState& R, GMax& G, 
 
 // Ablation variants (tools only, PHIP_FOLD_VARIANT): 1 = no state test
 // (every op unchanged: streaming cost alone).
-template <int V = 0>
 __global__ __launch_bounds__(kFoldThreads) void k_fold_block(
     const u32* __restrict__ huge_list, u32 nhuge, const u32* __restrict__ seg_slot,
     const u64* __restrict__ hoff, const u32* __restrict__ seg_count,
@@ -2778,14 +2555,14 @@ __global__ __launch_bounds__(kFoldThreads) void k_fold_block(
     u32* __restrict__ run_pos, RunState* __restrict__ run_st, u32* __restrict__ run_n,
     u8* __restrict__ seg_existed, u32* __restrict__ seg_exact_from,
     const u64* __restrict__ woff, const WinSum* __restrict__ sums, u32* __restrict__ win_run,
-    GMax* __restrict__ win_g, u64* __restrict__ dbg, u32 h_begin, u32 prio) {
+    GMax* __restrict__ win_g, u64* __restrict__ dbg, u32 h_begin) {
   __shared__ FoldShared sh;
   const u32 hs = h_begin + blockIdx.x;   // segments [h_begin, nhuge) of the list
   if (hs >= nhuge) return;
   // A hot segment's fold is one sequential chain of dependent rounds beside
   // the bandwidth-bound wave and thread folds: its waves take the SIMD's
   // issue priority.
-  if (prio) __builtin_amdgcn_s_setprio(3);
+  __builtin_amdgcn_s_setprio(3);
   const u64 t_begin = wall_clock64();
   u32 n_folded = 0;
   const u32 g = huge_list[hs];
@@ -2894,9 +2671,9 @@ __global__ __launch_bounds__(kFoldThreads) void k_fold_block(
     prof_mark(sh, 1, tp);
     ++n_folded;
     if (sh.exact_from == 0xFFFFFFFFu) {
-      fold_window_absorb<V>(pos, wlim, R, G, round, sh, rp, rs, tid);
+      fold_window_absorb(pos, wlim, R, G, round, sh, rp, rs, tid);
     } else {
-      fold_window<V>(pos, wlim, R, round, sh, rp, rs, tid);   // R: the exact state after
+      fold_window(pos, wlim, R, round, sh, rp, rs, tid);   // R: the exact state after
       G = gmax(G, gw);
     }
     if (sh.profiling && tid == 0) tp = wall_clock64();

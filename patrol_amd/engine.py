@@ -220,6 +220,27 @@ class GPURepo:
         dgs = [raw[25 * i + int(offs[i]):25 * (i + 1) + int(offs[i + 1])] for i in range(n)]
         return dgs, found[:n]
 
+    def export_states_device(self, names, name_offs, n: int):
+        """phip_export_datagrams with device pointers (names uint8 CUDA tensor,
+        name_offs int32[n+1]): each named bucket's MarshalBinary datagram
+        (bucket.go:51-68) written on the device, then its three big-endian
+        words read back as (added bits, taken bits, elapsed) int64 tensors and
+        found (bool), all on the device.  An absent bucket reads as zeros."""
+        import torch
+        dev = names.device
+        offs64 = name_offs.to(torch.int64)
+        total = int(offs64[-1] - offs64[0])
+        out = torch.zeros(_lib.BUCKET_FIXED_SIZE * max(n, 1) + total + 8, dtype=torch.uint8,
+                          device=dev)
+        found = torch.zeros(max(n, 1), dtype=torch.uint8, device=dev)
+        self._check(self.L.phip_export_datagrams(self.h, _ptr(names), _ptr(name_offs), n,
+                                                 _ptr(out), _ptr(found), DEVICE_PTRS))
+        base = _lib.BUCKET_FIXED_SIZE * torch.arange(n, dtype=torch.int64, device=dev) + \
+            (offs64[:-1] - offs64[0])
+        words = out[base.unsqueeze(1) + torch.arange(24, device=dev).unsqueeze(0)]   # [n, 24]
+        w = words.view(n, 3, 8).flip(2).contiguous().view(torch.int64).view(n, 3)   # big-endian
+        return w[:, 0], w[:, 1], w[:, 2], found[:n].bool()
+
     def snapshot(self, path=None):
         """The table as a raw image (phip_snapshot); written to `path` if given,
         else returned as a uint8 array."""
@@ -443,11 +464,14 @@ class GPUGroup:
         if rc != 0:
             raise PatrolHipError(rc, self.L.phip_group_last_error(self.g).decode(errors="replace"))
 
-    def receive(self, batches, now: int, combine: bool = True, rccl_self: bool = False):
+    def receive(self, batches, now: int, combine: bool = True, rccl_self: bool = False,
+                small_chunks: bool = False):
         """batches: one (names uint8, name_offs int32[n+1], added, taken, elapsed)
         tuple of CUDA tensors per local member -> (sent, merged) lists.
         rccl_self (PHIP_GROUP_RCCL_SELF, testing): every segment, the
-        member's own included, travels through ncclSend/ncclRecv."""
+        member's own included, travels through ncclSend/ncclRecv.
+        small_chunks (PHIP_GROUP_SMALL_CHUNKS, testing): the pipelined
+        exchange runs in chunks of 4096 messages."""
         k = len(batches)
         msgs = (phip_msgs * k)()
         for i, (names, offs, a, t, e) in enumerate(batches):
@@ -455,7 +479,8 @@ class GPUGroup:
                                 _ptr(e))
         sent, merged = (C.c_uint64 * k)(), (C.c_uint64 * k)()
         flags = DEVICE_PTRS | (_lib.ROUTE_COMBINE if combine else 0) | \
-            (_lib.GROUP_RCCL_SELF if rccl_self else 0)
+            (_lib.GROUP_RCCL_SELF if rccl_self else 0) | \
+            (_lib.GROUP_SMALL_CHUNKS if small_chunks else 0)
         self._check(self.L.phip_group_receive(self.g, msgs, int(now), sent, merged, flags))
         return [int(x) for x in sent], [int(x) for x in merged]
 

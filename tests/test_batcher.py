@@ -71,7 +71,7 @@ def test_batcher_threads_vs_oracle_in_arrival_order(pa, window_us):
     assert st["requests"] == n and st["errors"] == 0
     # requests were coalesced (with no window only while a batch runs, and a
     # small batch runs in one launch, so the no-window case coalesces less)
-    assert st["batches"] < (n // 2 if window_us else n)
+    assert st["batches"] < (n // 4 if window_us else n), st
     names = [r[1][0] for r in allr]
     o = O.Repo()
     ref = o.apply_mixed(np.zeros(n, np.uint8), names, [r[1][1] for r in allr],

@@ -96,15 +96,12 @@ def test_c2_full_size_vs_oracle(env):
 
 @pytest.mark.timeout(600)
 @pytest.mark.parametrize("first", [None, 3_000_000, 5_500_000, 9_000_001, 16_000_000])
-def test_receive_fused_classification_vs_oracle(env, first, monkeypatch):
-    """A 2^24-message batch: k_classify covers its first two of eight
-    segments, k_receive_fast classifies the rest as it goes (FuseCls).  The
-    first incast / -0.0 sits in a pre-classified segment, in a fused one, in
-    the last one, or nowhere; more follow it.  Statuses (merged on the fast
-    path before it, ordered from it on, incast replies) and the table equal
-    the oracle's."""
+def test_receive_dirty_positions_vs_oracle(env, first):
+    """A 2^24-message batch whose first incast / -0.0 sits early, in the
+    middle, near the end, or nowhere; more follow it.  The fast path merges
+    the clean prefix before it, the ordered path runs from it on (incast
+    replies, repo.go:78-90).  Statuses and the table equal the oracle's."""
     torch, bench, pa = env
-    monkeypatch.setenv("PHIP_FUSE_CLS", "1")
     dev = torch.device("cuda", 0)
     K, n, L = 1_000_000, 1 << 24, 21
     s = torch.cuda.Stream(dev)

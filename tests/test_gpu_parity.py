@@ -708,13 +708,17 @@ def test_table_full_refused_without_growth(pa, path):
     assert_same_dump(gpu_dump(g), o.dump())
 
 
-def test_near_full_table_one_new_hot_name_fits(pa):
+@pytest.mark.parametrize("hot_name", [b"one-new-hot-bucket", b"one-new-hot-bucket-" + b"L" * 60])
+def test_near_full_table_one_new_hot_name_fits(pa, hot_name):
     """PHIP_CFG_NO_GROW, a table a few buckets below its load limit, and a
     fast batch whose 60000 messages all name one new bucket:
     the insert step bounds its reservation by the batch's distinct missing
-    names (one), so the batch is applied instead of refused, exactly."""
+    names (one), so the batch is applied instead of refused, exactly.  With
+    a long name (arena-held, > 22 bytes) and an arena of 64 KiB, the arena
+    bytes are counted once too (60000 x 79 bytes would not fit)."""
     rng = np.random.default_rng(21)
-    g = pa.GPURepo(log2_slots=16, max_load_pct=90, grow=False)     # 58982 buckets allowed
+    g = pa.GPURepo(log2_slots=16, max_load_pct=90, grow=False,      # 58982 buckets allowed
+                   arena_bytes=1 << 16)
     o = O.Repo()
     K = 58900
     names = _gen.key_names(range(K))
@@ -722,7 +726,7 @@ def test_near_full_table_one_new_hot_name_fits(pa):
     g.seed(names, z, z, np.zeros(K, np.int64), np.full(K, _gen.T0, np.int64))
     o.seed(names, z, z, np.zeros(K, np.int64), np.full(K, _gen.T0, np.int64))
     n = 60000
-    hot = [b"one-new-hot-bucket"] * n
+    hot = [hot_name] * n
     for i in rng.integers(0, n, 500):
         hot[i] = names[int(i) % K]                 # some existing buckets too
     a, t, e = _gen.clean_states(rng, n)

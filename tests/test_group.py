@@ -38,15 +38,18 @@ def _dump(repo):
     return {k: (v.added, v.taken, v.elapsed, v.created) for k, v in repo.dump().items()}
 
 
-@pytest.mark.parametrize("mode,rccl_self", [("all", False), ("rank", False), ("all", True),
-                                             ("rank", True)])
-def test_group_receive_vs_oracle(pa, mode, rccl_self):
+@pytest.mark.parametrize("mode,rccl_self,small", [("all", False, False), ("rank", False, False),
+                                                   ("all", True, False), ("rank", True, False),
+                                                   ("rank", True, True)])
+def test_group_receive_vs_oracle(pa, mode, rccl_self, small):
     """Two owner-routed batches (the second large enough for the sender-side
     combine) merged through phip_group_receive equal the oracle's Receive of
     the same messages.  rccl_self (PHIP_GROUP_RCCL_SELF): the member's own
     segment travels through grouped ncclSend/ncclRecv to itself, so the
     per-peer exchange of the multi-GPU group (segment plan, counts, dtypes,
-    offsets) runs on this one GPU."""
+    offsets) runs on this one GPU.  small (PHIP_GROUP_SMALL_CHUNKS): the
+    exchange is pipelined in chunks of 4096 messages, so the 2^21 batch runs
+    512 pack / exchange rounds over the two send sets."""
     dev = torch.device("cuda", 0)
     rng = np.random.default_rng(61)
     if mode == "all":
@@ -60,7 +63,8 @@ def test_group_receive_vs_oracle(pa, mode, rccl_self):
     for k, n in enumerate((5000, 1 << 21)):
         names, a, t, e, dv = _batch(rng, n, 20000, dev)
         torch.cuda.synchronize()
-        sent, merged = g.receive([dv], _gen.T0 + k, combine=True, rccl_self=rccl_self)
+        sent, merged = g.receive([dv], _gen.T0 + k, combine=True, rccl_self=rccl_self,
+                                 small_chunks=small)
         assert sent == merged and 0 < merged[0] <= n
         if not rccl_self:
             assert merged[0] == n         # one owner: merged as it came, no pack
@@ -119,6 +123,53 @@ def test_shared_device_group_receive_vs_oracle(pa, world, dirty):
         assert sum(sent) == sum(merged) and sum(merged) <= world * n
         for names, a, t, e, _ in per:
             o.receive_soa(names, a, t, e, _gen.T0 + k)
+    want = o.dump()
+    got = {}
+    for r, repo in enumerate(g.repos):
+        d = _dump(repo)
+        for name in d:
+            h = torch.tensor([int(np.array([G.fnv1a64(name)], np.uint64).view(np.int64)[0])])
+            assert int(shard.owner_of(h, world)) == r
+        got.update(d)
+    assert len(got) == len(want)
+    assert all(got.get(k) == v for k, v in want.items())
+    g.close()
+
+
+@pytest.mark.parametrize("dirty", [0.0, 0.02])
+def test_shared_device_group_receive_pipelined_vs_oracle(pa, dirty):
+    """The pipelined exchange over many rounds (PHIP_GROUP_SMALL_CHUNKS:
+    chunks of 4096 messages) in a group of three shards on one GPU whose
+    members hold batches of different lengths, one of them empty: every
+    member runs the longest batch's number of rounds (the chunk counts ride
+    on the split-size exchange), sends empty chunks past its own batch, and
+    the owners' tables together equal the oracle's Receive of batch 0, 1, 2
+    in order.  With incasts and -0.0 fields the chunks holding them are
+    packed without the combine."""
+    from patrol_amd import shard
+    from oracle import go_semantics as G
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(900 + int(dirty * 100))
+    world = 3
+    g = pa.GPUGroup.open_all([0] * world, log2_slots=14)
+    o = O.Repo()
+    for k, sizes in enumerate(((30000, 5000, 0), (1 << 20, 70000, 4097))):
+        per = [_batch(rng, n, 30000, dev, dirty) if n else None for n in sizes]
+        empty = [torch.zeros(8, dtype=torch.uint8, device=dev), torch.zeros(1, dtype=torch.int32, device=dev)]
+        empty += [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(3)]
+        torch.cuda.synchronize()
+        sent, merged = g.receive([b[4] if b else empty for b in per], _gen.T0 + k, combine=True,
+                                 small_chunks=True)
+        assert sum(sent) == sum(merged) and sum(merged) <= sum(sizes)
+        # an owner receives chunk by chunk, sources in rank order within a
+        # chunk: the oracle applies the same interleaving (each source's
+        # order is kept, as Patrol's peers' datagrams interleave)
+        C = 4096
+        for c in range(max((n + C - 1) // C for n in sizes)):
+            for b, n in zip(per, sizes):
+                if b and c * C < n:
+                    sl = slice(c * C, min(n, (c + 1) * C))
+                    o.receive_soa(b[0][sl], b[1][sl], b[2][sl], b[3][sl], _gen.T0 + k)
     want = o.dump()
     got = {}
     for r, repo in enumerate(g.repos):

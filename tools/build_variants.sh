@@ -8,7 +8,7 @@ mkdir -p tools/var
 for spec in "$@"; do
   name=${spec%%:*}; defs=${spec#*:}
   /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -fPIC -ffp-contract=off -fno-fast-math -Wno-unused-value \
-    -Iinclude $defs -shared -o tools/var/$name.so patrol_amd/csrc/phip_engine.hip patrol_amd/csrc/phip_group.hip patrol_amd/csrc/phip_host.cpp patrol_amd/csrc/phip_udp.cpp patrol_amd/csrc/phip_batcher.cpp -lrccl &
+    -Iinclude -DPHIP_BUILD_ID='"variant-'$name'"' $defs -shared -o tools/var/$name.so patrol_amd/csrc/phip_engine.hip patrol_amd/csrc/phip_group.hip patrol_amd/csrc/phip_host.cpp patrol_amd/csrc/phip_udp.cpp patrol_amd/csrc/phip_batcher.cpp -lrccl &
 done
 wait
 ls -la tools/var

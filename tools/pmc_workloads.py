@@ -74,6 +74,9 @@ def main():
             "hbm_bytes_per_step": rd + wr,
             "algorithmic_bytes_per_step": bench["roofline"].get("algorithmic_bytes_per_step"),
             "bench_kernel_ms_per_step": bench["roofline"].get("kernel_ms_per_step"),
+            # phip_build_id of the library the counters ran on: bench.py uses
+            # this entry only for a run of the same build
+            "build_id": bench.get("build_id"),
             "source": f"profiles/{rnd}_{key}_kernels.json",
             "note": "per step; reads = size-bucketed TCC_EA0_RDREQ x 32/64/128 B, writes = "
                     "WRITE_SIZE; (S=3 - S=1)/2 over tools/profile_workload.sh runs",
