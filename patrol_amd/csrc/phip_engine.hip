@@ -786,11 +786,28 @@ int resolve_all(phip_handle* h, Src src, u32 n, const int64_t* now_arr, i64 now0
   u32 *slot, *miss;
   int rc;
   Sharded rsh;
+  const bool with_hot = n >= kHotMinBatch;
   if ((rc = ensure(h, B_SLOT, n, &slot)) || (rc = ensure(h, B_MISS, n, &miss)) ||
-      (rc = sharded(h, B_MSHARD, grid_for(n), kBlock, &rsh)))
+      (rc = with_hot ? sharded(h, B_MSHARD, (n + 63) / 64, 64, &rsh)
+                     : sharded(h, B_MSHARD, grid_for(n), kBlock, &rsh)))
     return rc;
   if ((rc = reset_ctr(h))) return rc;
-  {
+  if (with_hot) {
+    // the hot directory on stream3 (stream2 may be packing the op records),
+    // read-only on the table and the batch
+    const HotHdr* hot = nullptr;
+    const HotEntry* hdir = nullptr;
+    HIPCHK(h, hipEventRecord(h->ev_fork3, h->stream));
+    HIPCHK(h, hipStreamWaitEvent(h->stream3, h->ev_fork3, 0));
+    if ((rc = build_hot(h, src, n, h->stream3, &hot, &hdir))) return rc;
+    HIPCHK(h, hipEventRecord(h->ev_join3, h->stream3));
+    HIPCHK(h, hipStreamWaitEvent(h->stream, h->ev_join3, 0));
+    Launch l(h, "k_resolve");
+    const unsigned grid = (unsigned)std::max<u64>(
+        1, std::min<u64>(((u64)n + kResolveBlock - 1) / kResolveBlock, (u64)h->ncu * kResolvePerCU));
+    k_resolve_hot<Src><<<grid, kResolveBlock, 0, h->stream>>>(src, n, table(h), slot, rsh, h->ctr,
+                                                                 sv, hot, hdir);
+  } else {
     Launch l(h, "k_resolve");
     k_resolve<Src><<<grid_for(n), kBlock, 0, h->stream>>>(src, n, nullptr, table(h), slot, rsh,
                                                            h->ctr, sv);
@@ -879,7 +896,7 @@ int ordered(phip_handle* h, Src src, u32 n, const OpView& ov, const OutView& ow)
     HIPCHK(h, hipStreamWaitEvent(h->stream2, h->ev_fork, 0));
     {
       Launch l(h, "k_pack_ops", h->stream2);
-      k_pack_ops<<<grid_for(n), kBlock, 0, h->stream2>>>(ov, n, opr, nullptr);
+      k_pack_ops<<<grid_for(n, kBlock * kPackPer), kBlock, 0, h->stream2>>>(ov, n, opr);
     }
     HIPCHK(h, hipGetLastError());
     HIPCHK(h, hipEventRecord(h->ev_pack, h->stream2));
@@ -929,6 +946,11 @@ int ordered(phip_handle* h, Src src, u32 n, const OpView& ov, const OutView& ow)
   // Different segments touch different slots, so the folds may overlap: the
   // hot-bucket workgroups run on stream2 beside the wave and thread folds.
   if (nhuge) {
+    // k_huge_outputs stores only results that differ from the defaults
+    // (write_out_nd): the defaults go in first, as streams
+    if (ow.status) HIPCHK(h, hipMemsetAsync(ow.status, PHIP_ST_MERGED, n, h->stream));
+    if (ow.remaining) HIPCHK(h, hipMemsetAsync(ow.remaining, 0, (size_t)n * 8, h->stream));
+    if (ow.have) HIPCHK(h, hipMemsetAsync(ow.have, 0, (size_t)n * 8, h->stream));
     u64 *hoff, *woff;
     OpRec* hop;
     u32 *hval, *rpos, *runn, *wrun;

@@ -1130,6 +1130,91 @@ __global__ __launch_bounds__(kBlock) void k_resolve(Src src, u32 n, const u32* _
   if (miss.base) miss.append(blockIdx.x, missed, i);
 }
 
+// The first full resolve of a large ordered batch: k_resolve with C2's hot
+// directory (k_receive_fast's, built by the same sample on a side stream).
+// A name of <= kInlineName bytes found in the workgroup's LDS copy takes its
+// slot from there, with no table probe (C3: the Zipf head is most of the
+// ops); the rest probe.  Persistent workgroups, every wave walks its own
+// 64-op chunks (grid stride), a chunk's name offsets issued one chunk ahead.
+constexpr u32 kResolveBlock = 512;
+constexpr u32 kResolvePerCU = 4;
+template <class Src>
+__global__ __launch_bounds__(kResolveBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_resolve_hot(
+    Src src, u32 n, Table T, u32* __restrict__ slot_out, Sharded miss, u32* ctr, SortVals sv,
+    const HotHdr* __restrict__ hot, const HotEntry* __restrict__ hot_dir) {
+  __shared__ u32 hslot[kHotLds];   // directory index + 1 (0 = empty)
+  __shared__ u64 htag[kHotMax], hw0[kHotMax], hw1[kHotMax], hw2[kHotMax];
+  __shared__ u32 hrec[kHotMax];
+  const u32 nh = hot ? min(hot->n, kHotMax) : 0u;
+  for (u32 j = threadIdx.x; j < kHotLds; j += kResolveBlock) hslot[j] = 0;
+  __syncthreads();
+  for (u32 j = threadIdx.x; j < nh; j += kResolveBlock) {
+    const HotEntry d = hot_dir[j];
+    htag[j] = d.tag; hw0[j] = d.w0; hw1[j] = d.w1; hw2[j] = d.w2; hrec[j] = d.slot;
+    u32 hs = hot_home(d.tag);
+    while (atomicCAS(&hslot[hs], 0u, j + 1) != 0) hs = (hs + 1) & (kHotLds - 1);
+  }
+  __syncthreads();
+  constexpr u32 kWaves = kResolveBlock / 64;
+  const u32 lane = threadIdx.x & 63;
+  const u32 nchunks = (n + 63) / 64;
+  const u32 cstride = gridDim.x * kWaves;
+  u32 chunk = blockIdx.x * kWaves + __builtin_amdgcn_readfirstlane(threadIdx.x / 64);
+  u64 off = 0;
+  u32 len = 0;
+  if (chunk < nchunks) src.template get<true>(min(chunk * 64 + lane, n - 1), off, len);
+  for (; chunk < nchunks; chunk += cstride) {
+    const u32 i = chunk * 64 + lane;
+    const bool valid = i < n;
+    u64 w0, w1, w2;
+    load_words3<false>(src.blob, off, len, w0, w1, w2);
+    const u64 o = off;
+    const u32 l = len;
+    if (chunk + cstride < nchunks) src.template get<true>(min((chunk + cstride) * 64 + lane, n - 1), off, len);
+    if (valid && sv.val) sv.val[i] = i | ((u32)(sv.kind ? sv.kind[i] : sv.kind0) << kSortValKindShift);
+    Name nm;
+    short_name(w0, w1, w2, o, l, nm);
+    if (l > kShortName) {
+      if (l <= kInlineName) {
+        const u64* bw = reinterpret_cast<const u64*>(src.blob);
+        const u64 last = (o + l - 1) >> 3, w3i = (o >> 3) + 3;
+        inline_name(w0, w1, w2, bw[w3i < last ? w3i : last], o, l, nm);
+      } else {
+        load_name_wide<false>(src.blob, o, l, nm);
+      }
+    }
+    bool missed = false;
+    if (valid) {
+      const u64 tag = T.tag(nm.h);
+      int hidx = -1;
+      if (nh && l <= kInlineName) {
+        for (u32 hs = hot_home(tag);; hs = (hs + 1) & (kHotLds - 1)) {
+          const u32 e = hslot[hs];
+          if (!e) break;
+          if (htag[e - 1] == tag && hw0[e - 1] == nm.w0 && hw1[e - 1] == nm.w1 &&
+              hw2[e - 1] == nm.w2) {
+            hidx = (int)e - 1;
+            break;
+          }
+        }
+      }
+      if (hidx >= 0) {
+        slot_out[i] = hrec[hidx];
+      } else {
+        u32 s;
+        Rec r;
+        const int pr = probe(T, nm, src.blob, &s, &r);
+        if (pr == kFound) slot_out[i] = s;
+        else {
+          missed = true;
+          if (pr == kFull) atomicOr(&ctr[8], 1u);
+        }
+      }
+    }
+    if (miss.base) miss.append(chunk, missed, i);
+  }
+}
+
 // ------------------------------------------------------------- inserts ---
 // Round of the insert pipeline.  Claim: CAS an empty tag slot.  A same-tag
 // slot claimed in this round (not yet published) cannot be name-checked, so
@@ -1336,6 +1421,14 @@ struct OutView {
   phip_state* reply;
 };
 
+// Lane l's value when l is wave-uniform (a ballot's first set lane): a
+// v_readlane into a scalar register instead of an LDS permute.
+__device__ inline u64 lane_u64(u64 v, u32 l) {
+  const u32 lo = (u32)__builtin_amdgcn_readlane((int)(u32)v, (int)l);
+  const u32 hi = (u32)__builtin_amdgcn_readlane((int)(u32)(v >> 32), (int)l);
+  return ((u64)hi << 32) | lo;
+}
+
 // One op packed into 32 bytes (one aligned sector), in original order:
 //   TAKE:            x = Rate.Interval (0 = Tokens() is always 0),
 //                    y = float64(Freq) bits (capacity), z = float64(n) bits
@@ -1372,29 +1465,54 @@ __device__ inline SOp load_sop(const OpRec* ops, u32 v) {
 }
 
 // Pack: op i -> ops[i] (coalesced reads of the ABI columns, coalesced
-// 32-byte writes) and the sort value i | kind << 30.  The per-op integer
-// division of Rate.Interval happens here, once, not in every fold round.
-__global__ __launch_bounds__(kBlock) void k_pack_ops(OpView ov, u32 n, OpRec* __restrict__ ops,
-                                                     u32* __restrict__ val) {
-  u32 i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const u32 kind = ov.kind ? ov.kind[i] : ov.kind0;
-  OpRec r;
-  r.now = ov.now ? ov.now[i] : ov.now0;
-  if (kind == PHIP_OP_TAKE) {
-    const i64 f = ov.freq[i], p = ov.per[i];
-    r.x = (u64)rate_interval(f, p);
-    r.y = as_bits((double)f);             // bucket.go:192
-    r.z = as_bits((double)ov.count[i]);   // bucket.go:215
-  } else {
-    r.x = ov.a[i];
-    r.y = ov.t[i];
-    r.z = (u64)ov.e[i];
+// 32-byte writes).  The per-op integer division of Rate.Interval happens
+// here, once, not in every fold round.  kPackPer ops per thread, every
+// column load of all of them issued before the first is used (a stream
+// kernel needs the loads in flight: one op per thread left it at ~3 TB/s);
+// a column the view does not have is not read.
+constexpr u32 kPackPer = 4;
+__global__ __launch_bounds__(kBlock) void k_pack_ops(OpView ov, u32 n, OpRec* __restrict__ ops) {
+  const u32 i0 = blockIdx.x * (kBlock * kPackPer) + threadIdx.x;
+  u32 kd[kPackPer];
+  i64 nw[kPackPer], f[kPackPer], p[kPackPer];
+  u64 c[kPackPer], x[kPackPer], y[kPackPer], z[kPackPer];
+#pragma unroll
+  for (u32 j = 0; j < kPackPer; ++j) {
+    const u32 i = min(i0 + j * kBlock, n - 1);
+    kd[j] = ov.kind ? (u32)ld<true>(ov.kind + i) : ov.kind0;
+    nw[j] = ov.now ? ld<true>(ov.now + i) : ov.now0;
+    f[j] = ov.freq ? ld<true>(ov.freq + i) : 0;
+    p[j] = ov.per ? ld<true>(ov.per + i) : 0;
+    c[j] = ov.count ? ld<true>(ov.count + i) : 0;
+    x[j] = ov.a ? ld<true>(ov.a + i) : 0;
+    y[j] = ov.t ? ld<true>(ov.t + i) : 0;
+    z[j] = ov.e ? (u64)ld<true>(ov.e + i) : 0;
   }
-  ulonglong2* q = reinterpret_cast<ulonglong2*>(ops + i);
-  q[0] = ulonglong2{(u64)r.now, r.x};
-  q[1] = ulonglong2{r.y, r.z};
-  if (val) val[i] = i | (kind << kOpIdxBits);
+#pragma unroll
+  for (u32 j = 0; j < kPackPer; ++j) {
+    const u32 i = i0 + j * kBlock;
+    const bool take = i < n && kd[j] == PHIP_OP_TAKE;
+    // Rate.Interval (an int64 division, a long instruction sequence): the
+    // Takes of a wave usually share one rate, then it is divided once
+    const u64 tm = __ballot(take);
+    if (tm) {
+      const u32 l0 = (u32)__ffsll((long long)tm) - 1;
+      const i64 f0 = (i64)lane_u64((u64)f[j], l0), p0 = (i64)lane_u64((u64)p[j], l0);
+      i64 iv;
+      if (__ballot(take && (f[j] != f0 || p[j] != p0)) == 0) iv = rate_interval(f0, p0);
+      else iv = rate_interval(f[j], p[j]);
+      if (take) {
+        x[j] = (u64)iv;
+        y[j] = as_bits((double)f[j]);             // bucket.go:192
+        z[j] = as_bits((double)c[j]);             // bucket.go:215
+      }
+    }
+    if (i < n) {
+      ulonglong2* q = reinterpret_cast<ulonglong2*>(ops + i);
+      q[0] = ulonglong2{(u64)nw[j], x[j]};
+      q[1] = ulonglong2{y[j], z[j]};
+    }
+  }
 }
 
 struct FState {
@@ -1498,6 +1616,25 @@ __device__ inline void write_out_m(const OutView& o, u32 i, const OpOut& r, cons
   }
 }
 
+// write_out_m for outputs prefilled with the defaults (status MERGED,
+// remaining / have 0): only the values that differ are stored.  A hot
+// segment's ops are scattered over the whole batch, so every store is a
+// random write of its own; half of them are merges whose results are the
+// defaults (k_huge_outputs).
+template <u32 kOut>
+__device__ inline void write_out_nd(const OutView& o, u32 i, const OpOut& r, const FState& S) {
+  if constexpr ((kOut & kOutStatus) != 0) if (r.st != PHIP_ST_MERGED) o.status[i] = r.st;
+  if constexpr ((kOut & kOutRem) != 0) if (r.rem) o.remaining[i] = r.rem;
+  if constexpr ((kOut & kOutHave) != 0) if (r.have) o.have[i] = r.have;
+  if constexpr ((kOut & kOutReply) != 0) {
+    if (r.has_reply) {
+      phip_state st;
+      st.added = as_bits(S.a); st.taken = as_bits(S.t); st.elapsed = S.e; st.created = S.c;
+      o.reply[i] = st;
+    }
+  }
+}
+
 __device__ inline FState load_state(const Rec& r) {
   FState S;
   S.a = as_f64(dec_f64(r.added));
@@ -1569,13 +1706,6 @@ __global__ __launch_bounds__(kBlock) void k_fold_thread(
   store_state(r, S);
 }
 
-// Lane l's value when l is wave-uniform (a ballot's first set lane): a
-// v_readlane into a scalar register instead of an LDS permute.
-__device__ inline u64 lane_u64(u64 v, u32 l) {
-  const u32 lo = (u32)__builtin_amdgcn_readlane((int)(u32)v, (int)l);
-  const u32 hi = (u32)__builtin_amdgcn_readlane((int)(u32)(v >> 32), (int)l);
-  return ((u64)hi << 32) | lo;
-}
 __device__ inline FState lane_state(const FState& x, u32 l) {
   FState y;
   y.a = as_f64(lane_u64(as_bits(x.a), l));
@@ -2788,9 +2918,10 @@ __global__ __launch_bounds__(kBlock) void k_huge_outputs(
     seen[k] = S2;   // the reply state: the bucket right after the op
     if (j0 + k < p1) gj = gmax(gj, merge_contrib(op[k], val[k]));
   }
+  // (status, remaining and have were prefilled with the defaults, ordered())
 #pragma unroll
   for (u32 k = 0; k < kOutPer; ++k)
-    if (j0 + k < p1) write_out_m<kOut>(ow, val[k] & kOpIdxMask, o[k], seen[k]);
+    if (j0 + k < p1) write_out_nd<kOut>(ow, val[k] & kOpIdxMask, o[k], seen[k]);
   __syncthreads();   // the window's shared arrays are reused by the next
   }
 }

@@ -11,6 +11,7 @@
 #   bench NAME [ARGS]     python bench.py ARGS                           NAME.json / NAME.err
 #   gloo2 NAME [ARGS]     bench.py --gpus 2 --dist-backend gloo ARGS     (two ranks, one GPU)
 #   prof NAME [ARGS]      rocprofv3 --kernel-trace --stats over bench.py NAME/ (+ NAME.json)
+#   profpy NAME SCRIPT [ARGS]  rocprofv3 --kernel-trace --stats over python3 SCRIPT ARGS   NAME/
 #   pmc NAME [ARGS]       tools/profile_workload.sh TAG/NAME ARGS        (counter passes)
 #   py NAME SCRIPT [ARGS] python3 -u SCRIPT ARGS                         NAME.log
 set -u
@@ -59,6 +60,9 @@ for spec in "$@"; do
       name=$1; shift
       run 600 "$O/$name.log" rocprofv3 --kernel-trace --stats --output-format csv -d "$ROOT/$O/$name" -o run -- python3 -u bench.py "$@"
       grep '^{"metric"' "$O/$name.log" > "$O/$name.json" || true ;;
+    profpy)
+      name=$1; shift
+      run 600 "$O/$name.log" rocprofv3 --kernel-trace --stats --output-format csv -d "$ROOT/$O/$name" -o run -- python3 -u "$@" ;;
     pmc)
       name=$1; shift
       run 1200 "$O/$name.pmc.log" bash tools/profile_workload.sh "$TAG/$name" "$@" ;;
