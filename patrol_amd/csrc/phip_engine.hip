@@ -786,28 +786,14 @@ int resolve_all(phip_handle* h, Src src, u32 n, const int64_t* now_arr, i64 now0
   u32 *slot, *miss;
   int rc;
   Sharded rsh;
-  const bool with_hot = n >= kHotMinBatch;
   if ((rc = ensure(h, B_SLOT, n, &slot)) || (rc = ensure(h, B_MISS, n, &miss)) ||
-      (rc = with_hot ? sharded(h, B_MSHARD, (n + 63) / 64, 64, &rsh)
-                     : sharded(h, B_MSHARD, grid_for(n), kBlock, &rsh)))
+      (rc = sharded(h, B_MSHARD, grid_for(n), kBlock, &rsh)))
     return rc;
   if ((rc = reset_ctr(h))) return rc;
-  if (with_hot) {
-    // the hot directory on stream3 (stream2 may be packing the op records),
-    // read-only on the table and the batch
-    const HotHdr* hot = nullptr;
-    const HotEntry* hdir = nullptr;
-    HIPCHK(h, hipEventRecord(h->ev_fork3, h->stream));
-    HIPCHK(h, hipStreamWaitEvent(h->stream3, h->ev_fork3, 0));
-    if ((rc = build_hot(h, src, n, h->stream3, &hot, &hdir))) return rc;
-    HIPCHK(h, hipEventRecord(h->ev_join3, h->stream3));
-    HIPCHK(h, hipStreamWaitEvent(h->stream, h->ev_join3, 0));
-    Launch l(h, "k_resolve");
-    const unsigned grid = (unsigned)std::max<u64>(
-        1, std::min<u64>(((u64)n + kResolveBlock - 1) / kResolveBlock, (u64)h->ncu * kResolvePerCU));
-    k_resolve_hot<Src><<<grid, kResolveBlock, 0, h->stream>>>(src, n, table(h), slot, rsh, h->ctr,
-                                                                 sv, hot, hdir);
-  } else {
+  {
+    // (one op per thread; a persistent version that took the hot names'
+    // slots from C2's directory in LDS first lost: 1.85 against 1.49 ms on
+    // C3)
     Launch l(h, "k_resolve");
     k_resolve<Src><<<grid_for(n), kBlock, 0, h->stream>>>(src, n, nullptr, table(h), slot, rsh,
                                                            h->ctr, sv);

@@ -1130,91 +1130,6 @@ __global__ __launch_bounds__(kBlock) void k_resolve(Src src, u32 n, const u32* _
   if (miss.base) miss.append(blockIdx.x, missed, i);
 }
 
-// The first full resolve of a large ordered batch: k_resolve with C2's hot
-// directory (k_receive_fast's, built by the same sample on a side stream).
-// A name of <= kInlineName bytes found in the workgroup's LDS copy takes its
-// slot from there, with no table probe (C3: the Zipf head is most of the
-// ops); the rest probe.  Persistent workgroups, every wave walks its own
-// 64-op chunks (grid stride), a chunk's name offsets issued one chunk ahead.
-constexpr u32 kResolveBlock = 512;
-constexpr u32 kResolvePerCU = 4;
-template <class Src>
-__global__ __launch_bounds__(kResolveBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_resolve_hot(
-    Src src, u32 n, Table T, u32* __restrict__ slot_out, Sharded miss, u32* ctr, SortVals sv,
-    const HotHdr* __restrict__ hot, const HotEntry* __restrict__ hot_dir) {
-  __shared__ u32 hslot[kHotLds];   // directory index + 1 (0 = empty)
-  __shared__ u64 htag[kHotMax], hw0[kHotMax], hw1[kHotMax], hw2[kHotMax];
-  __shared__ u32 hrec[kHotMax];
-  const u32 nh = hot ? min(hot->n, kHotMax) : 0u;
-  for (u32 j = threadIdx.x; j < kHotLds; j += kResolveBlock) hslot[j] = 0;
-  __syncthreads();
-  for (u32 j = threadIdx.x; j < nh; j += kResolveBlock) {
-    const HotEntry d = hot_dir[j];
-    htag[j] = d.tag; hw0[j] = d.w0; hw1[j] = d.w1; hw2[j] = d.w2; hrec[j] = d.slot;
-    u32 hs = hot_home(d.tag);
-    while (atomicCAS(&hslot[hs], 0u, j + 1) != 0) hs = (hs + 1) & (kHotLds - 1);
-  }
-  __syncthreads();
-  constexpr u32 kWaves = kResolveBlock / 64;
-  const u32 lane = threadIdx.x & 63;
-  const u32 nchunks = (n + 63) / 64;
-  const u32 cstride = gridDim.x * kWaves;
-  u32 chunk = blockIdx.x * kWaves + __builtin_amdgcn_readfirstlane(threadIdx.x / 64);
-  u64 off = 0;
-  u32 len = 0;
-  if (chunk < nchunks) src.template get<true>(min(chunk * 64 + lane, n - 1), off, len);
-  for (; chunk < nchunks; chunk += cstride) {
-    const u32 i = chunk * 64 + lane;
-    const bool valid = i < n;
-    u64 w0, w1, w2;
-    load_words3<false>(src.blob, off, len, w0, w1, w2);
-    const u64 o = off;
-    const u32 l = len;
-    if (chunk + cstride < nchunks) src.template get<true>(min((chunk + cstride) * 64 + lane, n - 1), off, len);
-    if (valid && sv.val) sv.val[i] = i | ((u32)(sv.kind ? sv.kind[i] : sv.kind0) << kSortValKindShift);
-    Name nm;
-    short_name(w0, w1, w2, o, l, nm);
-    if (l > kShortName) {
-      if (l <= kInlineName) {
-        const u64* bw = reinterpret_cast<const u64*>(src.blob);
-        const u64 last = (o + l - 1) >> 3, w3i = (o >> 3) + 3;
-        inline_name(w0, w1, w2, bw[w3i < last ? w3i : last], o, l, nm);
-      } else {
-        load_name_wide<false>(src.blob, o, l, nm);
-      }
-    }
-    bool missed = false;
-    if (valid) {
-      const u64 tag = T.tag(nm.h);
-      int hidx = -1;
-      if (nh && l <= kInlineName) {
-        for (u32 hs = hot_home(tag);; hs = (hs + 1) & (kHotLds - 1)) {
-          const u32 e = hslot[hs];
-          if (!e) break;
-          if (htag[e - 1] == tag && hw0[e - 1] == nm.w0 && hw1[e - 1] == nm.w1 &&
-              hw2[e - 1] == nm.w2) {
-            hidx = (int)e - 1;
-            break;
-          }
-        }
-      }
-      if (hidx >= 0) {
-        slot_out[i] = hrec[hidx];
-      } else {
-        u32 s;
-        Rec r;
-        const int pr = probe(T, nm, src.blob, &s, &r);
-        if (pr == kFound) slot_out[i] = s;
-        else {
-          missed = true;
-          if (pr == kFull) atomicOr(&ctr[8], 1u);
-        }
-      }
-    }
-    if (miss.base) miss.append(chunk, missed, i);
-  }
-}
-
 // ------------------------------------------------------------- inserts ---
 // Round of the insert pipeline.  Claim: CAS an empty tag slot.  A same-tag
 // slot claimed in this round (not yet published) cannot be name-checked, so

@@ -9,6 +9,7 @@
 #   tests [PYTEST ARGS]   pytest -m gpu (e.g. 'tests -k fullsize')      tests.log
 #   smoke                 __graft_entry__.smoke()                        smoke.log
 #   bench NAME [ARGS]     python bench.py ARGS                           NAME.json / NAME.err
+#   benchv NAME VAR [ARGS] bench.py ARGS on tools/var/VAR.so (tools/build_variants.sh)
 #   gloo2 NAME [ARGS]     bench.py --gpus 2 --dist-backend gloo ARGS     (two ranks, one GPU)
 #   prof NAME [ARGS]      rocprofv3 --kernel-trace --stats over bench.py NAME/ (+ NAME.json)
 #   profpy NAME SCRIPT [ARGS]  rocprofv3 --kernel-trace --stats over python3 SCRIPT ARGS   NAME/
@@ -46,6 +47,13 @@ for spec in "$@"; do
       name=$1; shift
       echo "[$(date +%T)] bench $name: $*" | tee -a "$O/steps.log"
       timeout -k 10 900 python3 -u bench.py "$@" > "$O/$name.json" 2> "$O/$name.err"
+      rc=$?; echo "[$(date +%T)] rc=$rc" | tee -a "$O/steps.log"
+      tail -1 "$O/$name.json" | cut -c1-600
+      if [ $rc -ne 0 ]; then tail -30 "$O/$name.err"; exit $rc; fi ;;
+    benchv)   # benchv NAME VARIANT [ARGS]: bench.py on tools/var/VARIANT.so
+      name=$1; var=$2; shift 2
+      echo "[$(date +%T)] bench $name ($var): $*" | tee -a "$O/steps.log"
+      PATROLHIP_LIB=tools/var/$var.so timeout -k 10 900 python3 -u bench.py "$@" > "$O/$name.json" 2> "$O/$name.err"
       rc=$?; echo "[$(date +%T)] rc=$rc" | tee -a "$O/steps.log"
       tail -1 "$O/$name.json" | cut -c1-600
       if [ $rc -ne 0 ]; then tail -30 "$O/$name.err"; exit $rc; fi ;;
