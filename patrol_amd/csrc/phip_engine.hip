@@ -1401,18 +1401,24 @@ int small_datagrams(phip_handle* h, const uint8_t* bytes, const uint64_t* offs, 
 // ------------------------------------------------------- owner routing ----
 // The pack of phip_route_pack (and of phip_group_receive's chunks), queued on
 // stream `st` without a host synchronisation.
-// One wave per tile of `span` messages, eight per workgroup.  12 workgroups
+// One workgroup per tile of `span` messages.  12 workgroups
 // per CU: k_route_count holds 4 per CU, k_route_scatter 3, so both grids run
 // in whole rounds (no tail round of a quarter of the chip).
+// (tiles per CU: 12 = whole rounds of both grids; fewer, longer tiles also
+// mean fewer combined messages, one per hot name a workgroup saw)
+#ifndef PHIP_ROUTE_WG_PER_CU
+#define PHIP_ROUTE_WG_PER_CU 12
+#endif
 struct RoutePlan {
   u32 nblk, ntile, span;
   size_t cells;
 };
 static RoutePlan route_plan(const phip_handle* h, u32 n, u32 world) {
   RoutePlan p;
-  p.nblk = (u32)std::max<u64>(1, std::min<u64>((n + kRouteBlock - 1) / kRouteBlock, (u64)h->ncu * 12));
-  p.ntile = p.nblk * kRouteWaves;
-  p.span = (u32)(((u64)n + p.ntile - 1) / p.ntile + 63) & ~63u;
+  p.nblk = (u32)std::max<u64>(1, std::min<u64>((n + kRouteStep - 1) / kRouteStep,
+                                                (u64)h->ncu * PHIP_ROUTE_WG_PER_CU));
+  p.ntile = p.nblk;   // one tile per workgroup, a whole number of scatter steps
+  p.span = (u32)((((u64)n + p.ntile - 1) / p.ntile + kRouteStep - 1) / kRouteStep * kRouteStep);
   p.cells = (size_t)world * p.ntile;
   return p;
 }

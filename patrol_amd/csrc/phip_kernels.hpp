@@ -3026,13 +3026,19 @@ __global__ void k_dump_gather(const u32* __restrict__ list, u32 n, const Rec* __
 // Owner routing: the one exchange step of a sharded merge.
 // owner(name) = ((fnv1a64(name) >> 32) * world) >> 32 (patrol_amd.shard).
 //
-// Layout: every wave owns a contiguous tile of `span` messages.  The count
-// pass fills cells [owner][tile] with message and name-byte counts; their
-// exclusive scans are each (owner, tile)'s base in the owner-major send
-// buffers, so an owner's segment holds its messages tile after tile, each
-// tile's in their original order (a stable partition).  No barrier inside
-// the loops: a wave ranks its lanes per owner with ballots and keeps its own
-// running place per owner in LDS.
+// Layout: every workgroup owns a contiguous tile of `span` messages.  The
+// count pass fills cells [owner][tile] with message and name-byte counts;
+// their exclusive scans are each (owner, tile)'s base in the owner-major
+// send buffers, so an owner's segment holds its messages tile after tile,
+// each tile's in their original order (a stable partition).  The scatter
+// walks its tile in steps of kRouteStep messages, all eight waves together:
+// each wave ranks its own lanes per owner (ballots / DPP sums, a running
+// place per owner in the wave's LDS row), one barrier makes every wave's
+// totals visible, and a wave's messages for owner o follow those of the
+// waves before it.  So each step writes one contiguous run per owner and
+// column from the whole workgroup: a chip-wide handful of open output lines
+// per owner, where per-wave tiles kept ~30k partly written lines per XCD and
+// the L2 wrote them back in 32-byte pieces (2.4x the bytes, round 3).
 //
 // Sender-side combine (flag PHIP_ROUTE_COMBINE): a Zipf batch
 // puts most messages on a few names, and in the clean domain (no incast, no
@@ -3049,13 +3055,20 @@ constexpr u32 kRouteBlock = 512;
 constexpr u32 kRouteWaves = kRouteBlock / 64;
 constexpr u16 kRouteHot = 0x8000;   // route code: combined into hot entry (low bits)
 #ifndef PHIP_ROUTE_UNROLL
-#define PHIP_ROUTE_UNROLL 2
+#define PHIP_ROUTE_UNROLL 1   // chunks per wave and scatter step: 1 1.81 ms, 2 2.01 ms (100M, 8 owners)
 #endif
 constexpr u32 kRU = PHIP_ROUTE_UNROLL;   // chunks of 64 messages per wave step
 #ifndef PHIP_ROUTE_COUNT_UNROLL
 #define PHIP_ROUTE_COUNT_UNROLL 2
 #endif
 constexpr u32 kRUC = PHIP_ROUTE_COUNT_UNROLL;   // k_route_count's (it holds less per message)
+#ifndef PHIP_ROUTE_COUNT_CONTIG
+#define PHIP_ROUTE_COUNT_CONTIG 0   // waves count contiguous eighths of the tile (else interleaved): 0.71 vs 0.70 ms
+#endif
+#ifndef PHIP_ROUTE_COUNT_PACKED
+#define PHIP_ROUTE_COUNT_PACKED 0   // world <= 8: packed wave sums (else LDS atomics): 0.86 vs 0.70 ms
+#endif
+constexpr u32 kRouteStep = kRouteWaves * 64 * kRU;   // messages a scatter step takes
 
 __device__ inline u32 owner_of_hash(u64 h, u32 world) {
   return (u32)(((h >> 32) * (u64)world) >> 32);
@@ -3162,6 +3175,19 @@ __device__ inline void route_lds_load(RouteLds& L, const RouteHot* dir, u32 nh) 
   }
 }
 
+// What the scatter needs of the directory: the combined messages' names and
+// owners (it reads the route codes the count pass wrote, not the hash table).
+struct RouteNames {
+  u64 w0[kRouteHotMax], w1[kRouteHotMax];
+  u32 owner[kRouteHotMax];
+};
+__device__ inline void route_names_load(RouteNames& D, const RouteHot* dir, u32 nh) {
+  for (u32 j = threadIdx.x; j < nh; j += kRouteBlock) {
+    const RouteHot d = dir[j];
+    D.w0[j] = d.w0; D.w1[j] = d.w1; D.owner[j] = d.owner;
+  }
+}
+
 __device__ inline int route_hot_find(const RouteLds& L, const Name& nm) {
   const u32 tag = (u32)(nm.h >> 48);
   for (u32 hs = route_home(nm.h);; hs = (hs + 1) & (kRouteLds - 1)) {
@@ -3171,6 +3197,22 @@ __device__ inline int route_hot_find(const RouteLds& L, const Name& nm) {
     if ((v >> 16) == tag && L.h[e - 1] == nm.h && L.w0[e - 1] == nm.w0 && L.w1[e - 1] == nm.w1)
       return (int)e - 1;
   }
+}
+
+// Inclusive wave sum scan with DPP moves (VALU only; the row_shr /
+// row_bcast pattern of wave_incl_max).  All 64 lanes must be active.
+template <int Ctrl, int RowMask = 0xF>
+__device__ inline u32 dpp_u32(u32 v) {
+  return (u32)__builtin_amdgcn_update_dpp(0, (int)v, Ctrl, RowMask, 0xF, true);
+}
+__device__ inline u32 wave_incl_sum(u32 x) {
+  x += dpp_u32<0x111>(x);
+  x += dpp_u32<0x112>(x);
+  x += dpp_u32<0x114>(x);
+  x += dpp_u32<0x118>(x);
+  x += dpp_u32<0x142, 0xA>(x);
+  x += dpp_u32<0x143, 0xC>(x);
+  return x;
 }
 
 constexpr u32 kRoutePlain = 0, kRouteCombine = 1, kRouteRecount = 2;   // k_route_count modes
@@ -3198,11 +3240,21 @@ __global__ __launch_bounds__(kRouteBlock) void k_route_count(
   route_lds_load(L, dir, nh);
   __syncthreads();
   const u32 wave = threadIdx.x / 64, lane = threadIdx.x & 63;
-  const u32 tile = blockIdx.x * kRouteWaves + wave;
+  const u32 tile = blockIdx.x;
   const u64 t0 = (u64)tile * span, t1 = min((u64)n, t0 + span);
-  // kRUC chunks of 64 per step, their loads issued together (the loads of one
-  // message depend on each other; those of different chunks do not)
-  for (u64 b0 = t0; b0 < t1; b0 += 64 * kRUC) {
+  // kRUC chunks of 64 per wave step, their loads issued together (the loads
+  // of one message depend on each other; those of different chunks do not);
+  // the waves of the workgroup interleave over its tile
+  u32 acc_c = 0, acc_b = 0;   // world <= 8: lane o's totals for owner o
+#if PHIP_ROUTE_COUNT_CONTIG
+  // every wave a contiguous eighth of the tile (the tile is whole steps)
+  const u64 wspan = ((u64)span / kRouteWaves + 63) & ~63ull;
+  const u64 w0b = t0 + wave * wspan, wend = min(t1, w0b + wspan);
+  for (u64 b0 = w0b; b0 < wend; b0 += 64 * kRUC) {
+#else
+  const u64 wend = t1;
+  for (u64 b0 = t0 + (u64)wave * 64 * kRUC; b0 < t1; b0 += (u64)kRouteWaves * 64 * kRUC) {
+#endif
     u32 o[kRUC], len[kRUC];
     int hidx[kRUC];
     bool valid[kRUC];
@@ -3211,7 +3263,7 @@ __global__ __launch_bounds__(kRouteBlock) void k_route_count(
 #pragma unroll
     for (u32 u = 0; u < kRUC; ++u) {
       const u64 i = b0 + u * 64 + lane;
-      valid[u] = i < t1;
+      valid[u] = i < wend;   // (the last step of a wave's range may reach past it)
       const u32 ic = (u32)(valid[u] ? i : t0);
       src.template get<true>(ic, off[u], len[u]);
       if (comb) { ra[u] = ld<true>(a + ic); rt[u] = ld<true>(t + ic); }
@@ -3241,13 +3293,50 @@ __global__ __launch_bounds__(kRouteBlock) void k_route_count(
       if (valid[u]) code[i] = hidx[u] >= 0 ? (u16)(kRouteHot | (u32)hidx[u]) : (u16)o[u];
       if (hidx[u] >= 0) hit[hidx[u]] = 1;
     }
+    bool small = PHIP_ROUTE_COUNT_PACKED && world <= 8;
 #pragma unroll
-    for (u32 u = 0; u < kRUC; ++u) {   // the wave's own row: LDS atomics, no cross-lane loop
-      if (valid[u] && hidx[u] < 0) {
-        atomicAdd(&wc[wave][o[u]], 1u);
-        atomicAdd(&wb[wave][o[u]], len[u]);
+    for (u32 u = 0; u < kRUC; ++u) small &= !__ballot(valid[u] && hidx[u] < 0 && len[u] > 255);
+    if (small) {
+      // up to 8 owners: the chunks' counts and name bytes as packed wave
+      // sums (8-bit counts, four owners a register; 16-bit byte sums, two a
+      // register), lane o keeping owner o's totals: no LDS atomics (8
+      // owners' same-address atomics were half the LDS cycles)
+      u32 pc[2] = {0, 0}, pb[4] = {0, 0, 0, 0};
+#pragma unroll
+      for (u32 u = 0; u < kRUC; ++u) {
+        const bool take = valid[u] && hidx[u] < 0;
+#pragma unroll
+        for (u32 r = 0; r < 2; ++r) pc[r] += (take && (o[u] >> 2) == r) ? 1u << (8 * (o[u] & 3)) : 0u;
+#pragma unroll
+        for (u32 r = 0; r < 4; ++r) pb[r] += (take && (o[u] >> 1) == r) ? len[u] << (16 * (o[u] & 1)) : 0u;
+      }
+      const u32 ol = lane & 7;
+      u32 mc = 0, mb = 0;
+#pragma unroll
+      for (u32 r = 0; r < 2; ++r) {
+        const u32 tot = (u32)__builtin_amdgcn_readlane((int)wave_incl_sum(pc[r]), 63);
+        if ((ol >> 2) == r) mc = (tot >> (8 * (ol & 3))) & 0xFFu;
+      }
+#pragma unroll
+      for (u32 r = 0; r < 4; ++r) {
+        const u32 tot = (u32)__builtin_amdgcn_readlane((int)wave_incl_sum(pb[r]), 63);
+        if ((ol >> 1) == r) mb = (tot >> (16 * (ol & 1))) & 0xFFFFu;
+      }
+      acc_c += mc;
+      acc_b += mb;
+    } else {
+#pragma unroll
+      for (u32 u = 0; u < kRUC; ++u) {   // the wave's own row: LDS atomics, no cross-lane loop
+        if (valid[u] && hidx[u] < 0) {
+          atomicAdd(&wc[wave][o[u]], 1u);
+          atomicAdd(&wb[wave][o[u]], len[u]);
+        }
       }
     }
+  }
+  if (lane < world && lane < 8) {   // the packed sums' lane totals
+    wc[wave][lane] += acc_c;
+    wb[wave][lane] += acc_b;
   }
   __syncthreads();
   if (wave == kRouteWaves - 1) {   // the workgroup's combined messages
@@ -3258,9 +3347,14 @@ __global__ __launch_bounds__(kRouteBlock) void k_route_count(
     }
   }
   __syncthreads();
-  for (u32 o = lane; o < world; o += 64) {
-    cnt[(u64)o * ntile + tile] = wc[wave][o];
-    bytes[(u64)o * ntile + tile] = wb[wave][o];
+  if (wave == 0) {   // the workgroup's cells
+    for (u32 o = lane; o < world; o += 64) {
+      u32 c = 0, b = 0;
+#pragma unroll
+      for (u32 w = 0; w < kRouteWaves; ++w) { c += wc[w][o]; b += wb[w][o]; }
+      cnt[(u64)o * ntile + tile] = c;
+      bytes[(u64)o * ntile + tile] = b;
+    }
   }
 }
 
@@ -3296,22 +3390,6 @@ __device__ inline void route_place(bool take, u32 o, u32 len, u32* run, u32* run
     if (lane == leader) { run[ob] = base + __popcll(m); runb[ob] = bbase + tot; }
     rest &= ~m;
   }
-}
-
-// Inclusive wave sum scan with DPP moves (VALU only; the row_shr /
-// row_bcast pattern of wave_incl_max).  All 64 lanes must be active.
-template <int Ctrl, int RowMask = 0xF>
-__device__ inline u32 dpp_u32(u32 v) {
-  return (u32)__builtin_amdgcn_update_dpp(0, (int)v, Ctrl, RowMask, 0xF, true);
-}
-__device__ inline u32 wave_incl_sum(u32 x) {
-  x += dpp_u32<0x111>(x);
-  x += dpp_u32<0x112>(x);
-  x += dpp_u32<0x114>(x);
-  x += dpp_u32<0x118>(x);
-  x += dpp_u32<0x142, 0xA>(x);
-  x += dpp_u32<0x143, 0xC>(x);
-  return x;
 }
 
 // route_place for world <= 4 * NC (and 2 * NB == 4 * NC) and names of <= 255
@@ -3440,35 +3518,46 @@ __global__ __launch_bounds__(kRouteBlock) __attribute__((amdgpu_waves_per_eu(6, 
     const u16* __restrict__ code, const u32* __restrict__ cbase, const u32* __restrict__ bbase,
     u8* __restrict__ out_names, u32* __restrict__ out_lens, uint64_t* __restrict__ out_a,
     uint64_t* __restrict__ out_t, int64_t* __restrict__ out_e) {
-  __shared__ RouteLds L;
-  __shared__ u32 run[kRouteWaves][kRouteMaxWorld], runb[kRouteWaves][kRouteMaxWorld];
+  __shared__ RouteNames L;
+  // per step (two parities, so one barrier a step suffices): each wave's own
+  // running place per owner, and the workgroup's place before the step
+  __shared__ u32 lrun[2][kRouteWaves][kRouteMaxWorld], lrunb[2][kRouteWaves][kRouteMaxWorld];
+  __shared__ u32 run[2][kRouteMaxWorld], runb[2][kRouteMaxWorld];
   __shared__ u64 hmax[3][kRouteHotMax];
   __shared__ u32 hit[kRouteHotMax];
   __shared__ u32 nstage[kRouteWaves][kStageWords];
   const u32 nh = route_hot_n(hot, ctr);
   const u32 wave = threadIdx.x / 64, lane = threadIdx.x & 63;
-  const u32 tile = blockIdx.x * kRouteWaves + wave;
+  const u32 tile = blockIdx.x;
   for (u32 j = threadIdx.x; j < kRouteHotMax; j += kRouteBlock) {
     hit[j] = 0; hmax[0][j] = 0; hmax[1][j] = 0; hmax[2][j] = 0;
   }
-  for (u32 o = lane; o < world; o += 64) {
-    run[wave][o] = cbase[(u64)o * ntile + tile];
-    runb[wave][o] = bbase[(u64)o * ntile + tile];
-  }
-  route_lds_load(L, dir, nh);
+  if (wave == 0)
+    for (u32 o = lane; o < world; o += 64) {
+      run[0][o] = cbase[(u64)o * ntile + tile];
+      runb[0][o] = bbase[(u64)o * ntile + tile];
+    }
+  route_names_load(L, dir, nh);
   __syncthreads();
   const u64 t0 = (u64)tile * span, t1 = min((u64)n, t0 + span);
   u32* stg = nstage[wave];
-  // per owner lane: the run's start in this tile and the carried dword
-  u32 rt0 = lane < world ? runb[wave][lane] : 0u, pend = 0;
-  for (u64 b0 = t0; b0 < t1; b0 += 64 * kRU) {
-    u32 c[kRU], len[kRU];
+  u32 p = 0;
+  for (u64 s0 = t0; s0 < t1; s0 += kRouteStep, p ^= 1) {
+    u32* lr = lrun[p][wave];
+    u32* lrb = lrunb[p][wave];
+    for (u32 o = lane; o < world; o += 64) { lr[o] = 0; lrb[o] = 0; }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    u32 c[kRU], len[kRU], dst[kRU], dby[kRU], bo_l[kRU], be_l[kRU];
     u64 off[kRU], va[kRU], vt[kRU], w0[kRU], w1[kRU], w2[kRU];
     i64 ve[kRU];
     bool valid[kRU];
+    // (issuing the next step's loads before this step's barrier measured the
+    // same, 1.70 ms per 100M: the step is not bound by these loads' latency)
 #pragma unroll
     for (u32 u = 0; u < kRU; ++u) {   // every load unconditional (index clamped into the tile)
-      const u64 i = b0 + u * 64 + lane;
+      const u64 i = s0 + (u64)(wave * kRU + u) * 64 + lane;
       valid[u] = i < t1;
       const u32 ic = (u32)(valid[u] ? i : t0);
       c[u] = code[ic];
@@ -3478,6 +3567,8 @@ __global__ __launch_bounds__(kRouteBlock) __attribute__((amdgpu_waves_per_eu(6, 
     // the name as three aligned words (all of a name of <= 16 bytes)
 #pragma unroll
     for (u32 u = 0; u < kRU; ++u) load_words3<false>(src.blob, off[u], len[u], w0[u], w1[u], w2[u]);
+    // 1. this wave's ranks per owner, chunk after chunk (lane o keeps owner
+    //    o's byte run of every chunk for the name staging)
 #pragma unroll
     for (u32 u = 0; u < kRU; ++u) {
       const bool comb = valid[u] && (c[u] & kRouteHot);
@@ -3491,64 +3582,95 @@ __global__ __launch_bounds__(kRouteBlock) __attribute__((amdgpu_waves_per_eu(6, 
         if (ee > hmax[2][j]) atomicMax(&hmax[2][j], ee);
         hit[j] = 1;
       }
-      const u32 bo = lane < world ? runb[wave][lane] : 0u;   // owner runs before this chunk
-      u32 dst = 0, dby = 0;
+      bo_l[u] = lane < world ? lrb[lane] : 0u;
       const u32 pl = plain ? len[u] : 0u;
+      dst[u] = 0; dby[u] = 0;
       if (world <= 8 && !__ballot(pl > 255))
-        route_place_packed<2, 4>(plain, c[u], pl, run[wave], runb[wave], dst, dby);
+        route_place_packed<2, 4>(plain, c[u], pl, lr, lrb, dst[u], dby[u]);
       else if (world <= 16 && !__ballot(pl > 255))
-        route_place_packed<4, 8>(plain, c[u], pl, run[wave], runb[wave], dst, dby);
+        route_place_packed<4, 8>(plain, c[u], pl, lr, lrb, dst[u], dby[u]);
       else
-        route_place(plain, c[u], pl, run[wave], runb[wave], dst, dby);
-      const u32 be = lane < world ? runb[wave][lane] : 0u;
-      if (plain) {
-        out_lens[dst] = len[u];
-        out_a[dst] = va[u];
-        out_t[dst] = vt[u];
-        out_e[dst] = ve[u];
+        route_place(plain, c[u], pl, lr, lrb, dst[u], dby[u]);
+      be_l[u] = lane < world ? lrb[lane] : 0u;
+      c[u] = plain ? c[u] : 0xFFFFu;   // plain lanes keep their owner
+    }
+    __syncthreads();   // every wave's totals for this step are in LDS
+    // 2. this wave's base per owner: the workgroup's place before the step
+    //    plus the waves before this one (lane o: owner o); wave 0 also moves
+    //    the workgroup's place past the step (the other parity)
+    u32 pc = 0, pb = 0;
+    if (lane < world) {
+      pc = run[p][lane];
+      pb = runb[p][lane];
+      u32 tc = 0, tb = 0;
+#pragma unroll
+      for (u32 w = 0; w < kRouteWaves; ++w) {
+        const u32 xc = lrun[p][w][lane], xb = lrunb[p][w][lane];
+        if (w < wave) { pc += xc; pb += xb; }
+        tc += xc; tb += xb;
       }
+      if (wave == 0) {
+        run[p ^ 1][lane] = run[p][lane] + tc;
+        runb[p ^ 1][lane] = runb[p][lane] + tb;
+      }
+    }
+    // 3. the columns and the names
+#pragma unroll
+    for (u32 u = 0; u < kRU; ++u) {
+      const bool plain = c[u] != 0xFFFFu;
+      const u32 oo = plain ? c[u] : 0u;
+      const u32 d = (u32)__shfl((int)pc, (int)oo) + dst[u];
+      const u32 db = (u32)__shfl((int)pb, (int)oo) + dby[u];
+      if (plain) {
+        out_lens[d] = len[u];
+        out_a[d] = va[u];
+        out_t[d] = vt[u];
+        out_e[d] = ve[u];
+      }
+      // owner runs of this chunk [bo, be) (lane o), in the send buffer
+      const u32 bo = pb + bo_l[u], be = pb + be_l[u];
       const u32 sh = (u32)(off[u] & 7) * 8;
       const u64 n0 = sh ? (w0[u] >> sh) | (w1[u] << (64 - sh)) : w0[u];
       const u64 n1 = sh ? (w1[u] >> sh) | (w2[u] << (64 - sh)) : w1[u];
       if (!__ballot(plain && len[u] > 16)) {
-        route_names_staged(out_names, stg, world, plain, c[u], len[u], dby, n0, n1, bo, be, rt0, pend);
-      } else {   // a longer name: flush, bytes, and a new run from here
-        route_flush_pend(out_names, world, bo, rt0, pend);
-        if (plain) {
-          if (len[u] <= 16) {
+        // a run's first and last dwords are shared with the runs of other
+        // waves or steps: stored byte by byte (t0 = bo, pend flushed)
+        u32 pend = 0;
+        route_names_staged(out_names, stg, world, plain, oo, plain ? len[u] : 0u, db, n0, n1, bo,
+                           be, bo, pend);
+        route_flush_pend(out_names, world, be, bo, pend);
+      } else if (plain) {   // a longer name in the chunk: every name byte by byte
+        if (len[u] <= 16) {
 #pragma unroll
-            for (u32 k = 0; k < 16; ++k)
-              if (k < len[u]) out_names[dby + k] = (u8)((k < 8 ? n0 >> (8 * k) : n1 >> (8 * (k - 8))) & 0xFFu);
-          } else {
-            for (u32 k = 0; k < len[u]; ++k) out_names[dby + k] = src.blob[off[u] + k];
-          }
+          for (u32 k = 0; k < 16; ++k)
+            if (k < len[u]) out_names[db + k] = (u8)((k < 8 ? n0 >> (8 * k) : n1 >> (8 * (k - 8))) & 0xFFu);
+        } else {
+          for (u32 k = 0; k < len[u]; ++k) out_names[db + k] = src.blob[off[u] + k];
         }
-        rt0 = be;
-        pend = 0;
       }
     }
   }
-  route_flush_pend(out_names, world, lane < world ? runb[wave][lane] : 0u, rt0, pend);
   __syncthreads();
   if (wave != kRouteWaves - 1 || !nh) return;
-  // The workgroup's combined messages, in directory order, after this tile.
+  // The workgroup's combined messages, in directory order, after its tile
+  // (run[p] / runb[p]: its place after the last step).
   constexpr u64 kNaN = 0x7FF8000000000000ull;   // "no value": a merge never adopts NaN
   for (u32 j0 = 0; j0 < nh; j0 += 64) {
     const u32 j = j0 + lane;
     const bool on = j < nh && hit[j];
     const u32 o = on ? L.owner[j] : 0u;
-    const u32 len = on ? (u32)(L.w0[j] & 0xFFu) : 0u;
-    u32 dst = 0, dby = 0;
-    route_place(on, o, len, run[wave], runb[wave], dst, dby);
+    const u32 ln = on ? (u32)(L.w0[j] & 0xFFu) : 0u;
+    u32 d = 0, db = 0;
+    route_place(on, o, ln, run[p], runb[p], d, db);
     if (!on) continue;
     const u64 ma = hmax[0][j], mt = hmax[1][j];
-    out_lens[dst] = len;
-    out_a[dst] = ma ? dec_f64(ma) : kNaN;
-    out_t[dst] = mt ? dec_f64(mt) : kNaN;
-    out_e[dst] = (i64)(hmax[2][j] ^ kSign);
-    for (u32 k = 0; k < len; ++k) {   // name byte k is canonical byte k + 2
+    out_lens[d] = ln;
+    out_a[d] = ma ? dec_f64(ma) : kNaN;
+    out_t[d] = mt ? dec_f64(mt) : kNaN;
+    out_e[d] = (i64)(hmax[2][j] ^ kSign);
+    for (u32 k = 0; k < ln; ++k) {   // name byte k is canonical byte k + 2
       const u32 cb = k + 2;
-      out_names[dby + k] = (u8)((cb < 8 ? L.w0[j] >> (8 * cb) : L.w1[j] >> (8 * (cb - 8))) & 0xFFu);
+      out_names[db + k] = (u8)((cb < 8 ? L.w0[j] >> (8 * cb) : L.w1[j] >> (8 * (cb - 8))) & 0xFFu);
     }
   }
 }

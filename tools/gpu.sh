@@ -13,6 +13,7 @@
 #   gloo2 NAME [ARGS]     bench.py --gpus 2 --dist-backend gloo ARGS     (two ranks, one GPU)
 #   prof NAME [ARGS]      rocprofv3 --kernel-trace --stats over bench.py NAME/ (+ NAME.json)
 #   profpy NAME SCRIPT [ARGS]  rocprofv3 --kernel-trace --stats over python3 SCRIPT ARGS   NAME/
+#   passes NAME REGEX [ARGS]  tools/pmc_passes.sh over kernels matching REGEX (PMC_PASSES: ';'-list)
 #   pmc NAME [ARGS]       tools/profile_workload.sh TAG/NAME ARGS        (counter passes)
 #   py NAME SCRIPT [ARGS] python3 -u SCRIPT ARGS                         NAME.log
 set -u
@@ -71,6 +72,9 @@ for spec in "$@"; do
     profpy)
       name=$1; shift
       run 600 "$O/$name.log" rocprofv3 --kernel-trace --stats --output-format csv -d "$ROOT/$O/$name" -o run -- python3 -u "$@" ;;
+    passes)   # passes NAME REGEX [BENCH ARGS]: tools/pmc_passes.sh counter passes ($PMC_PASSES)
+      name=$1; rx=$2; shift 2
+      run 1200 "$O/$name.passes.log" bash tools/pmc_passes.sh "$TAG/$name" "$rx" "$@" ;;
     pmc)
       name=$1; shift
       run 1200 "$O/$name.pmc.log" bash tools/profile_workload.sh "$TAG/$name" "$@" ;;
