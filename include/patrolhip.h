@@ -506,9 +506,10 @@ phip_handle* phip_group_handle(phip_group* g, uint32_t i);
  * hot names at the sender), the members exchange the packed segments (one
  * all-to-all of the split sizes, then grouped send/recv per column), and
  * every owner merges what it received (phip_receive_soa, `now` for buckets
- * it creates).  The pack and the exchange are pipelined by chunks of 2^24
- * messages (the pack of chunk k+1 runs while chunk k travels); an owner
- * receives chunk by chunk, sources in rank order within a chunk, every
+ * it creates).  The pack, the exchange and the merge are pipelined by chunks
+ * of 2^24 messages (while chunk k travels, the pack of chunk k+1 and the
+ * owner's merge of chunk k-1 run); an owner merges chunk by chunk (one
+ * phip_receive_soa each), sources in rank order within a chunk, every
  * source's messages in their order (as peers' datagrams interleave in
  * Patrol: per-bucket order from one source is kept).  Every member runs the
  * longest batch's number of rounds (a shorter batch sends empty chunks).  sent[i] /

@@ -1423,23 +1423,26 @@ static RoutePlan route_plan(const phip_handle* h, u32 n, u32 world) {
   return p;
 }
 
-// Scratch of a pack of up to n messages (B_ROUTE: the per-(owner, tile)
-// cells, the route codes, its own counters) and the scans' temporary
-// storage (B_TEMP), sized before anything is queued: the packs of a
-// pipelined exchange reuse them in stream order, never reallocated midway.
+// Scratch of a pack of up to n messages, all in B_ROUTE: the per-(owner,
+// tile) cells, the route codes, its own counter block and the scans'
+// temporary storage.  Sized before anything is queued: the packs of a
+// pipelined exchange reuse it in stream order, and the owner's merges that
+// run beside them (phip_group_receive) touch none of it.
 static int route_scratch(phip_handle* h, u32 n, u32 world, u8** base, u32** pctr, size_t* scan_bytes,
-                  u8** temp) {
+                         u8** temp) {
   const RoutePlan p = route_plan(h, n, world);
-  // cells | codes | the pack's own counter block (16-byte aligned)
-  const size_t ctr_off = (4 * p.cells * sizeof(u32) + 2 * (size_t)n + 15) & ~(size_t)15;
-  int rc;
-  if ((rc = ensure(h, B_ROUTE, ctr_off + kCtrWords * sizeof(u32), base))) return rc;
-  *pctr = (u32*)(*base + ctr_off);
   size_t tb = 0;
   HIPCHK(h, rocprim::exclusive_scan(nullptr, tb, (u32*)nullptr, (u32*)nullptr, 0u, p.cells,
                                     rocprim::plus<u32>(), h->stream));
+  // cells | codes | counter block | scan temp (16-byte aligned parts)
+  const size_t ctr_off = (4 * p.cells * sizeof(u32) + 2 * (size_t)n + 15) & ~(size_t)15;
+  const size_t tmp_off = (ctr_off + kCtrWords * sizeof(u32) + 255) & ~(size_t)255;
+  int rc;
+  if ((rc = ensure(h, B_ROUTE, tmp_off + tb, base))) return rc;
+  *pctr = (u32*)(*base + ctr_off);
   *scan_bytes = tb;
-  return ensure(h, B_TEMP, tb, temp);
+  *temp = *base + tmp_off;
+  return PHIP_OK;
 }
 
 // Sender-side combine: the hot names of a strided sample of the

@@ -10,10 +10,11 @@
 // of each chunk's exchange.  With one process per GPU the calling thread is
 // the member's thread.
 //
-// Owner-routed Receive is pipelined by chunks of kChunk messages: the pack of
-// chunk k+1 (pack stream) runs while chunk k travels (exchange stream: the
-// split sizes, then the grouped per-peer send/recv), over two send sets; the
-// owner merges everything it received once, on the handle's stream.
+// Owner-routed Receive is pipelined by chunks of kChunk messages, over two
+// send sets and two receive sets: while chunk k travels (exchange stream: the
+// split sizes, then the grouped per-peer send/recv), the pack of chunk k+1
+// (pack stream) and the owner's merge of chunk k-1 (the handle's stream) run
+// beside it.
 //
 // Members sharing one GPU (phip_group_open_all with a device listed more
 // than once: several shards' tables on one device, e.g. to rehearse an
@@ -107,6 +108,16 @@ struct SendSet {
   bool x_pending = false;   // ev_x recorded for an exchange reading this set
 };
 
+// One chunk's received segments (sources in rank order), merged while the
+// next chunk travels.
+struct RecvSet {
+  Buf names, lens, offs, a, t, e;
+  u64 n = 0;                      // messages received into it
+  hipEvent_t ev_recv = nullptr;   // its exchange (exchange stream)
+  hipEvent_t ev_merged = nullptr; // its merge (handle stream)
+  bool merge_pending = false;     // ev_merged recorded for a merge reading it
+};
+
 struct Member {
   phip_handle* h = nullptr;
   bool own = false;            // opened by the group (phip_group_open_all)
@@ -116,8 +127,7 @@ struct Member {
   hipStream_t sp = nullptr, sx = nullptr;   // pack stream, exchange stream
   hipEvent_t ev_done = nullptr;             // the call's last exchange
   SendSet set[2];
-  // receive side: every chunk's segments, chunk-major, sources in rank order
-  Buf r_names, r_lens, r_offs, r_a, r_t, r_e;
+  RecvSet rset[2];             // chunk k is received into rset[k & 1]
   Buf scan_tmp, ae;
   u64* host_k = nullptr;       // pinned [world]: this member's chunk count, to every peer
   u64 k_local = 0;             // (shared-device groups read each other's)
@@ -270,27 +280,34 @@ Seg send_seg(const u64* hs, u32 W, u32 p) {
   return g;
 }
 
-// The owner's merge of n received messages (lengths, packed names, states):
+// The owner's merge of one received chunk (lengths, packed names, states):
 // name offsets by an inclusive scan of the lengths, then phip_receive_soa
-// (chunks in order; in each, sources in rank order, each in its order).
-int merge_received(Member& mb, hipStream_t st, u64 n, int64_t now) {
-  GHIP(mb, mb.r_offs.ensure(n * 4 + 8));
-  u32* offs = (u32*)mb.r_offs.p;
-  const u32* lens = (const u32*)mb.r_lens.p;
-  GHIP(mb, hipMemsetAsync(offs, 0, sizeof(u32), st));
-  size_t tb = 0;
-  GHIP(mb, rocprim::inclusive_scan(nullptr, tb, lens, offs + 1, (size_t)n, rocprim::plus<u32>(), st));
-  GHIP(mb, mb.scan_tmp.ensure(tb));
-  GHIP(mb, rocprim::inclusive_scan(mb.scan_tmp.p, tb, lens, offs + 1, (size_t)n,
-                                   rocprim::plus<u32>(), st));
-  phip_msgs rm{};
-  rm.n = (u32)n;
-  rm.names = (const uint8_t*)mb.r_names.p;
-  rm.name_offs = offs;
-  rm.added = (const u64*)mb.r_a.p;
-  rm.taken = (const u64*)mb.r_t.p;
-  rm.elapsed = (const int64_t*)mb.r_e.p;
-  GPHIP(mb, phip_receive_soa(mb.h, &rm, now, nullptr, PHIP_DEVICE_PTRS));
+// (sources in rank order, each in its order), on the handle's stream behind
+// the chunk's exchange.
+int merge_chunk(Member& mb, RecvSet& rs, hipStream_t st, int64_t now) {
+  if (rs.n) {
+    const u64 n = rs.n;
+    GHIP(mb, hipStreamWaitEvent(st, rs.ev_recv, 0));
+    GHIP(mb, rs.offs.ensure(n * 4 + 8));
+    u32* offs = (u32*)rs.offs.p;
+    const u32* lens = (const u32*)rs.lens.p;
+    GHIP(mb, hipMemsetAsync(offs, 0, sizeof(u32), st));
+    size_t tb = 0;
+    GHIP(mb, rocprim::inclusive_scan(nullptr, tb, lens, offs + 1, (size_t)n, rocprim::plus<u32>(), st));
+    GHIP(mb, mb.scan_tmp.ensure(tb));
+    GHIP(mb, rocprim::inclusive_scan(mb.scan_tmp.p, tb, lens, offs + 1, (size_t)n,
+                                     rocprim::plus<u32>(), st));
+    phip_msgs rm{};
+    rm.n = (u32)n;
+    rm.names = (const uint8_t*)rs.names.p;
+    rm.name_offs = offs;
+    rm.added = (const u64*)rs.a.p;
+    rm.taken = (const u64*)rs.t.p;
+    rm.elapsed = (const int64_t*)rs.e.p;
+    GPHIP(mb, phip_receive_soa(mb.h, &rm, now, nullptr, PHIP_DEVICE_PTRS));
+  }
+  GHIP(mb, hipEventRecord(rs.ev_merged, st));
+  rs.merge_pending = true;
   return PHIP_OK;
 }
 
@@ -308,33 +325,35 @@ phip_msgs chunk_of(const phip_msgs& in, u64 chunk, u64 k) {
   return c;
 }
 
-// Room in the receive buffers for `n` more messages and `nb` more name bytes
-// after the `msgs` / `bytes` already received (kept, on the exchange stream).
-int recv_room(Member& mb, u64 msgs, u64 bytes, u64 n, u64 nb) {
-  GHIP(mb, mb.r_lens.grow_keep((msgs + n) * 4 + 4, msgs * 4, mb.sx));
-  GHIP(mb, mb.r_a.grow_keep((msgs + n) * 8 + 8, msgs * 8, mb.sx));
-  GHIP(mb, mb.r_t.grow_keep((msgs + n) * 8 + 8, msgs * 8, mb.sx));
-  GHIP(mb, mb.r_e.grow_keep((msgs + n) * 8 + 8, msgs * 8, mb.sx));
-  GHIP(mb, mb.r_names.grow_keep(bytes + nb + 64, bytes, mb.sx));
+// Room in a receive set for n messages and nb name bytes, once the merge
+// of the chunk it held before is done.
+int recv_room(Member& mb, RecvSet& rs, u64 n, u64 nb) {
+  if (rs.merge_pending) GHIP(mb, hipEventSynchronize(rs.ev_merged));
+  rs.merge_pending = false;
+  GHIP(mb, rs.lens.ensure(n * 4 + 4));
+  GHIP(mb, rs.a.ensure(n * 8 + 8));
+  GHIP(mb, rs.t.ensure(n * 8 + 8));
+  GHIP(mb, rs.e.ensure(n * 8 + 8));
+  GHIP(mb, rs.names.ensure(nb + 64));
   return PHIP_OK;
 }
 
-// One segment from a source's send set (src) into this member's receive
-// buffers at chunk base (m0, b0), on stream st.
-int copy_seg(Member& mb, const SendSet& src, const Seg& s_, const Seg& d_, u64 m0, u64 b0,
+// One segment from a source's send set (src) into receive set rs, on
+// stream st.
+int copy_seg(Member& mb, const SendSet& src, const Seg& s_, const Seg& d_, RecvSet& rs,
              hipStream_t st) {
   if (!d_.rc) return PHIP_OK;
-  GHIP(mb, hipMemcpyAsync((u32*)mb.r_lens.p + m0 + d_.ro, (const u32*)src.lens.p + s_.so, d_.rc * 4,
+  GHIP(mb, hipMemcpyAsync((u32*)rs.lens.p + d_.ro, (const u32*)src.lens.p + s_.so, d_.rc * 4,
                           hipMemcpyDeviceToDevice, st));
   if (d_.rbytes)
-    GHIP(mb, hipMemcpyAsync((uint8_t*)mb.r_names.p + b0 + d_.rb, (const uint8_t*)src.names.p + s_.sb,
+    GHIP(mb, hipMemcpyAsync((uint8_t*)rs.names.p + d_.rb, (const uint8_t*)src.names.p + s_.sb,
                             d_.rbytes, hipMemcpyDeviceToDevice, st));
-  GHIP(mb, hipMemcpyAsync((u64*)mb.r_a.p + m0 + d_.ro, (const u64*)src.a.p + s_.so, d_.rc * 8,
+  GHIP(mb, hipMemcpyAsync((u64*)rs.a.p + d_.ro, (const u64*)src.a.p + s_.so, d_.rc * 8,
                           hipMemcpyDeviceToDevice, st));
-  GHIP(mb, hipMemcpyAsync((u64*)mb.r_t.p + m0 + d_.ro, (const u64*)src.t.p + s_.so, d_.rc * 8,
+  GHIP(mb, hipMemcpyAsync((u64*)rs.t.p + d_.ro, (const u64*)src.t.p + s_.so, d_.rc * 8,
                           hipMemcpyDeviceToDevice, st));
-  GHIP(mb, hipMemcpyAsync((int64_t*)mb.r_e.p + m0 + d_.ro, (const int64_t*)src.e.p + s_.so,
-                          d_.rc * 8, hipMemcpyDeviceToDevice, st));
+  GHIP(mb, hipMemcpyAsync((int64_t*)rs.e.p + d_.ro, (const int64_t*)src.e.p + s_.so, d_.rc * 8,
+                          hipMemcpyDeviceToDevice, st));
   return PHIP_OK;
 }
 
@@ -417,7 +436,7 @@ int member_receive(phip_group* g, Member& mb, const phip_msgs& in, int64_t now, 
   int rc;
   if ((rc = pack(0)) || (rc = sizes(0))) return rc;
   if (k_local > 1 && (rc = pack(1))) return rc;
-  u64 K = 1, n_send = 0, recv_msgs = 0, recv_bytes = 0;
+  u64 K = 1, n_send = 0, recv_msgs = 0;
   u64 packed = k_local > 1 ? 2 : 1;   // chunks whose pack is queued
   std::vector<Seg> plan;
   void* tm = phip_host::timing_begin(mb.h, "rccl_exchange", mb.sx);
@@ -445,10 +464,11 @@ int member_receive(phip_group* g, Member& mb, const phip_msgs& in, int64_t now, 
       c_recv += plan[p].rc;
       b_recv += plan[p].rbytes;
     }
-    if (recv_msgs + c_recv > 0xFFFFFFFFull || recv_bytes + b_recv > 0xFFFFFFFFull)
-      return fail(mb, PHIP_ERR_INVALID, "routed batch of %llu messages / %llu name bytes exceeds 2^32",
-                  (unsigned long long)(recv_msgs + c_recv), (unsigned long long)(recv_bytes + b_recv));
-    if ((rc = recv_room(mb, recv_msgs, recv_bytes, c_recv, b_recv))) return rc;
+    if (c_recv > 0xFFFFFFFFull || b_recv > 0xFFFFFFFFull)
+      return fail(mb, PHIP_ERR_INVALID, "routed chunk of %llu messages / %llu name bytes exceeds 2^32",
+                  (unsigned long long)c_recv, (unsigned long long)b_recv);
+    RecvSet& rs = mb.rset[k & 1];
+    if ((rc = recv_room(mb, rs, c_recv, b_recv))) return rc;
     // 4. the segments: one send and one receive per peer and column; this
     //    member's own segment is a device copy unless rccl_self
     if (g->shared) {
@@ -459,7 +479,7 @@ int member_receive(phip_group* g, Member& mb, const phip_msgs& in, int64_t now, 
           return fail(mb, PHIP_ERR_INVALID, "internal: member %u sends %llu/%llu, %u expects %llu/%llu",
                       p, (unsigned long long)s_.sc, (unsigned long long)s_.sbytes, mb.rank,
                       (unsigned long long)plan[p].rc, (unsigned long long)plan[p].rbytes);
-        if ((rc = copy_seg(mb, src.set[k & 1], s_, plan[p], recv_msgs, recv_bytes, mb.sx))) return rc;
+        if ((rc = copy_seg(mb, src.set[k & 1], s_, plan[p], rs, mb.sx))) return rc;
       }
     } else {
       const Seg& own = plan[mb.rank];
@@ -467,31 +487,36 @@ int member_receive(phip_group* g, Member& mb, const phip_msgs& in, int64_t now, 
         return fail(mb, PHIP_ERR_INVALID, "internal: own segment %llu/%llu vs %llu/%llu",
                     (unsigned long long)own.sc, (unsigned long long)own.sbytes,
                     (unsigned long long)own.rc, (unsigned long long)own.rbytes);
-      if (!rccl_self && (rc = copy_seg(mb, ss, own, own, recv_msgs, recv_bytes, mb.sx))) return rc;
+      if (!rccl_self && (rc = copy_seg(mb, ss, own, own, rs, mb.sx))) return rc;
       GNCCL(mb, ncclGroupStart());
       for (u32 p = 0; p < W; ++p) {
         if (p == mb.rank && !rccl_self) continue;
         const Seg& x = plan[p];
-        const u64 mo = recv_msgs + x.ro, bo = recv_bytes + x.rb;
         GNCCL(mb, ncclSend((u32*)ss.lens.p + x.so, x.sc, ncclUint32, p, mb.comm, mb.sx));
-        GNCCL(mb, ncclRecv((u32*)mb.r_lens.p + mo, x.rc, ncclUint32, p, mb.comm, mb.sx));
+        GNCCL(mb, ncclRecv((u32*)rs.lens.p + x.ro, x.rc, ncclUint32, p, mb.comm, mb.sx));
         GNCCL(mb, ncclSend((uint8_t*)ss.names.p + x.sb, x.sbytes, ncclUint8, p, mb.comm, mb.sx));
-        GNCCL(mb, ncclRecv((uint8_t*)mb.r_names.p + bo, x.rbytes, ncclUint8, p, mb.comm, mb.sx));
+        GNCCL(mb, ncclRecv((uint8_t*)rs.names.p + x.rb, x.rbytes, ncclUint8, p, mb.comm, mb.sx));
         GNCCL(mb, ncclSend((u64*)ss.a.p + x.so, x.sc, ncclUint64, p, mb.comm, mb.sx));
-        GNCCL(mb, ncclRecv((u64*)mb.r_a.p + mo, x.rc, ncclUint64, p, mb.comm, mb.sx));
+        GNCCL(mb, ncclRecv((u64*)rs.a.p + x.ro, x.rc, ncclUint64, p, mb.comm, mb.sx));
         GNCCL(mb, ncclSend((u64*)ss.t.p + x.so, x.sc, ncclUint64, p, mb.comm, mb.sx));
-        GNCCL(mb, ncclRecv((u64*)mb.r_t.p + mo, x.rc, ncclUint64, p, mb.comm, mb.sx));
+        GNCCL(mb, ncclRecv((u64*)rs.t.p + x.ro, x.rc, ncclUint64, p, mb.comm, mb.sx));
         GNCCL(mb, ncclSend((u64*)ss.e.p + x.so, x.sc, ncclUint64, p, mb.comm, mb.sx));
-        GNCCL(mb, ncclRecv((int64_t*)mb.r_e.p + mo, x.rc, ncclUint64, p, mb.comm, mb.sx));
+        GNCCL(mb, ncclRecv((int64_t*)rs.e.p + x.ro, x.rc, ncclUint64, p, mb.comm, mb.sx));
       }
       GNCCL(mb, ncclGroupEnd());
     }
     GHIP(mb, hipEventRecord(ss.ev_x, mb.sx));
+    GHIP(mb, hipEventRecord(rs.ev_recv, mb.sx));
     ss.x_pending = true;
+    rs.n = c_recv;
     n_send += c_send;
     recv_msgs += c_recv;
-    recv_bytes += b_recv;
+    // 6. the owner's merge of chunk k-1 beside chunk k's exchange (chunk
+    //    order: the merges queue on the handle's stream; a shared-device
+    //    member merges before it waits for its copies)
+    const bool merge_prev = k >= 1;
     if (g->shared) {
+      if (merge_prev && (rc = merge_chunk(mb, mb.rset[(k - 1) & 1], st, now))) return rc;
       // every member has copied chunk k out of every set k & 1 before any
       // packs chunk k + 2 into it
       GHIP(mb, hipEventSynchronize(ss.ev_x));
@@ -510,15 +535,18 @@ int member_receive(phip_group* g, Member& mb, const phip_msgs& in, int64_t now, 
         packed = k + 3;
       }
     }
+    if (!g->shared && merge_prev && (rc = merge_chunk(mb, mb.rset[(k - 1) & 1], st, now)))
+      return rc;
   }
   phip_host::timing_end(mb.h, tm);
   if (sent) *sent = n_send;
   if (merged) *merged = recv_msgs;
-  // 6. the owner's merge, on the handle's stream behind the last exchange
+  // the last chunk's merge; the handle's stream ends behind every exchange
+  // (the next call's packs reuse the send sets)
+  if ((rc = merge_chunk(mb, mb.rset[(K - 1) & 1], st, now))) return rc;
   GHIP(mb, hipEventRecord(mb.ev_done, mb.sx));
   GHIP(mb, hipStreamWaitEvent(st, mb.ev_done, 0));
-  if (recv_msgs == 0) return PHIP_OK;
-  return merge_received(mb, st, recv_msgs, now);
+  return PHIP_OK;
 }
 
 __global__ void k_max_into(int64_t* __restrict__ dst, const int64_t* __restrict__ src, u64 n) {
@@ -570,9 +598,12 @@ void destroy(phip_group* g) {
       for (hipEvent_t ev : {ss.ev_pack, ss.ev_sz, ss.ev_x})
         if (ev) (void)hipEventDestroy(ev);
     }
-    for (Buf* b : {&mb.r_names, &mb.r_lens, &mb.r_offs, &mb.r_a, &mb.r_t, &mb.r_e, &mb.scan_tmp,
-                   &mb.ae})
-      b->release();
+    for (RecvSet& rs : mb.rset) {
+      for (Buf* b : {&rs.names, &rs.lens, &rs.offs, &rs.a, &rs.t, &rs.e}) b->release();
+      for (hipEvent_t ev : {rs.ev_recv, rs.ev_merged})
+        if (ev) (void)hipEventDestroy(ev);
+    }
+    for (Buf* b : {&mb.scan_tmp, &mb.ae}) b->release();
     if (mb.host_k) (void)hipHostFree(mb.host_k);
     if (mb.ev_done) (void)hipEventDestroy(mb.ev_done);
     if (mb.sp) (void)hipStreamDestroy(mb.sp);
@@ -598,6 +629,12 @@ int alloc_member_state(phip_group* g) {
           hipEventCreateWithFlags(&ss.ev_sz, hipEventDisableTiming) != hipSuccess ||
           hipEventCreateWithFlags(&ss.ev_x, hipEventDisableTiming) != hipSuccess)
         return PHIP_ERR_HIP;
+    for (RecvSet& rs : mb.rset) {
+      rs.merge_pending = false;
+      if (hipEventCreateWithFlags(&rs.ev_recv, hipEventDisableTiming) != hipSuccess ||
+          hipEventCreateWithFlags(&rs.ev_merged, hipEventDisableTiming) != hipSuccess)
+        return PHIP_ERR_HIP;
+    }
   }
   return PHIP_OK;
 }

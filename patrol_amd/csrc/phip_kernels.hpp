@@ -3446,6 +3446,9 @@ __device__ inline void route_place_packed(bool take, u32 o, u32 len, u32* run, u
 // A chunk with a longer name takes the byte path (route_names_bytes) after a
 // flush, and the next chunk starts a new run.
 constexpr u32 kStageWords = (64 * 16) / 4 + 2 * kRouteMaxWorld;
+#ifndef PHIP_ROUTE_DIAG
+#define PHIP_ROUTE_DIAG 0   // TEMP timing breakdown
+#endif
 
 __device__ inline void route_store_bytes(u8* out, u32 from, u32 to, u32 word_start, u32 word) {
   for (u32 x = from; x < to; ++x) out[x] = (u8)(word >> (8 * (x - word_start)));
@@ -3470,11 +3473,10 @@ __device__ inline void route_names_staged(u8* __restrict__ out, u32* stg, u32 wo
   const u32 so = be - bo, lead = bo & 3u;
   const u32 dcnt = (lane < world && so) ? (lead + so + 3) >> 2 : 0u;
   const u32 pstart = wave_incl_sum(dcnt) - dcnt;   // dwords, exclusive over owners
-  const u32 total = (u32)__builtin_amdgcn_readlane((int)(pstart + dcnt), 63);
   if (dcnt && lead) stg[pstart] = pend;   // the run's first dword: bytes before bo
   const u32 oo = o & 63u;
   const u32 ps_o = (u32)__shfl((int)pstart, (int)oo), bo_o = (u32)__shfl((int)bo, (int)oo);
-  if (plain) {
+  if (plain && !(PHIP_ROUTE_DIAG & 4)) {
     u8* sb = reinterpret_cast<u8*>(stg);
     const u32 p = ps_o * 4 + (bo_o & 3u) + (dby - bo_o);
 #pragma unroll
@@ -3484,23 +3486,24 @@ __device__ inline void route_names_staged(u8* __restrict__ out, u32* stg, u32 wo
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  // The stores: lanes in groups of G per owner (G = 64 / world rounded up to
+  // a power of two), group g storing owner g's staged dwords G at a time, so
+  // a lane's owner and run are fixed for the whole chunk (a search of the
+  // owners per staged dword cost a third of the name stores).
   u32* outw = reinterpret_cast<u32*>(out);
-  for (u32 tb = 0; tb < total; tb += 64) {   // uniform: every lane takes part in the shuffles
-    const u32 t = tb + lane;
-    // owner of staged dword t: the last owner with a run whose dwords start at or before t
-    u32 w = 0;
-    for (u32 x = 0; x < world; ++x) {
-      const u32 sx = (u32)__builtin_amdgcn_readlane((int)pstart, (int)x);
-      const u32 dx = (u32)__builtin_amdgcn_readlane((int)dcnt, (int)x);
-      if (dx && sx <= t) w = x;
-    }
-    const u32 bw = (u32)__shfl((int)bo, (int)w), ew = (u32)__shfl((int)be, (int)w);
-    const u32 tw = (u32)__shfl((int)t0, (int)w), sw = (u32)__shfl((int)pstart, (int)w);
-    const u32 gdw = (bw >> 2) + (t - sw);
-    const u32 word = stg[min(t, total - 1)];
-    if (t < total && 4 * gdw + 4 <= ew) {   // complete
-      if (4 * gdw >= tw) outw[gdw] = word;
-      else route_store_bytes(out, tw, 4 * gdw + 4, 4 * gdw, word);   // the tile's first dword
+  const u32 lg = 6u - (world <= 1 ? 0u : 32u - (u32)__builtin_clz(world - 1));
+  const u32 og = min(lane >> lg, 63u), k0 = lane & ((1u << lg) - 1u);
+  const u32 ps_g = (u32)__shfl((int)pstart, (int)og), dc_g = og < world ? (u32)__shfl((int)dcnt, (int)og) : 0u;
+  const u32 bw = (u32)__shfl((int)bo, (int)og), ew = (u32)__shfl((int)be, (int)og);
+  const u32 tw = (u32)__shfl((int)t0, (int)og);
+  for (u32 k = k0; __ballot(k < dc_g) && !(PHIP_ROUTE_DIAG & 8); k += 1u << lg) {
+    if (k < dc_g) {
+      const u32 gdw = (bw >> 2) + k;
+      const u32 word = stg[ps_g + k];
+      if (4 * gdw + 4 <= ew) {   // complete
+        if (4 * gdw >= tw) outw[gdw] = word;
+        else route_store_bytes(out, tw, 4 * gdw + 4, 4 * gdw, word);   // the tile's first dword
+      }
     }
   }
   // the carried dword: lane o keeps the one holding its run's end
@@ -3621,7 +3624,7 @@ __global__ __launch_bounds__(kRouteBlock) __attribute__((amdgpu_waves_per_eu(6, 
       const u32 oo = plain ? c[u] : 0u;
       const u32 d = (u32)__shfl((int)pc, (int)oo) + dst[u];
       const u32 db = (u32)__shfl((int)pb, (int)oo) + dby[u];
-      if (plain) {
+      if (plain && !(PHIP_ROUTE_DIAG & 2)) {
         out_lens[d] = len[u];
         out_a[d] = va[u];
         out_t[d] = vt[u];
@@ -3629,6 +3632,7 @@ __global__ __launch_bounds__(kRouteBlock) __attribute__((amdgpu_waves_per_eu(6, 
       }
       // owner runs of this chunk [bo, be) (lane o), in the send buffer
       const u32 bo = pb + bo_l[u], be = pb + be_l[u];
+      if (PHIP_ROUTE_DIAG & 1) continue;
       const u32 sh = (u32)(off[u] & 7) * 8;
       const u64 n0 = sh ? (w0[u] >> sh) | (w1[u] << (64 - sh)) : w0[u];
       const u64 n1 = sh ? (w1[u] >> sh) | (w2[u] << (64 - sh)) : w1[u];

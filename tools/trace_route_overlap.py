@@ -12,9 +12,11 @@ member a Zipf(1.1) batch of --n messages (three 2^24-message chunks at the
 default), and runs two warmup and three timed phip_group_receive calls.
 
 `show` reads the trace and reports, for the last call, every pack kernel
-(k_route_*) and every exchange copy (__amd_rocclr_copyBuffer) by stream,
-and the time during which a pack and a copy ran at the same moment: the
-pack of chunk k+1 beside the copies of chunk k.
+(k_route_*) and every exchange copy (__amd_rocclr_copyBuffer, or the RCCL kernels of an
+RCCL group) by stream,
+and the time during which a pack and a copy ran at the same moment (the
+pack of chunk k+1 beside the copies of chunk k), and a merge and a copy
+(the owner's merge of chunk k-1 beside them).
 """
 import argparse
 import csv
@@ -72,7 +74,7 @@ def show(args):
     pack = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in call
             if short(r).startswith("k_route_")]
     copy = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in call
-            if "copyBuffer" in r["Kernel_Name"]]
+            if "copyBuffer" in r["Kernel_Name"] or "nccl" in r["Kernel_Name"].lower()]
     merge = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in call
              if short(r) == "k_receive_fast"]
 
@@ -107,6 +109,7 @@ def show(args):
         "pack_busy_us": total(P) / 1e3, "copy_busy_us": total(X) / 1e3,
         "merge_busy_us": total(M) / 1e3,
         "pack_and_copy_overlap_us": inter(P, X) / 1e3,
+        "merge_and_copy_overlap_us": inter(M, X) / 1e3,
         "timeline": [dict(kernel=short(r)[:40], queue=r.get("Queue_Id", r.get("Stream_Id")),
                           start_us=(int(r["Start_Timestamp"]) - t0) / 1e3,
                           end_us=(int(r["End_Timestamp"]) - t0) / 1e3) for r in call],
