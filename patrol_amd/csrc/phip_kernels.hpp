@@ -3446,9 +3446,6 @@ __device__ inline void route_place_packed(bool take, u32 o, u32 len, u32* run, u
 // A chunk with a longer name takes the byte path (route_names_bytes) after a
 // flush, and the next chunk starts a new run.
 constexpr u32 kStageWords = (64 * 16) / 4 + 2 * kRouteMaxWorld;
-#ifndef PHIP_ROUTE_DIAG
-#define PHIP_ROUTE_DIAG 0   // TEMP timing breakdown
-#endif
 
 __device__ inline void route_store_bytes(u8* out, u32 from, u32 to, u32 word_start, u32 word) {
   for (u32 x = from; x < to; ++x) out[x] = (u8)(word >> (8 * (x - word_start)));
@@ -3476,7 +3473,7 @@ __device__ inline void route_names_staged(u8* __restrict__ out, u32* stg, u32 wo
   if (dcnt && lead) stg[pstart] = pend;   // the run's first dword: bytes before bo
   const u32 oo = o & 63u;
   const u32 ps_o = (u32)__shfl((int)pstart, (int)oo), bo_o = (u32)__shfl((int)bo, (int)oo);
-  if (plain && !(PHIP_ROUTE_DIAG & 4)) {
+  if (plain) {
     u8* sb = reinterpret_cast<u8*>(stg);
     const u32 p = ps_o * 4 + (bo_o & 3u) + (dby - bo_o);
 #pragma unroll
@@ -3496,7 +3493,7 @@ __device__ inline void route_names_staged(u8* __restrict__ out, u32* stg, u32 wo
   const u32 ps_g = (u32)__shfl((int)pstart, (int)og), dc_g = og < world ? (u32)__shfl((int)dcnt, (int)og) : 0u;
   const u32 bw = (u32)__shfl((int)bo, (int)og), ew = (u32)__shfl((int)be, (int)og);
   const u32 tw = (u32)__shfl((int)t0, (int)og);
-  for (u32 k = k0; __ballot(k < dc_g) && !(PHIP_ROUTE_DIAG & 8); k += 1u << lg) {
+  for (u32 k = k0; __ballot(k < dc_g); k += 1u << lg) {
     if (k < dc_g) {
       const u32 gdw = (bw >> 2) + k;
       const u32 word = stg[ps_g + k];
@@ -3624,7 +3621,7 @@ __global__ __launch_bounds__(kRouteBlock) __attribute__((amdgpu_waves_per_eu(6, 
       const u32 oo = plain ? c[u] : 0u;
       const u32 d = (u32)__shfl((int)pc, (int)oo) + dst[u];
       const u32 db = (u32)__shfl((int)pb, (int)oo) + dby[u];
-      if (plain && !(PHIP_ROUTE_DIAG & 2)) {
+      if (plain) {
         out_lens[d] = len[u];
         out_a[d] = va[u];
         out_t[d] = vt[u];
@@ -3632,7 +3629,6 @@ __global__ __launch_bounds__(kRouteBlock) __attribute__((amdgpu_waves_per_eu(6, 
       }
       // owner runs of this chunk [bo, be) (lane o), in the send buffer
       const u32 bo = pb + bo_l[u], be = pb + be_l[u];
-      if (PHIP_ROUTE_DIAG & 1) continue;
       const u32 sh = (u32)(off[u] & 7) * 8;
       const u64 n0 = sh ? (w0[u] >> sh) | (w1[u] << (64 - sh)) : w0[u];
       const u64 n1 = sh ? (w1[u] >> sh) | (w2[u] << (64 - sh)) : w1[u];

@@ -7,7 +7,8 @@
 
 `run` (under rocprofv3 --kernel-trace) opens a shared-device group of
 --world members on GPU 0 (phip_group_open_all with the device listed
---world times: the multi-member exchange by device copies), gives every
+--world times: the multi-member exchange by device copies; at --world 1
+the RCCL send/recv to itself, PHIP_GROUP_RCCL_SELF), gives every
 member a Zipf(1.1) batch of --n messages (three 2^24-message chunks at the
 default), and runs two warmup and three timed phip_group_receive calls.
 
@@ -47,7 +48,8 @@ def run(args):
     import time
     for j in range(5):
         t0 = time.perf_counter()
-        sent, merged = g.receive(batches, bench.T0 + j, combine=True)
+        sent, merged = g.receive(batches, bench.T0 + j, combine=True,
+                                 rccl_self=args.world == 1)
         torch.cuda.synchronize()
         print(f"call {j}: {1e3 * (time.perf_counter() - t0):.2f} ms sent {sent} merged {merged}",
               flush=True)
