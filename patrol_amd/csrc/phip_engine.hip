@@ -791,12 +791,12 @@ int resolve_all(phip_handle* h, Src src, u32 n, const int64_t* now_arr, i64 now0
     return rc;
   if ((rc = reset_ctr(h))) return rc;
   {
-    // (one op per thread; a persistent version that took the hot names'
+    // (kResPer ops per thread; a persistent version that took the hot names'
     // slots from C2's directory in LDS first lost: 1.85 against 1.49 ms on
-    // C3)
+    // C3 with one op per thread)
     Launch l(h, "k_resolve");
-    k_resolve<Src><<<grid_for(n), kBlock, 0, h->stream>>>(src, n, nullptr, table(h), slot, rsh,
-                                                           h->ctr, sv);
+    k_resolve_batch<Src><<<grid_for(n, kBlock * kResPer), kBlock, 0, h->stream>>>(
+        src, n, table(h), slot, rsh, h->ctr, sv);
   }
   HIPCHK(h, hipGetLastError());
   u32 nmiss = 0;

@@ -1130,6 +1130,67 @@ __global__ __launch_bounds__(kBlock) void k_resolve(Src src, u32 n, const u32* _
   if (miss.base) miss.append(blockIdx.x, missed, i);
 }
 
+// k_resolve over a whole batch (no list; the ordered path's first resolve):
+// kResPer ops per thread, every round's loads of all of them issued together
+// (name offsets, name words, home record), so a thread keeps kResPer
+// dependent chains in flight at the same occupancy; a short name found in
+// its home slot needs no probe loop (k_receive_fast's test).  Same results
+// as k_resolve.
+constexpr u32 kResPer = 2;   // (3: 78 VGPRs, 6 waves a SIMD; 4: 100, 4 waves; both slower)
+template <class Src>
+__global__ __launch_bounds__(kBlock) void k_resolve_batch(Src src, u32 n, Table T,
+                                                          u32* __restrict__ slot_out, Sharded miss,
+                                                          u32* ctr, SortVals sv) {
+  const u32 i0 = blockIdx.x * (kBlock * kResPer) + threadIdx.x;
+  u64 off[kResPer], w0[kResPer], w1[kResPer], w2[kResPer];
+  u32 len[kResPer];
+#pragma unroll
+  for (u32 k = 0; k < kResPer; ++k) src.get(min(i0 + k * kBlock, n - 1), off[k], len[k]);
+#pragma unroll
+  for (u32 k = 0; k < kResPer; ++k) load_words3<false>(src.blob, off[k], len[k], w0[k], w1[k], w2[k]);
+  Name nm[kResPer];
+  u64 tag[kResPer];
+  u32 s[kResPer];
+  Rec cur[kResPer];
+#pragma unroll
+  for (u32 k = 0; k < kResPer; ++k) {
+    if (len[k] <= kShortName) short_name(w0[k], w1[k], w2[k], off[k], len[k], nm[k]);
+    else load_name_wide<false>(src.blob, off[k], len[k], nm[k]);
+    tag[k] = T.tag(nm[k].h);
+    s[k] = T.home(tag[k]);
+    cur[k] = load_rec48(&T.recs[s[k]]);
+  }
+#pragma unroll
+  for (u32 k = 0; k < kResPer; ++k) {
+    const u32 i = i0 + k * kBlock;
+    bool missed = false;
+    if (i < n) {
+      if (sv.val) sv.val[i] = i | ((u32)(sv.kind ? sv.kind[i] : sv.kind0) << kSortValKindShift);
+      const bool shortname = len[k] <= kShortName;
+      const bool hit = shortname && cur[k].tag == tag[k] &&
+                       (cur[k].name0 & ~0xFF00ull) == nm[k].w0 && cur[k].name1 == nm[k].w1 &&
+                       (rec_flags(cur[k]) & kRecPublished);
+      int pr = kFound;
+      u32 sk = s[k];
+      if (!hit) {
+        if (shortname && cur[k].tag == 0) {
+          pr = kMiss;
+        } else {
+          Rec r;
+          pr = probe(T, nm[k], src.blob, &sk, &r);
+        }
+      }
+      if (pr == kFound) {
+        slot_out[i] = sk;
+      } else {
+        missed = true;
+        if (pr == kFull) atomicOr(&ctr[8], 1u);
+      }
+    }
+    if (miss.base) miss.append(blockIdx.x * kResPer + k, missed, i);
+  }
+}
+
 // ------------------------------------------------------------- inserts ---
 // Round of the insert pipeline.  Claim: CAS an empty tag slot.  A same-tag
 // slot claimed in this round (not yet published) cannot be name-checked, so
