@@ -3500,12 +3500,14 @@ __device__ inline void route_place_packed(bool take, u32 o, u32 len, u32* run, u
 // they have in out_names, and the dwords the chunk completes are stored with
 // one dword store each (byte stores of 64 lanes scattered over 8 owners made
 // the scatter L2-request bound).  Per owner (lane o < world):
-//   t0   the owner's first byte of this run of the tile (bytes before it in
-//        its first dword belong to the tile before: stored one by one)
-//   pend the dword holding the run's end, not yet complete: carried to the
-//        next chunk, stored byte by byte at the end of the tile
-// A chunk with a longer name takes the byte path (route_names_bytes) after a
-// flush, and the next chunk starts a new run.
+//   t0   the first byte this call may store whole dwords from (bytes before
+//        it in its first dword belong to another run: stored one by one)
+//   pend the dword holding the run's end, not yet complete, returned to the
+//        caller, who stores its bytes (route_flush_pend)
+// k_route_scatter passes t0 = the run's start and flushes pend after every
+// chunk: a run's first and last dwords are shared with the runs of other
+// waves and steps.  A chunk with a longer name stores every name byte by
+// byte instead.
 constexpr u32 kStageWords = (64 * 16) / 4 + 2 * kRouteMaxWorld;
 
 __device__ inline void route_store_bytes(u8* out, u32 from, u32 to, u32 word_start, u32 word) {
