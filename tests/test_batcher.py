@@ -29,7 +29,11 @@ def pa():
     return patrol_amd
 
 
-@pytest.mark.parametrize("window_us", [0, 50])
+# 200 µs: Python threads re-submit after a batch completes at a pace the GIL
+# sets (a few µs a thread), so a 50 µs window caught 8 or fewer of the 48 on
+# a loaded host (1955 batches for 7200 requests) and the coalescing bound
+# below depended on the host, not on the batcher
+@pytest.mark.parametrize("window_us", [0, 200])
 def test_batcher_threads_vs_oracle_in_arrival_order(pa, window_us):
     threads, per_thread, K = 48, 150, 120
     repo = pa.GPURepo(log2_slots=12)
