@@ -90,12 +90,16 @@ def parse():
                    help="c3: replica elapsed drawn below the local clock (U[0, now - created): "
                         "Takes refill, succeed and deny) or ahead of it (round 1's input: every "
                         "Take clamps last to now, dt = 0)")
+    p.add_argument("--classify", action="store_true",
+                   help="A/B only: c2 classifies every batch before merging (PHIP_RECV_CLASSIFY) "
+                        "instead of the speculative receive")
     p.add_argument("--no-status", action="store_true",
                    help="A/B only: the C2 step does not write the per-message status column")
     p.add_argument("--name-len", type=int, default=0,
                    help="c2: pad every bucket name to this many bytes (e.g. 32: the arena path)")
     p.add_argument("--no-routed", action="store_true",
                    help="c2: skip the owner_routed (strong-scaling) object")
+    p.add_argument("--no-c3", action="store_true", help="c2: skip the c3 object")
     p.add_argument("--no-c4", action="store_true", help="c2: skip the c4 object")
     p.add_argument("--no-ae", action="store_true", help="c2: skip the anti_entropy object")
     p.add_argument("--c4-keys", type=int, default=125_000_000,
@@ -254,7 +258,11 @@ def cpu_baseline(args, K, ids_host):
                         max=float(max(vals)), runs=CPU_REPS, messages=m)
     del repo
     top, one = max(runs), min(runs)
+    best = max(runs, key=lambda k: runs[k]["median"])
     return dict(value=runs[top]["median"], unit="merges/s", cores=top, kind="port", **host_cpu(),
+                best=dict(threads=best, value=runs[best]["median"],
+                          note="the thread count with the highest median; `value` is the nproc "
+                               "figure SURVEY §8d asks for (lock collapse on LocalRepo's RWMutex)"),
                 what="Go-semantics C++ restatement (oracle/patrol_oracle.cc: LocalRepo's "
                      "RWMutex map + per-bucket mutex, ReplicatedRepo.Receive's loop body)",
                 sample=f"the first {runs[top]['messages']} step-0 messages (Zipf {args.zipf} over "
@@ -357,11 +365,77 @@ def c3_inputs(args, torch, dev, K, base, gen):
                 steps=steps)
 
 
+def c3_cpu(args, torch, c, K, base, step_idx, threads=None, reps=CPU_REPS):
+    """C3's stream through the Go-structured restatement (oracle) on a
+    bounded prefix of step `step_idx`, on a freshly seeded map: one thread
+    in stream order (orc_bench_mixed), and 16 / nproc threads
+    (orc_bench_mixed_mt: each bucket's ops on one worker in stream order,
+    the global map lock and the bucket mutex per op, as concurrent Go
+    handlers take them).  The first run (1 thread, the step's own clock)
+    starts from the state the GPU's step started from when that step ran on
+    a fresh table: its statuses and `remaining` are returned beside the
+    timing dict for the in-run parity check (a prefix's results depend only
+    on the ops before it)."""
+    from oracle import oracle as O
+    L = O.lib()
+    n, ids, steps = c["n"], c["ids"], c["steps"]
+    kind, freq, per, cnt = c["kind"], c["freq"], c["per"], c["cnt"]
+    keys = torch.arange(base, base + K, dtype=torch.int64)
+    kb, ko = names_for_ids(torch, keys)
+    kb_np, ko_np = kb.numpy(), ko.numpy().astype(np.uint32)
+    del kb, ko, keys
+    z = np.zeros(K, np.uint64)
+    m = min(args.cpu_sample // 2, n)
+    sb, so = names_for_ids(torch, ids[:m].cpu() + base)
+    sb_np, so_np = sb.numpy(), so.numpy().astype(np.uint32)
+    now, a, t, e = steps[step_idx]
+    cols = [x[:m].cpu().numpy() for x in (kind, now, freq, per, cnt, a, t, e)]
+    orepo = O.Repo()
+    L.orc_repo_seed(orepo.h, kb_np, ko_np, K, z, z, np.zeros(K, np.int64), np.full(K, T0, np.int64))
+    runs = {}
+    rep = 0
+    first = None
+    for th in (threads or cpu_thread_counts(args)):
+        mm = m if 1 < th <= 16 else min(m, CPU_SLOW_SAMPLE // 2)
+        f = L.orc_bench_mixed if th == 1 else L.orc_bench_mixed_mt
+        extra = () if th == 1 else (th,)
+        vals = []
+        for _ in range(reps):
+            st = np.zeros(mm, np.uint8)
+            rm = np.zeros(mm, np.uint64)
+            # each run one second of clock later than the last (Takes refill)
+            nw = cols[1][:mm] + rep * 10**9
+            rep += 1
+            secs = f(orepo.h, cols[0], sb_np, so_np, mm, nw, cols[2], cols[3],
+                     cols[4].view(np.uint64), cols[5].view(np.uint64), cols[6].view(np.uint64),
+                     cols[7], st, rm, *extra)
+            if first is None:
+                first = (st, rm)
+            vals.append(mm / secs)
+        runs[th] = dict(median=float(np.median(vals)), min=float(min(vals)),
+                        max=float(max(vals)), runs=reps, ops=mm)
+    del orepo
+    top, one = max(runs), min(runs)
+    best = max(runs, key=lambda k: runs[k]["median"])
+    out = dict(value=runs[top]["median"], unit="ops/s", cores=top, kind="port", **host_cpu(),
+               what="Go-semantics C++ restatement (oracle/patrol_oracle.cc)",
+               sample=f"first {runs[top]['ops']} ops of a timed-stream step (Zipf {args.zipf} "
+                      f"over {K} buckets), {top} threads (nproc; each bucket's ops on one "
+                      f"worker, in stream order); median of {reps} runs, each run's "
+                      "clock 1 s after the last",
+               best=dict(threads=best, value=runs[best]["median"]),
+               by_threads={str(k): v for k, v in sorted(runs.items())},
+               single_thread=dict(value=runs[one]["median"], min=runs[one]["min"],
+                                  max=runs[one]["max"],
+                                  sample=f"{runs[one]['ops']} ops, 1 thread, median of {reps}"))
+    return out, first
+
+
 def run_c3(args, torch, dev, repo, rank, K, base, gen):
     """The C3 bench step over c3_inputs(): phip_apply_mixed with statuses and
     `remaining` written, every array resident in HBM."""
     c = c3_inputs(args, torch, dev, K, base, gen)
-    n, ids, blob, offs, steps = c["n"], c["ids"], c["blob"], c["offs"], c["steps"]
+    n, blob, offs, steps = c["n"], c["blob"], c["offs"], c["steps"]
     kind, freq, per, cnt = c["kind"], c["freq"], c["per"], c["cnt"]
     status = torch.empty(n, dtype=torch.uint8, device=dev)
     rem = torch.empty(n, dtype=torch.int64, device=dev)
@@ -373,59 +447,100 @@ def run_c3(args, torch, dev, repo, rank, K, base, gen):
                                 status=status, remaining=rem)
 
     def cpu():
-        """The same stream through the Go-structured restatement (oracle) on a
-        bounded prefix: one thread in stream order (orc_bench_mixed), and 16 /
-        nproc threads (orc_bench_mixed_mt: each bucket's ops on one worker in
-        stream order, the global map lock and the bucket mutex per op, as
-        concurrent Go handlers take them).  `value` is the nproc figure."""
-        from oracle import oracle as O
-        L = O.lib()
-        keys = torch.arange(base, base + K, dtype=torch.int64)
-        kb, ko = names_for_ids(torch, keys)
-        kb_np, ko_np = kb.numpy(), ko.numpy().astype(np.uint32)
-        del kb, ko, keys
-        z = np.zeros(K, np.uint64)
-        m = min(args.cpu_sample // 2, n)
-        sb, so = names_for_ids(torch, ids[:m].cpu() + base)
-        sb_np, so_np = sb.numpy(), so.numpy().astype(np.uint32)
-        now, a, t, e = steps[args.warmup]
-        cols = [x[:m].cpu().numpy() for x in (kind, now, freq, per, cnt, a, t, e)]
-        orepo = O.Repo()
-        L.orc_repo_seed(orepo.h, kb_np, ko_np, K, z, z, np.zeros(K, np.int64),
-                        np.full(K, T0, np.int64))
-        runs = {}
-        rep = 0
-        for th in cpu_thread_counts(args):
-            mm = m if 1 < th <= 16 else min(m, CPU_SLOW_SAMPLE // 2)
-            st = np.zeros(mm, np.uint8)
-            rm = np.zeros(mm, np.uint64)
-            f = L.orc_bench_mixed if th == 1 else L.orc_bench_mixed_mt
-            extra = () if th == 1 else (th,)
-            vals = []
-            for _ in range(CPU_REPS):
-                # each run one second of clock later than the last (Takes refill)
-                nw = cols[1][:mm] + rep * 10**9
-                rep += 1
-                secs = f(orepo.h, cols[0], sb_np, so_np, mm, nw, cols[2], cols[3],
-                         cols[4].view(np.uint64), cols[5].view(np.uint64), cols[6].view(np.uint64),
-                         cols[7], st, rm, *extra)
-                vals.append(mm / secs)
-            runs[th] = dict(median=float(np.median(vals)), min=float(min(vals)),
-                            max=float(max(vals)), runs=CPU_REPS, ops=mm)
-        del orepo
-        top, one = max(runs), min(runs)
-        return dict(value=runs[top]["median"], unit="ops/s", cores=top, kind="port", **host_cpu(),
-                    what="Go-semantics C++ restatement (oracle/patrol_oracle.cc)",
-                    sample=f"first {runs[top]['ops']} ops of the timed stream (Zipf {args.zipf} "
-                           f"over {K} buckets), {top} threads (nproc; each bucket's ops on one "
-                           f"worker, in stream order); median of {CPU_REPS} runs, each run's "
-                           "clock 1 s after the last",
-                    by_threads={str(k): v for k, v in sorted(runs.items())},
-                    single_thread=dict(value=runs[one]["median"], min=runs[one]["min"],
-                                       max=runs[one]["max"],
-                                       sample=f"{runs[one]['ops']} ops, 1 thread, median of "
-                                              f"{CPU_REPS}"))
+        return c3_cpu(args, torch, c, K, base, args.warmup)[0]
     return n, step, cpu
+
+
+def c3_workload(args, n, K, L):
+    return (f"C3 mixed: {n} ops (50% Take 100:1s n=1, 50% Merge), Zipf({args.zipf}) over "
+            f"{K} buckets (2^{L} slots), per-bucket order kept, replica "
+            f"elapsed {args.c3_clock} the local clock")
+
+
+def run_c3_leg(args, torch, dist, dev, local, rank, world):
+    """The `c3` object (BASELINE configs[2]): 50M mixed ops
+    per step, 50% Take(100:1s, n=1) and 50% replica merges, Zipf(1.1) over a
+    10M-bucket table (2^25 slots), per-bucket order kept, replica clocks
+    below the local clock, through phip_apply_mixed with statuses and
+    `remaining` written (bucket.go:186-225 driven by api.go:67-74, and
+    repo.go:54-92).  Every rank runs its own table (weak scaling, no
+    exchange).
+
+    `verified` (in-run parity): the untimed first step runs on the freshly
+    seeded table; the restatement (oracle) replays that step's first ops on
+    a freshly seeded map inside the CPU-baseline leg, and their statuses and
+    `remaining` must equal the GPU's bit for bit (a prefix's results depend
+    only on the ops before it)."""
+    import argparse as _ap
+    import patrol_amd
+    K, L = args.keys, args.log2_slots
+    ca = _ap.Namespace(**vars(args))
+    ca.warmup, ca.steps = 1, max(1, min(args.steps, 5))
+    ca.c3_clock = "below"
+    gen = torch.Generator(device=dev).manual_seed(args.seed + 303 + 7919 * rank)
+    base = rank * K
+    repo = patrol_amd.GPURepo(device=local, log2_slots=L, arena_bytes=1 << 20)
+    repo.use_torch_stream()
+    keys = torch.arange(base, base + K, dtype=torch.int64, device=dev)
+    kb, ko = names_for_ids(torch, keys)
+    st = torch.zeros((K, 4), dtype=torch.int64, device=dev)
+    st[:, 3] = T0
+    torch.cuda.synchronize()
+    repo.seed_device(kb, ko, st, K)
+    del kb, ko, st, keys
+    c = c3_inputs(ca, torch, dev, K, base, gen)
+    n, blob, offs, steps = c["n"], c["blob"], c["offs"], c["steps"]
+    kind, freq, per, cnt = c["kind"], c["freq"], c["per"], c["cnt"]
+    status = torch.empty(n, dtype=torch.uint8, device=dev)
+    rem = torch.empty(n, dtype=torch.int64, device=dev)
+    torch.cuda.synchronize()
+    first = {}
+
+    def step(j):
+        now, a, t, e = steps[j]
+        repo.apply_mixed_device(n, kind, blob, offs, now, freq, per, cnt, a, t, e,
+                                status=status, remaining=rem)
+        if j == 0:   # the verification step (untimed warmup, fresh table)
+            torch.cuda.synchronize()
+            first["st"] = status[:CPU_SLOW_SAMPLE].cpu().numpy()
+            first["rm"] = rem[:CPU_SLOW_SAMPLE].cpu().numpy().view(np.uint64)
+    el = _timed_steps(dist, torch, dev, args, ca.warmup, ca.steps, step)
+    repo.close()
+    del status, rem
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cpu, ref = c3_cpu(ca, torch, c, K, base, 0)
+    else:   # parity only (one thread, one run)
+        _, ref = c3_cpu(ca, torch, c, K, base, 0, threads=[1], reps=1)
+    mm = ref[0].size
+    bad_st = int((first["st"][:mm] != ref[0]).sum())
+    bad_rm = int((first["rm"][:mm] != ref[1]).sum())
+    ok = torch.tensor([int(bad_st == 0 and bad_rm == 0)], dtype=torch.int64, device=dev)
+    verified = int(_coll(dist, args, torch, ok, "sum").item()) == world
+    del c
+    step_s = el / ca.steps
+    bpo = 88.5   # SURVEY §8d: Take 89 B, Merge 88 B
+    achieved = bpo * n / step_s / 1e9
+    workload = c3_workload(ca, n, K, L)
+    build = patrol_amd.build_id()
+    traffic, traffic_src = pmc_traffic("c3", workload, "whole step", build)
+    out = {
+        "metric": "mixed Take+Merge ops/sec (C3: per-bucket ordered)",
+        "value": world * n * ca.steps / el, "unit": "ops/s", "scaling": "weak", "n_gpus": world,
+        "steps": ca.steps, "warmup": ca.warmup, "ms_per_step": step_s * 1e3,
+        "workload": workload,
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "traffic_source": traffic_src, "kernel": "whole step",
+                     "algorithmic_bytes_per_step": bpo * n},
+        "verified": verified,
+        "verify": {"ops_checked": mm, "status_mismatches": bad_st, "remaining_mismatches": bad_rm,
+                   "reference": "oracle/patrol_oracle.cc (orc_bench_mixed) replaying the first "
+                                f"{mm} ops of the untimed first step on a freshly seeded map"},
+    }
+    if cpu is not None:
+        out["cpu_baseline"] = cpu
+    return out
 
 
 def run_c4(args, torch, dev, repo, rank, world, K, gen):
@@ -455,6 +570,8 @@ def run_c4(args, torch, dev, repo, rank, world, K, gen):
 
     merged = []
     group = repo._group = open_group(args, dist_module(), repo, rank, world)
+    if group is not None:
+        group.set_timing(True)
 
     def step(j):
         a, t, e = batches[j]
@@ -527,6 +644,21 @@ def open_group(args, dist, repo, rank, world):
     obj = [patrol_amd.GPUGroup.unique_id() if rank == 0 else None]
     dist.broadcast_object_list(obj, src=0)
     return patrol_amd.GPUGroup.open_rank(repo, obj[0], world, rank)
+
+
+def group_diag(group, world, stages, names):
+    """What a multi-GPU record needs to explain itself: the RCCL the
+    group's communicator runs on (version, ncclCommCount, the librccl its
+    symbols resolved to, every librccl mapped in this process) and rank 0's
+    per-stage busy ms per step (HIP events around each chunk's work on its
+    own stream: the stages overlap, phip_group_stage_ms)."""
+    if group is None:
+        return {}
+    out = {"rccl": dict(group.rccl_info(), world=world)}
+    if stages:
+        out["stage_busy_ms"] = {nm: float(np.mean([s[k] for s in stages]))
+                                for nm, k in zip(names, ("pack", "exchange", "merge"))}
+    return out
 
 
 LEG_LIMIT_S = 300   # each extra leg's watchdog (main())
@@ -723,6 +855,9 @@ def run_c4_leg(args, torch, dist, dev, local, rank, world):
     torch.cuda.synchronize()
     group = open_group(args, dist, repo, rank, world)
     merged = []
+    stages = []
+    if group is not None:
+        group.set_timing(True)
 
     def step(j):
         a, t, e = batches[j]
@@ -730,6 +865,8 @@ def run_c4_leg(args, torch, dist, dev, local, rank, world):
             _, got = group.receive([(blob, offs, a, t, e)], T0 + j, combine=True,
                                    rccl_self=world == 1)
             k = got[0]
+            if j >= warm:   # (the call ends host-synchronised: reading its events adds no wait)
+                stages.append(group.stage_ms())
         else:
             rb, ro, ra, rt, re = shard.route_messages_native(blob, offs, a, t, e, repo,
                                                              combine=True)
@@ -771,6 +908,7 @@ def run_c4_leg(args, torch, dist, dev, local, rank, world):
                       device=dev)
     sm = _coll(dist, args, torch, tt.clone(), "sum")
     mx = _coll(dist, args, torch, tt.clone(), "max")
+    diag = group_diag(group, world, stages, ("pack", "exchange", "merge"))
     if group is not None:
         group.close()
     repo.close()
@@ -794,6 +932,7 @@ def run_c4_leg(args, torch, dist, dev, local, rank, world):
                  "phip_receive_soa"),
         "rehearsal": rehearsal,
         "setup_s": t_setup,
+        **diag,
         "verified": verified,
         "verify": {"sampled_buckets": S, "found_exactly_once": found_once, "mismatched": bad,
                    "reference": "independent per-id max-reduce of every rank's messages over all "
@@ -842,6 +981,9 @@ def run_ae_leg(args, torch, dist, dev, local, rank, world):
     flat = reps.view(-1)
     torch.cuda.synchronize()
     group = open_group(args, dist, repo, rank, world)
+    stages = []
+    if group is not None:
+        group.set_timing(True)
 
     def writes(j):
         idx, dt, de = rounds[j]
@@ -857,6 +999,8 @@ def run_ae_leg(args, torch, dist, dev, local, rank, world):
     def step(j):
         writes(j)
         exchange()
+        if group is not None and j >= warm:
+            stages.append(group.stage_ms())
     el = _timed_steps(dist, torch, dev, args, warm, steps, step)
 
     # ---- the verification round
@@ -884,6 +1028,7 @@ def run_ae_leg(args, torch, dist, dev, local, rank, world):
     converged = int(cnt.item()) == world and int(lo_hi[1]) == -int(lo_hi[2])
     go_all = _coll(dist, args, torch, torch.tensor([int(go)], dtype=torch.int64, device=dev), "sum")
     go_ok = int(go_all.item()) == world
+    diag = group_diag(group, world, stages, ("local_join", "allreduce", "apply"))
     if group is not None:
         group.close()
     repo.close()
@@ -906,6 +1051,7 @@ def run_ae_leg(args, torch, dist, dev, local, rank, world):
                  if group is not None else
                  "gloo rehearsal: phip_ae_local_max + torch all_reduce(MAX) + phip_ae_apply"),
         "rehearsal": args.dist_backend != "nccl",
+        **diag,
         "verified": converged and go_ok, "converged": converged,
         "verify": {"sampled_buckets": 4096, "replicas_checked": R * world, "go_merge_equal": go_ok,
                    "reference": "float64 max of every replica's decoded added/taken and int max of "
@@ -943,6 +1089,8 @@ def run_c5(args, torch, dev, repo, rank, world, gen):
     flat = reps.view(-1)
     torch.cuda.synchronize()
     group = repo._group = open_group(args, dist_module(), repo, rank, world)
+    if group is not None:
+        group.set_timing(True)
 
     def step(j):
         idx, dt, de = rounds[j]
@@ -1108,7 +1256,7 @@ def main():
             def step(j):
                 a, t, e = batches[j]
                 repo.receive_soa(blob, a, t, e, T0 + j, name_offs=offs, n=n, status=c2_status,
-                                 device=True)
+                                 device=True, classify=args.classify)
 
     for j in range(args.warmup):
         step(j)
@@ -1170,7 +1318,8 @@ def main():
         step_s = el / args.steps
         extra["allreduce_bytes"] = allreduce_bytes
         extra["replicas_total"] = R * world
-        ar_ms = kms.get("rccl_allreduce")
+        grp = getattr(repo, "_group", None)
+        ar_ms = grp.stage_ms()["exchange"] if grp is not None and world > 1 else None
         if ar_ms:   # HIP events around the RCCL call (phip_group_anti_entropy)
             algbw = allreduce_bytes / (ar_ms / 1e3) / 1e9
             extra["allreduce_ms"] = ar_ms
@@ -1188,8 +1337,9 @@ def main():
         # the sender-side combine, not the n messages it sent
         extra["messages_sent_per_step_rank0"] = n
         extra["messages_merged_per_step_rank0"] = float(np.mean(c4_merged))
-        if "rccl_exchange" in kms:   # the grouped send/recv of the packed segments
-            extra["exchange_ms"] = kms["rccl_exchange"]
+        grp = getattr(repo, "_group", None)
+        if grp is not None:   # rank 0's stage busy time of the last step
+            extra["stage_busy_ms"] = grp.stage_ms()
     elif args.workload == "route":
         # the pack's algorithmic bytes: read the message (offset 4 + name +
         # 24), write it owner-major (length 4 + name + 24); names ~7 B
@@ -1206,9 +1356,7 @@ def main():
         bpo = 88.5
         dom_name, dom_ms = "whole step", el / args.steps * 1e3
         unit, metric = "ops/s", METRIC + " [C3: mixed Take+Merge ops/sec]"
-        workload = (f"C3 mixed: {n} ops (50% Take 100:1s n=1, 50% Merge), Zipf({args.zipf}) over "
-                    f"{K} buckets (2^{args.log2_slots} slots), per-bucket order kept, replica "
-                    f"elapsed {args.c3_clock} the local clock")
+        workload = c3_workload(args, n, K, args.log2_slots)
         extra["c3_clock"] = args.c3_clock
     else:
         bpo = BYTES_PER_MERGE
@@ -1251,6 +1399,9 @@ def main():
                    "slots_per_gpu": 1 << args.log2_slots, "parallelism": f"shard{world}",
                    "name_bytes": args.name_len or "2-8 (b<id>)",
                    "world_size": world,
+                   # the headline is C2 weak scaling: every rank merges its own
+                   # pre-routed stream, no owner routing (that is owner_routed / c4)
+                   "exchange": False,
                    "dist_backend": args.dist_backend if dist.is_initialized() else None},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
@@ -1285,6 +1436,8 @@ def main():
         if args.workload == "c2":
             del batches, blob, offs, ids
         legs = [("owner_routed", run_routed)]
+        if not args.no_c3:
+            legs.append(("c3", run_c3_leg))
         if not args.no_c4:
             legs.append(("c4", run_c4_leg))
         if not args.no_ae:

@@ -106,6 +106,10 @@ enum {
 #define PHIP_GROUP_SMALL_CHUNKS 0x8u /* phip_group_receive (testing): pipeline the exchange in
                                         chunks of 4096 messages instead of 2^24, so that small
                                         batches run many pack / exchange rounds */
+#define PHIP_RECV_CLASSIFY 0x10u /* phip_receive_soa: classify the batch before merging (its
+                                    clean prefix merged at once, the ordered path from the first
+                                    incast / -0.0 on) instead of merging it speculatively; the
+                                    results are the same, this is for A/B measurements */
 
 /* phip_config.flags */
 #define PHIP_CFG_NO_GROW 0x1u   /* refuse (PHIP_ERR_FULL / PHIP_ERR_ARENA) instead of growing */
@@ -235,7 +239,8 @@ int phip_get(phip_handle* h, const uint8_t* name, uint32_t len, phip_state* out)
  * restarted node through incast, repo.go:96-106).  phip_snapshot writes
  * phip_snapshot_bytes(h) bytes into a host buffer: a 64-byte header (magic
  * "PHIPSNP1", ABI version, log2_slots, bucket count, arena bytes), the 2^L
- * slot records as they lie in HBM (64 B each), then the used long-name arena.
+ * slot records as they lie in HBM (128 B each: state and name in the first 64,
+ * speculation scratch after them), then the used long-name arena.
  * phip_restore loads such an image into a handle opened with the same
  * log2_slots (and an arena at least as large): the table is reproduced
  * exactly, with no rehash.  phip_dump + phip_seed is the portable route
@@ -269,7 +274,12 @@ int phip_dump(phip_handle* h, uint8_t* names, uint64_t names_cap, uint64_t* name
 int phip_receive_datagrams(phip_handle* h, const uint8_t* bytes, const uint64_t* offs, uint32_t n,
                            int64_t now, const phip_results* res, uint32_t* stop_index,
                            uint32_t flags);
-/* The same loop over pre-decoded states. */
+/* The same loop over pre-decoded states.  A batch of 2^16 messages or more
+ * is merged speculatively: every clean message at once, with each record's
+ * pre-batch state kept; the buckets that incasts or -0.0 fields name (the
+ * only ones whose results depend on order) are then set back and replayed
+ * in batch order.  PHIP_RECV_CLASSIFY classifies first instead (same
+ * results). */
 int phip_receive_soa(phip_handle* h, const phip_msgs* m, int64_t now, const phip_results* res,
                      uint32_t flags);
 /* LocalRepo.UpsertBucket for each state, in order. */
@@ -527,6 +537,24 @@ int phip_group_receive(phip_group* g, const phip_msgs* batches, int64_t now, uin
  * replica of every member is the CvRDT join of all of them. */
 int phip_group_anti_entropy(phip_group* g, int64_t* const* replicas, uint32_t nrep,
                             uint64_t nbuckets, uint32_t flags);
+/* Stage timing of the group's calls (off by default): with it on, every
+ * later phip_group_receive / phip_group_anti_entropy records HIP events
+ * around each chunk's work on the stream it runs on, and
+ * phip_group_stage_ms reads member i's busy time of the last call per stage
+ * (the sum over its chunks): ms[0] pack (phip_route_pack; the local join of
+ * an anti-entropy round), ms[1] exchange (split sizes and segments over RCCL
+ * or device copies; the all-reduce), ms[2] the owner's merges (the apply).
+ * The stages overlap, so their sum can exceed the call.  The read
+ * synchronises on the events. */
+int phip_group_set_timing(phip_group* g, int on);
+int phip_group_stage_ms(phip_group* g, uint32_t i, float* ms /* [3] */);
+/* The RCCL member i's communicator runs on: ncclGetVersion, ncclCommCount
+ * (must equal the world; 0 for a shared-device group, which has none) and
+ * the path of the librccl the library's RCCL symbols resolved to (dladdr).
+ * A process that loaded another librccl first (torch's, same soname
+ * librccl.so.1) shares that one copy. */
+int phip_group_rccl_info(phip_group* g, uint32_t i, int32_t* version, int32_t* comm_count,
+                         char* lib_path, uint32_t path_cap);
 
 /* ---- diagnostics ---- */
 /* Per-kernel timing of the last hot-path call (every call since

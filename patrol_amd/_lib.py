@@ -28,6 +28,7 @@ EXPORTS = [
     "phip_table_stats", "phip_group_unique_id", "phip_group_open_all", "phip_group_open_rank",
     "phip_group_close", "phip_group_last_error", "phip_group_world", "phip_group_local",
     "phip_group_handle", "phip_group_receive", "phip_group_anti_entropy",
+    "phip_group_set_timing", "phip_group_stage_ms", "phip_group_rccl_info",
 ]
 
 PHIP_OK = 0
@@ -45,6 +46,7 @@ CFG_FIXED_SEED = 0x4
 ROUTE_COMBINE = 0x2
 GROUP_RCCL_SELF = 0x4
 GROUP_SMALL_CHUNKS = 0x8
+RECV_CLASSIFY = 0x10
 PACKET_SIZE = 256
 BUCKET_FIXED_SIZE = 25   # PHIP_BUCKET_FIXED_SIZE: added, taken, elapsed, name length
 
@@ -195,5 +197,9 @@ def load(path: str = LIB_PATH):
     L.phip_group_receive.argtypes = [vp, C.POINTER(phip_msgs), i64, C.POINTER(u64),
                                      C.POINTER(u64), u32]
     L.phip_group_anti_entropy.argtypes = [vp, C.POINTER(vp), u32, u64, u32]
+    L.phip_group_set_timing.argtypes = [vp, C.c_int]
+    L.phip_group_stage_ms.argtypes = [vp, u32, C.POINTER(C.c_float)]
+    L.phip_group_rccl_info.argtypes = [vp, u32, C.POINTER(C.c_int32), C.POINTER(C.c_int32),
+                                       C.c_char_p, u32]
     _lib = L
     return L

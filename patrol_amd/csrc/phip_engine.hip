@@ -61,6 +61,7 @@ enum BufId {
   B_OPS, B_HOFF, B_HOP, B_HVAL, B_RPOS, B_RST, B_RUNN, B_SEGEX, B_WOFF, B_SUMS, B_WRUN,
   B_WING, B_SEGXF, B_FOLDDBG, B_SMALL, B_HUGE2, B_LONG2,
   B_STATES, B_NAME1, B_HOT, B_ROUTE, B_EXPORT, B_MSHARD, B_MSCNT, B_DEDUP, B_DSET, B_TSTATS, B_SEGT, B_RHOT,
+  B_SPECSET, B_PICK, B_PA, B_PT, B_PE, B_PST, B_PREM, B_PHAVE, B_PREP,
   B_COUNT_
 };
 
@@ -122,6 +123,7 @@ struct phip_handle {
   size_t pool_used = 0;
   u8* small_pin = nullptr;   // pinned staging of small ordered batches (both ways)
   size_t small_pin_cap = 0;
+  u32 spec_epoch = 0;        // epoch of the last speculative receive batch (1..kEpochMax)
 };
 
 namespace {
@@ -175,11 +177,12 @@ inline unsigned grid_for(u64 n, unsigned block = kBlock) {
   return (unsigned)std::max<u64>(1, (n + block - 1) / block);
 }
 
-// Event-timed launch helper.
+// Event-timed launch helper (the pool entry is held by index: a nested
+// Launch may grow the pool).
 struct Launch {
   phip_handle* h;
   const char* name;
-  Timing* t = nullptr;
+  size_t idx = ~size_t(0);
   hipStream_t s;
   Launch(phip_handle* h_, const char* n, hipStream_t st = nullptr)
       : h(h_), name(n), s(st ? st : h_->stream) {
@@ -193,13 +196,14 @@ struct Launch {
       }
       h->event_pool.push_back(tm);
     }
-    t = &h->event_pool[h->pool_used++];
-    t->name = n;
-    if (hipEventRecord(t->a, s) != hipSuccess) t = nullptr;
+    idx = h->pool_used++;
+    h->event_pool[idx].name = n;
+    if (hipEventRecord(h->event_pool[idx].a, s) != hipSuccess) idx = ~size_t(0);
   }
   ~Launch() {
-    if (t) {
-      if (hipEventRecord(t->b, s) == hipSuccess) h->timings.push_back(*t);
+    if (idx < h->event_pool.size()) {
+      Timing& t = h->event_pool[idx];
+      if (hipEventRecord(t.b, s) == hipSuccess) h->timings.push_back(t);
     }
   }
 };
@@ -677,9 +681,24 @@ int dedupe_names(phip_handle* h, Src src, const u32* list, u32 n, u32** out, u32
 // device-scope atomic to one record (134 ms per 100M-message batch through
 // k_receive_list).  Returns the misses of the second pass
 // (names dropped by k_dedupe for a shared tag) in *nmiss2, listed in B_MISS.
+// Speculation context of a batch (spec_receive): its epoch and, once the
+// batch had dirty messages, the tag set of their names (those buckets are
+// replayed by the ordered path, so their misses are not inserted here).
+struct SpecCtx {
+  u32 ep = 0;
+  const u64* set = nullptr;
+  u32 bits = 0;
+};
+
+template <class Src>
+int spec_apply(phip_handle* h, SoaIn<Src> in, u32 n, u8* status, u32 ep, u32* nlist, u32* ndirty);
+template <class Src>
+int keep_misses(phip_handle* h, Src src, u32 nlist, const SpecCtx& sp, u32* nkeep);
+
 template <class Src>
 int finish_many_misses(phip_handle* h, Src src, const uint64_t* a, const uint64_t* t,
-                       const int64_t* e, u32 nmiss, u32 prefix, i64 now, u8* status, u32* nmiss2) {
+                       const int64_t* e, u32 nmiss, u32 prefix, i64 now, u8* status, u32* nmiss2,
+                       const SpecCtx* sp) {
   u32* miss = (u32*)h->buf[B_MISS].p;
   int rc;
   // 1. distinct names
@@ -695,9 +714,18 @@ int finish_many_misses(phip_handle* h, Src src, const uint64_t* a, const uint64_
     k_first_seen<Src><<<grid_for(nmiss), kBlock, 0, h->stream>>>(src, nmiss, miss, table(h));
     HIPCHK(h, hipGetLastError());
   }
-  // 4. the fast pass again
+  // 4. the fast pass again (a speculative batch: speculatively again, at the
+  //    same epoch, so the records it first touched keep their pre-batch
+  //    state; its set-aside and dirty-bucket entries are dropped again)
   u32 fd = prefix;
-  if ((rc = fast_apply(h, SoaIn<Src>{src, a, t, e}, src, prefix, status, &fd, nmiss2))) return rc;
+  if (sp) {
+    u32 nd = 0;
+    if ((rc = spec_apply(h, SoaIn<Src>{src, a, t, e}, prefix, status, sp->ep, nmiss2, &nd)))
+      return rc;
+    if (sp->set && *nmiss2 && (rc = keep_misses(h, src, *nmiss2, *sp, nmiss2))) return rc;
+  } else if ((rc = fast_apply(h, SoaIn<Src>{src, a, t, e}, src, prefix, status, &fd, nmiss2))) {
+    return rc;
+  }
   // 5. PHIP_ST_CREATED after the second pass wrote its statuses
   if (status && n_claimed) {
     Launch l(h, "k_mark_created");
@@ -712,11 +740,11 @@ int finish_many_misses(phip_handle* h, Src src, const uint64_t* a, const uint64_
 // creator tracking (PHIP_ST_CREATED on the first message of a new bucket).
 template <class Src>
 int finish_misses(phip_handle* h, Src src, const uint64_t* a, const uint64_t* t, const int64_t* e,
-                  u32 nmiss, u32 prefix, i64 now, u8* status) {
+                  u32 nmiss, u32 prefix, i64 now, u8* status, const SpecCtx* sp = nullptr) {
   if (nmiss == 0) return PHIP_OK;
   int rc;
   if (nmiss >= kManyMisses &&
-      (rc = finish_many_misses(h, src, a, t, e, nmiss, prefix, now, status, &nmiss)))
+      (rc = finish_many_misses(h, src, a, t, e, nmiss, prefix, now, status, &nmiss, sp)))
     return rc;
   if (nmiss == 0) return PHIP_OK;
   u32* miss = (u32*)h->buf[B_MISS].p;
@@ -1213,11 +1241,173 @@ int finish_receive(phip_handle* h, Src src, const uint64_t* a, const uint64_t* t
   return ordered(h, shifted(src, k), stop - k, ov, shifted(ow, k));
 }
 
-// Receive-mode batch (decoded): the fast path over its clean prefix, the
-// ordered path from its first incast or -0.0 on.
+// ------------------------------------------------- speculative receive ----
+// A decoded Receive batch without the classification pass:
+// k_receive_fast<Spec> merges every clean message at once, sets the dirty
+// ones (incast / -0.0) aside and keeps the pre-batch state of every record it
+// merges into (epoch + undo state, phip_device.hpp).  A batch with no dirty
+// message is then final; otherwise only the buckets its dirty messages name
+// depend on order, and those are set back and replayed in batch order.
+
+// Clear every record's epoch (k_spec_sweep) before the epoch values cycle.
+int spec_sweep(phip_handle* h) {
+  {
+    Launch l(h, "k_spec_sweep");
+    k_spec_sweep<<<grid_for(h->cap), kBlock, 0, h->stream>>>(table(h), h->cap);
+  }
+  HIPCHK(h, hipGetLastError());
+  h->spec_epoch = 0;
+  return PHIP_OK;
+}
+
+// The speculative fast pass over messages [0, n) at epoch ep: the hot
+// directory on stream2 beside the status fill, then k_receive_fast<Spec>.
+// *nlist entries land in B_MISS: misses, and the *ndirty set-aside dirty
+// messages (kSpecDirtyBit).
+template <class Src>
+int spec_apply(phip_handle* h, SoaIn<Src> in, u32 n, u8* status, u32 ep, u32* nlist, u32* ndirty) {
+  u32* miss;
+  int rc;
+  Sharded msh;
+  if ((rc = ensure(h, B_MISS, n, &miss)) ||
+      (rc = sharded(h, B_MSHARD, (n + 63) / 64, 64, &msh, false)))
+    return rc;
+  k_batch_reset<<<1, kShards, 0, h->stream>>>(h->ctr, msh.cnt);
+  HIPCHK(h, hipGetLastError());
+  const HotHdr* hot = nullptr;
+  const HotEntry* hot_dir = nullptr;
+  if (n >= kHotMinBatch) {
+    HIPCHK(h, hipEventRecord(h->ev_fork, h->stream));
+    if ((rc = fork_hot(h, in.src, n, &hot, &hot_dir))) return rc;
+  }
+  if (status) HIPCHK(h, hipMemsetAsync(status, PHIP_ST_MERGED, n, h->stream));
+  if ((rc = join_hot(h, hot))) return rc;
+  {
+    Launch l(h, "k_receive_fast");
+    k_receive_fast<SoaIn<Src>, true><<<fast_grid(h, n), kFastBlock, 0, h->stream>>>(
+        in, 0, n, table(h), msh, h->ctr, hot, hot_dir, ep);
+  }
+  HIPCHK(h, hipGetLastError());
+  if ((rc = pack_sharded(h, msh, 2, miss, nlist))) return rc;
+  if ((rc = check_flags(h))) return rc;
+  *ndirty = h->ctr_host[kCtrSpecDirty];
+  h->stats[0] = h->ctr_host[11];
+  h->stats[1] = 0;
+  h->stats[2] = *nlist - *ndirty;
+  return PHIP_OK;
+}
+
+// rocprim::select of `in`[0..n) by `pred` into `out`; the count into *m.
+template <class It, class Pred>
+int select_into(phip_handle* h, It in, u32 n, u32* out, Pred pred, u32* m) {
+  size_t tb = 0;
+  HIPCHK(h, rocprim::select(nullptr, tb, in, out, h->ctr + 19, (size_t)n, pred, h->stream));
+  u8* temp;
+  int rc;
+  if ((rc = ensure(h, B_TEMP, tb, &temp))) return rc;
+  {
+    Launch l(h, "select");
+    HIPCHK(h, rocprim::select(temp, tb, in, out, h->ctr + 19, (size_t)n, pred, h->stream));
+  }
+  if ((rc = read_ctr(h))) return rc;
+  *m = h->ctr_host[19];
+  return PHIP_OK;
+}
+
+// The misses of B_MISS[0..nlist) to insert and merge here (not set aside,
+// not naming a dirty bucket), back into B_MISS.
+template <class Src>
+int keep_misses(phip_handle* h, Src src, u32 nlist, const SpecCtx& sp, u32* nkeep) {
+  u32 *miss = (u32*)h->buf[B_MISS].p, *tmp;
+  int rc;
+  if ((rc = ensure(h, B_PICK, nlist, &tmp))) return rc;
+  HIPCHK(h, hipMemcpyAsync(tmp, miss, (size_t)nlist * 4, hipMemcpyDeviceToDevice, h->stream));
+  return select_into(h, tmp, nlist, miss, MissKeep<Src>{src, table(h), sp.set, sp.bits}, nkeep);
+}
+
+template <class Src>
+int spec_receive(phip_handle* h, Src src, const uint64_t* a, const uint64_t* t, const int64_t* e,
+                 u32 n, i64 now, const OutView& ow) {
+  int rc;
+  if (h->spec_epoch >= kEpochMax && (rc = spec_sweep(h))) return rc;
+  SpecCtx sp;
+  sp.ep = ++h->spec_epoch;
+  u32 nlist = 0, ndirty = 0;
+  if ((rc = spec_apply(h, SoaIn<Src>{src, a, t, e}, n, ow.status, sp.ep, &nlist, &ndirty)))
+    return rc;
+  if (ndirty == 0) return finish_misses(h, src, a, t, e, nlist, n, now, ow.status, &sp);
+
+  // 1. the dirty names' tags
+  u32 bits = 10;
+  while ((1ull << bits) < 4ull * ndirty) ++bits;
+  u64* set;
+  if ((rc = ensure(h, B_SPECSET, size_t(1) << bits, &set))) return rc;
+  HIPCHK(h, hipMemsetAsync(set, 0, (size_t(1) << bits) * 8, h->stream));
+  {
+    Launch l(h, "k_tagset_add");
+    k_tagset_add<Src><<<grid_for(nlist), kBlock, 0, h->stream>>>(src, (const u32*)h->buf[B_MISS].p,
+                                                                  nlist, table(h), set, bits);
+  }
+  HIPCHK(h, hipGetLastError());
+  sp.set = set;
+  sp.bits = bits;
+  // 2. every other bucket: its misses created and merged (commuting merges)
+  u32 nkeep = 0;
+  if ((rc = keep_misses(h, src, nlist, sp, &nkeep)) ||
+      (rc = finish_misses(h, src, a, t, e, nkeep, n, now, ow.status, &sp)))
+    return rc;
+  // 3. the dirty buckets' messages, in batch order (after the inserts above:
+  //    a grown table has moved records, the undo state with them)
+  u32* pick;
+  u32 m = 0;
+  if ((rc = ensure(h, B_PICK, n, &pick)) ||
+      (rc = select_into(h, rocprim::counting_iterator<u32>(0), n, pick,
+                        TagIn<Src>{src, table(h), set, bits}, &m)))
+    return rc;
+  if (m == 0) return set_err(h, PHIP_ERR_INVALID, "internal: no message names a dirty bucket");
+  // 4. their buckets back to the pre-batch state
+  {
+    Launch l(h, "k_spec_restore");
+    k_spec_restore<Src><<<grid_for(m), kBlock, 0, h->stream>>>(src, pick, m, table(h), sp.ep);
+  }
+  HIPCHK(h, hipGetLastError());
+  // 5. replayed by the ordered path (the Go loop on those buckets' messages)
+  uint64_t *pa, *pt;
+  int64_t* pe;
+  if ((rc = ensure(h, B_PA, m, &pa)) || (rc = ensure(h, B_PT, m, &pt)) ||
+      (rc = ensure(h, B_PE, m, &pe)))
+    return rc;
+  k_gather_states<<<grid_for(m), kBlock, 0, h->stream>>>(pick, m, a, t, e, pa, pt, pe);
+  HIPCHK(h, hipGetLastError());
+  OutView po{};
+  if (ow.status && (rc = ensure(h, B_PST, m, &po.status))) return rc;
+  if (ow.remaining && (rc = ensure(h, B_PREM, m, &po.remaining))) return rc;
+  if (ow.have && (rc = ensure(h, B_PHAVE, m, &po.have))) return rc;
+  if (ow.reply) {
+    if ((rc = ensure(h, B_PREP, m, &po.reply))) return rc;
+    HIPCHK(h, hipMemsetAsync(po.reply, 0, (size_t)m * sizeof(phip_state), h->stream));
+  }
+  OpView ov{};
+  ov.kind = nullptr; ov.kind0 = PHIP_OP_RECEIVE;
+  ov.now = nullptr; ov.now0 = now;
+  ov.a = pa; ov.t = pt; ov.e = pe;
+  if ((rc = ordered(h, Picked<Src>{src.blob, src, pick}, m, ov, po))) return rc;
+  k_scatter_outs<<<grid_for(m), kBlock, 0, h->stream>>>(pick, m, po.status, po.remaining, po.have,
+                                                        po.reply, ow.status, ow.remaining, ow.have,
+                                                        ow.reply);
+  HIPCHK(h, hipGetLastError());
+  return PHIP_OK;
+}
+
+// Receive-mode batch (decoded).  A batch of kSpecMinBatch messages or more is
+// merged speculatively (spec_receive) unless `classify`; otherwise the fast
+// path runs over its clean prefix and the ordered path from its first incast
+// or -0.0 on.
 template <class Src>
 int receive_decoded(phip_handle* h, Src src, const uint64_t* a, const uint64_t* t,
-                    const int64_t* e, u32 n, i64 now, const OutView& ow) {
+                    const int64_t* e, u32 n, i64 now, const OutView& ow, bool classify = false) {
+  if (!classify && n >= kSpecMinBatch && n < kSpecDirtyBit)
+    return spec_receive(h, src, a, t, e, n, now, ow);
   int rc;
   // The hot directory (read-only on the table and the batch) is built on
   // stream2 while the batch is classified.
@@ -1568,10 +1758,12 @@ extern "C" {
 
 int phip_abi_version(void) { return PHIP_ABI_VERSION; }
 
-#ifndef PHIP_BUILD_ID
-#error "PHIP_BUILD_ID is set by patrol_amd/Makefile (a hash of the sources)"
-#endif
+// phip_build_id: patrol_amd/Makefile links it from build/build_id.o (a hash
+// of every source and the flags); single-command builds of the sources
+// (tools/build_variants.sh) name theirs with -DPHIP_BUILD_ID.
+#ifdef PHIP_BUILD_ID
 const char* phip_build_id(void) { return PHIP_BUILD_ID; }
+#endif
 
 int phip_open(const phip_config* cfg, phip_handle** out) {
   if (!cfg || !out) return PHIP_ERR_INVALID;
@@ -1843,6 +2035,8 @@ int phip_restore(phip_handle* h, const uint8_t* in, uint64_t len) {
     HIPCHK(h, hipMemcpyAsync(h->arena, p + h->cap * sizeof(Rec), hd.arena_used, hipMemcpyHostToDevice, h->stream));
   HIPCHK(h, hipMemsetAsync(h->aux, 0, h->cap * sizeof(u32), h->stream));
   HIPCHK(h, hipMemcpyAsync(h->arena_cursor, &hd.arena_used, sizeof(u64), hipMemcpyHostToDevice, h->stream));
+  // the image's speculation epochs belong to the handle that wrote it
+  if (int rc = spec_sweep(h)) return rc;
   HIPCHK(h, hipStreamSynchronize(h->stream));
   h->n_buckets = hd.n_buckets;
   h->seed = hd.reserved[0];   // the image's placement
@@ -1965,7 +2159,8 @@ int phip_receive_soa(phip_handle* h, const phip_msgs* m, int64_t now, const phip
       (rc = stage(h, B_A, m->added, n, dev, &a)) || (rc = stage(h, B_T, m->taken, n, dev, &t)) ||
       (rc = stage(h, B_E, m->elapsed, n, dev, &e)) || (rc = outputs(h, res, n, dev, &ow)))
     return rc;
-  if ((rc = receive_decoded(h, src, a, t, e, n, now, ow))) return after_error(h, rc);
+  if ((rc = receive_decoded(h, src, a, t, e, n, now, ow, flags & PHIP_RECV_CLASSIFY)))
+    return after_error(h, rc);
   return copy_outputs(h, res, n, dev, ow);
 }
 
@@ -2494,14 +2689,4 @@ int route_pack(phip_handle* h, void* stream, const phip_msgs* m, uint32_t world,
 }
 const char* last_error(phip_handle* h) { return h ? h->err.c_str() : ""; }
 int handle_device(const phip_handle* h) { return h ? h->device : -1; }
-void* timing_begin(phip_handle* h, const char* name, void* stream) {
-  if (!h) return nullptr;
-  std::lock_guard<std::mutex> g(h->mu);
-  return h->timing ? new Launch(h, name, (hipStream_t)stream) : nullptr;
-}
-void timing_end(phip_handle* h, void* token) {
-  if (!h || !token) return;
-  std::lock_guard<std::mutex> g(h->mu);
-  delete static_cast<Launch*>(token);   // records the end event
-}
 }  // namespace phip_host

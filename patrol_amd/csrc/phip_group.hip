@@ -24,6 +24,8 @@
 // its peers' buffers with device copies; the all-reduce is an element-wise
 // max over the members' joins.  The packing, segment offsets, source order
 // and merge are the same code as the RCCL path.
+#include <dlfcn.h>
+
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -63,25 +65,6 @@ struct Buf {
     if (e == hipSuccess) cap = want;
     return e;
   }
-  // Grow to `bytes`, keeping the first `used` bytes (copied on stream s).
-  hipError_t grow_keep(size_t bytes, size_t used, hipStream_t s) {
-    if (cap >= bytes) return hipSuccess;
-    const size_t want = std::max(bytes, cap * 2) + 64;
-    void* np = nullptr;
-    hipError_t e = hipMalloc(&np, want);
-    if (e != hipSuccess) return e;
-    if (p && used) {
-      if ((e = hipMemcpyAsync(np, p, used, hipMemcpyDeviceToDevice, s)) != hipSuccess ||
-          (e = hipStreamSynchronize(s)) != hipSuccess) {
-        (void)hipFree(np);
-        return e;
-      }
-    }
-    if (p) (void)hipFree(p);
-    p = np;
-    cap = want;
-    return hipSuccess;
-  }
   void release() {
     if (p) (void)hipFree(p);
     p = nullptr;
@@ -89,10 +72,10 @@ struct Buf {
   }
 };
 
-// Messages per pipelined chunk.  A chunk's name bytes are bounded by
-// kChunk x 231 (PHIP_MAX_NAME_LEN), so the send sets are sized from the
-// batch's message count alone (no host read of its name offsets): 3.9 GB of
-// name space per set at full size, laid out for 288 GB of HBM.
+// Messages per pipelined chunk.  The send sets' name space is sized from the
+// chunks' real name bytes (the batch's offsets at the chunk boundaries, one
+// small read per call), so a name of any length fits and a set holds no more
+// than its largest chunk needs.
 constexpr uint32_t kChunk = 1u << 24;
 constexpr uint32_t kSmallChunk = 1u << 12;   // PHIP_GROUP_SMALL_CHUNKS
 
@@ -118,6 +101,42 @@ struct RecvSet {
   bool merge_pending = false;     // ev_merged recorded for a merge reading it
 };
 
+// Busy spans of one group call per stage (0 pack, 1 exchange, 2 merge):
+// event pairs recorded around each chunk's work on the stream it runs on,
+// summed after the call (phip_group_stage_ms).
+struct StageTimer {
+  std::vector<hipEvent_t> ev[3];   // pairs per stage: [2k] start, [2k+1] end
+  size_t used[3] = {0, 0, 0};
+  bool on = false;
+  void reset() { used[0] = used[1] = used[2] = 0; }
+  hipError_t mark(int s, hipStream_t st) {
+    if (!on) return hipSuccess;
+    if (used[s] == ev[s].size()) {
+      hipEvent_t e;
+      hipError_t r = hipEventCreate(&e);
+      if (r != hipSuccess) return r;
+      ev[s].push_back(e);
+    }
+    return hipEventRecord(ev[s][used[s]++], st);
+  }
+  hipError_t sum(int s, float* ms) {
+    *ms = 0;
+    for (size_t k = 0; k + 1 < used[s]; k += 2) {
+      float x = 0;
+      hipError_t r = hipEventSynchronize(ev[s][k + 1]);
+      if (r == hipSuccess) r = hipEventElapsedTime(&x, ev[s][k], ev[s][k + 1]);
+      if (r != hipSuccess) return r;
+      *ms += x;
+    }
+    return hipSuccess;
+  }
+  void release() {
+    for (auto& v : ev)
+      for (hipEvent_t e : v) (void)hipEventDestroy(e);
+    for (auto& v : ev) v.clear();
+  }
+};
+
 struct Member {
   phip_handle* h = nullptr;
   bool own = false;            // opened by the group (phip_group_open_all)
@@ -128,9 +147,10 @@ struct Member {
   hipEvent_t ev_done = nullptr;             // the call's last exchange
   SendSet set[2];
   RecvSet rset[2];             // chunk k is received into rset[k & 1]
-  Buf scan_tmp, ae;
+  Buf scan_tmp, ae, bounds;
   u64* host_k = nullptr;       // pinned [world]: this member's chunk count, to every peer
   u64 k_local = 0;             // (shared-device groups read each other's)
+  StageTimer tm;
   std::string err;
 };
 
@@ -288,6 +308,7 @@ int merge_chunk(Member& mb, RecvSet& rs, hipStream_t st, int64_t now) {
   if (rs.n) {
     const u64 n = rs.n;
     GHIP(mb, hipStreamWaitEvent(st, rs.ev_recv, 0));
+    GHIP(mb, mb.tm.mark(2, st));
     GHIP(mb, rs.offs.ensure(n * 4 + 8));
     u32* offs = (u32*)rs.offs.p;
     const u32* lens = (const u32*)rs.lens.p;
@@ -305,6 +326,7 @@ int merge_chunk(Member& mb, RecvSet& rs, hipStream_t st, int64_t now) {
     rm.taken = (const u64*)rs.t.p;
     rm.elapsed = (const int64_t*)rs.e.p;
     GPHIP(mb, phip_receive_soa(mb.h, &rm, now, nullptr, PHIP_DEVICE_PTRS));
+    GHIP(mb, mb.tm.mark(2, st));
   }
   GHIP(mb, hipEventRecord(rs.ev_merged, st));
   rs.merge_pending = true;
@@ -357,6 +379,13 @@ int copy_seg(Member& mb, const SendSet& src, const Seg& s_, const Seg& d_, RecvS
   return PHIP_OK;
 }
 
+// name_offs at the chunk boundaries: out[k] = offs[min(k * chunk, n)].
+__global__ void k_chunk_bounds(const uint32_t* __restrict__ offs, u32 n, u64 chunk, u64 kc,
+                               u32* __restrict__ out) {
+  const u64 k = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k <= kc) out[k] = offs[k * chunk < n ? k * chunk : n];
+}
+
 int member_receive(phip_group* g, Member& mb, const phip_msgs& in, int64_t now, uint64_t* sent,
                    uint64_t* merged, uint32_t flags) {
   const u32 W = g->world;
@@ -367,6 +396,7 @@ int member_receive(phip_group* g, Member& mb, const phip_msgs& in, int64_t now, 
   // send/recv pair to itself), so that the per-peer exchange below runs at
   // world 1, on one GPU, with the plan the multi-GPU group uses
   const bool rccl_self = (flags & PHIP_GROUP_RCCL_SELF) && !g->shared;
+  mb.tm.reset();
   if (W == 1 && !rccl_self) {
     // One owner: every message is this member's, so there is nothing to
     // pack or exchange; the batch is merged as it came (the sender-side
@@ -374,7 +404,9 @@ int member_receive(phip_group* g, Member& mb, const phip_msgs& in, int64_t now, 
     if (sent) *sent = n;
     if (merged) *merged = n;
     if (n == 0) return PHIP_OK;
+    GHIP(mb, mb.tm.mark(2, st));
     GPHIP(mb, phip_receive_soa(mb.h, &in, now, nullptr, PHIP_DEVICE_PTRS));
+    GHIP(mb, mb.tm.mark(2, st));
     return PHIP_OK;
   }
   // The batch's producers are on the handle's stream: both pipeline streams
@@ -388,8 +420,22 @@ int member_receive(phip_group* g, Member& mb, const phip_msgs& in, int64_t now, 
   mb.k_local = k_local;
   for (u32 p = 0; p < W; ++p) mb.host_k[p] = k_local;
   const u64 cmax = std::max<u64>(1, std::min<u64>(n, chunk));
-  for (SendSet& ss : mb.set) {
-    GHIP(mb, ss.names.ensure(cmax * PHIP_MAX_NAME_LEN + 64));
+  // name bytes per chunk: the offsets at the chunk boundaries
+  u64 set_bytes[2] = {0, 0};
+  if (n) {
+    std::vector<u32> bnd(k_local + 1);
+    GHIP(mb, mb.bounds.ensure((k_local + 1) * 4));
+    k_chunk_bounds<<<(unsigned)((k_local + 1 + 255) / 256), 256, 0, st>>>(
+        in.name_offs, n, chunk, k_local, (u32*)mb.bounds.p);
+    GHIP(mb, hipGetLastError());
+    GHIP(mb, hipMemcpyAsync(bnd.data(), mb.bounds.p, (k_local + 1) * 4, hipMemcpyDeviceToHost, st));
+    GHIP(mb, hipStreamSynchronize(st));
+    for (u64 k = 0; k < k_local; ++k)
+      set_bytes[k & 1] = std::max<u64>(set_bytes[k & 1], (u64)(bnd[k + 1] - bnd[k]));
+  }
+  for (u32 si = 0; si < 2; ++si) {
+    SendSet& ss = mb.set[si];
+    GHIP(mb, ss.names.ensure(set_bytes[si] + 64));
     GHIP(mb, ss.lens.ensure(cmax * 4 + 4));
     GHIP(mb, ss.a.ensure(cmax * 8 + 8));
     GHIP(mb, ss.t.ensure(cmax * 8 + 8));
@@ -408,11 +454,13 @@ int member_receive(phip_group* g, Member& mb, const phip_msgs& in, int64_t now, 
     if (ss.x_pending) GHIP(mb, hipStreamWaitEvent(mb.sp, ss.ev_x, 0));
     const phip_msgs c = chunk_of(in, chunk, k);
     u64* sz = (u64*)ss.sizes.p;
+    GHIP(mb, mb.tm.mark(0, mb.sp));
     if (phip_host::route_pack(mb.h, mb.sp, &c, W, dir, (uint8_t*)ss.names.p, (uint32_t*)ss.lens.p,
                               (uint64_t*)ss.a.p, (uint64_t*)ss.t.p, (int64_t*)ss.e.p, sz, sz + W) !=
         PHIP_OK)
       return fail(mb, PHIP_ERR_HIP, "route pack: %s", phip_host::last_error(mb.h));
     GHIP(mb, hipMemcpyAsync(sz + 2 * W, mb.host_k, W * 8, hipMemcpyHostToDevice, mb.sp));
+    GHIP(mb, mb.tm.mark(0, mb.sp));
     GHIP(mb, hipEventRecord(ss.ev_pack, mb.sp));
     return PHIP_OK;
   };
@@ -422,6 +470,7 @@ int member_receive(phip_group* g, Member& mb, const phip_msgs& in, int64_t now, 
     SendSet& ss = mb.set[k & 1];
     u64* sz = (u64*)ss.sizes.p;
     GHIP(mb, hipStreamWaitEvent(mb.sx, ss.ev_pack, 0));
+    GHIP(mb, mb.tm.mark(1, mb.sx));
     if (!g->shared) {
       GNCCL(mb, ncclGroupStart());
       GNCCL(mb, ncclAllToAll(sz, sz + 3 * W, 1, ncclUint64, mb.comm, mb.sx));
@@ -430,6 +479,7 @@ int member_receive(phip_group* g, Member& mb, const phip_msgs& in, int64_t now, 
       GNCCL(mb, ncclGroupEnd());
     }
     GHIP(mb, hipMemcpyAsync(ss.host, sz, 6 * W * sizeof(u64), hipMemcpyDeviceToHost, mb.sx));
+    GHIP(mb, mb.tm.mark(1, mb.sx));
     GHIP(mb, hipEventRecord(ss.ev_sz, mb.sx));
     return PHIP_OK;
   };
@@ -439,7 +489,6 @@ int member_receive(phip_group* g, Member& mb, const phip_msgs& in, int64_t now, 
   u64 K = 1, n_send = 0, recv_msgs = 0;
   u64 packed = k_local > 1 ? 2 : 1;   // chunks whose pack is queued
   std::vector<Seg> plan;
-  void* tm = phip_host::timing_begin(mb.h, "rccl_exchange", mb.sx);
   for (u64 k = 0; k < K; ++k) {
     SendSet& ss = mb.set[k & 1];
     GHIP(mb, hipEventSynchronize(ss.ev_sz));
@@ -471,6 +520,7 @@ int member_receive(phip_group* g, Member& mb, const phip_msgs& in, int64_t now, 
     if ((rc = recv_room(mb, rs, c_recv, b_recv))) return rc;
     // 4. the segments: one send and one receive per peer and column; this
     //    member's own segment is a device copy unless rccl_self
+    GHIP(mb, mb.tm.mark(1, mb.sx));
     if (g->shared) {
       for (u32 p = 0; p < W; ++p) {
         const Member& src = g->m[p];
@@ -505,6 +555,7 @@ int member_receive(phip_group* g, Member& mb, const phip_msgs& in, int64_t now, 
       }
       GNCCL(mb, ncclGroupEnd());
     }
+    GHIP(mb, mb.tm.mark(1, mb.sx));
     GHIP(mb, hipEventRecord(ss.ev_x, mb.sx));
     GHIP(mb, hipEventRecord(rs.ev_recv, mb.sx));
     ss.x_pending = true;
@@ -538,7 +589,6 @@ int member_receive(phip_group* g, Member& mb, const phip_msgs& in, int64_t now, 
     if (!g->shared && merge_prev && (rc = merge_chunk(mb, mb.rset[(k - 1) & 1], st, now)))
       return rc;
   }
-  phip_host::timing_end(mb.h, tm);
   if (sent) *sent = n_send;
   if (merged) *merged = recv_msgs;
   // the last chunk's merge; the handle's stream ends behind every exchange
@@ -556,14 +606,19 @@ __global__ void k_max_into(int64_t* __restrict__ dst, const int64_t* __restrict_
 
 int member_anti_entropy(phip_group* g, Member& mb, int64_t* reps, uint32_t nrep, uint64_t B) {
   GHIP(mb, hipSetDevice(mb.device));
+  mb.tm.reset();
+  hipStream_t st = (hipStream_t)phip_host::handle_stream(mb.h);
   if (g->world == 1) {   // nothing to exchange: the fused local join
+    GHIP(mb, mb.tm.mark(0, st));
     GPHIP(mb, phip_ae_join(mb.h, reps, nrep, B, PHIP_DEVICE_PTRS));
+    GHIP(mb, mb.tm.mark(0, st));
     return PHIP_OK;
   }
-  hipStream_t st = (hipStream_t)phip_host::handle_stream(mb.h);
   GHIP(mb, mb.ae.ensure((size_t)3 * B * 8 * (g->shared ? 2 : 1)));
   int64_t* j = (int64_t*)mb.ae.p;
+  GHIP(mb, mb.tm.mark(0, st));
   GPHIP(mb, phip_ae_local_max(mb.h, reps, nrep, B, j, PHIP_DEVICE_PTRS));
+  GHIP(mb, mb.tm.mark(0, st));
   if (g->shared) {   // the all-reduce: every member's join, max'd element-wise
     if (!g->bar.wait()) return fail(mb, PHIP_ERR_INVALID, "another member failed");
     int64_t* jm = j + 3 * B;
@@ -575,13 +630,17 @@ int member_anti_entropy(phip_group* g, Member& mb, int64_t* reps, uint32_t nrep,
     }
     GHIP(mb, hipStreamSynchronize(st));
     if (!g->bar.wait()) return fail(mb, PHIP_ERR_INVALID, "another member failed");
+    GHIP(mb, mb.tm.mark(2, st));
     GPHIP(mb, phip_ae_apply(mb.h, reps, nrep, B, jm, PHIP_DEVICE_PTRS));
+    GHIP(mb, mb.tm.mark(2, st));
     return PHIP_OK;
   }
-  void* tm = phip_host::timing_begin(mb.h, "rccl_allreduce");
+  GHIP(mb, mb.tm.mark(1, st));
   GNCCL(mb, ncclAllReduce(j, j, 3 * B, ncclInt64, ncclMax, mb.comm, st));
-  phip_host::timing_end(mb.h, tm);
+  GHIP(mb, mb.tm.mark(1, st));
+  GHIP(mb, mb.tm.mark(2, st));
   GPHIP(mb, phip_ae_apply(mb.h, reps, nrep, B, j, PHIP_DEVICE_PTRS));
+  GHIP(mb, mb.tm.mark(2, st));
   return PHIP_OK;
 }
 
@@ -603,7 +662,8 @@ void destroy(phip_group* g) {
       for (hipEvent_t ev : {rs.ev_recv, rs.ev_merged})
         if (ev) (void)hipEventDestroy(ev);
     }
-    for (Buf* b : {&mb.scan_tmp, &mb.ae}) b->release();
+    for (Buf* b : {&mb.scan_tmp, &mb.ae, &mb.bounds}) b->release();
+    mb.tm.release();
     if (mb.host_k) (void)hipHostFree(mb.host_k);
     if (mb.ev_done) (void)hipEventDestroy(mb.ev_done);
     if (mb.sp) (void)hipStreamDestroy(mb.sp);
@@ -743,6 +803,39 @@ int phip_group_receive(phip_group* g, const phip_msgs* batches, int64_t now, uin
     return member_receive(g, g->m[i], batches[i], now, sent ? sent + i : nullptr,
                           merged ? merged + i : nullptr, flags);
   });
+}
+
+int phip_group_set_timing(phip_group* g, int on) {
+  if (!g) return PHIP_ERR_INVALID;
+  for (Member& mb : g->m) mb.tm.on = on != 0;
+  return PHIP_OK;
+}
+
+int phip_group_stage_ms(phip_group* g, uint32_t i, float* ms) {
+  if (!g || !ms || i >= g->m.size()) return PHIP_ERR_INVALID;
+  Member& mb = g->m[i];
+  if (hipSetDevice(mb.device) != hipSuccess) return PHIP_ERR_HIP;
+  for (int s = 0; s < 3; ++s)
+    if (mb.tm.sum(s, &ms[s]) != hipSuccess) return PHIP_ERR_HIP;
+  return PHIP_OK;
+}
+
+int phip_group_rccl_info(phip_group* g, uint32_t i, int32_t* version, int32_t* comm_count,
+                         char* lib_path, uint32_t path_cap) {
+  if (!g || i >= g->m.size()) return PHIP_ERR_INVALID;
+  const Member& mb = g->m[i];
+  int v = 0;
+  if (ncclGetVersion(&v) != ncclSuccess) return PHIP_ERR_RCCL;
+  if (version) *version = v;
+  int c = 0;
+  if (mb.comm && ncclCommCount(mb.comm, &c) != ncclSuccess) return PHIP_ERR_RCCL;
+  if (comm_count) *comm_count = c;
+  if (lib_path && path_cap) {
+    Dl_info di{};
+    const char* p = dladdr((const void*)&ncclGetVersion, &di) && di.dli_fname ? di.dli_fname : "";
+    std::snprintf(lib_path, path_cap, "%s", p);
+  }
+  return PHIP_OK;
 }
 
 int phip_group_anti_entropy(phip_group* g, int64_t* const* replicas, uint32_t nrep,

@@ -11,13 +11,6 @@ namespace phip_host {
 void* handle_stream(phip_handle* h);
 int handle_device(const phip_handle* h);
 
-// A timed region on `stream` (the handle's when null; HIP events, like the
-// engine's own kernels; nothing when timing is off): the group's RCCL calls
-// show up in phip_last_timings under `name`.  timing_end takes what
-// timing_begin gave.
-void* timing_begin(phip_handle* h, const char* name, void* stream = nullptr);
-void timing_end(phip_handle* h, void* token);
-
 // Owner routing as phip_route_pack does it, queued on `stream` (a hipStream_t
 // of the handle's device) with no host synchronisation: the pipelined
 // exchange of phip_group_receive packs chunk k+1 while chunk k travels.

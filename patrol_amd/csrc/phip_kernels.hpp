@@ -1,9 +1,10 @@
 // HIP kernels of libpatrolhip (gfx950).  Host orchestration: phip_engine.hip.
 //
-// Table: recs[2^L] 64-byte slot records (tag, state and name in one HBM
-// burst) + aux[2^L] u32 scratch used only by inserting/seeding batches.
-// Home slot = top L bits of tag * 2^64/phi (Fibonacci hashing), linear
-// probing; a lookup touches one 64-byte record per probe step.
+// Table: recs[2^L] 128-byte slot records (tag, state and name in the first
+// 64 bytes, the speculative batch's undo state after them) + aux[2^L] u32
+// scratch used only by inserting/seeding batches.  Home slot = top L bits of
+// a seeded mix of the tag, linear probing; a lookup reads the first 48 or 64
+// bytes of one record per probe step.
 #pragma once
 #include <type_traits>
 
@@ -203,9 +204,11 @@ struct Sharded {
 // A batch's counters in one launch: ctr[16] zero except ctr[5] (first
 // malformed datagram) and ctr[kCtrDirty] (first dirty message), which start
 // at "none"; and, when given, a sharded list's kShards counters.
+constexpr u32 kCtrSpecDirty = 18;   // dirty messages a speculative fast pass set aside
 __global__ __launch_bounds__(kShards) void k_batch_reset(u32* ctr, u32* shard_cnt) {
   const u32 t = threadIdx.x;
   if (t < 16) ctr[t] = (t == 5 || t == 12) ? ~0u : 0u;
+  if (t == kCtrSpecDirty) ctr[t] = 0;
   if (shard_cnt) shard_cnt[t] = 0;
 }
 
@@ -291,6 +294,18 @@ __device__ inline Rec load_rec(const Rec* p) {
   r.created = (i64)(((u64)d.y << 32) | d.x);
   r.name2 = ((u64)d.w << 32) | d.z;
   return r;
+}
+
+// The first 64 bytes of a record (everything but the undo state) as four
+// 16-byte stores.
+__device__ inline void store_rec64(Rec* p, const Rec& r) {
+  uint4* q = reinterpret_cast<uint4*>(p);
+  q[0] = make_uint4((u32)r.tag, (u32)(r.tag >> 32), (u32)r.added, (u32)(r.added >> 32));
+  q[1] = make_uint4((u32)r.taken, (u32)(r.taken >> 32), (u32)(u64)r.elapsed,
+                    (u32)((u64)r.elapsed >> 32));
+  q[2] = make_uint4((u32)r.name0, (u32)(r.name0 >> 32), (u32)r.name1, (u32)(r.name1 >> 32));
+  q[3] = make_uint4((u32)(u64)r.created, (u32)((u64)r.created >> 32), (u32)r.name2,
+                    (u32)(r.name2 >> 32));
 }
 
 // The first 48 bytes only (tag, state, name words 0-1); name2 and created
@@ -821,12 +836,38 @@ __device__ inline bool tail_match(const u64 (&htail)[kHotTailWords][kHotMax], u3
   return eq;
 }
 
-// Messages [lo, n) of the batch (lo a multiple of 64: a segment of a batch
-// classified segment by segment, or 0).
-template <class In>
+// Speculative merge (Spec): the first merge of batch epoch `ep` into a record
+// moves the record's epoch to ep by a CAS on name0; the winner stores the
+// state it read as the undo state.  No merge of the batch reaches the record
+// before that CAS (every merger first sees epoch ep or loses the CAS to the
+// winner), so the state the winner read is the record's pre-batch state.
+__device__ inline void spec_log(Rec* r, u64 name0, u64 a, u64 t, i64 e, u32 ep) {
+  if (rec_epoch(name0) == ep) return;
+  if (atomicCAS(&r->name0, name0, with_epoch(name0, ep)) == name0) {
+    r->undo_added = a;
+    r->undo_taken = t;
+    r->undo_elapsed = e;
+  }
+}
+// A set-aside entry of a speculative batch's miss list: a dirty message.
+constexpr u32 kSpecDirtyBit = 0x80000000u;
+// Decoded Receive batches of this many messages or more are merged
+// speculatively (below it the classification pass costs a few µs).
+constexpr u32 kSpecMinBatch = kHotMinBatch;
+
+// Messages [lo, n) of the batch (lo a multiple of 64, or 0).
+//
+// Spec = false: the batch was classified first (k_classify) and only its
+// clean prefix is merged.
+// Spec = true (speculative receive, no classification pass): every clean
+// message is merged, the dirty ones (incast / -0.0, replica_dirty) are set
+// aside in the miss list with kSpecDirtyBit, and every record the batch
+// merges into keeps its pre-batch state (spec_log).  The host then fixes the
+// buckets the dirty messages name (phip_engine.hip spec_receive).
+template <class In, bool Spec = false>
 __global__ __launch_bounds__(kFastBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_receive_fast(
     In in, u32 lo, u32 n, Table T, Sharded miss, u32* ctr,
-    const HotHdr* __restrict__ hot, const HotEntry* __restrict__ hot_dir) {
+    const HotHdr* __restrict__ hot, const HotEntry* __restrict__ hot_dir, u32 ep = 0) {
   __shared__ u32 hslot[kHotLds];        // directory index + 1 (0 = empty)
   __shared__ u64 htag[kHotMax], hw0[kHotMax], hw1[kHotMax], hw2[kHotMax];
   __shared__ u32 hrec[kHotMax], haoff[kHotMax];
@@ -904,7 +945,14 @@ __global__ __launch_bounds__(kFastBlock) __attribute__((amdgpu_waves_per_eu(8, 8
     const u64 ea = enc_replica_nz(ra), et = enc_replica_nz(rt), ee = (u64)re ^ kSign;
 
     bool missed = false;
-    if (valid) {
+    u32 entry = i;
+    bool dirt = false;
+    if constexpr (Spec) dirt = valid && replica_dirty(ra, rt, re);
+    if (dirt) {   // set aside (speculative batch): the host orders its bucket
+      missed = true;
+      entry = i | kSpecDirtyBit;
+      ++hits;   // (counted apart below: hits holds set-aside messages in Spec)
+    } else if (valid) {
       int hidx = -1;
       if (nh) {
         for (u32 hs = hot_home(tag);; hs = (hs + 1) & (kHotLds - 1)) {
@@ -922,7 +970,7 @@ __global__ __launch_bounds__(kFastBlock) __attribute__((amdgpu_waves_per_eu(8, 8
         }
       }
       if (hidx >= 0) {
-        ++hits;
+        if constexpr (!Spec) ++hits;
         if (ea > hmax[0][hidx]) atomicMax(&hmax[0][hidx], ea);
         if (et > hmax[1][hidx]) atomicMax(&hmax[1][hidx], et);
         if (ee > hmax[2][hidx]) atomicMax(&hmax[2][hidx], ee);
@@ -942,6 +990,9 @@ __global__ __launch_bounds__(kFastBlock) __attribute__((amdgpu_waves_per_eu(8, 8
         }
         if (pr == kFound) {
           Rec* r = &T.recs[s];
+          if constexpr (Spec) {
+            if (rec_epoch(cur.name0) != ep) spec_log(r, cur.name0, cur.added, cur.taken, cur.elapsed, ep);
+          }
           if (ea > cur.added) atomicMax(&r->added, ea);
           if (et > cur.taken) atomicMax(&r->taken, et);
           if (ee > ((u64)cur.elapsed ^ kSign)) atomicMax(&r->elapsed, (i64)(ee ^ kSign));
@@ -951,12 +1002,12 @@ __global__ __launch_bounds__(kFastBlock) __attribute__((amdgpu_waves_per_eu(8, 8
         }
       }
     }
-    miss.append(chunk, missed, i);
+    miss.append(chunk, missed, entry);
   }
   if (hits) atomicAdd(&hhits, hits);
   __syncthreads();
   if (threadIdx.x == 0) {
-    if (hhits) atomicAdd(&ctr[10], hhits);
+    if (hhits) atomicAdd(&ctr[Spec ? kCtrSpecDirty : 10], hhits);
     if (blockIdx.x == 0) ctr[11] = nh;
   }
 
@@ -966,10 +1017,158 @@ __global__ __launch_bounds__(kFastBlock) __attribute__((amdgpu_waves_per_eu(8, 8
     if (!(xa | xt | xe)) continue;
     Rec* r = &T.recs[hrec[j]];
     const u64 ca = r->added, ct = r->taken, ce = (u64)r->elapsed ^ kSign;
+    if constexpr (Spec) spec_log(r, r->name0, ca, ct, (i64)(ce ^ kSign), ep);
     if (xa > ca) atomicMax(&r->added, xa);
     if (xt > ct) atomicMax(&r->taken, xt);
     if (xe > ce) atomicMax(&r->elapsed, (i64)(xe ^ kSign));
   }
+}
+
+// ------------------------------------------------ speculative receive ----
+// The dirty messages of a speculative batch (incasts, -0.0 fields) are the
+// only ones whose outcome depends on order, and only within their own
+// bucket (repo.go:78-90: an incast replies with the state at its position;
+// bucket.go:250-256: the first +-0 seen is kept).  So the buckets they name
+// (by tag: a name sharing a tag with a dirty one is handled the same way,
+// which is always exact) are set back to their pre-batch state (undo) and
+// all of their messages are replayed in batch order by the ordered path;
+// every other bucket's messages commute and are final after the fast pass.
+
+// Every record's epoch cleared: before an epoch value is reused, and after a
+// restore from a snapshot image.
+__global__ __launch_bounds__(kBlock) void k_spec_sweep(Table T, u64 cap) {
+  const u64 s = (u64)blockIdx.x * kBlock + threadIdx.x;
+  if (s >= cap) return;
+  Rec* r = &T.recs[s];
+  const u64 w0 = r->name0;
+  if (rec_epoch(w0)) r->name0 = with_epoch(w0, 0);
+}
+
+// Open-addressing set of 64-bit table tags (0 = empty), 2^bits entries.
+__device__ inline u32 tagset_home(u64 tag, u32 bits) {
+  return (u32)((tag * 0x9E3779B97F4A7C15ull) >> (64 - bits));
+}
+__device__ inline bool tagset_has(const u64* __restrict__ set, u32 bits, u64 tag) {
+  const u32 mask = (1u << bits) - 1;
+  for (u32 h = tagset_home(tag, bits);; h = (h + 1) & mask) {
+    const u64 v = set[h];
+    if (v == tag) return true;
+    if (v == 0) return false;
+  }
+}
+template <class Src>
+__device__ inline u64 name_tag(const Src& src, u32 i, const Table& T) {
+  u64 off; u32 len;
+  src.get(i, off, len);
+  Name nm;
+  load_name_wide<false>(src.blob, off, len, nm);
+  return T.tag(nm.h);
+}
+
+// The tags of the names of the set-aside entries (kSpecDirtyBit) of
+// list[0..n).
+template <class Src>
+__global__ __launch_bounds__(kBlock) void k_tagset_add(Src src, const u32* __restrict__ list, u32 n,
+                                                      Table T, u64* set, u32 bits) {
+  const u32 j = blockIdx.x * kBlock + threadIdx.x;
+  if (j >= n) return;
+  const u32 v = list[j];
+  if (!(v & kSpecDirtyBit)) return;
+  const u64 tag = name_tag(src, v & ~kSpecDirtyBit, T);
+  const u32 mask = (1u << bits) - 1;
+  for (u32 h = tagset_home(tag, bits);; h = (h + 1) & mask) {
+    const u64 v = set[h];
+    if (v == tag) return;
+    if (v == 0) {
+      const u64 old = atomicCAS((unsigned long long*)&set[h], 0ull, (unsigned long long)tag);
+      if (old == 0 || old == tag) return;
+    }
+  }
+}
+
+// rocprim::select predicates: messages whose tag is in the set (over batch
+// indices), and the misses to keep (a list entry not set aside and not in
+// the set).
+template <class Src>
+struct TagIn {
+  Src src;
+  Table T;
+  const u64* set;
+  u32 bits;
+  __device__ bool operator()(u32 i) const { return tagset_has(set, bits, name_tag(src, i, T)); }
+};
+template <class Src>
+struct MissKeep {
+  Src src;
+  Table T;
+  const u64* set;
+  u32 bits;
+  __device__ bool operator()(u32 v) const {
+    return !(v & kSpecDirtyBit) && !tagset_has(set, bits, name_tag(src, v, T));
+  }
+};
+
+// The picked messages' records back to their pre-batch state (those the
+// batch merged into: epoch ep).  Many messages name one record; they all
+// write the same undo state.
+template <class Src>
+__global__ __launch_bounds__(kBlock) void k_spec_restore(Src src, const u32* __restrict__ pick, u32 m,
+                                                        Table T, u32 ep) {
+  const u32 j = blockIdx.x * kBlock + threadIdx.x;
+  if (j >= m) return;
+  u64 off; u32 len;
+  src.get(pick[j], off, len);
+  Name nm;
+  load_name_wide<false>(src.blob, off, len, nm);
+  u32 s;
+  Rec cur;
+  if (probe(T, nm, src.blob, &s, &cur) != kFound || rec_epoch(cur.name0) != ep) return;
+  Rec* r = &T.recs[s];
+  const u64 a = r->undo_added, t = r->undo_taken;
+  const i64 e = r->undo_elapsed;
+  r->added = a;
+  r->taken = t;
+  r->elapsed = e;
+}
+
+// A sub-batch of a batch: message j of the view is message pick[j].
+template <class Src>
+struct Picked {
+  const u8* blob;
+  Src src;
+  const u32* pick;
+  template <bool NT = false>
+  __device__ inline void get(u32 j, u64& off, u32& len) const {
+    src.template get<NT>(pick[j], off, len);
+  }
+};
+
+// The picked messages' replica columns, gathered in pick order.
+__global__ __launch_bounds__(kBlock) void k_gather_states(const u32* __restrict__ pick, u32 m,
+                                                         const uint64_t* __restrict__ a,
+                                                         const uint64_t* __restrict__ t,
+                                                         const int64_t* __restrict__ e,
+                                                         uint64_t* ga, uint64_t* gt, int64_t* ge) {
+  const u32 j = blockIdx.x * kBlock + threadIdx.x;
+  if (j >= m) return;
+  const u32 i = pick[j];
+  ga[j] = a[i];
+  gt[j] = t[i];
+  ge[j] = e[i];
+}
+
+// The sub-batch's results back to the picked positions.
+__global__ __launch_bounds__(kBlock) void k_scatter_outs(
+    const u32* __restrict__ pick, u32 m, const u8* __restrict__ st, const uint64_t* __restrict__ rem,
+    const uint64_t* __restrict__ hv, const phip_state* __restrict__ rep, u8* status,
+    uint64_t* remaining, uint64_t* have, phip_state* reply) {
+  const u32 j = blockIdx.x * kBlock + threadIdx.x;
+  if (j >= m) return;
+  const u32 i = pick[j];
+  if (status) status[i] = st[j];
+  if (remaining) remaining[i] = rem[j];
+  if (have) have[i] = hv[j];
+  if (reply) reply[i] = rep[j];
 }
 
 // The messages of a list (the fast batch's misses, after the insert
@@ -1262,7 +1461,7 @@ __global__ void k_publish(Src src, u32 base, u32 n, const u32* __restrict__ clai
     r.name0 = (nm.w0 & 0xFFu) | (a << 32);
   }
   r.name0 = with_flags(r.name0, kRecPublished | kRecNew);
-  T.recs[s] = r;
+  store_rec64(&T.recs[s], r);
   T.aux[s] = 0xFFFFFFFFu;
 }
 
@@ -1324,6 +1523,13 @@ __global__ __launch_bounds__(kBlock) void k_rehash(const Rec* __restrict__ old,
   Rec* q = &T.recs[d];
   q->added = r.added; q->taken = r.taken; q->elapsed = r.elapsed;
   q->name0 = r.name0; q->name1 = r.name1; q->created = r.created; q->name2 = r.name2;
+  // a table that grows in the middle of a speculative batch (its misses'
+  // inserts) keeps the undo state of the records the batch touched
+  if (rec_epoch(r.name0)) {
+    q->undo_added = old[s].undo_added;
+    q->undo_taken = old[s].undo_taken;
+    q->undo_elapsed = old[s].undo_elapsed;
+  }
   T.aux[d] = old_aux[s];
 }
 
@@ -2652,8 +2858,6 @@ __device__ inline void fold_window_absorb(u32 pos, u32 lim, FState& R, GMax& G, 
   G = gend;
 }
 
-// Ablation variants (tools only, PHIP_FOLD_VARIANT): 1 = no state test
-// (every op unchanged: streaming cost alone).
 __global__ __launch_bounds__(kFoldThreads) void k_fold_block(
     const u32* __restrict__ huge_list, u32 nhuge, const u32* __restrict__ seg_slot,
     const u64* __restrict__ hoff, const u32* __restrict__ seg_count,

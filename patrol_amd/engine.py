@@ -337,14 +337,18 @@ class GPURepo:
         return stop.value
 
     def receive_soa(self, names, added, taken, elapsed, now: int, name_offs=None, n=None,
-                    status=None, device=False):
+                    status=None, device=False, classify=False, reply=None):
         """Receive over decoded states.  With device=True every array is a torch
-        CUDA tensor (names = uint8 blob, name_offs = int32/uint32 offsets)."""
+        CUDA tensor (names = uint8 blob, name_offs = int32/uint32 offsets;
+        reply: an int64 [n, 4] tensor for the phip_state replies).
+        classify=True: PHIP_RECV_CLASSIFY (classification pass first, no
+        speculation; the same results)."""
+        fl = _lib.RECV_CLASSIFY if classify else 0
         if device:
             m = phip_msgs(n, 0, _ptr(names), _ptr(name_offs), _ptr(added), _ptr(taken), _ptr(elapsed))
-            res = phip_results(_ptr(status), None, None, None)
+            res = phip_results(_ptr(status), None, None, _ptr(reply))
             self._check(self.L.phip_receive_soa(self.h, C.byref(m), int(now), C.byref(res),
-                                                DEVICE_PTRS))
+                                                DEVICE_PTRS | fl))
             return None
         n = len(names)
         blob, offs = names_blob(names)
@@ -352,7 +356,7 @@ class GPURepo:
         m = phip_msgs(n, 0, blob.ctypes.data, offs.ctypes.data, a.ctypes.data, t.ctypes.data,
                       e.ctypes.data)
         res, st, _, _, reply = self._results(n, want_reply=True)
-        self._check(self.L.phip_receive_soa(self.h, C.byref(m), int(now), C.byref(res), 0))
+        self._check(self.L.phip_receive_soa(self.h, C.byref(m), int(now), C.byref(res), fl))
         return dict(status=st[:n], reply=reply[:n])
 
     def upsert_soa(self, names, added, taken, elapsed, now: int):
@@ -483,6 +487,38 @@ class GPUGroup:
             (_lib.GROUP_SMALL_CHUNKS if small_chunks else 0)
         self._check(self.L.phip_group_receive(self.g, msgs, int(now), sent, merged, flags))
         return [int(x) for x in sent], [int(x) for x in merged]
+
+    def set_timing(self, on: bool = True):
+        """phip_group_set_timing: per-stage event timing of later calls."""
+        self._check(self.L.phip_group_set_timing(self.g, 1 if on else 0))
+
+    def stage_ms(self, i: int = 0):
+        """phip_group_stage_ms: member i's busy ms of the last call per stage
+        -> dict(pack, exchange, merge) (anti-entropy: local join, all-reduce,
+        apply)."""
+        ms = (C.c_float * 3)()
+        self._check(self.L.phip_group_stage_ms(self.g, i, ms))
+        return dict(pack=float(ms[0]), exchange=float(ms[1]), merge=float(ms[2]))
+
+    def rccl_info(self, i: int = 0):
+        """phip_group_rccl_info: the RCCL member i runs on -> dict(version,
+        comm_count, lib_path, mapped): `mapped` lists every librccl this
+        process has mapped (/proc/self/maps), to show one copy is shared."""
+        v, c = C.c_int32(), C.c_int32()
+        buf = C.create_string_buffer(4096)
+        self._check(self.L.phip_group_rccl_info(self.g, i, C.byref(v), C.byref(c), buf, 4096))
+        mapped = set()
+        try:
+            with open("/proc/self/maps") as f:
+                for line in f:
+                    p = line.split()[-1] if len(line.split()) >= 6 else ""
+                    if "librccl" in p:
+                        mapped.add(os.path.realpath(p))
+        except OSError:
+            pass
+        return dict(version=int(v.value), comm_count=int(c.value),
+                    lib_path=os.path.realpath(buf.value.decode()) if buf.value else None,
+                    mapped=sorted(mapped))
 
     def anti_entropy(self, replicas):
         """replicas: one contiguous int64 CUDA tensor [R, 3, B] per local member."""

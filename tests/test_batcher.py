@@ -105,3 +105,25 @@ def test_batcher_api_take_reference_table(pa):
                (r["code"], r["body"]), r
     b.close()
     repo.close()
+
+
+def test_batcher_coalesces_native_clients_at_50us(pa):
+    """Coalescing at a µs window with native client threads (tools/take_load,
+    C++, one blocking phip_batcher_take per request, as Go runs one
+    goroutine per HTTP request): 48 threads, a 50 µs window.  Every request
+    completes and batches hold several requests on average (the batch's GPU
+    call is ~25 µs, so the threads waiting on one batch meet in the next)."""
+    import json as _json
+    import subprocess
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools",
+                       "take_load")
+    if not os.path.exists(exe):
+        pytest.fail("tools/take_load is not built (patrol_amd/Makefile builds it)")
+    out = subprocess.run([exe, "48", "300", "50", "100000", "0"], capture_output=True, text=True,
+                         timeout=120)
+    assert out.returncode == 0, out.stderr
+    r = _json.loads(out.stdout.strip().splitlines()[-1])
+    assert r["requests"] == 48 * 300
+    assert r["ok_fraction"] > 0.0
+    assert r["mean_batch"] >= 4.0, r
+    assert r["batches"] <= 48 * 300 // 4, r

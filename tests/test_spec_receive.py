@@ -1,0 +1,268 @@
+"""Speculative receive (phip_receive_soa on batches of >= 2^16 messages,
+DESIGN.md §3.3) against the oracle and against the classify-first path.
+
+The fast pass merges every clean message at once and keeps each record's
+pre-batch state (epoch + undo state); the buckets named by incasts or -0.0
+fields are set back and replayed in batch order (repo.go:54-92,
+bucket.go:240-263).  Bar: bit-exact statuses, incast replies and tables.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+from oracle import oracle as O  # noqa: E402
+from tests import _gen  # noqa: E402
+
+SEC = 10**9
+NEG0 = np.uint64(0x8000000000000000)
+
+
+@pytest.fixture(scope="module")
+def pa():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import patrol_amd
+    return patrol_amd
+
+
+def dump(repo):
+    d = {k: (v.added, v.taken, v.elapsed, v.created) for k, v in repo.dump().items()}
+    assert len(repo) == len(d)
+    return d
+
+
+def same(g, o):
+    assert len(g) == len(o)
+    bad = [k for k in o if g.get(k) != o[k]]
+    assert not bad, [(k, g.get(k), o[k]) for k in bad[:5]]
+
+
+def f64(x):
+    return np.float64(x).view(np.uint64)
+
+
+def seeded(pa, rng, K, log2_slots=17, negative=0.0, **kw):
+    """K buckets b0..b{K-1} on the GPU (spec and classify handles) and in
+    the oracle; a fraction `negative` of them holds negative added/taken
+    (where a -0.0 replica's place in the batch decides the sign of zero)."""
+    names = _gen.key_names(np.arange(K))
+    a, t, e = _gen.clean_states(rng, K)
+    neg = rng.random(K) < negative
+    a[neg] = (-np.abs(a[neg].view(np.float64)) - 1.0).view(np.uint64)
+    t[neg] = (-np.abs(t[neg].view(np.float64)) - 2.0).view(np.uint64)
+    created = _gen.T0 - rng.integers(0, SEC, K)
+    gs = pa.GPURepo(log2_slots=log2_slots, **kw)
+    gc = pa.GPURepo(log2_slots=log2_slots, **kw)
+    for g in (gs, gc):
+        g.seed(names, a, t, e, created)
+    o = O.Repo()
+    o.seed(names, a, t, e, created)
+    return gs, gc, o
+
+
+def run_all(gs, gc, o, names, a, t, e, now):
+    out = gs.receive_soa(names, a, t, e, now)
+    ref = gc.receive_soa(names, a, t, e, now, classify=True)
+    st, ra, rt, re = o.receive_soa(names, a, t, e, now)
+    for res in (out, ref):
+        assert np.array_equal(res["status"], st), np.nonzero(res["status"] != st)[0][:8]
+        rep = (st & 0x7F) == 2
+        assert np.array_equal(res["reply"]["a"][rep], ra[rep])
+        assert np.array_equal(res["reply"]["t"][rep], rt[rep])
+        assert np.array_equal(res["reply"]["e"][rep], re[rep])
+    return st
+
+
+def sprinkle(rng, ids, a, t, e, K, *, incast_hot=0, incast_cold=0, incast_new=0, negzero=0):
+    """Dirty messages at random positions: incasts (all-zero states) naming
+    the hottest ids, random existing ids and absent ids; -0.0 fields."""
+    n = ids.size
+    hot = np.bincount(ids, minlength=1).argsort()[::-1][:4]
+    for cnt, pool in ((incast_hot, hot), (incast_cold, None), (incast_new, "new")):
+        pos = rng.choice(n, cnt, replace=False) if cnt else []
+        for p in pos:
+            if pool is None:
+                ids[p] = rng.integers(0, K)
+            elif isinstance(pool, str):
+                ids[p] = K + 10**6 + rng.integers(0, 50)
+            else:
+                ids[p] = pool[rng.integers(0, len(pool))]
+            a[p], t[p], e[p] = 0, 0, 0
+    if negzero:
+        pos = rng.choice(n, negzero, replace=False)
+        for p in pos:
+            (a if rng.random() < 0.5 else t)[p] = NEG0
+
+
+@pytest.mark.parametrize("kind", ["incast_hot", "incast_cold_new", "negzero", "dirty_mix"])
+def test_spec_dirty_batches_vs_oracle_and_classify(pa, kind):
+    rng = np.random.default_rng({"incast_hot": 21, "incast_cold_new": 22, "negzero": 23,
+                                 "dirty_mix": 24}[kind])
+    K = 20000
+    gs, gc, o = seeded(pa, rng, K, negative=0.3 if kind == "negzero" else 0.0)
+    n = 1 << 18
+    ids = _gen.zipf_ids(rng, n, K + 2000)   # ~some new keys: the miss path too
+    a, t, e = _gen.clean_states(rng, n)
+    if kind == "incast_hot":
+        sprinkle(rng, ids, a, t, e, K, incast_hot=5)
+    elif kind == "incast_cold_new":
+        sprinkle(rng, ids, a, t, e, K, incast_cold=40, incast_new=20)
+    elif kind == "negzero":
+        # replicas +0 / -0 / small negatives racing on buckets whose local
+        # state is negative: Go keeps the first zero it sees
+        z = rng.random(n) < 0.02
+        a[z] = np.where(rng.random(int(z.sum())) < 0.5, np.uint64(0), NEG0)
+        z = rng.random(n) < 0.02
+        t[z] = np.where(rng.random(int(z.sum())) < 0.5, np.uint64(0), NEG0)
+        sprinkle(rng, ids, a, t, e, K, incast_hot=2, incast_cold=5)
+    else:
+        a, t, e = _gen.dirty_states(rng, n)
+    names = _gen.key_names(ids)
+    now = _gen.T0 + 5 * SEC
+    run_all(gs, gc, o, names, a, t, e, now)
+    same(dump(gs), o.dump())
+    same(dump(gc), o.dump())
+    # a clean batch after it (the next epoch) over the same keys
+    a2, t2, e2 = _gen.clean_states(rng, n)
+    run_all(gs, gc, o, names, a2, t2, e2, now + SEC)
+    same(dump(gs), o.dump())
+
+
+def test_spec_dirty_with_many_new_buckets(pa):
+    """Over 2^16 new names (the dedupe + second speculative pass) with
+    incasts and -0.0 fields on new and existing buckets."""
+    rng = np.random.default_rng(31)
+    K = 5000
+    gs, gc, o = seeded(pa, rng, K, log2_slots=16)
+    n = 1 << 19
+    ids = np.concatenate([_gen.zipf_ids(rng, n // 2, K),
+                          K + rng.permutation(n // 2)[: n // 2] % (3 * n // 8)])
+    ids = ids[rng.permutation(n)]
+    a, t, e = _gen.clean_states(rng, n)
+    sprinkle(rng, ids, a, t, e, K, incast_hot=3, incast_cold=30, negzero=40)
+    # incasts naming new buckets (created by an earlier message or by them)
+    pos = rng.choice(n, 40, replace=False)
+    a[pos], t[pos], e[pos] = 0, 0, 0
+    names = _gen.key_names(ids)
+    run_all(gs, gc, o, names, a, t, e, _gen.T0 + 3 * SEC)
+    same(dump(gs), o.dump())
+    same(dump(gc), o.dump())
+
+
+@pytest.mark.parametrize("tag_bits", [9, 14])
+def test_spec_narrow_tags(pa, tag_bits):
+    """Names sharing a tag with a dirty name are replayed with it (tags
+    truncated to force it): still exact."""
+    rng = np.random.default_rng(40 + tag_bits)
+    K = 20000
+    gs, gc, o = seeded(pa, rng, K, debug_tag_bits=tag_bits)
+    n = 1 << 17
+    ids = _gen.zipf_ids(rng, n, K + 1000)
+    a, t, e = _gen.clean_states(rng, n)
+    sprinkle(rng, ids, a, t, e, K, incast_hot=2, incast_cold=20, incast_new=5, negzero=10)
+    names = _gen.key_names(ids)
+    run_all(gs, gc, o, names, a, t, e, _gen.T0 + SEC)
+    same(dump(gs), o.dump())
+
+
+def test_spec_table_grows_mid_batch(pa):
+    """The batch's new buckets rehash the table before the dirty buckets
+    are set back: their undo states move with the records."""
+    rng = np.random.default_rng(51)
+    K = 3000
+    gs, gc, o = seeded(pa, rng, K, log2_slots=12)
+    n = 1 << 17
+    ids = np.where(rng.random(n) < 0.5, _gen.zipf_ids(rng, n, K), K + rng.integers(0, 20000, n))
+    a, t, e = _gen.clean_states(rng, n)
+    sprinkle(rng, ids, a, t, e, K, incast_hot=3, incast_cold=30, negzero=20)
+    names = _gen.key_names(ids)
+    cap0 = gs.capacity()
+    run_all(gs, gc, o, names, a, t, e, _gen.T0 + SEC)
+    assert gs.capacity() > cap0
+    same(dump(gs), o.dump())
+
+
+def test_spec_epoch_cycle(pa):
+    """More speculative batches than epoch values: bucket X is merged by
+    batch 0, left alone while the epochs cycle, then named by a dirty batch
+    that runs at batch 0's epoch value again (after the sweep).  A record
+    whose stale epoch matched would skip its undo state and restore batch
+    0's."""
+    rng = np.random.default_rng(61)
+    K = 4000
+    gs, gc, o = seeded(pa, rng, K, log2_slots=14)
+    n = 1 << 16
+    X = K - 1
+    others = _gen.zipf_ids(rng, n, K - 1)
+    now = _gen.T0
+    for j in range(66):
+        ids = others.copy()
+        a, t, e = _gen.clean_states(rng, n)
+        if j in (0, 63):   # X merged early in the batch (its record grows)
+            ids[10:20] = X
+            a[10:20] = f64(2e6 + j)
+            t[10:20] = f64(1e6 + j)
+        if j == 63:        # ... then an incast on X: its reply is the state at that point
+            ids[30] = X
+            a[30], t[30], e[30] = 0, 0, 0
+            ids[40:50] = X
+            a[40:50] = f64(3e6)
+        names = _gen.key_names(ids)
+        now += SEC
+        if j in (0, 1, 62, 63, 64, 65):
+            run_all(gs, gc, o, names, a, t, e, now)
+        else:
+            gs.receive_soa(names, a, t, e, now)
+            gc.receive_soa(names, a, t, e, now, classify=True)
+            o.receive_soa(names, a, t, e, now)
+    same(dump(gs), o.dump())
+
+
+def test_spec_back_to_back_device_batches(pa):
+    """Three device-resident batches back to back through phip_receive_soa
+    (no host copy): one with new buckets, one with incasts and -0.0 fields
+    late in the batch, one clean; statuses and replies checked per batch."""
+    import torch
+    rng = np.random.default_rng(71)
+    K = 30000
+    gs, gc, o = seeded(pa, rng, K, log2_slots=17)
+    n = 1 << 18
+    dev = torch.device("cuda", 0)
+    batches = []
+    for j in range(3):
+        ids = _gen.zipf_ids(rng, n, K + (3000 if j == 0 else 0))
+        a, t, e = _gen.clean_states(rng, n)
+        if j == 1:
+            late = np.arange(n - 5000, n)
+            pos = rng.choice(late, 30, replace=False)
+            a[pos], t[pos], e[pos] = 0, 0, 0
+            pos = rng.choice(late, 30, replace=False)
+            t[pos] = NEG0
+        batches.append((ids, a, t, e))
+    outs = []
+    for j, (ids, a, t, e) in enumerate(batches):
+        names = _gen.key_names(ids)
+        offs = np.zeros(n + 1, np.int64)
+        offs[1:] = np.cumsum([len(s) for s in names])
+        blob = np.frombuffer(b"".join(names) + b"\0" * 8, np.uint8)
+        tb = torch.from_numpy(blob.copy()).to(dev)
+        to = torch.from_numpy(offs.astype(np.int32)).to(dev)
+        ta, tt, te = (torch.from_numpy(x.view(np.int64).copy()).to(dev) for x in (a, t, e))
+        status = torch.zeros(n, dtype=torch.uint8, device=dev)
+        reply = torch.zeros((n, 4), dtype=torch.int64, device=dev)
+        gs.receive_soa(tb, ta, tt, te, _gen.T0 + j * SEC, name_offs=to, n=n, status=status,
+                       device=True, reply=reply)
+        outs.append((status, reply, tb, to, ta, tt, te))
+    torch.cuda.synchronize()
+    for j, (ids, a, t, e) in enumerate(batches):
+        names = _gen.key_names(ids)
+        st, ra, rt, re = o.receive_soa(names, a, t, e, _gen.T0 + j * SEC)
+        status, reply = outs[j][0].cpu().numpy(), outs[j][1].cpu().numpy()
+        assert np.array_equal(status, st), (j, np.nonzero(status != st)[0][:8])
+        rep = (st & 0x7F) == 2
+        assert np.array_equal(reply[rep, 0].view(np.uint64), ra[rep])
+        assert np.array_equal(reply[rep, 1].view(np.uint64), rt[rep])
+        assert np.array_equal(reply[rep, 2], re[rep])
+    same(dump(gs), o.dump())
