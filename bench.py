@@ -90,6 +90,9 @@ def parse():
                    help="c3: replica elapsed drawn below the local clock (U[0, now - created): "
                         "Takes refill, succeed and deny) or ahead of it (round 1's input: every "
                         "Take clamps last to now, dt = 0)")
+    p.add_argument("--sync-receive", action="store_true",
+                   help="A/B only: c2 calls phip_receive_soa synchronously instead of queueing "
+                        "each batch (PHIP_RECV_ASYNC) and flushing at the end of the timed steps")
     p.add_argument("--classify", action="store_true",
                    help="A/B only: c2 classifies every batch before merging (PHIP_RECV_CLASSIFY) "
                         "instead of the speculative receive")
@@ -1256,10 +1259,12 @@ def main():
             def step(j):
                 a, t, e = batches[j]
                 repo.receive_soa(blob, a, t, e, T0 + j, name_offs=offs, n=n, status=c2_status,
-                                 device=True, classify=args.classify)
+                                 device=True, classify=args.classify,
+                                 queue=not (args.sync_receive or args.classify))
 
     for j in range(args.warmup):
         step(j)
+    repo.flush()   # (a queued receive batch: finished and checked here)
     # HIP events around every kernel of the timed steps, kept by the library
     # and read once after the timed region (reading them synchronises).
     # (c5's step reads its own per-call timings from the shard layer.)
@@ -1275,6 +1280,7 @@ def main():
         tl = step(j)
         if tl is not None:
             step_tl.append(tl)
+    repo.flush()   # the last queued batch finished (its misses / dirty buckets) inside the timing
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

@@ -106,6 +106,14 @@ enum {
 #define PHIP_GROUP_SMALL_CHUNKS 0x8u /* phip_group_receive (testing): pipeline the exchange in
                                         chunks of 4096 messages instead of 2^24, so that small
                                         batches run many pack / exchange rounds */
+#define PHIP_RECV_ASYNC 0x20u /* phip_receive_soa with PHIP_DEVICE_PTRS, >= 2^16 messages: the
+                                 call queues the batch's merge and returns; the batch is
+                                 finished (misses created, incast / -0.0 buckets replayed,
+                                 outputs final) by the handle's next call or phip_flush, which
+                                 also returns its error.  The inputs and outputs must stay
+                                 untouched until then.  Each call then overlaps the next
+                                 batch's hot-bucket directory with the previous batch's
+                                 counter read-back. */
 #define PHIP_RECV_CLASSIFY 0x10u /* phip_receive_soa: classify the batch before merging (its
                                     clean prefix merged at once, the ordered path from the first
                                     incast / -0.0 on) instead of merging it speculatively; the

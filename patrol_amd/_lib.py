@@ -47,6 +47,7 @@ ROUTE_COMBINE = 0x2
 GROUP_RCCL_SELF = 0x4
 GROUP_SMALL_CHUNKS = 0x8
 RECV_CLASSIFY = 0x10
+RECV_ASYNC = 0x20
 PACKET_SIZE = 256
 BUCKET_FIXED_SIZE = 25   # PHIP_BUCKET_FIXED_SIZE: added, taken, elapsed, name length
 

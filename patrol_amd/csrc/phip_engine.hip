@@ -61,7 +61,7 @@ enum BufId {
   B_OPS, B_HOFF, B_HOP, B_HVAL, B_RPOS, B_RST, B_RUNN, B_SEGEX, B_WOFF, B_SUMS, B_WRUN,
   B_WING, B_SEGXF, B_FOLDDBG, B_SMALL, B_HUGE2, B_LONG2,
   B_STATES, B_NAME1, B_HOT, B_ROUTE, B_EXPORT, B_MSHARD, B_MSCNT, B_DEDUP, B_DSET, B_TSTATS, B_SEGT, B_RHOT,
-  B_SPECSET, B_PICK, B_PA, B_PT, B_PE, B_PST, B_PREM, B_PHAVE, B_PREP,
+  B_SPECSET, B_PICK, B_PA, B_PT, B_PE, B_PST, B_PREM, B_PHAVE, B_PREP, B_HOT2, B_HOT3,
   B_COUNT_
 };
 
@@ -124,6 +124,22 @@ struct phip_handle {
   u8* small_pin = nullptr;   // pinned staging of small ordered batches (both ways)
   size_t small_pin_cap = 0;
   u32 spec_epoch = 0;        // epoch of the last speculative receive batch (1..kEpochMax)
+  // PHIP_RECV_ASYNC: a speculative batch whose fast pass is queued and whose
+  // counters (misses, set-aside messages) are read, and whose remaining work
+  // runs, at the handle's next call (or phip_flush)
+  struct Pending {
+    bool active = false;
+    NamesOffs src{};
+    const uint64_t *a = nullptr, *t = nullptr;
+    const int64_t* e = nullptr;
+    u32 n = 0;
+    i64 now = 0;
+    OutView ow{};
+    u32 ep = 0;
+  } pend;
+  hipEvent_t ev_ctr = nullptr;   // the counters of a queued fast pass reached ctr_host
+  hipEvent_t ev_next = nullptr;  // the next batch's directory, built ahead on stream2
+  u32 hot_parity = 0;            // B_HOT2 / B_HOT3: one directory per batch in flight
 };
 
 namespace {
@@ -237,13 +253,23 @@ int check_flags(phip_handle* h) {
 
 // Every entry point binds the handle's device first: Go goroutines migrate
 // across OS threads, and the HIP current device is per thread.
-int begin_call(phip_handle* h) {
+struct HotDir;
+int finish_pending(phip_handle* h, HotDir* next = nullptr);
+int after_error(phip_handle* h, int rc);
+
+// (finish_queued: a batch PHIP_RECV_ASYNC queued is finished first, and its
+// error is this call's)
+int begin_call(phip_handle* h, bool finish_queued = true) {
   h->err.clear();
   if (h->timing && !h->timing_accumulate) {
     h->timings.clear();
     h->pool_used = 0;
   }
   HIPCHK(h, hipSetDevice(h->device));
+  if (finish_queued && h->pend.active) {
+    int rc = finish_pending(h);
+    if (rc) return after_error(h, rc);
+  }
   return PHIP_OK;
 }
 
@@ -503,7 +529,7 @@ int after_error(phip_handle* h, int rc) {
 // the header/directory to hand to k_receive_fast (nullptr: none).
 template <class Src>
 int build_hot(phip_handle* h, Src src, u32 n, hipStream_t st, const HotHdr** hdr_out,
-              const HotEntry** dir_out) {
+              const HotEntry** dir_out, BufId hot_buf = B_HOT) {
   *hdr_out = nullptr;
   *dir_out = nullptr;
   if (n < kHotMinBatch) return PHIP_OK;
@@ -511,7 +537,7 @@ int build_hot(phip_handle* h, Src src, u32 n, hipStream_t st, const HotHdr** hdr
   const size_t zero_bytes = 2 * kCnt * sizeof(u32) + kHotHist * sizeof(u32) + sizeof(HotHdr);
   u8* base;
   int rc;
-  if ((rc = ensure(h, B_HOT, zero_bytes + kHotMax * sizeof(HotEntry), &base))) return rc;
+  if ((rc = ensure(h, hot_buf, zero_bytes + kHotMax * sizeof(HotEntry), &base))) return rc;
   u32* ckeys = (u32*)base;
   u32* ccnt = ckeys + kCnt;
   u32* hist = ccnt + kCnt;
@@ -582,7 +608,8 @@ int pack_sharded(phip_handle* h, const Sharded& sh, u32 total_slot, u32* out, u3
 }
 
 template <class Src>
-int fork_hot(phip_handle* h, Src src, u32 n, const HotHdr** hot, const HotEntry** hot_dir);
+int fork_hot(phip_handle* h, Src src, u32 n, const HotHdr** hot, const HotEntry** hot_dir,
+             BufId hot_buf = B_HOT);
 
 // Enqueue order matters at this size (2 ms per 100M messages): the counter
 // reset and the classification go first, so the GPU starts reading the batch
@@ -648,7 +675,8 @@ int fast_apply(phip_handle* h, In in, HotSrc hsrc, u32 n, u8* status, u32* first
 }
 
 template <class Src>
-int fork_hot(phip_handle* h, Src src, u32 n, const HotHdr** hot, const HotEntry** hot_dir);
+int fork_hot(phip_handle* h, Src src, u32 n, const HotHdr** hot, const HotEntry** hot_dir,
+             BufId hot_buf);
 
 // One message per distinct name of list[0..n) (k_dedupe) into B_DEDUP.
 template <class Src>
@@ -691,7 +719,8 @@ struct SpecCtx {
 };
 
 template <class Src>
-int spec_apply(phip_handle* h, SoaIn<Src> in, u32 n, u8* status, u32 ep, u32* nlist, u32* ndirty);
+int spec_apply(phip_handle* h, SoaIn<Src> in, u32 n, u8* status, u32 ep, u32* nlist, u32* ndirty,
+               bool nested = false);
 template <class Src>
 int keep_misses(phip_handle* h, Src src, u32 nlist, const SpecCtx& sp, u32* nkeep);
 
@@ -720,7 +749,7 @@ int finish_many_misses(phip_handle* h, Src src, const uint64_t* a, const uint64_
   u32 fd = prefix;
   if (sp) {
     u32 nd = 0;
-    if ((rc = spec_apply(h, SoaIn<Src>{src, a, t, e}, prefix, status, sp->ep, nmiss2, &nd)))
+    if ((rc = spec_apply(h, SoaIn<Src>{src, a, t, e}, prefix, status, sp->ep, nmiss2, &nd, true)))
       return rc;
     if (sp->set && *nmiss2 && (rc = keep_misses(h, src, *nmiss2, *sp, nmiss2))) return rc;
   } else if ((rc = fast_apply(h, SoaIn<Src>{src, a, t, e}, src, prefix, status, &fd, nmiss2))) {
@@ -772,7 +801,8 @@ int finish_misses(phip_handle* h, Src src, const uint64_t* a, const uint64_t* t,
 
 // Start the hot directory of a fast batch on stream2 (joined by join_hot).
 template <class Src>
-int fork_hot(phip_handle* h, Src src, u32 n, const HotHdr** hot, const HotEntry** hot_dir) {
+int fork_hot(phip_handle* h, Src src, u32 n, const HotHdr** hot, const HotEntry** hot_dir,
+             BufId hot_buf) {
   *hot = nullptr;
   *hot_dir = nullptr;
   if (n < kHotMinBatch) return PHIP_OK;
@@ -780,7 +810,7 @@ int fork_hot(phip_handle* h, Src src, u32 n, const HotHdr** hot, const HotEntry*
   // only for the batch's producers, not for k_classify)
   HIPCHK(h, hipStreamWaitEvent(h->stream2, h->ev_fork, 0));
   int rc;
-  if ((rc = build_hot(h, src, n, h->stream2, hot, hot_dir))) return rc;
+  if ((rc = build_hot(h, src, n, h->stream2, hot, hot_dir, hot_buf))) return rc;
   HIPCHK(h, hipEventRecord(h->ev_join, h->stream2));
   return PHIP_OK;
 }
@@ -1260,12 +1290,44 @@ int spec_sweep(phip_handle* h) {
   return PHIP_OK;
 }
 
-// The speculative fast pass over messages [0, n) at epoch ep: the hot
-// directory on stream2 beside the status fill, then k_receive_fast<Spec>.
-// *nlist entries land in B_MISS: misses, and the *ndirty set-aside dirty
-// messages (kSpecDirtyBit).
+// A hot directory built ahead (PHIP_RECV_ASYNC: the next batch's, queued on
+// stream2 behind the batch before it).
+struct HotDir {
+  const HotHdr* hot = nullptr;
+  const HotEntry* dir = nullptr;
+  bool ready = false;
+};
+
+// A top-level speculative batch's directory buffer (batches in flight
+// alternate; nested passes, e.g. finish_many_misses', use B_HOT).
+inline BufId next_hot_buf(phip_handle* h) {
+  h->hot_parity ^= 1;
+  return h->hot_parity ? B_HOT3 : B_HOT2;
+}
+
+// The directory of a batch queued ahead on stream2, behind everything the
+// handle's stream holds so far (the batch's producers); joined through
+// ev_next.
 template <class Src>
-int spec_apply(phip_handle* h, SoaIn<Src> in, u32 n, u8* status, u32 ep, u32* nlist, u32* ndirty) {
+int hot_ahead(phip_handle* h, Src src, u32 n, HotDir* d) {
+  d->ready = false;
+  if (n < kHotMinBatch) return PHIP_OK;
+  HIPCHK(h, hipEventRecord(h->ev_fork, h->stream));
+  HIPCHK(h, hipStreamWaitEvent(h->stream2, h->ev_fork, 0));
+  int rc;
+  if ((rc = build_hot(h, src, n, h->stream2, &d->hot, &d->dir, next_hot_buf(h)))) return rc;
+  HIPCHK(h, hipEventRecord(h->ev_next, h->stream2));
+  d->ready = true;
+  return PHIP_OK;
+}
+
+// The speculative fast pass over messages [0, n) at epoch ep, queued: the hot
+// directory on stream2 beside the status fill (unless `pre` brings one),
+// k_receive_fast<Spec>, the shard scan of its list and the counters' copy
+// to the host (ev_ctr).  spec_collect reads them.
+template <class Src>
+int spec_launch(phip_handle* h, SoaIn<Src> in, u32 n, u8* status, u32 ep, const HotDir* pre,
+                bool nested = false) {
   u32* miss;
   int rc;
   Sharded msh;
@@ -1274,27 +1336,65 @@ int spec_apply(phip_handle* h, SoaIn<Src> in, u32 n, u8* status, u32 ep, u32* nl
     return rc;
   k_batch_reset<<<1, kShards, 0, h->stream>>>(h->ctr, msh.cnt);
   HIPCHK(h, hipGetLastError());
-  const HotHdr* hot = nullptr;
-  const HotEntry* hot_dir = nullptr;
-  if (n >= kHotMinBatch) {
-    HIPCHK(h, hipEventRecord(h->ev_fork, h->stream));
-    if ((rc = fork_hot(h, in.src, n, &hot, &hot_dir))) return rc;
+  HotDir d;
+  if (pre && pre->ready) {
+    d = *pre;
+    if (status) HIPCHK(h, hipMemsetAsync(status, PHIP_ST_MERGED, n, h->stream));
+    HIPCHK(h, hipStreamWaitEvent(h->stream, h->ev_next, 0));
+  } else {
+    if (n >= kHotMinBatch) {
+      HIPCHK(h, hipEventRecord(h->ev_fork, h->stream));
+      if ((rc = fork_hot(h, in.src, n, &d.hot, &d.dir, nested ? B_HOT : next_hot_buf(h))))
+        return rc;
+    }
+    if (status) HIPCHK(h, hipMemsetAsync(status, PHIP_ST_MERGED, n, h->stream));
+    if ((rc = join_hot(h, d.hot))) return rc;
   }
-  if (status) HIPCHK(h, hipMemsetAsync(status, PHIP_ST_MERGED, n, h->stream));
-  if ((rc = join_hot(h, hot))) return rc;
   {
     Launch l(h, "k_receive_fast");
     k_receive_fast<SoaIn<Src>, true><<<fast_grid(h, n), kFastBlock, 0, h->stream>>>(
-        in, 0, n, table(h), msh, h->ctr, hot, hot_dir, ep);
+        in, 0, n, table(h), msh, h->ctr, d.hot, d.dir, ep);
   }
   HIPCHK(h, hipGetLastError());
-  if ((rc = pack_sharded(h, msh, 2, miss, nlist))) return rc;
+  HIPCHK(h, hipMemsetAsync(h->ctr + 13, 0, sizeof(u32), h->stream));
+  k_shard_scan<<<1, kShards, 0, h->stream>>>(msh.cnt, h->ctr + 2, h->ctr + 13);
+  HIPCHK(h, hipGetLastError());
+  HIPCHK(h, hipMemcpyAsync(h->ctr_host, h->ctr, kCtrWords * sizeof(u32), hipMemcpyDeviceToHost,
+                           h->stream));
+  HIPCHK(h, hipEventRecord(h->ev_ctr, h->stream));
+  return PHIP_OK;
+}
+
+// The queued pass's counters: *nlist entries of its list packed into B_MISS
+// (misses, and the *ndirty set-aside dirty messages, kSpecDirtyBit).
+int spec_collect(phip_handle* h, u32 n, u32* nlist, u32* ndirty) {
+  HIPCHK(h, hipEventSynchronize(h->ev_ctr));
+  int rc;
   if ((rc = check_flags(h))) return rc;
+  *nlist = h->ctr_host[2];
   *ndirty = h->ctr_host[kCtrSpecDirty];
+  if (*nlist) {
+    Sharded msh;
+    if ((rc = sharded(h, B_MSHARD, (n + 63) / 64, 64, &msh, false))) return rc;
+    Launch l(h, "k_shard_compact");
+    dim3 grid(grid_for(h->ctr_host[13]), kShards);
+    k_shard_compact<<<grid, 256, 0, h->stream>>>(msh.base, msh.cap, msh.cnt,
+                                                 (u32*)h->buf[B_MISS].p);
+    HIPCHK(h, hipGetLastError());
+  }
   h->stats[0] = h->ctr_host[11];
   h->stats[1] = 0;
   h->stats[2] = *nlist - *ndirty;
   return PHIP_OK;
+}
+
+// The speculative fast pass, synchronously (spec_launch + spec_collect).
+template <class Src>
+int spec_apply(phip_handle* h, SoaIn<Src> in, u32 n, u8* status, u32 ep, u32* nlist, u32* ndirty,
+               bool nested) {
+  int rc;
+  if ((rc = spec_launch(h, in, n, status, ep, nullptr, nested))) return rc;
+  return spec_collect(h, n, nlist, ndirty);
 }
 
 // rocprim::select of `in`[0..n) by `pred` into `out`; the count into *m.
@@ -1325,16 +1425,14 @@ int keep_misses(phip_handle* h, Src src, u32 nlist, const SpecCtx& sp, u32* nkee
   return select_into(h, tmp, nlist, miss, MissKeep<Src>{src, table(h), sp.set, sp.bits}, nkeep);
 }
 
+// Everything after a speculative pass: its misses, and the buckets its
+// set-aside messages name.
 template <class Src>
-int spec_receive(phip_handle* h, Src src, const uint64_t* a, const uint64_t* t, const int64_t* e,
-                 u32 n, i64 now, const OutView& ow) {
+int spec_finish(phip_handle* h, Src src, const uint64_t* a, const uint64_t* t, const int64_t* e,
+                u32 n, i64 now, const OutView& ow, u32 ep, u32 nlist, u32 ndirty) {
   int rc;
-  if (h->spec_epoch >= kEpochMax && (rc = spec_sweep(h))) return rc;
   SpecCtx sp;
-  sp.ep = ++h->spec_epoch;
-  u32 nlist = 0, ndirty = 0;
-  if ((rc = spec_apply(h, SoaIn<Src>{src, a, t, e}, n, ow.status, sp.ep, &nlist, &ndirty)))
-    return rc;
+  sp.ep = ep;
   if (ndirty == 0) return finish_misses(h, src, a, t, e, nlist, n, now, ow.status, &sp);
 
   // 1. the dirty names' tags
@@ -1399,6 +1497,44 @@ int spec_receive(phip_handle* h, Src src, const uint64_t* a, const uint64_t* t, 
   return PHIP_OK;
 }
 
+// The next epoch (clearing every record's epoch before the values cycle).
+int spec_next_epoch(phip_handle* h, u32* ep) {
+  int rc;
+  if (h->spec_epoch >= kEpochMax && (rc = spec_sweep(h))) return rc;
+  *ep = ++h->spec_epoch;
+  return PHIP_OK;
+}
+
+template <class Src>
+int spec_receive(phip_handle* h, Src src, const uint64_t* a, const uint64_t* t, const int64_t* e,
+                 u32 n, i64 now, const OutView& ow) {
+  int rc;
+  u32 ep = 0, nlist = 0, ndirty = 0;
+  if ((rc = spec_next_epoch(h, &ep)) ||
+      (rc = spec_apply(h, SoaIn<Src>{src, a, t, e}, n, ow.status, ep, &nlist, &ndirty)))
+    return rc;
+  return spec_finish(h, src, a, t, e, n, now, ow, ep, nlist, ndirty);
+}
+
+// PHIP_RECV_ASYNC: finish the queued batch (its counters, misses and dirty
+// buckets).  `next` (optional): the directory the next batch queued ahead on
+// stream2, joined before anything here changes the table, and dropped when
+// the table was rehashed.
+int finish_pending(phip_handle* h, HotDir* next) {
+  if (!h->pend.active) return PHIP_OK;
+  const phip_handle::Pending p = h->pend;
+  h->pend.active = false;
+  u32 nlist = 0, ndirty = 0;
+  int rc;
+  if ((rc = spec_collect(h, p.n, &nlist, &ndirty))) return rc;
+  if (!nlist && !ndirty) return PHIP_OK;
+  if (next && next->ready) HIPCHK(h, hipStreamWaitEvent(h->stream, h->ev_next, 0));
+  const u64 g0 = h->grows;
+  rc = spec_finish(h, p.src, p.a, p.t, p.e, p.n, p.now, p.ow, p.ep, nlist, ndirty);
+  if (next && h->grows != g0) next->ready = false;
+  return rc;
+}
+
 // Receive-mode batch (decoded).  A batch of kSpecMinBatch messages or more is
 // merged speculatively (spec_receive) unless `classify`; otherwise the fast
 // path runs over its clean prefix and the ordered path from its first incast
@@ -1406,9 +1542,9 @@ int spec_receive(phip_handle* h, Src src, const uint64_t* a, const uint64_t* t, 
 template <class Src>
 int receive_decoded(phip_handle* h, Src src, const uint64_t* a, const uint64_t* t,
                     const int64_t* e, u32 n, i64 now, const OutView& ow, bool classify = false) {
+  int rc;
   if (!classify && n >= kSpecMinBatch && n < kSpecDirtyBit)
     return spec_receive(h, src, a, t, e, n, now, ow);
-  int rc;
   // The hot directory (read-only on the table and the batch) is built on
   // stream2 while the batch is classified.
   u32 fd = n, nmiss = 0;
@@ -1812,6 +1948,8 @@ int phip_open(const phip_config* cfg, phip_handle** out) {
   if ((e = hipEventCreateWithFlags(&h->ev_gather3, hipEventDisableTiming)) != hipSuccess)
     return fail(e);
   if ((e = hipEventCreateWithFlags(&h->ev_pack, hipEventDisableTiming)) != hipSuccess) return fail(e);
+  if ((e = hipEventCreateWithFlags(&h->ev_ctr, hipEventDisableTiming)) != hipSuccess) return fail(e);
+  if ((e = hipEventCreateWithFlags(&h->ev_next, hipEventDisableTiming)) != hipSuccess) return fail(e);
   if ((e = hipMalloc(&h->recs, h->cap * sizeof(Rec))) != hipSuccess) return fail(e);
   if ((e = hipMalloc(&h->aux, h->cap * sizeof(u32))) != hipSuccess) return fail(e);
   if ((e = hipMalloc(&h->arena, h->arena_cap + 64)) != hipSuccess) return fail(e);
@@ -1833,6 +1971,7 @@ void phip_close(phip_handle* h) {
   // earlier calls return.
   if (!h) return;
   (void)hipSetDevice(h->device);
+  if (h->pend.active) (void)after_error(h, finish_pending(h));   // a queued PHIP_RECV_ASYNC batch
   if (h->stream) (void)hipStreamSynchronize(h->stream);
   if (h->stream2) (void)hipStreamSynchronize(h->stream2);
   if (h->stream3) (void)hipStreamSynchronize(h->stream3);
@@ -1857,6 +1996,8 @@ void phip_close(phip_handle* h) {
   if (h->ev_gather) (void)hipEventDestroy(h->ev_gather);
   if (h->ev_gather3) (void)hipEventDestroy(h->ev_gather3);
   if (h->ev_pack) (void)hipEventDestroy(h->ev_pack);
+  if (h->ev_ctr) (void)hipEventDestroy(h->ev_ctr);
+  if (h->ev_next) (void)hipEventDestroy(h->ev_next);
   if (h->stream2) (void)hipStreamDestroy(h->stream2);
   if (h->stream3) (void)hipStreamDestroy(h->stream3);
   if (h->stream4) (void)hipStreamDestroy(h->stream4);
@@ -1874,13 +2015,24 @@ const char* phip_last_error(const phip_handle* h) { return h ? h->err.c_str() : 
 int phip_flush(phip_handle* h) {
   if (!h) return PHIP_ERR_INVALID;
   std::lock_guard<std::mutex> g(h->mu);
-  HIPCHK(h, hipSetDevice(h->device));
+  if (int rc0 = begin_call(h)) return rc0;   // (finishes a queued PHIP_RECV_ASYNC batch)
   HIPCHK(h, hipStreamSynchronize(h->stream));
   return PHIP_OK;
 }
 
-uint64_t phip_len(phip_handle* h) { return h ? h->n_buckets : 0; }
-uint64_t phip_capacity(phip_handle* h) { return h ? h->cap : 0; }
+// (a queued PHIP_RECV_ASYNC batch is finished first: its new buckets count)
+uint64_t phip_len(phip_handle* h) {
+  if (!h) return 0;
+  std::lock_guard<std::mutex> g(h->mu);
+  (void)begin_call(h);
+  return h->n_buckets;
+}
+uint64_t phip_capacity(phip_handle* h) {
+  if (!h) return 0;
+  std::lock_guard<std::mutex> g(h->mu);
+  (void)begin_call(h);
+  return h->cap;
+}
 
 int phip_seed(phip_handle* h, const uint8_t* names, const uint32_t* name_offs, uint32_t n,
               const phip_state* states, uint32_t flags) {
@@ -2139,11 +2291,42 @@ int phip_receive_soa(phip_handle* h, const phip_msgs* m, int64_t now, const phip
                      uint32_t flags) {
   if (!h || !m) return PHIP_ERR_INVALID;
   std::lock_guard<std::mutex> g(h->mu);
-  if (int rc0 = begin_call(h)) return rc0;
+  bool dev = flags & PHIP_DEVICE_PTRS;
   u32 n = m->n;
+  const bool async = (flags & PHIP_RECV_ASYNC) && dev && !(flags & PHIP_RECV_CLASSIFY) &&
+                     n >= kSpecMinBatch && n < kSpecDirtyBit && m->names && m->name_offs &&
+                     m->added && m->taken && m->elapsed;
+  if (async) {
+    // Queue this batch's directory behind everything queued so far, finish
+    // the batch queued before (its counters arrive while the directory is
+    // built), then queue this one's fast pass and return.
+    if (int rc0 = begin_call(h, false)) return rc0;
+    NamesOffs src{m->names, m->name_offs};
+    HotDir next;
+    int rc;
+    if ((rc = hot_ahead(h, src, n, &next)) || (rc = finish_pending(h, &next)))
+      return after_error(h, rc);
+    OutView ow{};
+    if ((rc = outputs(h, res, n, true, &ow))) return rc;
+    u32 ep = 0;
+    if ((rc = spec_next_epoch(h, &ep)) ||
+        (rc = spec_launch(h, SoaIn<NamesOffs>{src, m->added, m->taken, m->elapsed}, n, ow.status,
+                          ep, &next)))
+      return after_error(h, rc);
+    h->pend.active = true;
+    h->pend.src = src;
+    h->pend.a = m->added;
+    h->pend.t = m->taken;
+    h->pend.e = m->elapsed;
+    h->pend.n = n;
+    h->pend.now = now;
+    h->pend.ow = ow;
+    h->pend.ep = ep;
+    return PHIP_OK;
+  }
+  if (int rc0 = begin_call(h)) return rc0;
   if (n == 0) return PHIP_OK;
   if (!m->names || !m->name_offs || !m->added || !m->taken || !m->elapsed) return PHIP_ERR_INVALID;
-  bool dev = flags & PHIP_DEVICE_PTRS;
   if (!dev && !names_ok(m->name_offs, n)) return set_err(h, PHIP_ERR_NAME_TOO_LARGE, "name > 231 bytes");
   int rc;
   if (!dev) {
@@ -2636,7 +2819,7 @@ void phip_set_timing(phip_handle* h, int on) {
 int phip_set_stream(phip_handle* h, void* stream) {
   if (!h) return PHIP_ERR_INVALID;
   std::lock_guard<std::mutex> g(h->mu);
-  HIPCHK(h, hipSetDevice(h->device));
+  if (int rc0 = begin_call(h)) return rc0;
   // work already queued on the previous stream comes first
   HIPCHK(h, hipStreamSynchronize(h->stream));
   h->stream = stream ? (hipStream_t)stream : h->own_stream;

@@ -220,10 +220,13 @@ def test_spec_epoch_cycle(pa):
     same(dump(gs), o.dump())
 
 
-def test_spec_back_to_back_device_batches(pa):
+@pytest.mark.parametrize("queue", [False, True])
+def test_spec_back_to_back_device_batches(pa, queue):
     """Three device-resident batches back to back through phip_receive_soa
     (no host copy): one with new buckets, one with incasts and -0.0 fields
-    late in the batch, one clean; statuses and replies checked per batch."""
+    late in the batch, one clean; statuses and replies checked per batch.
+    queue: PHIP_RECV_ASYNC, each batch finished by the next call, the last
+    by flush()."""
     import torch
     rng = np.random.default_rng(71)
     K = 30000
@@ -253,8 +256,9 @@ def test_spec_back_to_back_device_batches(pa):
         status = torch.zeros(n, dtype=torch.uint8, device=dev)
         reply = torch.zeros((n, 4), dtype=torch.int64, device=dev)
         gs.receive_soa(tb, ta, tt, te, _gen.T0 + j * SEC, name_offs=to, n=n, status=status,
-                       device=True, reply=reply)
+                       device=True, reply=reply, queue=queue)
         outs.append((status, reply, tb, to, ta, tt, te))
+    gs.flush()
     torch.cuda.synchronize()
     for j, (ids, a, t, e) in enumerate(batches):
         names = _gen.key_names(ids)
@@ -265,4 +269,34 @@ def test_spec_back_to_back_device_batches(pa):
         assert np.array_equal(reply[rep, 0].view(np.uint64), ra[rep])
         assert np.array_equal(reply[rep, 1].view(np.uint64), rt[rep])
         assert np.array_equal(reply[rep, 2], re[rep])
+    same(dump(gs), o.dump())
+
+
+def test_spec_queued_batch_finished_by_other_calls(pa):
+    """A queued batch (PHIP_RECV_ASYNC) with incasts is finished by whatever
+    call comes next on the handle: a lookup sees its merges and replays."""
+    import torch
+    rng = np.random.default_rng(81)
+    K = 10000
+    gs, gc, o = seeded(pa, rng, K, log2_slots=16)
+    n = 1 << 17
+    ids = _gen.zipf_ids(rng, n, K + 500)
+    a, t, e = _gen.clean_states(rng, n)
+    sprinkle(rng, ids, a, t, e, K, incast_hot=2, incast_cold=10, negzero=10)
+    names = _gen.key_names(ids)
+    offs = np.zeros(n + 1, np.int64)
+    offs[1:] = np.cumsum([len(s) for s in names])
+    dev = torch.device("cuda", 0)
+    tb = torch.from_numpy(np.frombuffer(b"".join(names) + b"\0" * 8, np.uint8).copy()).to(dev)
+    to = torch.from_numpy(offs.astype(np.int32)).to(dev)
+    ta, tt, te = (torch.from_numpy(x.view(np.int64).copy()).to(dev) for x in (a, t, e))
+    status = torch.zeros(n, dtype=torch.uint8, device=dev)
+    gs.receive_soa(tb, ta, tt, te, _gen.T0, name_offs=to, n=n, status=status, device=True,
+                   queue=True)
+    st, _, _, _ = o.receive_soa(names, a, t, e, _gen.T0)
+    hot = names[int(np.bincount(ids).argmax())]
+    got = gs.get(hot)   # finishes the queued batch first
+    want = o.dump()[hot]
+    assert (got.added, got.taken, got.elapsed) == want[:3]
+    assert np.array_equal(status.cpu().numpy(), st)
     same(dump(gs), o.dump())
