@@ -140,6 +140,7 @@ struct phip_handle {
   hipEvent_t ev_ctr = nullptr;   // the counters of a queued fast pass reached ctr_host
   hipEvent_t ev_next = nullptr;  // the next batch's directory, built ahead on stream2
   u32 hot_parity = 0;            // B_HOT2 / B_HOT3: one directory per batch in flight
+  void* dir_zeroed[3] = {nullptr, nullptr, nullptr};   // B_HOT, B_HOT2, B_HOT3 count tables
 };
 
 namespace {
@@ -533,29 +534,33 @@ int build_hot(phip_handle* h, Src src, u32 n, hipStream_t st, const HotHdr** hdr
   *hdr_out = nullptr;
   *dir_out = nullptr;
   if (n < kHotMinBatch) return PHIP_OK;
-  constexpr size_t kCnt = size_t(1) << kHotCntBits;
-  const size_t zero_bytes = 2 * kCnt * sizeof(u32) + kHotHist * sizeof(u32) + sizeof(HotHdr);
+  constexpr size_t kCnt = size_t(1) << kDirCntBits;
+  const size_t tab_bytes = 2 * kCnt * sizeof(u32);
   u8* base;
   int rc;
-  if ((rc = ensure(h, hot_buf, zero_bytes + kHotMax * sizeof(HotEntry), &base))) return rc;
+  if ((rc = ensure(h, hot_buf, tab_bytes + sizeof(HotHdr) + kHotMax * sizeof(HotEntry), &base)))
+    return rc;
   u32* ckeys = (u32*)base;
   u32* ccnt = ckeys + kCnt;
-  u32* hist = ccnt + kCnt;
-  HotHdr* hdr = (HotHdr*)(hist + kHotHist);
+  HotHdr* hdr = (HotHdr*)(ccnt + kCnt);
   HotEntry* dir = (HotEntry*)(hdr + 1);
-  HIPCHK(h, hipMemsetAsync(base, 0, zero_bytes, st));
-  const u32 stride = std::max<u32>(64, (n + kHotSampleMax - 1) / kHotSampleMax);
+  // the count table is cleared by k_dir_pick after each use: zeroed here
+  // only when the buffer is new
+  void*& zeroed = h->dir_zeroed[hot_buf == B_HOT ? 0 : hot_buf == B_HOT2 ? 1 : 2];
+  if (zeroed != base) {
+    HIPCHK(h, hipMemsetAsync(base, 0, tab_bytes, st));
+    zeroed = base;
+  }
+  const u32 stride = std::max<u32>(64, (n + kDirSamples - 1) / kDirSamples);
   const u32 nsample = (n + stride - 1) / stride;
   {
-    Launch l(h, "k_hot_sample", st);
-    k_hot_sample<Src><<<grid_for(nsample, kHotSamplePerBlock), 256, 0, st>>>(
-        src, n, stride, nsample, table(h), ckeys, ccnt);
+    Launch l(h, "k_dir_count", st);
+    k_dir_count<Src><<<grid_for(nsample, 256), 256, 0, st>>>(src, n, stride, nsample, table(h),
+                                                               ckeys, ccnt);
   }
   {
-    Launch l(h, "k_hot_select", st);
-    k_hot_hist<<<grid_for(kCnt), kBlock, 0, st>>>(ccnt, hist);
-    k_hot_select<<<1, 256, 0, st>>>(hist, hdr, kHotMax);
-    k_hot_build<<<grid_for(kCnt), kBlock, 0, st>>>(ckeys, ccnt, hdr, table(h), dir);
+    Launch l(h, "k_dir_pick", st);
+    k_dir_pick<<<1, kDirPickThreads, 0, st>>>(ckeys, ccnt, table(h), hdr, dir, kHotMax);
   }
   HIPCHK(h, hipGetLastError());
   *hdr_out = hdr;

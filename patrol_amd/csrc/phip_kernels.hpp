@@ -488,9 +488,11 @@ constexpr u32 kHotLds = PHIP_HOT_LDS;     // LDS lookup slots (power of 2, >= 1.
 // kernels hold less per entry in LDS than k_receive_fast.
 constexpr u32 kRouteHotMax = 512;
 static_assert(kHotLds * 2 >= kRouteHotMax * 3 && kHotLds * 2 >= kHotMax * 3, "LDS lookup load");
-constexpr u32 kHotCntBits = 18;       // sample count table: 2^18 (slot+1, count) pairs
-constexpr u32 kHotSampleMax = 1u << 17;   // samples per batch (half the count table)
-constexpr u32 kHotSamplePerBlock = 1024;   // 128 workgroups: the chain runs beside k_classify on stream2 (512 one-sample workgroups queued behind its blocks and delayed the join)
+// The route combine's sample (k_route_sample): a 2^18-entry count table,
+// 2^17 samples, 1024 per workgroup (its chain runs beside the pack)
+constexpr u32 kHotCntBits = 18;
+constexpr u32 kHotSampleMax = 1u << 17;
+constexpr u32 kHotSamplePerBlock = 1024;
 constexpr u32 kHotHist = 4096;        // histogram bins of sample counts
 constexpr u32 kHotMinCount = 8;       // sample hits for a bucket to qualify
 // Smaller batches skip the directory.  2^16, not larger: a skewed batch of a
@@ -523,49 +525,6 @@ struct HotHdr {
 };
 
 __device__ inline u32 hot_home(u64 tag) { return (u32)(tag ^ (tag >> 29)) & (kHotLds - 1); }
-
-// Sample j = message j*stride: resolve it and count its
-// slot, aggregated per workgroup in LDS first (a hot slot is sampled by most
-// lanes; one global atomic per workgroup and slot keeps it off one address).
-template <class Src>
-__global__ __launch_bounds__(256) void k_hot_sample(Src src, u32 n, u32 stride, u32 nsample, Table T,
-                                                    u32* __restrict__ ckeys, u32* __restrict__ ccnt) {
-  constexpr u32 kPer = kHotSamplePerBlock / 256;
-  constexpr u32 kL = 2 * kHotSamplePerBlock;
-  __shared__ u32 lkey[kL], lcnt[kL];
-  for (u32 e = threadIdx.x; e < kL; e += 256) { lkey[e] = 0; lcnt[e] = 0; }
-  __syncthreads();
-  for (u32 r = 0; r < kPer; ++r) {
-    const u32 j = blockIdx.x * kHotSamplePerBlock + r * 256 + threadIdx.x;
-    const u64 i = (u64)j * stride;
-    if (j >= nsample || i >= n) continue;
-    u64 off; u32 len;
-    src.template get<true>((u32)i, off, len);
-    Name nm;
-    load_name_wide<true>(src.blob, off, len, nm);
-    u32 s;
-    Rec rec;
-    if (probe(T, nm, src.blob, &s, &rec) != kFound) continue;
-    u32 h = (s * 2654435761u) & (kL - 1);
-    for (;;) {   // at most kHotSamplePerBlock distinct keys in 2x as many entries
-      const u32 old = atomicCAS(&lkey[h], 0u, s + 1);
-      if (old == 0 || old == s + 1) { atomicAdd(&lcnt[h], 1u); break; }
-      h = (h + 1) & (kL - 1);
-    }
-  }
-  __syncthreads();
-  constexpr u32 mask = (1u << kHotCntBits) - 1;
-  for (u32 e = threadIdx.x; e < kL; e += 256) {
-    const u32 key = lkey[e];
-    if (!key) continue;
-    u32 h = ((key - 1) * 2654435761u) >> (32 - kHotCntBits);
-    for (u32 k = 0; k <= mask; ++k) {
-      const u32 old = atomicCAS(&ckeys[h], 0u, key);
-      if (old == 0 || old == key) { atomicAdd(&ccnt[h], lcnt[e]); break; }
-      h = (h + 1) & mask;
-    }
-  }
-}
 
 __global__ void k_hot_hist(const u32* __restrict__ ccnt, u32* __restrict__ hist) {
   const u32 e = blockIdx.x * blockDim.x + threadIdx.x;
@@ -602,36 +561,131 @@ __global__ __launch_bounds__(256) void k_hot_select(const u32* __restrict__ hist
   }
 }
 
-__global__ void k_hot_build(const u32* __restrict__ ckeys, const u32* __restrict__ ccnt, HotHdr* hdr,
-                            Table T, HotEntry* __restrict__ dir) {
-  const u32 e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= (1u << kHotCntBits)) return;
-  const u32 c = ccnt[e];
-  if (c < kHotMinCount || c < hdr->thresh) return;
-  const u32 idx = atomicAdd(&hdr->n, 1u);
-  if (idx >= kHotMax) return;   // cannot happen: the threshold bounds the count
-  const u32 s = ckeys[e] - 1;
-  const Rec r = load_rec(&T.recs[s]);
-  HotEntry d;
-  const bool arena = (r.name0 & 0xFFu) > kInlineName;
-  d.tag = r.tag;
-  d.w0 = arena ? (r.name0 & 0xFFu) : (r.name0 & ~0xFF00ull);
-  d.w1 = r.name1;
-  d.w2 = r.name2;
-  d.slot = s;
-  d.aoff = arena ? (u32)(r.name0 >> 32) : 0u;
-  const u32 len = (u32)(r.name0 & 0xFFu);
-  for (u32 k = 0; k < kHotTailWords; ++k) d.tail[k] = 0;
-  if (arena && len <= kHotTailName) {
-    const u64 a0 = (r.name0 >> 32) + 16;
-    const u64* p = reinterpret_cast<const u64*>(T.arena + (a0 & ~7ull));
-    const u32 sh = (u32)(a0 & 7) * 8, lastw = ((u32)(a0 & 7) + len - 17) >> 3;
-    for (u32 k = 0; 8 * k < len - 16; ++k) {
-      const u32 m = len - 16 - 8 * k;
-      d.tail[k] = low_bytes(str_word(p, sh, k, lastw), m);
+// The receive batch's directory in two launches (the route combine's chain
+// above takes four and a 2 MB memset; without a classification pass beside
+// it, a receive batch's directory sits in front of the fast kernel):
+//   k_dir_count  one sample per lane (2^16 samples), counted per workgroup
+//                in LDS, then in a 2^17-entry global table;
+//   k_dir_pick   one workgroup: a histogram of the counts, the threshold,
+//                the entries, and the table cleared again for the next
+//                batch (it starts zeroed once, when allocated).
+constexpr u32 kDirCntBits = 17;
+constexpr u32 kDirSamples = 1u << 16;
+constexpr u32 kDirPickThreads = 1024;
+
+template <class Src>
+__global__ __launch_bounds__(256) void k_dir_count(Src src, u32 n, u32 stride, u32 nsample, Table T,
+                                                   u32* __restrict__ ckeys, u32* __restrict__ ccnt) {
+  constexpr u32 kL = 512;
+  __shared__ u32 lkey[kL], lcnt[kL];
+  for (u32 e = threadIdx.x; e < kL; e += 256) { lkey[e] = 0; lcnt[e] = 0; }
+  __syncthreads();
+  const u32 j = blockIdx.x * 256 + threadIdx.x;
+  const u64 i = (u64)j * stride;
+  if (j < nsample && i < n) {
+    u64 off; u32 len;
+    src.template get<true>((u32)i, off, len);
+    Name nm;
+    load_name_wide<true>(src.blob, off, len, nm);
+    u32 s;
+    Rec rec;
+    if (probe(T, nm, src.blob, &s, &rec) == kFound) {
+      for (u32 h = (s * 2654435761u) & (kL - 1);; h = (h + 1) & (kL - 1)) {
+        const u32 old = atomicCAS(&lkey[h], 0u, s + 1);
+        if (old == 0 || old == s + 1) { atomicAdd(&lcnt[h], 1u); break; }
+      }
     }
   }
-  dir[idx] = d;
+  __syncthreads();
+  constexpr u32 mask = (1u << kDirCntBits) - 1;
+  for (u32 e = threadIdx.x; e < kL; e += 256) {
+    const u32 key = lkey[e];
+    if (!key) continue;
+    for (u32 h = ((key - 1) * 2654435761u) >> (32 - kDirCntBits), k = 0; k <= mask;
+         ++k, h = (h + 1) & mask) {
+      const u32 old = atomicCAS(&ckeys[h], 0u, key);
+      if (old == 0 || old == key) { atomicAdd(&ccnt[h], lcnt[e]); break; }
+    }
+  }
+}
+
+__global__ __launch_bounds__(kDirPickThreads) void k_dir_pick(u32* __restrict__ ckeys,
+                                                              u32* __restrict__ ccnt, Table T,
+                                                              HotHdr* hdr, HotEntry* __restrict__ dir,
+                                                              u32 maxn) {
+  constexpr u32 kBins = 4096, kPer = kBins / kDirPickThreads, kCnt = 1u << kDirCntBits;
+  __shared__ u32 hist[kBins];
+  __shared__ u32 part[kDirPickThreads];
+  __shared__ u32 best, nsel;
+  const u32 t = threadIdx.x;
+  for (u32 b = t; b < kBins; b += kDirPickThreads) hist[b] = 0;
+  if (t == 0) { best = kBins; nsel = 0; }
+  __syncthreads();
+  for (u32 e = t; e < kCnt; e += kDirPickThreads) {
+    const u32 c = ccnt[e];
+    if (c >= kHotMinCount) atomicAdd(&hist[c < kBins ? c : kBins - 1], 1u);
+  }
+  __syncthreads();
+  // the lowest count t >= kHotMinCount with at most maxn entries counted t
+  // or more: a suffix sum over the bins (kPer bins a thread, then the
+  // threads' sums scanned from the top)
+  u32 mine = 0;
+#pragma unroll
+  for (u32 k = 0; k < kPer; ++k) mine += hist[t * kPer + k];
+  part[t] = mine;
+  __syncthreads();
+  for (u32 d = 1; d < kDirPickThreads; d <<= 1) {   // part[t] = sum of part[t..]
+    const u32 x = t + d < kDirPickThreads ? part[t + d] : 0u;
+    __syncthreads();
+    part[t] += x;
+    __syncthreads();
+  }
+  u32 run = part[t] - mine;   // entries in the bins above this thread's
+  u32 lo = kBins;
+  for (int b = (int)kPer - 1; b >= 0; --b) {
+    run += hist[t * kPer + b];
+    if (run <= maxn) lo = t * kPer + b;
+  }
+  atomicMin(&best, lo);
+  __syncthreads();
+  const u32 th = best > kHotMinCount ? best : kHotMinCount;
+  for (u32 e = t; e < kCnt; e += kDirPickThreads) {
+    const u32 key = ckeys[e];
+    if (!key) continue;
+    const u32 c = ccnt[e];
+    ckeys[e] = 0;   // the table starts the next batch cleared
+    ccnt[e] = 0;
+    if (c < th) continue;
+    const u32 idx = atomicAdd(&nsel, 1u);
+    if (idx >= maxn) continue;   // cannot happen: the threshold bounds the count
+    const u32 s = key - 1;
+    const Rec r = load_rec(&T.recs[s]);
+    HotEntry d;
+    const bool arena = (r.name0 & 0xFFu) > kInlineName;
+    d.tag = r.tag;
+    d.w0 = arena ? (r.name0 & 0xFFu) : (r.name0 & ~0xFF00ull);
+    d.w1 = r.name1;
+    d.w2 = r.name2;
+    d.slot = s;
+    d.aoff = arena ? (u32)(r.name0 >> 32) : 0u;
+    const u32 len = (u32)(r.name0 & 0xFFu);
+    for (u32 k = 0; k < kHotTailWords; ++k) d.tail[k] = 0;
+    if (arena && len <= kHotTailName) {
+      const u64 a0 = (r.name0 >> 32) + 16;
+      const u64* p = reinterpret_cast<const u64*>(T.arena + (a0 & ~7ull));
+      const u32 sh = (u32)(a0 & 7) * 8, lastw = ((u32)(a0 & 7) + len - 17) >> 3;
+      for (u32 k = 0; 8 * k < len - 16; ++k) {
+        const u32 m = len - 16 - 8 * k;
+        d.tail[k] = low_bytes(str_word(p, sh, k, lastw), m);
+      }
+    }
+    dir[idx] = d;
+  }
+  __syncthreads();
+  if (t == 0) {
+    hdr->n = min(nsel, maxn);
+    hdr->thresh = th;
+  }
 }
 
 // ----------------------------------------------------- fast receive --------
