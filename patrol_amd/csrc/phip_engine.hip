@@ -1388,7 +1388,7 @@ int spec_collect(phip_handle* h, u32 n, u32* nlist, u32* ndirty) {
     HIPCHK(h, hipGetLastError());
   }
   h->stats[0] = h->ctr_host[11];
-  h->stats[1] = 0;
+  h->stats[1] = h->ctr_host[10];
   h->stats[2] = *nlist - *ndirty;
   return PHIP_OK;
 }

@@ -927,7 +927,7 @@ __global__ __launch_bounds__(kFastBlock) __attribute__((amdgpu_waves_per_eu(8, 8
   __shared__ u32 hrec[kHotMax], haoff[kHotMax];
   __shared__ u64 htail[kHotTailWords][kHotMax];
   __shared__ u64 hmax[3][kHotMax];      // per-workgroup maxima (elapsed biased by 2^63)
-  __shared__ u32 hhits;
+  __shared__ u32 hhits, hdirty;
 
   // Gate (k_classify ran before, over every message up to n): only the clean
   // prefix is applied, the messages before the first dirty one
@@ -940,7 +940,7 @@ __global__ __launch_bounds__(kFastBlock) __attribute__((amdgpu_waves_per_eu(8, 8
   for (u32 j = threadIdx.x; j < kHotMax; j += kFastBlock) {
     hmax[0][j] = 0; hmax[1][j] = 0; hmax[2][j] = 0;
   }
-  if (threadIdx.x == 0) hhits = 0;
+  if (threadIdx.x == 0) { hhits = 0; hdirty = 0; }
   __syncthreads();
   for (u32 j = threadIdx.x; j < nh; j += kFastBlock) {
     const HotEntry d = hot_dir[j];
@@ -1005,7 +1005,7 @@ __global__ __launch_bounds__(kFastBlock) __attribute__((amdgpu_waves_per_eu(8, 8
     if (dirt) {   // set aside (speculative batch): the host orders its bucket
       missed = true;
       entry = i | kSpecDirtyBit;
-      ++hits;   // (counted apart below: hits holds set-aside messages in Spec)
+      hits += 1u << 16;   // (Spec: set-aside messages in the high half, < 2^16 a lane)
     } else if (valid) {
       int hidx = -1;
       if (nh) {
@@ -1024,7 +1024,7 @@ __global__ __launch_bounds__(kFastBlock) __attribute__((amdgpu_waves_per_eu(8, 8
         }
       }
       if (hidx >= 0) {
-        if constexpr (!Spec) ++hits;
+        ++hits;
         if (ea > hmax[0][hidx]) atomicMax(&hmax[0][hidx], ea);
         if (et > hmax[1][hidx]) atomicMax(&hmax[1][hidx], et);
         if (ee > hmax[2][hidx]) atomicMax(&hmax[2][hidx], ee);
@@ -1058,10 +1058,12 @@ __global__ __launch_bounds__(kFastBlock) __attribute__((amdgpu_waves_per_eu(8, 8
     }
     miss.append(chunk, missed, entry);
   }
-  if (hits) atomicAdd(&hhits, hits);
+  if (hits & 0xFFFFu) atomicAdd(&hhits, hits & 0xFFFFu);
+  if (Spec && (hits >> 16)) atomicAdd(&hdirty, hits >> 16);
   __syncthreads();
   if (threadIdx.x == 0) {
-    if (hhits) atomicAdd(&ctr[Spec ? kCtrSpecDirty : 10], hhits);
+    if (hhits) atomicAdd(&ctr[10], hhits);
+    if (Spec && hdirty) atomicAdd(&ctr[kCtrSpecDirty], hdirty);
     if (blockIdx.x == 0) ctr[11] = nh;
   }
 
