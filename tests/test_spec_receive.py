@@ -178,9 +178,9 @@ def test_spec_table_grows_mid_batch(pa):
     a, t, e = _gen.clean_states(rng, n)
     sprinkle(rng, ids, a, t, e, K, incast_hot=3, incast_cold=30, negzero=20)
     names = _gen.key_names(ids)
-    cap0 = gs.capacity()
+    cap0 = gs.capacity
     run_all(gs, gc, o, names, a, t, e, _gen.T0 + SEC)
-    assert gs.capacity() > cap0
+    assert gs.capacity > cap0
     same(dump(gs), o.dump())
 
 
