@@ -93,9 +93,6 @@ def parse():
     p.add_argument("--sync-receive", action="store_true",
                    help="A/B only: c2 calls phip_receive_soa synchronously instead of queueing "
                         "each batch (PHIP_RECV_ASYNC) and flushing at the end of the timed steps")
-    p.add_argument("--classify", action="store_true",
-                   help="A/B only: c2 classifies every batch before merging (PHIP_RECV_CLASSIFY) "
-                        "instead of the speculative receive")
     p.add_argument("--no-status", action="store_true",
                    help="A/B only: the C2 step does not write the per-message status column")
     p.add_argument("--name-len", type=int, default=0,
@@ -1259,9 +1256,9 @@ def main():
             def step(j):
                 a, t, e = batches[j]
                 repo.receive_soa(blob, a, t, e, T0 + j, name_offs=offs, n=n, status=c2_status,
-                                 device=True, classify=args.classify,
-                                 queue=not (args.sync_receive or args.classify))
+                                 device=True, queue=not args.sync_receive)
 
+    extra = {}
     for j in range(args.warmup):
         step(j)
     repo.flush()   # (a queued receive batch: finished and checked here)
@@ -1292,6 +1289,10 @@ def main():
             launches[name] = launches.get(name, 0) + 1
     kern = {k: [v / (args.steps if step_tl else 1)] for k, v in kern.items()}
     repo.set_timing(False)
+    if args.workload == "c2":
+        st4 = repo.last_stats()   # the last batch: directory entries, folded through it, misses
+        extra["hot_directory"] = {"entries": int(st4[0]), "folded": int(st4[1]),
+                                  "misses": int(st4[2])}
     if world > 1:
         tt = torch.tensor([el], dtype=torch.float64,
                           device=dev if args.dist_backend == "nccl" else "cpu")
@@ -1300,7 +1301,6 @@ def main():
 
     total = world * n * args.steps
     kms = {k: float(np.mean(v)) for k, v in kern.items()}
-    extra = {}
     if args.workload == "c5":
         # bytes of the two local passes per round (reads R*24, writes 24;
         # then reads 24 + R*24 per bucket) over their kernel time; k_ae_apply

@@ -107,17 +107,13 @@ enum {
                                         chunks of 4096 messages instead of 2^24, so that small
                                         batches run many pack / exchange rounds */
 #define PHIP_RECV_ASYNC 0x20u /* phip_receive_soa with PHIP_DEVICE_PTRS, >= 2^16 messages: the
-                                 call queues the batch's merge and returns; the batch is
-                                 finished (misses created, incast / -0.0 buckets replayed,
-                                 outputs final) by the handle's next call or phip_flush, which
-                                 also returns its error.  The inputs and outputs must stay
-                                 untouched until then.  Each call then overlaps the next
-                                 batch's hot-bucket directory with the previous batch's
-                                 counter read-back. */
-#define PHIP_RECV_CLASSIFY 0x10u /* phip_receive_soa: classify the batch before merging (its
-                                    clean prefix merged at once, the ordered path from the first
-                                    incast / -0.0 on) instead of merging it speculatively; the
-                                    results are the same, this is for A/B measurements */
+                                 call queues the batch and returns; the batch is finished
+                                 (misses created, a dirty suffix through the ordered path,
+                                 outputs final) by the handle's next call or phip_flush,
+                                 which also returns its error.  Inputs and outputs must stay
+                                 untouched until then.  A receive call queues its batch's
+                                 classification and hot directory behind the batch before
+                                 it, so the host's read-back of that batch overlaps them. */
 
 /* phip_config.flags */
 #define PHIP_CFG_NO_GROW 0x1u   /* refuse (PHIP_ERR_FULL / PHIP_ERR_ARENA) instead of growing */
@@ -247,8 +243,7 @@ int phip_get(phip_handle* h, const uint8_t* name, uint32_t len, phip_state* out)
  * restarted node through incast, repo.go:96-106).  phip_snapshot writes
  * phip_snapshot_bytes(h) bytes into a host buffer: a 64-byte header (magic
  * "PHIPSNP1", ABI version, log2_slots, bucket count, arena bytes), the 2^L
- * slot records as they lie in HBM (128 B each: state and name in the first 64,
- * speculation scratch after them), then the used long-name arena.
+ * slot records as they lie in HBM (64 B each), then the used long-name arena.
  * phip_restore loads such an image into a handle opened with the same
  * log2_slots (and an arena at least as large): the table is reproduced
  * exactly, with no rehash.  phip_dump + phip_seed is the portable route
@@ -282,12 +277,7 @@ int phip_dump(phip_handle* h, uint8_t* names, uint64_t names_cap, uint64_t* name
 int phip_receive_datagrams(phip_handle* h, const uint8_t* bytes, const uint64_t* offs, uint32_t n,
                            int64_t now, const phip_results* res, uint32_t* stop_index,
                            uint32_t flags);
-/* The same loop over pre-decoded states.  A batch of 2^16 messages or more
- * is merged speculatively: every clean message at once, with each record's
- * pre-batch state kept; the buckets that incasts or -0.0 fields name (the
- * only ones whose results depend on order) are then set back and replayed
- * in batch order.  PHIP_RECV_CLASSIFY classifies first instead (same
- * results). */
+/* The same loop over pre-decoded states. */
 int phip_receive_soa(phip_handle* h, const phip_msgs* m, int64_t now, const phip_results* res,
                      uint32_t flags);
 /* LocalRepo.UpsertBucket for each state, in order. */

@@ -46,7 +46,6 @@ CFG_FIXED_SEED = 0x4
 ROUTE_COMBINE = 0x2
 GROUP_RCCL_SELF = 0x4
 GROUP_SMALL_CHUNKS = 0x8
-RECV_CLASSIFY = 0x10
 RECV_ASYNC = 0x20
 PACKET_SIZE = 256
 BUCKET_FIXED_SIZE = 25   # PHIP_BUCKET_FIXED_SIZE: added, taken, elapsed, name length
@@ -198,9 +197,12 @@ def load(path: str = LIB_PATH):
     L.phip_group_receive.argtypes = [vp, C.POINTER(phip_msgs), i64, C.POINTER(u64),
                                      C.POINTER(u64), u32]
     L.phip_group_anti_entropy.argtypes = [vp, C.POINTER(vp), u32, u64, u32]
-    L.phip_group_set_timing.argtypes = [vp, C.c_int]
-    L.phip_group_stage_ms.argtypes = [vp, u32, C.POINTER(C.c_float)]
-    L.phip_group_rccl_info.argtypes = [vp, u32, C.POINTER(C.c_int32), C.POINTER(C.c_int32),
-                                       C.c_char_p, u32]
+    # (round 5's entry points: a variant library built from older sources for
+    # an A/B run, PATROLHIP_LIB, lacks them)
+    if hasattr(L, "phip_group_set_timing"):
+        L.phip_group_set_timing.argtypes = [vp, C.c_int]
+        L.phip_group_stage_ms.argtypes = [vp, u32, C.POINTER(C.c_float)]
+        L.phip_group_rccl_info.argtypes = [vp, u32, C.POINTER(C.c_int32), C.POINTER(C.c_int32),
+                                           C.c_char_p, u32]
     _lib = L
     return L

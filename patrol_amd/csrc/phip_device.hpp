@@ -167,26 +167,18 @@ __host__ __device__ inline bool state_is_zero(u64 a_bits, u64 t_bits, i64 e) {
 }
 
 // ------------------------------------------------------------ table -----
-// One slot record per 128-byte L2 line.  Its first 64 bytes hold everything
-// a lookup and a merge touch, ordered so that the Receive fast path reads
-// only the first 48 bytes (three 16-byte loads) for names of up to 14 bytes:
+// One 64-byte slot record = one HBM burst holding everything a lookup and a
+// merge touch, ordered so that the Receive fast path reads only the first
+// 48 bytes (three 16-byte loads) for names of up to 14 bytes:
 //   [ 0,16) tag, added     tag = FNV-1a 64 of the name (0 = empty; a 0 hash is stored as 1)
 //   [16,32) taken, elapsed added/taken are E-encoded float64
 //   [32,48) name0, name1   canonical name words 0-1
 //   [48,64) created, name2 canonical name word 2
-//   [64,88) undo state     the state before the current speculative batch
-//                          first touched the record (valid while the epoch
-//                          bits of name0 equal the batch's epoch)
-// The second half costs no HBM traffic on the merge path: a probe's 48-byte
-// read fetches the whole 128-byte line either way (records are hash-placed,
-// so the neighbour a 64-byte record would share its line with is a random
-// other bucket), and the undo write lands in a line the merge dirties anyway.
 // Canonical name (24 bytes, words name0..name2): byte 0 = len, byte 1 = flags
-// (kRec* in bits 0-1, the record's speculation epoch in bits 2-7), then len
-// <= 22: bytes 2..2+len = the name, zero padded (names of up to 14 bytes end
-// in name1, so name2 = 0); len > 22: bytes 4..7 = arena offset, bytes 8..23 =
-// the first 16 bytes (fast reject), full name in the arena.
-struct alignas(128) Rec {
+// (kRec*), then len <= 22: bytes 2..2+len = the name, zero padded (names of
+// up to 14 bytes end in name1, so name2 = 0); len > 22: bytes 4..7 = arena
+// offset, bytes 8..23 = the first 16 bytes (fast reject), full name in the arena.
+struct alignas(64) Rec {
   u64 tag;
   u64 added;
   u64 taken;
@@ -195,12 +187,8 @@ struct alignas(128) Rec {
   u64 name1;
   i64 created;
   u64 name2;
-  u64 undo_added;
-  u64 undo_taken;
-  i64 undo_elapsed;
-  u64 pad[5];
 };
-static_assert(sizeof(Rec) == 128, "slot record must be one 128-byte L2 line");
+static_assert(sizeof(Rec) == 64, "slot record must be one 64-byte burst");
 
 constexpr u32 kInlineName = 22;
 constexpr u32 kShortName = 14;     // fits name0/name1: the 48-byte fast path
@@ -209,19 +197,6 @@ constexpr u64 kRecNew = 2u;         // created by the current batch
 
 __host__ __device__ inline u32 rec_flags(const Rec& r) { return (u32)((r.name0 >> 8) & 0xFFu); }
 __host__ __device__ inline u64 with_flags(u64 w0, u64 f) { return (w0 & ~0xFF00ull) | (f << 8); }
-
-// Speculation epoch (flags bits 2-7 of name0): 1..kEpochMax, 0 = none.  A
-// speculative Receive batch runs at epoch e; the first merge of the batch
-// into a record moves its epoch to e by a CAS on name0 and the winner saves
-// the state it read as the record's undo state.  The handle cycles e through
-// 1..kEpochMax and clears every record's epoch (k_spec_sweep) before reusing
-// a value.
-constexpr u32 kEpochShift = 10;
-constexpr u32 kEpochMax = 63;
-__host__ __device__ inline u32 rec_epoch(u64 w0) { return (u32)(w0 >> kEpochShift) & 63u; }
-__host__ __device__ inline u64 with_epoch(u64 w0, u32 e) {
-  return (w0 & ~(63ull << kEpochShift)) | ((u64)e << kEpochShift);
-}
 
 constexpr u64 kFnvOffset = 0xcbf29ce484222325ull;
 constexpr u64 kFnvPrime = 0x100000001b3ull;

@@ -61,7 +61,6 @@ enum BufId {
   B_OPS, B_HOFF, B_HOP, B_HVAL, B_RPOS, B_RST, B_RUNN, B_SEGEX, B_WOFF, B_SUMS, B_WRUN,
   B_WING, B_SEGXF, B_FOLDDBG, B_SMALL, B_HUGE2, B_LONG2,
   B_STATES, B_NAME1, B_HOT, B_ROUTE, B_EXPORT, B_MSHARD, B_MSCNT, B_DEDUP, B_DSET, B_TSTATS, B_SEGT, B_RHOT,
-  B_SPECSET, B_PICK, B_PA, B_PT, B_PE, B_PST, B_PREM, B_PHAVE, B_PREP, B_HOT2, B_HOT3,
   B_COUNT_
 };
 
@@ -123,10 +122,9 @@ struct phip_handle {
   size_t pool_used = 0;
   u8* small_pin = nullptr;   // pinned staging of small ordered batches (both ways)
   size_t small_pin_cap = 0;
-  u32 spec_epoch = 0;        // epoch of the last speculative receive batch (1..kEpochMax)
-  // PHIP_RECV_ASYNC: a speculative batch whose fast pass is queued and whose
-  // counters (misses, set-aside messages) are read, and whose remaining work
-  // runs, at the handle's next call (or phip_flush)
+  // PHIP_RECV_ASYNC: a decoded batch whose fast pass is queued; its counters
+  // are read, and its misses / dirty suffix finished, at the handle's next
+  // call (or phip_flush)
   struct Pending {
     bool active = false;
     NamesOffs src{};
@@ -135,12 +133,8 @@ struct phip_handle {
     u32 n = 0;
     i64 now = 0;
     OutView ow{};
-    u32 ep = 0;
   } pend;
-  hipEvent_t ev_ctr = nullptr;   // the counters of a queued fast pass reached ctr_host
-  hipEvent_t ev_next = nullptr;  // the next batch's directory, built ahead on stream2
-  u32 hot_parity = 0;            // B_HOT2 / B_HOT3: one directory per batch in flight
-  void* dir_zeroed[3] = {nullptr, nullptr, nullptr};   // B_HOT, B_HOT2, B_HOT3 count tables
+  hipEvent_t ev_ctr = nullptr;   // a queued batch's counters reached ctr_host
 };
 
 namespace {
@@ -254,8 +248,7 @@ int check_flags(phip_handle* h) {
 
 // Every entry point binds the handle's device first: Go goroutines migrate
 // across OS threads, and the HIP current device is per thread.
-struct HotDir;
-int finish_pending(phip_handle* h, HotDir* next = nullptr);
+int finish_pending(phip_handle* h, bool* worked = nullptr);
 int after_error(phip_handle* h, int rc);
 
 // (finish_queued: a batch PHIP_RECV_ASYNC queued is finished first, and its
@@ -530,37 +523,33 @@ int after_error(phip_handle* h, int rc) {
 // the header/directory to hand to k_receive_fast (nullptr: none).
 template <class Src>
 int build_hot(phip_handle* h, Src src, u32 n, hipStream_t st, const HotHdr** hdr_out,
-              const HotEntry** dir_out, BufId hot_buf = B_HOT) {
+              const HotEntry** dir_out) {
   *hdr_out = nullptr;
   *dir_out = nullptr;
   if (n < kHotMinBatch) return PHIP_OK;
-  constexpr size_t kCnt = size_t(1) << kDirCntBits;
-  const size_t tab_bytes = 2 * kCnt * sizeof(u32);
+  constexpr size_t kCnt = size_t(1) << kHotCntBits;
+  const size_t zero_bytes = 2 * kCnt * sizeof(u32) + kHotHist * sizeof(u32) + sizeof(HotHdr);
   u8* base;
   int rc;
-  if ((rc = ensure(h, hot_buf, tab_bytes + sizeof(HotHdr) + kHotMax * sizeof(HotEntry), &base)))
-    return rc;
+  if ((rc = ensure(h, B_HOT, zero_bytes + kHotMax * sizeof(HotEntry), &base))) return rc;
   u32* ckeys = (u32*)base;
   u32* ccnt = ckeys + kCnt;
-  HotHdr* hdr = (HotHdr*)(ccnt + kCnt);
+  u32* hist = ccnt + kCnt;
+  HotHdr* hdr = (HotHdr*)(hist + kHotHist);
   HotEntry* dir = (HotEntry*)(hdr + 1);
-  // the count table is cleared by k_dir_pick after each use: zeroed here
-  // only when the buffer is new
-  void*& zeroed = h->dir_zeroed[hot_buf == B_HOT ? 0 : hot_buf == B_HOT2 ? 1 : 2];
-  if (zeroed != base) {
-    HIPCHK(h, hipMemsetAsync(base, 0, tab_bytes, st));
-    zeroed = base;
-  }
-  const u32 stride = std::max<u32>(64, (n + kDirSamples - 1) / kDirSamples);
+  HIPCHK(h, hipMemsetAsync(base, 0, zero_bytes, st));
+  const u32 stride = std::max<u32>(64, (n + kHotSampleMax - 1) / kHotSampleMax);
   const u32 nsample = (n + stride - 1) / stride;
   {
-    Launch l(h, "k_dir_count", st);
-    k_dir_count<Src><<<grid_for(nsample, 256), 256, 0, st>>>(src, n, stride, nsample, table(h),
-                                                               ckeys, ccnt);
+    Launch l(h, "k_hot_sample", st);
+    k_hot_sample<Src><<<grid_for(nsample, kHotSamplePerBlock), 256, 0, st>>>(
+        src, n, stride, nsample, table(h), ckeys, ccnt);
   }
   {
-    Launch l(h, "k_dir_pick", st);
-    k_dir_pick<<<1, kDirPickThreads, 0, st>>>(ckeys, ccnt, table(h), hdr, dir, kHotMax);
+    Launch l(h, "k_hot_select", st);
+    k_hot_hist<<<grid_for(kCnt), kBlock, 0, st>>>(ccnt, hist);
+    k_hot_select<<<1, 256, 0, st>>>(hist, hdr, kHotMax);
+    k_hot_build<<<grid_for(kCnt), kBlock, 0, st>>>(ckeys, ccnt, hdr, table(h), dir);
   }
   HIPCHK(h, hipGetLastError());
   *hdr_out = hdr;
@@ -613,30 +602,39 @@ int pack_sharded(phip_handle* h, const Sharded& sh, u32 total_slot, u32* out, u3
 }
 
 template <class Src>
-int fork_hot(phip_handle* h, Src src, u32 n, const HotHdr** hot, const HotEntry** hot_dir,
-             BufId hot_buf = B_HOT);
+int fork_hot(phip_handle* h, Src src, u32 n, const HotHdr** hot, const HotEntry** hot_dir);
+
+// A fast batch in three parts, so that a queued batch (PHIP_RECV_ASYNC) can
+// put the next batch's front in front of its own read-back:
+//   front    counter reset, hot directory (stream2), status fill, k_classify;
+//   back     k_receive_fast (after the directory), its miss shards' scan,
+//            the counters to the host (read_ctr, or queued: ev_ctr);
+//   collect  the miss list packed from the host's counters, flags, stats.
+struct FastFront {
+  const HotHdr* hot = nullptr;
+  const HotEntry* dir = nullptr;
+};
 
 // Enqueue order matters at this size (2 ms per 100M messages): the counter
 // reset and the classification go first, so the GPU starts reading the batch
 // while the host still enqueues the hot-directory chain on stream2 (about
 // 0.1 ms of API calls that used to sit in front of k_classify).
+// (shards: zero the miss list's shard counters here too, in the same
+// launch; a queued batch's next front leaves them to fast_back, as the
+// batch before it still has to pack its list from them)
 template <class In, class HotSrc>
-int fast_apply(phip_handle* h, In in, HotSrc hsrc, u32 n, u8* status, u32* first_dirty,
-               u32* nmiss) {
-  u32* miss;
+int fast_front(phip_handle* h, In in, HotSrc hsrc, u32 n, u8* status, FastFront* ff,
+               bool shards = true) {
   int rc;
+  *ff = FastFront{};
   Sharded msh;
-  if ((rc = ensure(h, B_MISS, n, &miss)) ||
-      (rc = sharded(h, B_MSHARD, (n + 63) / 64, 64, &msh, false)))
-    return rc;
-  k_batch_reset<<<1, kShards, 0, h->stream>>>(h->ctr, msh.cnt);
+  if (shards && (rc = sharded(h, B_MSHARD, (n + 63) / 64, 64, &msh, false))) return rc;
+  k_batch_reset<<<1, kShards, 0, h->stream>>>(h->ctr, shards ? msh.cnt : nullptr);
   HIPCHK(h, hipGetLastError());
   const bool with_hot = n >= kHotMinBatch;
   // A small batch classifies in a few µs, less than the directory chain
   // takes: that chain goes first then.
   const bool hot_first = n < (1u << 23);
-  const HotHdr* hot = nullptr;
-  const HotEntry* hot_dir = nullptr;
   // Statuses: the fast kernel merges most of the batch and writes none; the
   // column is filled with PHIP_ST_MERGED up front on the main stream, and
   // every message the kernel leaves is written again after it
@@ -645,7 +643,7 @@ int fast_apply(phip_handle* h, In in, HotSrc hsrc, u32 n, u8* status, u32* first
   // fill on stream2 beside the classification slowed the classification
   // more than it cost here.
   if (with_hot) HIPCHK(h, hipEventRecord(h->ev_fork, h->stream));
-  if (with_hot && hot_first && (rc = fork_hot(h, hsrc, n, &hot, &hot_dir))) return rc;
+  if (with_hot && hot_first && (rc = fork_hot(h, hsrc, n, &ff->hot, &ff->dir))) return rc;
   if (status) HIPCHK(h, hipMemsetAsync(status, PHIP_ST_MERGED, n, h->stream));
   {
     Launch l(h, "k_classify");
@@ -660,18 +658,50 @@ int fast_apply(phip_handle* h, In in, HotSrc hsrc, u32 n, u8* status, u32* first
     if (!done) k_classify<In><<<grid_for(n), kBlock, 0, h->stream>>>(in, n, h->ctr);
   }
   HIPCHK(h, hipGetLastError());
-  if (with_hot && !hot_first && (rc = fork_hot(h, hsrc, n, &hot, &hot_dir))) return rc;
-  // The fast kernel is enqueued behind the classification without a host
-  // round trip; it reads the counters itself.
-  if ((rc = join_hot(h, hot))) return rc;
+  if (with_hot && !hot_first && (rc = fork_hot(h, hsrc, n, &ff->hot, &ff->dir))) return rc;
+  return PHIP_OK;
+}
+
+// The fast kernel is enqueued behind the classification without a host
+// round trip; it reads the counters itself.
+template <class In>
+int fast_back(phip_handle* h, In in, u32 n, const FastFront& ff, bool queued) {
+  u32* miss;
+  int rc;
+  Sharded msh;
+  if ((rc = ensure(h, B_MISS, n, &miss)) ||
+      (rc = sharded(h, B_MSHARD, (n + 63) / 64, 64, &msh, queued)))
+    return rc;
+  if ((rc = join_hot(h, ff.hot))) return rc;
   {
     Launch l(h, "k_receive_fast");
     k_receive_fast<In><<<fast_grid(h, n), kFastBlock, 0, h->stream>>>(in, 0, n, table(h), msh,
-                                                                      h->ctr, hot, hot_dir);
+                                                                      h->ctr, ff.hot, ff.dir);
   }
   HIPCHK(h, hipGetLastError());
-  if ((rc = pack_sharded(h, msh, 2, miss, nmiss))) return rc;
+  HIPCHK(h, hipMemsetAsync(h->ctr + 13, 0, sizeof(u32), h->stream));
+  k_shard_scan<<<1, kShards, 0, h->stream>>>(msh.cnt, h->ctr + 2, h->ctr + 13);
+  HIPCHK(h, hipGetLastError());
+  if (!queued) return read_ctr(h);
+  HIPCHK(h, hipMemcpyAsync(h->ctr_host, h->ctr, kCtrWords * sizeof(u32), hipMemcpyDeviceToHost,
+                           h->stream));
+  HIPCHK(h, hipEventRecord(h->ev_ctr, h->stream));
+  return PHIP_OK;
+}
+
+int fast_collect(phip_handle* h, u32 n, u32* first_dirty, u32* nmiss) {
+  int rc;
   if ((rc = check_flags(h))) return rc;
+  *nmiss = h->ctr_host[2];
+  if (*nmiss) {
+    Sharded msh;
+    if ((rc = sharded(h, B_MSHARD, (n + 63) / 64, 64, &msh, false))) return rc;
+    Launch l(h, "k_shard_compact");
+    dim3 grid(grid_for(h->ctr_host[13]), kShards);
+    k_shard_compact<<<grid, 256, 0, h->stream>>>(msh.base, msh.cap, msh.cnt,
+                                                 (u32*)h->buf[B_MISS].p);
+    HIPCHK(h, hipGetLastError());
+  }
   *first_dirty = std::min<u32>(h->ctr_host[kCtrDirty], n);
   h->stats[0] = h->ctr_host[11];
   h->stats[1] = h->ctr_host[10];
@@ -679,9 +709,24 @@ int fast_apply(phip_handle* h, In in, HotSrc hsrc, u32 n, u8* status, u32* first
   return PHIP_OK;
 }
 
+// The whole fast path of a batch (SoaIn or WireIn; hsrc: its names for the
+// hot-directory sample), synchronously: resets the batch's counters,
+// classifies, builds the hot directory on stream2 and applies the batch's
+// clean prefix: the messages before the first dirty one (*first_dirty; n if
+// none) and before the first malformed datagram (ctr[5]).  The prefix's
+// misses (*nmiss of them) are listed in B_MISS.
+template <class In, class HotSrc>
+int fast_apply(phip_handle* h, In in, HotSrc hsrc, u32 n, u8* status, u32* first_dirty,
+               u32* nmiss) {
+  int rc;
+  FastFront ff;
+  if ((rc = fast_front(h, in, hsrc, n, status, &ff)) || (rc = fast_back(h, in, n, ff, false)))
+    return rc;
+  return fast_collect(h, n, first_dirty, nmiss);
+}
+
 template <class Src>
-int fork_hot(phip_handle* h, Src src, u32 n, const HotHdr** hot, const HotEntry** hot_dir,
-             BufId hot_buf);
+int fork_hot(phip_handle* h, Src src, u32 n, const HotHdr** hot, const HotEntry** hot_dir);
 
 // One message per distinct name of list[0..n) (k_dedupe) into B_DEDUP.
 template <class Src>
@@ -714,25 +759,9 @@ int dedupe_names(phip_handle* h, Src src, const u32* list, u32 n, u32** out, u32
 // device-scope atomic to one record (134 ms per 100M-message batch through
 // k_receive_list).  Returns the misses of the second pass
 // (names dropped by k_dedupe for a shared tag) in *nmiss2, listed in B_MISS.
-// Speculation context of a batch (spec_receive): its epoch and, once the
-// batch had dirty messages, the tag set of their names (those buckets are
-// replayed by the ordered path, so their misses are not inserted here).
-struct SpecCtx {
-  u32 ep = 0;
-  const u64* set = nullptr;
-  u32 bits = 0;
-};
-
-template <class Src>
-int spec_apply(phip_handle* h, SoaIn<Src> in, u32 n, u8* status, u32 ep, u32* nlist, u32* ndirty,
-               bool nested = false);
-template <class Src>
-int keep_misses(phip_handle* h, Src src, u32 nlist, const SpecCtx& sp, u32* nkeep);
-
 template <class Src>
 int finish_many_misses(phip_handle* h, Src src, const uint64_t* a, const uint64_t* t,
-                       const int64_t* e, u32 nmiss, u32 prefix, i64 now, u8* status, u32* nmiss2,
-                       const SpecCtx* sp) {
+                       const int64_t* e, u32 nmiss, u32 prefix, i64 now, u8* status, u32* nmiss2) {
   u32* miss = (u32*)h->buf[B_MISS].p;
   int rc;
   // 1. distinct names
@@ -748,18 +777,9 @@ int finish_many_misses(phip_handle* h, Src src, const uint64_t* a, const uint64_
     k_first_seen<Src><<<grid_for(nmiss), kBlock, 0, h->stream>>>(src, nmiss, miss, table(h));
     HIPCHK(h, hipGetLastError());
   }
-  // 4. the fast pass again (a speculative batch: speculatively again, at the
-  //    same epoch, so the records it first touched keep their pre-batch
-  //    state; its set-aside and dirty-bucket entries are dropped again)
+  // 4. the fast pass again
   u32 fd = prefix;
-  if (sp) {
-    u32 nd = 0;
-    if ((rc = spec_apply(h, SoaIn<Src>{src, a, t, e}, prefix, status, sp->ep, nmiss2, &nd, true)))
-      return rc;
-    if (sp->set && *nmiss2 && (rc = keep_misses(h, src, *nmiss2, *sp, nmiss2))) return rc;
-  } else if ((rc = fast_apply(h, SoaIn<Src>{src, a, t, e}, src, prefix, status, &fd, nmiss2))) {
-    return rc;
-  }
+  if ((rc = fast_apply(h, SoaIn<Src>{src, a, t, e}, src, prefix, status, &fd, nmiss2))) return rc;
   // 5. PHIP_ST_CREATED after the second pass wrote its statuses
   if (status && n_claimed) {
     Launch l(h, "k_mark_created");
@@ -774,11 +794,11 @@ int finish_many_misses(phip_handle* h, Src src, const uint64_t* a, const uint64_
 // creator tracking (PHIP_ST_CREATED on the first message of a new bucket).
 template <class Src>
 int finish_misses(phip_handle* h, Src src, const uint64_t* a, const uint64_t* t, const int64_t* e,
-                  u32 nmiss, u32 prefix, i64 now, u8* status, const SpecCtx* sp = nullptr) {
+                  u32 nmiss, u32 prefix, i64 now, u8* status) {
   if (nmiss == 0) return PHIP_OK;
   int rc;
   if (nmiss >= kManyMisses &&
-      (rc = finish_many_misses(h, src, a, t, e, nmiss, prefix, now, status, &nmiss, sp)))
+      (rc = finish_many_misses(h, src, a, t, e, nmiss, prefix, now, status, &nmiss)))
     return rc;
   if (nmiss == 0) return PHIP_OK;
   u32* miss = (u32*)h->buf[B_MISS].p;
@@ -806,8 +826,7 @@ int finish_misses(phip_handle* h, Src src, const uint64_t* a, const uint64_t* t,
 
 // Start the hot directory of a fast batch on stream2 (joined by join_hot).
 template <class Src>
-int fork_hot(phip_handle* h, Src src, u32 n, const HotHdr** hot, const HotEntry** hot_dir,
-             BufId hot_buf) {
+int fork_hot(phip_handle* h, Src src, u32 n, const HotHdr** hot, const HotEntry** hot_dir) {
   *hot = nullptr;
   *hot_dir = nullptr;
   if (n < kHotMinBatch) return PHIP_OK;
@@ -815,7 +834,7 @@ int fork_hot(phip_handle* h, Src src, u32 n, const HotHdr** hot, const HotEntry*
   // only for the batch's producers, not for k_classify)
   HIPCHK(h, hipStreamWaitEvent(h->stream2, h->ev_fork, 0));
   int rc;
-  if ((rc = build_hot(h, src, n, h->stream2, hot, hot_dir, hot_buf))) return rc;
+  if ((rc = build_hot(h, src, n, h->stream2, hot, hot_dir))) return rc;
   HIPCHK(h, hipEventRecord(h->ev_join, h->stream2));
   return PHIP_OK;
 }
@@ -1276,285 +1295,34 @@ int finish_receive(phip_handle* h, Src src, const uint64_t* a, const uint64_t* t
   return ordered(h, shifted(src, k), stop - k, ov, shifted(ow, k));
 }
 
-// ------------------------------------------------- speculative receive ----
-// A decoded Receive batch without the classification pass:
-// k_receive_fast<Spec> merges every clean message at once, sets the dirty
-// ones (incast / -0.0) aside and keeps the pre-batch state of every record it
-// merges into (epoch + undo state, phip_device.hpp).  A batch with no dirty
-// message is then final; otherwise only the buckets its dirty messages name
-// depend on order, and those are set back and replayed in batch order.
-
-// Clear every record's epoch (k_spec_sweep) before the epoch values cycle.
-int spec_sweep(phip_handle* h) {
-  {
-    Launch l(h, "k_spec_sweep");
-    k_spec_sweep<<<grid_for(h->cap), kBlock, 0, h->stream>>>(table(h), h->cap);
-  }
-  HIPCHK(h, hipGetLastError());
-  h->spec_epoch = 0;
-  return PHIP_OK;
-}
-
-// A hot directory built ahead (PHIP_RECV_ASYNC: the next batch's, queued on
-// stream2 behind the batch before it).
-struct HotDir {
-  const HotHdr* hot = nullptr;
-  const HotEntry* dir = nullptr;
-  bool ready = false;
-};
-
-// A top-level speculative batch's directory buffer (batches in flight
-// alternate; nested passes, e.g. finish_many_misses', use B_HOT).
-inline BufId next_hot_buf(phip_handle* h) {
-  h->hot_parity ^= 1;
-  return h->hot_parity ? B_HOT3 : B_HOT2;
-}
-
-// The directory of a batch queued ahead on stream2, behind everything the
-// handle's stream holds so far (the batch's producers); joined through
-// ev_next.
-template <class Src>
-int hot_ahead(phip_handle* h, Src src, u32 n, HotDir* d) {
-  d->ready = false;
-  if (n < kHotMinBatch) return PHIP_OK;
-  HIPCHK(h, hipEventRecord(h->ev_fork, h->stream));
-  HIPCHK(h, hipStreamWaitEvent(h->stream2, h->ev_fork, 0));
-  int rc;
-  if ((rc = build_hot(h, src, n, h->stream2, &d->hot, &d->dir, next_hot_buf(h)))) return rc;
-  HIPCHK(h, hipEventRecord(h->ev_next, h->stream2));
-  d->ready = true;
-  return PHIP_OK;
-}
-
-// The speculative fast pass over messages [0, n) at epoch ep, queued: the hot
-// directory on stream2 beside the status fill (unless `pre` brings one),
-// k_receive_fast<Spec>, the shard scan of its list and the counters' copy
-// to the host (ev_ctr).  spec_collect reads them.
-template <class Src>
-int spec_launch(phip_handle* h, SoaIn<Src> in, u32 n, u8* status, u32 ep, const HotDir* pre,
-                bool nested = false) {
-  u32* miss;
-  int rc;
-  Sharded msh;
-  if ((rc = ensure(h, B_MISS, n, &miss)) ||
-      (rc = sharded(h, B_MSHARD, (n + 63) / 64, 64, &msh, false)))
-    return rc;
-  k_batch_reset<<<1, kShards, 0, h->stream>>>(h->ctr, msh.cnt);
-  HIPCHK(h, hipGetLastError());
-  HotDir d;
-  if (pre && pre->ready) {
-    d = *pre;
-    if (status) HIPCHK(h, hipMemsetAsync(status, PHIP_ST_MERGED, n, h->stream));
-    HIPCHK(h, hipStreamWaitEvent(h->stream, h->ev_next, 0));
-  } else {
-    if (n >= kHotMinBatch) {
-      HIPCHK(h, hipEventRecord(h->ev_fork, h->stream));
-      if ((rc = fork_hot(h, in.src, n, &d.hot, &d.dir, nested ? B_HOT : next_hot_buf(h))))
-        return rc;
-    }
-    if (status) HIPCHK(h, hipMemsetAsync(status, PHIP_ST_MERGED, n, h->stream));
-    if ((rc = join_hot(h, d.hot))) return rc;
-  }
-  {
-    Launch l(h, "k_receive_fast");
-    k_receive_fast<SoaIn<Src>, true><<<fast_grid(h, n), kFastBlock, 0, h->stream>>>(
-        in, 0, n, table(h), msh, h->ctr, d.hot, d.dir, ep);
-  }
-  HIPCHK(h, hipGetLastError());
-  HIPCHK(h, hipMemsetAsync(h->ctr + 13, 0, sizeof(u32), h->stream));
-  k_shard_scan<<<1, kShards, 0, h->stream>>>(msh.cnt, h->ctr + 2, h->ctr + 13);
-  HIPCHK(h, hipGetLastError());
-  HIPCHK(h, hipMemcpyAsync(h->ctr_host, h->ctr, kCtrWords * sizeof(u32), hipMemcpyDeviceToHost,
-                           h->stream));
-  HIPCHK(h, hipEventRecord(h->ev_ctr, h->stream));
-  return PHIP_OK;
-}
-
-// The queued pass's counters: *nlist entries of its list packed into B_MISS
-// (misses, and the *ndirty set-aside dirty messages, kSpecDirtyBit).
-int spec_collect(phip_handle* h, u32 n, u32* nlist, u32* ndirty) {
-  HIPCHK(h, hipEventSynchronize(h->ev_ctr));
-  int rc;
-  if ((rc = check_flags(h))) return rc;
-  *nlist = h->ctr_host[2];
-  *ndirty = h->ctr_host[kCtrSpecDirty];
-  if (*nlist) {
-    Sharded msh;
-    if ((rc = sharded(h, B_MSHARD, (n + 63) / 64, 64, &msh, false))) return rc;
-    Launch l(h, "k_shard_compact");
-    dim3 grid(grid_for(h->ctr_host[13]), kShards);
-    k_shard_compact<<<grid, 256, 0, h->stream>>>(msh.base, msh.cap, msh.cnt,
-                                                 (u32*)h->buf[B_MISS].p);
-    HIPCHK(h, hipGetLastError());
-  }
-  h->stats[0] = h->ctr_host[11];
-  h->stats[1] = h->ctr_host[10];
-  h->stats[2] = *nlist - *ndirty;
-  return PHIP_OK;
-}
-
-// The speculative fast pass, synchronously (spec_launch + spec_collect).
-template <class Src>
-int spec_apply(phip_handle* h, SoaIn<Src> in, u32 n, u8* status, u32 ep, u32* nlist, u32* ndirty,
-               bool nested) {
-  int rc;
-  if ((rc = spec_launch(h, in, n, status, ep, nullptr, nested))) return rc;
-  return spec_collect(h, n, nlist, ndirty);
-}
-
-// rocprim::select of `in`[0..n) by `pred` into `out`; the count into *m.
-template <class It, class Pred>
-int select_into(phip_handle* h, It in, u32 n, u32* out, Pred pred, u32* m) {
-  size_t tb = 0;
-  HIPCHK(h, rocprim::select(nullptr, tb, in, out, h->ctr + 19, (size_t)n, pred, h->stream));
-  u8* temp;
-  int rc;
-  if ((rc = ensure(h, B_TEMP, tb, &temp))) return rc;
-  {
-    Launch l(h, "select");
-    HIPCHK(h, rocprim::select(temp, tb, in, out, h->ctr + 19, (size_t)n, pred, h->stream));
-  }
-  if ((rc = read_ctr(h))) return rc;
-  *m = h->ctr_host[19];
-  return PHIP_OK;
-}
-
-// The misses of B_MISS[0..nlist) to insert and merge here (not set aside,
-// not naming a dirty bucket), back into B_MISS.
-template <class Src>
-int keep_misses(phip_handle* h, Src src, u32 nlist, const SpecCtx& sp, u32* nkeep) {
-  u32 *miss = (u32*)h->buf[B_MISS].p, *tmp;
-  int rc;
-  if ((rc = ensure(h, B_PICK, nlist, &tmp))) return rc;
-  HIPCHK(h, hipMemcpyAsync(tmp, miss, (size_t)nlist * 4, hipMemcpyDeviceToDevice, h->stream));
-  return select_into(h, tmp, nlist, miss, MissKeep<Src>{src, table(h), sp.set, sp.bits}, nkeep);
-}
-
-// Everything after a speculative pass: its misses, and the buckets its
-// set-aside messages name.
-template <class Src>
-int spec_finish(phip_handle* h, Src src, const uint64_t* a, const uint64_t* t, const int64_t* e,
-                u32 n, i64 now, const OutView& ow, u32 ep, u32 nlist, u32 ndirty) {
-  int rc;
-  SpecCtx sp;
-  sp.ep = ep;
-  if (ndirty == 0) return finish_misses(h, src, a, t, e, nlist, n, now, ow.status, &sp);
-
-  // 1. the dirty names' tags
-  u32 bits = 10;
-  while ((1ull << bits) < 4ull * ndirty) ++bits;
-  u64* set;
-  if ((rc = ensure(h, B_SPECSET, size_t(1) << bits, &set))) return rc;
-  HIPCHK(h, hipMemsetAsync(set, 0, (size_t(1) << bits) * 8, h->stream));
-  {
-    Launch l(h, "k_tagset_add");
-    k_tagset_add<Src><<<grid_for(nlist), kBlock, 0, h->stream>>>(src, (const u32*)h->buf[B_MISS].p,
-                                                                  nlist, table(h), set, bits);
-  }
-  HIPCHK(h, hipGetLastError());
-  sp.set = set;
-  sp.bits = bits;
-  // 2. every other bucket: its misses created and merged (commuting merges)
-  u32 nkeep = 0;
-  if ((rc = keep_misses(h, src, nlist, sp, &nkeep)) ||
-      (rc = finish_misses(h, src, a, t, e, nkeep, n, now, ow.status, &sp)))
-    return rc;
-  // 3. the dirty buckets' messages, in batch order (after the inserts above:
-  //    a grown table has moved records, the undo state with them)
-  u32* pick;
-  u32 m = 0;
-  if ((rc = ensure(h, B_PICK, n, &pick)) ||
-      (rc = select_into(h, rocprim::counting_iterator<u32>(0), n, pick,
-                        TagIn<Src>{src, table(h), set, bits}, &m)))
-    return rc;
-  if (m == 0) return set_err(h, PHIP_ERR_INVALID, "internal: no message names a dirty bucket");
-  // 4. their buckets back to the pre-batch state
-  {
-    Launch l(h, "k_spec_restore");
-    k_spec_restore<Src><<<grid_for(m), kBlock, 0, h->stream>>>(src, pick, m, table(h), sp.ep);
-  }
-  HIPCHK(h, hipGetLastError());
-  // 5. replayed by the ordered path (the Go loop on those buckets' messages)
-  uint64_t *pa, *pt;
-  int64_t* pe;
-  if ((rc = ensure(h, B_PA, m, &pa)) || (rc = ensure(h, B_PT, m, &pt)) ||
-      (rc = ensure(h, B_PE, m, &pe)))
-    return rc;
-  k_gather_states<<<grid_for(m), kBlock, 0, h->stream>>>(pick, m, a, t, e, pa, pt, pe);
-  HIPCHK(h, hipGetLastError());
-  OutView po{};
-  if (ow.status && (rc = ensure(h, B_PST, m, &po.status))) return rc;
-  if (ow.remaining && (rc = ensure(h, B_PREM, m, &po.remaining))) return rc;
-  if (ow.have && (rc = ensure(h, B_PHAVE, m, &po.have))) return rc;
-  if (ow.reply) {
-    if ((rc = ensure(h, B_PREP, m, &po.reply))) return rc;
-    HIPCHK(h, hipMemsetAsync(po.reply, 0, (size_t)m * sizeof(phip_state), h->stream));
-  }
-  OpView ov{};
-  ov.kind = nullptr; ov.kind0 = PHIP_OP_RECEIVE;
-  ov.now = nullptr; ov.now0 = now;
-  ov.a = pa; ov.t = pt; ov.e = pe;
-  if ((rc = ordered(h, Picked<Src>{src.blob, src, pick}, m, ov, po))) return rc;
-  k_scatter_outs<<<grid_for(m), kBlock, 0, h->stream>>>(pick, m, po.status, po.remaining, po.have,
-                                                        po.reply, ow.status, ow.remaining, ow.have,
-                                                        ow.reply);
-  HIPCHK(h, hipGetLastError());
-  return PHIP_OK;
-}
-
-// The next epoch (clearing every record's epoch before the values cycle).
-int spec_next_epoch(phip_handle* h, u32* ep) {
-  int rc;
-  if (h->spec_epoch >= kEpochMax && (rc = spec_sweep(h))) return rc;
-  *ep = ++h->spec_epoch;
-  return PHIP_OK;
-}
-
-template <class Src>
-int spec_receive(phip_handle* h, Src src, const uint64_t* a, const uint64_t* t, const int64_t* e,
-                 u32 n, i64 now, const OutView& ow) {
-  int rc;
-  u32 ep = 0, nlist = 0, ndirty = 0;
-  if ((rc = spec_next_epoch(h, &ep)) ||
-      (rc = spec_apply(h, SoaIn<Src>{src, a, t, e}, n, ow.status, ep, &nlist, &ndirty)))
-    return rc;
-  return spec_finish(h, src, a, t, e, n, now, ow, ep, nlist, ndirty);
-}
-
-// PHIP_RECV_ASYNC: finish the queued batch (its counters, misses and dirty
-// buckets).  `next` (optional): the directory the next batch queued ahead on
-// stream2, joined before anything here changes the table, and dropped when
-// the table was rehashed.
-int finish_pending(phip_handle* h, HotDir* next) {
-  if (!h->pend.active) return PHIP_OK;
-  const phip_handle::Pending p = h->pend;
-  h->pend.active = false;
-  u32 nlist = 0, ndirty = 0;
-  int rc;
-  if ((rc = spec_collect(h, p.n, &nlist, &ndirty))) return rc;
-  if (!nlist && !ndirty) return PHIP_OK;
-  if (next && next->ready) HIPCHK(h, hipStreamWaitEvent(h->stream, h->ev_next, 0));
-  const u64 g0 = h->grows;
-  rc = spec_finish(h, p.src, p.a, p.t, p.e, p.n, p.now, p.ow, p.ep, nlist, ndirty);
-  if (next && h->grows != g0) next->ready = false;
-  return rc;
-}
-
-// Receive-mode batch (decoded).  A batch of kSpecMinBatch messages or more is
-// merged speculatively (spec_receive) unless `classify`; otherwise the fast
-// path runs over its clean prefix and the ordered path from its first incast
-// or -0.0 on.
+// Receive-mode batch (decoded): the fast path over its clean prefix, the
+// ordered path from its first incast or -0.0 on.
 template <class Src>
 int receive_decoded(phip_handle* h, Src src, const uint64_t* a, const uint64_t* t,
-                    const int64_t* e, u32 n, i64 now, const OutView& ow, bool classify = false) {
+                    const int64_t* e, u32 n, i64 now, const OutView& ow) {
   int rc;
-  if (!classify && n >= kSpecMinBatch && n < kSpecDirtyBit)
-    return spec_receive(h, src, a, t, e, n, now, ow);
   // The hot directory (read-only on the table and the batch) is built on
   // stream2 while the batch is classified.
   u32 fd = n, nmiss = 0;
   if ((rc = fast_apply(h, SoaIn<Src>{src, a, t, e}, src, n, ow.status, &fd, &nmiss))) return rc;
   return finish_receive(h, src, a, t, e, n, fd, nmiss, now, ow);
+}
+
+// PHIP_RECV_ASYNC: the queued batch's counters, then what its fast pass left
+// (misses, the dirty suffix).  *worked: whether anything was left (its work
+// has used the counters and maybe moved the table).
+int finish_pending(phip_handle* h, bool* worked) {
+  if (worked) *worked = false;
+  if (!h->pend.active) return PHIP_OK;
+  const phip_handle::Pending p = h->pend;
+  h->pend.active = false;
+  HIPCHK(h, hipEventSynchronize(h->ev_ctr));
+  u32 fd = p.n, nmiss = 0;
+  int rc;
+  if ((rc = fast_collect(h, p.n, &fd, &nmiss))) return rc;
+  if (nmiss == 0 && fd >= p.n) return PHIP_OK;
+  if (worked) *worked = true;
+  return finish_receive(h, p.src, p.a, p.t, p.e, p.n, fd, nmiss, p.now, p.ow);
 }
 
 // Whether an op's phip_results.reply entry is written (step_sop): Takes,
@@ -1954,7 +1722,6 @@ int phip_open(const phip_config* cfg, phip_handle** out) {
     return fail(e);
   if ((e = hipEventCreateWithFlags(&h->ev_pack, hipEventDisableTiming)) != hipSuccess) return fail(e);
   if ((e = hipEventCreateWithFlags(&h->ev_ctr, hipEventDisableTiming)) != hipSuccess) return fail(e);
-  if ((e = hipEventCreateWithFlags(&h->ev_next, hipEventDisableTiming)) != hipSuccess) return fail(e);
   if ((e = hipMalloc(&h->recs, h->cap * sizeof(Rec))) != hipSuccess) return fail(e);
   if ((e = hipMalloc(&h->aux, h->cap * sizeof(u32))) != hipSuccess) return fail(e);
   if ((e = hipMalloc(&h->arena, h->arena_cap + 64)) != hipSuccess) return fail(e);
@@ -2002,7 +1769,6 @@ void phip_close(phip_handle* h) {
   if (h->ev_gather3) (void)hipEventDestroy(h->ev_gather3);
   if (h->ev_pack) (void)hipEventDestroy(h->ev_pack);
   if (h->ev_ctr) (void)hipEventDestroy(h->ev_ctr);
-  if (h->ev_next) (void)hipEventDestroy(h->ev_next);
   if (h->stream2) (void)hipStreamDestroy(h->stream2);
   if (h->stream3) (void)hipStreamDestroy(h->stream3);
   if (h->stream4) (void)hipStreamDestroy(h->stream4);
@@ -2192,8 +1958,6 @@ int phip_restore(phip_handle* h, const uint8_t* in, uint64_t len) {
     HIPCHK(h, hipMemcpyAsync(h->arena, p + h->cap * sizeof(Rec), hd.arena_used, hipMemcpyHostToDevice, h->stream));
   HIPCHK(h, hipMemsetAsync(h->aux, 0, h->cap * sizeof(u32), h->stream));
   HIPCHK(h, hipMemcpyAsync(h->arena_cursor, &hd.arena_used, sizeof(u64), hipMemcpyHostToDevice, h->stream));
-  // the image's speculation epochs belong to the handle that wrote it
-  if (int rc = spec_sweep(h)) return rc;
   HIPCHK(h, hipStreamSynchronize(h->stream));
   h->n_buckets = hd.n_buckets;
   h->seed = hd.reserved[0];   // the image's placement
@@ -2298,26 +2062,26 @@ int phip_receive_soa(phip_handle* h, const phip_msgs* m, int64_t now, const phip
   std::lock_guard<std::mutex> g(h->mu);
   bool dev = flags & PHIP_DEVICE_PTRS;
   u32 n = m->n;
-  const bool async = (flags & PHIP_RECV_ASYNC) && dev && !(flags & PHIP_RECV_CLASSIFY) &&
-                     n >= kSpecMinBatch && n < kSpecDirtyBit && m->names && m->name_offs &&
-                     m->added && m->taken && m->elapsed;
-  if (async) {
-    // Queue this batch's directory behind everything queued so far, finish
-    // the batch queued before (its counters arrive while the directory is
-    // built), then queue this one's fast pass and return.
+  if ((flags & PHIP_RECV_ASYNC) && dev && n >= kHotMinBatch && m->names && m->name_offs &&
+      m->added && m->taken && m->elapsed) {
+    // Queue this batch's front (reset, directory, status fill,
+    // classification) behind the batch queued before, read that batch's
+    // counters meanwhile and finish it, then queue this batch's fast pass
+    // and return.  A previous batch that left work (misses, a dirty suffix)
+    // used the counters and the directory buffers: the front is queued again.
     if (int rc0 = begin_call(h, false)) return rc0;
     NamesOffs src{m->names, m->name_offs};
-    HotDir next;
-    int rc;
-    if ((rc = hot_ahead(h, src, n, &next)) || (rc = finish_pending(h, &next)))
-      return after_error(h, rc);
+    SoaIn<NamesOffs> in{src, m->added, m->taken, m->elapsed};
     OutView ow{};
+    FastFront ff;
+    int rc;
+    bool worked = false;
     if ((rc = outputs(h, res, n, true, &ow))) return rc;
-    u32 ep = 0;
-    if ((rc = spec_next_epoch(h, &ep)) ||
-        (rc = spec_launch(h, SoaIn<NamesOffs>{src, m->added, m->taken, m->elapsed}, n, ow.status,
-                          ep, &next)))
-      return after_error(h, rc);
+    const bool prev = h->pend.active;
+    if ((rc = fast_front(h, in, src, n, ow.status, &ff, !prev))) return after_error(h, rc);
+    if (prev && (rc = finish_pending(h, &worked))) return after_error(h, rc);
+    if (worked && (rc = fast_front(h, in, src, n, ow.status, &ff))) return after_error(h, rc);
+    if ((rc = fast_back(h, in, n, ff, true))) return after_error(h, rc);
     h->pend.active = true;
     h->pend.src = src;
     h->pend.a = m->added;
@@ -2326,7 +2090,6 @@ int phip_receive_soa(phip_handle* h, const phip_msgs* m, int64_t now, const phip
     h->pend.n = n;
     h->pend.now = now;
     h->pend.ow = ow;
-    h->pend.ep = ep;
     return PHIP_OK;
   }
   if (int rc0 = begin_call(h)) return rc0;
@@ -2347,8 +2110,7 @@ int phip_receive_soa(phip_handle* h, const phip_msgs* m, int64_t now, const phip
       (rc = stage(h, B_A, m->added, n, dev, &a)) || (rc = stage(h, B_T, m->taken, n, dev, &t)) ||
       (rc = stage(h, B_E, m->elapsed, n, dev, &e)) || (rc = outputs(h, res, n, dev, &ow)))
     return rc;
-  if ((rc = receive_decoded(h, src, a, t, e, n, now, ow, flags & PHIP_RECV_CLASSIFY)))
-    return after_error(h, rc);
+  if ((rc = receive_decoded(h, src, a, t, e, n, now, ow))) return after_error(h, rc);
   return copy_outputs(h, res, n, dev, ow);
 }
 

@@ -1,10 +1,9 @@
 // HIP kernels of libpatrolhip (gfx950).  Host orchestration: phip_engine.hip.
 //
-// Table: recs[2^L] 128-byte slot records (tag, state and name in the first
-// 64 bytes, the speculative batch's undo state after them) + aux[2^L] u32
-// scratch used only by inserting/seeding batches.  Home slot = top L bits of
-// a seeded mix of the tag, linear probing; a lookup reads the first 48 or 64
-// bytes of one record per probe step.
+// Table: recs[2^L] 64-byte slot records (tag, state and name in one HBM
+// burst) + aux[2^L] u32 scratch used only by inserting/seeding batches.
+// Home slot = top L bits of tag * 2^64/phi (Fibonacci hashing), linear
+// probing; a lookup touches one 64-byte record per probe step.
 #pragma once
 #include <type_traits>
 
@@ -204,11 +203,9 @@ struct Sharded {
 // A batch's counters in one launch: ctr[16] zero except ctr[5] (first
 // malformed datagram) and ctr[kCtrDirty] (first dirty message), which start
 // at "none"; and, when given, a sharded list's kShards counters.
-constexpr u32 kCtrSpecDirty = 18;   // dirty messages a speculative fast pass set aside
 __global__ __launch_bounds__(kShards) void k_batch_reset(u32* ctr, u32* shard_cnt) {
   const u32 t = threadIdx.x;
   if (t < 16) ctr[t] = (t == 5 || t == 12) ? ~0u : 0u;
-  if (t == kCtrSpecDirty) ctr[t] = 0;
   if (shard_cnt) shard_cnt[t] = 0;
 }
 
@@ -294,18 +291,6 @@ __device__ inline Rec load_rec(const Rec* p) {
   r.created = (i64)(((u64)d.y << 32) | d.x);
   r.name2 = ((u64)d.w << 32) | d.z;
   return r;
-}
-
-// The first 64 bytes of a record (everything but the undo state) as four
-// 16-byte stores.
-__device__ inline void store_rec64(Rec* p, const Rec& r) {
-  uint4* q = reinterpret_cast<uint4*>(p);
-  q[0] = make_uint4((u32)r.tag, (u32)(r.tag >> 32), (u32)r.added, (u32)(r.added >> 32));
-  q[1] = make_uint4((u32)r.taken, (u32)(r.taken >> 32), (u32)(u64)r.elapsed,
-                    (u32)((u64)r.elapsed >> 32));
-  q[2] = make_uint4((u32)r.name0, (u32)(r.name0 >> 32), (u32)r.name1, (u32)(r.name1 >> 32));
-  q[3] = make_uint4((u32)(u64)r.created, (u32)((u64)r.created >> 32), (u32)r.name2,
-                    (u32)(r.name2 >> 32));
 }
 
 // The first 48 bytes only (tag, state, name words 0-1); name2 and created
@@ -488,11 +473,9 @@ constexpr u32 kHotLds = PHIP_HOT_LDS;     // LDS lookup slots (power of 2, >= 1.
 // kernels hold less per entry in LDS than k_receive_fast.
 constexpr u32 kRouteHotMax = 512;
 static_assert(kHotLds * 2 >= kRouteHotMax * 3 && kHotLds * 2 >= kHotMax * 3, "LDS lookup load");
-// The route combine's sample (k_route_sample): a 2^18-entry count table,
-// 2^17 samples, 1024 per workgroup (its chain runs beside the pack)
-constexpr u32 kHotCntBits = 18;
-constexpr u32 kHotSampleMax = 1u << 17;
-constexpr u32 kHotSamplePerBlock = 1024;
+constexpr u32 kHotCntBits = 18;       // sample count table: 2^18 (slot+1, count) pairs
+constexpr u32 kHotSampleMax = 1u << 17;   // samples per batch (half the count table)
+constexpr u32 kHotSamplePerBlock = 1024;   // 128 workgroups: the chain runs beside k_classify on stream2 (512 one-sample workgroups queued behind its blocks and delayed the join)
 constexpr u32 kHotHist = 4096;        // histogram bins of sample counts
 constexpr u32 kHotMinCount = 8;       // sample hits for a bucket to qualify
 // Smaller batches skip the directory.  2^16, not larger: a skewed batch of a
@@ -525,6 +508,49 @@ struct HotHdr {
 };
 
 __device__ inline u32 hot_home(u64 tag) { return (u32)(tag ^ (tag >> 29)) & (kHotLds - 1); }
+
+// Sample j = message j*stride: resolve it and count its
+// slot, aggregated per workgroup in LDS first (a hot slot is sampled by most
+// lanes; one global atomic per workgroup and slot keeps it off one address).
+template <class Src>
+__global__ __launch_bounds__(256) void k_hot_sample(Src src, u32 n, u32 stride, u32 nsample, Table T,
+                                                    u32* __restrict__ ckeys, u32* __restrict__ ccnt) {
+  constexpr u32 kPer = kHotSamplePerBlock / 256;
+  constexpr u32 kL = 2 * kHotSamplePerBlock;
+  __shared__ u32 lkey[kL], lcnt[kL];
+  for (u32 e = threadIdx.x; e < kL; e += 256) { lkey[e] = 0; lcnt[e] = 0; }
+  __syncthreads();
+  for (u32 r = 0; r < kPer; ++r) {
+    const u32 j = blockIdx.x * kHotSamplePerBlock + r * 256 + threadIdx.x;
+    const u64 i = (u64)j * stride;
+    if (j >= nsample || i >= n) continue;
+    u64 off; u32 len;
+    src.template get<true>((u32)i, off, len);
+    Name nm;
+    load_name_wide<true>(src.blob, off, len, nm);
+    u32 s;
+    Rec rec;
+    if (probe(T, nm, src.blob, &s, &rec) != kFound) continue;
+    u32 h = (s * 2654435761u) & (kL - 1);
+    for (;;) {   // at most kHotSamplePerBlock distinct keys in 2x as many entries
+      const u32 old = atomicCAS(&lkey[h], 0u, s + 1);
+      if (old == 0 || old == s + 1) { atomicAdd(&lcnt[h], 1u); break; }
+      h = (h + 1) & (kL - 1);
+    }
+  }
+  __syncthreads();
+  constexpr u32 mask = (1u << kHotCntBits) - 1;
+  for (u32 e = threadIdx.x; e < kL; e += 256) {
+    const u32 key = lkey[e];
+    if (!key) continue;
+    u32 h = ((key - 1) * 2654435761u) >> (32 - kHotCntBits);
+    for (u32 k = 0; k <= mask; ++k) {
+      const u32 old = atomicCAS(&ckeys[h], 0u, key);
+      if (old == 0 || old == key) { atomicAdd(&ccnt[h], lcnt[e]); break; }
+      h = (h + 1) & mask;
+    }
+  }
+}
 
 __global__ void k_hot_hist(const u32* __restrict__ ccnt, u32* __restrict__ hist) {
   const u32 e = blockIdx.x * blockDim.x + threadIdx.x;
@@ -561,131 +587,36 @@ __global__ __launch_bounds__(256) void k_hot_select(const u32* __restrict__ hist
   }
 }
 
-// The receive batch's directory in two launches (the route combine's chain
-// above takes four and a 2 MB memset; without a classification pass beside
-// it, a receive batch's directory sits in front of the fast kernel):
-//   k_dir_count  one sample per lane (2^16 samples), counted per workgroup
-//                in LDS, then in a 2^17-entry global table;
-//   k_dir_pick   one workgroup: a histogram of the counts, the threshold,
-//                the entries, and the table cleared again for the next
-//                batch (it starts zeroed once, when allocated).
-constexpr u32 kDirCntBits = 17;
-constexpr u32 kDirSamples = 1u << 16;
-constexpr u32 kDirPickThreads = 1024;
-
-template <class Src>
-__global__ __launch_bounds__(256) void k_dir_count(Src src, u32 n, u32 stride, u32 nsample, Table T,
-                                                   u32* __restrict__ ckeys, u32* __restrict__ ccnt) {
-  constexpr u32 kL = 512;
-  __shared__ u32 lkey[kL], lcnt[kL];
-  for (u32 e = threadIdx.x; e < kL; e += 256) { lkey[e] = 0; lcnt[e] = 0; }
-  __syncthreads();
-  const u32 j = blockIdx.x * 256 + threadIdx.x;
-  const u64 i = (u64)j * stride;
-  if (j < nsample && i < n) {
-    u64 off; u32 len;
-    src.template get<true>((u32)i, off, len);
-    Name nm;
-    load_name_wide<true>(src.blob, off, len, nm);
-    u32 s;
-    Rec rec;
-    if (probe(T, nm, src.blob, &s, &rec) == kFound) {
-      for (u32 h = (s * 2654435761u) & (kL - 1);; h = (h + 1) & (kL - 1)) {
-        const u32 old = atomicCAS(&lkey[h], 0u, s + 1);
-        if (old == 0 || old == s + 1) { atomicAdd(&lcnt[h], 1u); break; }
-      }
+__global__ void k_hot_build(const u32* __restrict__ ckeys, const u32* __restrict__ ccnt, HotHdr* hdr,
+                            Table T, HotEntry* __restrict__ dir) {
+  const u32 e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (1u << kHotCntBits)) return;
+  const u32 c = ccnt[e];
+  if (c < kHotMinCount || c < hdr->thresh) return;
+  const u32 idx = atomicAdd(&hdr->n, 1u);
+  if (idx >= kHotMax) return;   // cannot happen: the threshold bounds the count
+  const u32 s = ckeys[e] - 1;
+  const Rec r = load_rec(&T.recs[s]);
+  HotEntry d;
+  const bool arena = (r.name0 & 0xFFu) > kInlineName;
+  d.tag = r.tag;
+  d.w0 = arena ? (r.name0 & 0xFFu) : (r.name0 & ~0xFF00ull);
+  d.w1 = r.name1;
+  d.w2 = r.name2;
+  d.slot = s;
+  d.aoff = arena ? (u32)(r.name0 >> 32) : 0u;
+  const u32 len = (u32)(r.name0 & 0xFFu);
+  for (u32 k = 0; k < kHotTailWords; ++k) d.tail[k] = 0;
+  if (arena && len <= kHotTailName) {
+    const u64 a0 = (r.name0 >> 32) + 16;
+    const u64* p = reinterpret_cast<const u64*>(T.arena + (a0 & ~7ull));
+    const u32 sh = (u32)(a0 & 7) * 8, lastw = ((u32)(a0 & 7) + len - 17) >> 3;
+    for (u32 k = 0; 8 * k < len - 16; ++k) {
+      const u32 m = len - 16 - 8 * k;
+      d.tail[k] = low_bytes(str_word(p, sh, k, lastw), m);
     }
   }
-  __syncthreads();
-  constexpr u32 mask = (1u << kDirCntBits) - 1;
-  for (u32 e = threadIdx.x; e < kL; e += 256) {
-    const u32 key = lkey[e];
-    if (!key) continue;
-    for (u32 h = ((key - 1) * 2654435761u) >> (32 - kDirCntBits), k = 0; k <= mask;
-         ++k, h = (h + 1) & mask) {
-      const u32 old = atomicCAS(&ckeys[h], 0u, key);
-      if (old == 0 || old == key) { atomicAdd(&ccnt[h], lcnt[e]); break; }
-    }
-  }
-}
-
-__global__ __launch_bounds__(kDirPickThreads) void k_dir_pick(u32* __restrict__ ckeys,
-                                                              u32* __restrict__ ccnt, Table T,
-                                                              HotHdr* hdr, HotEntry* __restrict__ dir,
-                                                              u32 maxn) {
-  constexpr u32 kBins = 4096, kPer = kBins / kDirPickThreads, kCnt = 1u << kDirCntBits;
-  __shared__ u32 hist[kBins];
-  __shared__ u32 part[kDirPickThreads];
-  __shared__ u32 best, nsel;
-  const u32 t = threadIdx.x;
-  for (u32 b = t; b < kBins; b += kDirPickThreads) hist[b] = 0;
-  if (t == 0) { best = kBins; nsel = 0; }
-  __syncthreads();
-  for (u32 e = t; e < kCnt; e += kDirPickThreads) {
-    const u32 c = ccnt[e];
-    if (c >= kHotMinCount) atomicAdd(&hist[c < kBins ? c : kBins - 1], 1u);
-  }
-  __syncthreads();
-  // the lowest count t >= kHotMinCount with at most maxn entries counted t
-  // or more: a suffix sum over the bins (kPer bins a thread, then the
-  // threads' sums scanned from the top)
-  u32 mine = 0;
-#pragma unroll
-  for (u32 k = 0; k < kPer; ++k) mine += hist[t * kPer + k];
-  part[t] = mine;
-  __syncthreads();
-  for (u32 d = 1; d < kDirPickThreads; d <<= 1) {   // part[t] = sum of part[t..]
-    const u32 x = t + d < kDirPickThreads ? part[t + d] : 0u;
-    __syncthreads();
-    part[t] += x;
-    __syncthreads();
-  }
-  u32 run = part[t] - mine;   // entries in the bins above this thread's
-  u32 lo = kBins;
-  for (int b = (int)kPer - 1; b >= 0; --b) {
-    run += hist[t * kPer + b];
-    if (run <= maxn) lo = t * kPer + b;
-  }
-  atomicMin(&best, lo);
-  __syncthreads();
-  const u32 th = best > kHotMinCount ? best : kHotMinCount;
-  for (u32 e = t; e < kCnt; e += kDirPickThreads) {
-    const u32 key = ckeys[e];
-    if (!key) continue;
-    const u32 c = ccnt[e];
-    ckeys[e] = 0;   // the table starts the next batch cleared
-    ccnt[e] = 0;
-    if (c < th) continue;
-    const u32 idx = atomicAdd(&nsel, 1u);
-    if (idx >= maxn) continue;   // cannot happen: the threshold bounds the count
-    const u32 s = key - 1;
-    const Rec r = load_rec(&T.recs[s]);
-    HotEntry d;
-    const bool arena = (r.name0 & 0xFFu) > kInlineName;
-    d.tag = r.tag;
-    d.w0 = arena ? (r.name0 & 0xFFu) : (r.name0 & ~0xFF00ull);
-    d.w1 = r.name1;
-    d.w2 = r.name2;
-    d.slot = s;
-    d.aoff = arena ? (u32)(r.name0 >> 32) : 0u;
-    const u32 len = (u32)(r.name0 & 0xFFu);
-    for (u32 k = 0; k < kHotTailWords; ++k) d.tail[k] = 0;
-    if (arena && len <= kHotTailName) {
-      const u64 a0 = (r.name0 >> 32) + 16;
-      const u64* p = reinterpret_cast<const u64*>(T.arena + (a0 & ~7ull));
-      const u32 sh = (u32)(a0 & 7) * 8, lastw = ((u32)(a0 & 7) + len - 17) >> 3;
-      for (u32 k = 0; 8 * k < len - 16; ++k) {
-        const u32 m = len - 16 - 8 * k;
-        d.tail[k] = low_bytes(str_word(p, sh, k, lastw), m);
-      }
-    }
-    dir[idx] = d;
-  }
-  __syncthreads();
-  if (t == 0) {
-    hdr->n = min(nsel, maxn);
-    hdr->thresh = th;
-  }
+  dir[idx] = d;
 }
 
 // ----------------------------------------------------- fast receive --------
@@ -890,44 +821,18 @@ __device__ inline bool tail_match(const u64 (&htail)[kHotTailWords][kHotMax], u3
   return eq;
 }
 
-// Speculative merge (Spec): the first merge of batch epoch `ep` into a record
-// moves the record's epoch to ep by a CAS on name0; the winner stores the
-// state it read as the undo state.  No merge of the batch reaches the record
-// before that CAS (every merger first sees epoch ep or loses the CAS to the
-// winner), so the state the winner read is the record's pre-batch state.
-__device__ inline void spec_log(Rec* r, u64 name0, u64 a, u64 t, i64 e, u32 ep) {
-  if (rec_epoch(name0) == ep) return;
-  if (atomicCAS(&r->name0, name0, with_epoch(name0, ep)) == name0) {
-    r->undo_added = a;
-    r->undo_taken = t;
-    r->undo_elapsed = e;
-  }
-}
-// A set-aside entry of a speculative batch's miss list: a dirty message.
-constexpr u32 kSpecDirtyBit = 0x80000000u;
-// Decoded Receive batches of this many messages or more are merged
-// speculatively (below it the classification pass costs a few µs).
-constexpr u32 kSpecMinBatch = kHotMinBatch;
-
-// Messages [lo, n) of the batch (lo a multiple of 64, or 0).
-//
-// Spec = false: the batch was classified first (k_classify) and only its
-// clean prefix is merged.
-// Spec = true (speculative receive, no classification pass): every clean
-// message is merged, the dirty ones (incast / -0.0, replica_dirty) are set
-// aside in the miss list with kSpecDirtyBit, and every record the batch
-// merges into keeps its pre-batch state (spec_log).  The host then fixes the
-// buckets the dirty messages name (phip_engine.hip spec_receive).
-template <class In, bool Spec = false>
+// Messages [lo, n) of the batch (lo a multiple of 64: a segment of a batch
+// classified segment by segment, or 0).
+template <class In>
 __global__ __launch_bounds__(kFastBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_receive_fast(
     In in, u32 lo, u32 n, Table T, Sharded miss, u32* ctr,
-    const HotHdr* __restrict__ hot, const HotEntry* __restrict__ hot_dir, u32 ep = 0) {
+    const HotHdr* __restrict__ hot, const HotEntry* __restrict__ hot_dir) {
   __shared__ u32 hslot[kHotLds];        // directory index + 1 (0 = empty)
   __shared__ u64 htag[kHotMax], hw0[kHotMax], hw1[kHotMax], hw2[kHotMax];
   __shared__ u32 hrec[kHotMax], haoff[kHotMax];
   __shared__ u64 htail[kHotTailWords][kHotMax];
   __shared__ u64 hmax[3][kHotMax];      // per-workgroup maxima (elapsed biased by 2^63)
-  __shared__ u32 hhits, hdirty;
+  __shared__ u32 hhits;
 
   // Gate (k_classify ran before, over every message up to n): only the clean
   // prefix is applied, the messages before the first dirty one
@@ -940,7 +845,7 @@ __global__ __launch_bounds__(kFastBlock) __attribute__((amdgpu_waves_per_eu(8, 8
   for (u32 j = threadIdx.x; j < kHotMax; j += kFastBlock) {
     hmax[0][j] = 0; hmax[1][j] = 0; hmax[2][j] = 0;
   }
-  if (threadIdx.x == 0) { hhits = 0; hdirty = 0; }
+  if (threadIdx.x == 0) hhits = 0;
   __syncthreads();
   for (u32 j = threadIdx.x; j < nh; j += kFastBlock) {
     const HotEntry d = hot_dir[j];
@@ -999,14 +904,7 @@ __global__ __launch_bounds__(kFastBlock) __attribute__((amdgpu_waves_per_eu(8, 8
     const u64 ea = enc_replica_nz(ra), et = enc_replica_nz(rt), ee = (u64)re ^ kSign;
 
     bool missed = false;
-    u32 entry = i;
-    bool dirt = false;
-    if constexpr (Spec) dirt = valid && replica_dirty(ra, rt, re);
-    if (dirt) {   // set aside (speculative batch): the host orders its bucket
-      missed = true;
-      entry = i | kSpecDirtyBit;
-      hits += 1u << 16;   // (Spec: set-aside messages in the high half, < 2^16 a lane)
-    } else if (valid) {
+    if (valid) {
       int hidx = -1;
       if (nh) {
         for (u32 hs = hot_home(tag);; hs = (hs + 1) & (kHotLds - 1)) {
@@ -1044,9 +942,6 @@ __global__ __launch_bounds__(kFastBlock) __attribute__((amdgpu_waves_per_eu(8, 8
         }
         if (pr == kFound) {
           Rec* r = &T.recs[s];
-          if constexpr (Spec) {
-            if (rec_epoch(cur.name0) != ep) spec_log(r, cur.name0, cur.added, cur.taken, cur.elapsed, ep);
-          }
           if (ea > cur.added) atomicMax(&r->added, ea);
           if (et > cur.taken) atomicMax(&r->taken, et);
           if (ee > ((u64)cur.elapsed ^ kSign)) atomicMax(&r->elapsed, (i64)(ee ^ kSign));
@@ -1056,14 +951,12 @@ __global__ __launch_bounds__(kFastBlock) __attribute__((amdgpu_waves_per_eu(8, 8
         }
       }
     }
-    miss.append(chunk, missed, entry);
+    miss.append(chunk, missed, i);
   }
-  if (hits & 0xFFFFu) atomicAdd(&hhits, hits & 0xFFFFu);
-  if (Spec && (hits >> 16)) atomicAdd(&hdirty, hits >> 16);
+  if (hits) atomicAdd(&hhits, hits);
   __syncthreads();
   if (threadIdx.x == 0) {
     if (hhits) atomicAdd(&ctr[10], hhits);
-    if (Spec && hdirty) atomicAdd(&ctr[kCtrSpecDirty], hdirty);
     if (blockIdx.x == 0) ctr[11] = nh;
   }
 
@@ -1073,158 +966,10 @@ __global__ __launch_bounds__(kFastBlock) __attribute__((amdgpu_waves_per_eu(8, 8
     if (!(xa | xt | xe)) continue;
     Rec* r = &T.recs[hrec[j]];
     const u64 ca = r->added, ct = r->taken, ce = (u64)r->elapsed ^ kSign;
-    if constexpr (Spec) spec_log(r, r->name0, ca, ct, (i64)(ce ^ kSign), ep);
     if (xa > ca) atomicMax(&r->added, xa);
     if (xt > ct) atomicMax(&r->taken, xt);
     if (xe > ce) atomicMax(&r->elapsed, (i64)(xe ^ kSign));
   }
-}
-
-// ------------------------------------------------ speculative receive ----
-// The dirty messages of a speculative batch (incasts, -0.0 fields) are the
-// only ones whose outcome depends on order, and only within their own
-// bucket (repo.go:78-90: an incast replies with the state at its position;
-// bucket.go:250-256: the first +-0 seen is kept).  So the buckets they name
-// (by tag: a name sharing a tag with a dirty one is handled the same way,
-// which is always exact) are set back to their pre-batch state (undo) and
-// all of their messages are replayed in batch order by the ordered path;
-// every other bucket's messages commute and are final after the fast pass.
-
-// Every record's epoch cleared: before an epoch value is reused, and after a
-// restore from a snapshot image.
-__global__ __launch_bounds__(kBlock) void k_spec_sweep(Table T, u64 cap) {
-  const u64 s = (u64)blockIdx.x * kBlock + threadIdx.x;
-  if (s >= cap) return;
-  Rec* r = &T.recs[s];
-  const u64 w0 = r->name0;
-  if (rec_epoch(w0)) r->name0 = with_epoch(w0, 0);
-}
-
-// Open-addressing set of 64-bit table tags (0 = empty), 2^bits entries.
-__device__ inline u32 tagset_home(u64 tag, u32 bits) {
-  return (u32)((tag * 0x9E3779B97F4A7C15ull) >> (64 - bits));
-}
-__device__ inline bool tagset_has(const u64* __restrict__ set, u32 bits, u64 tag) {
-  const u32 mask = (1u << bits) - 1;
-  for (u32 h = tagset_home(tag, bits);; h = (h + 1) & mask) {
-    const u64 v = set[h];
-    if (v == tag) return true;
-    if (v == 0) return false;
-  }
-}
-template <class Src>
-__device__ inline u64 name_tag(const Src& src, u32 i, const Table& T) {
-  u64 off; u32 len;
-  src.get(i, off, len);
-  Name nm;
-  load_name_wide<false>(src.blob, off, len, nm);
-  return T.tag(nm.h);
-}
-
-// The tags of the names of the set-aside entries (kSpecDirtyBit) of
-// list[0..n).
-template <class Src>
-__global__ __launch_bounds__(kBlock) void k_tagset_add(Src src, const u32* __restrict__ list, u32 n,
-                                                      Table T, u64* set, u32 bits) {
-  const u32 j = blockIdx.x * kBlock + threadIdx.x;
-  if (j >= n) return;
-  const u32 v = list[j];
-  if (!(v & kSpecDirtyBit)) return;
-  const u64 tag = name_tag(src, v & ~kSpecDirtyBit, T);
-  const u32 mask = (1u << bits) - 1;
-  for (u32 h = tagset_home(tag, bits);; h = (h + 1) & mask) {
-    const u64 v = set[h];
-    if (v == tag) return;
-    if (v == 0) {
-      const u64 old = atomicCAS((unsigned long long*)&set[h], 0ull, (unsigned long long)tag);
-      if (old == 0 || old == tag) return;
-    }
-  }
-}
-
-// rocprim::select predicates: messages whose tag is in the set (over batch
-// indices), and the misses to keep (a list entry not set aside and not in
-// the set).
-template <class Src>
-struct TagIn {
-  Src src;
-  Table T;
-  const u64* set;
-  u32 bits;
-  __device__ bool operator()(u32 i) const { return tagset_has(set, bits, name_tag(src, i, T)); }
-};
-template <class Src>
-struct MissKeep {
-  Src src;
-  Table T;
-  const u64* set;
-  u32 bits;
-  __device__ bool operator()(u32 v) const {
-    return !(v & kSpecDirtyBit) && !tagset_has(set, bits, name_tag(src, v, T));
-  }
-};
-
-// The picked messages' records back to their pre-batch state (those the
-// batch merged into: epoch ep).  Many messages name one record; they all
-// write the same undo state.
-template <class Src>
-__global__ __launch_bounds__(kBlock) void k_spec_restore(Src src, const u32* __restrict__ pick, u32 m,
-                                                        Table T, u32 ep) {
-  const u32 j = blockIdx.x * kBlock + threadIdx.x;
-  if (j >= m) return;
-  u64 off; u32 len;
-  src.get(pick[j], off, len);
-  Name nm;
-  load_name_wide<false>(src.blob, off, len, nm);
-  u32 s;
-  Rec cur;
-  if (probe(T, nm, src.blob, &s, &cur) != kFound || rec_epoch(cur.name0) != ep) return;
-  Rec* r = &T.recs[s];
-  const u64 a = r->undo_added, t = r->undo_taken;
-  const i64 e = r->undo_elapsed;
-  r->added = a;
-  r->taken = t;
-  r->elapsed = e;
-}
-
-// A sub-batch of a batch: message j of the view is message pick[j].
-template <class Src>
-struct Picked {
-  const u8* blob;
-  Src src;
-  const u32* pick;
-  template <bool NT = false>
-  __device__ inline void get(u32 j, u64& off, u32& len) const {
-    src.template get<NT>(pick[j], off, len);
-  }
-};
-
-// The picked messages' replica columns, gathered in pick order.
-__global__ __launch_bounds__(kBlock) void k_gather_states(const u32* __restrict__ pick, u32 m,
-                                                         const uint64_t* __restrict__ a,
-                                                         const uint64_t* __restrict__ t,
-                                                         const int64_t* __restrict__ e,
-                                                         uint64_t* ga, uint64_t* gt, int64_t* ge) {
-  const u32 j = blockIdx.x * kBlock + threadIdx.x;
-  if (j >= m) return;
-  const u32 i = pick[j];
-  ga[j] = a[i];
-  gt[j] = t[i];
-  ge[j] = e[i];
-}
-
-// The sub-batch's results back to the picked positions.
-__global__ __launch_bounds__(kBlock) void k_scatter_outs(
-    const u32* __restrict__ pick, u32 m, const u8* __restrict__ st, const uint64_t* __restrict__ rem,
-    const uint64_t* __restrict__ hv, const phip_state* __restrict__ rep, u8* status,
-    uint64_t* remaining, uint64_t* have, phip_state* reply) {
-  const u32 j = blockIdx.x * kBlock + threadIdx.x;
-  if (j >= m) return;
-  const u32 i = pick[j];
-  if (status) status[i] = st[j];
-  if (remaining) remaining[i] = rem[j];
-  if (have) have[i] = hv[j];
-  if (reply) reply[i] = rep[j];
 }
 
 // The messages of a list (the fast batch's misses, after the insert
@@ -1517,7 +1262,7 @@ __global__ void k_publish(Src src, u32 base, u32 n, const u32* __restrict__ clai
     r.name0 = (nm.w0 & 0xFFu) | (a << 32);
   }
   r.name0 = with_flags(r.name0, kRecPublished | kRecNew);
-  store_rec64(&T.recs[s], r);
+  T.recs[s] = r;
   T.aux[s] = 0xFFFFFFFFu;
 }
 
@@ -1579,13 +1324,6 @@ __global__ __launch_bounds__(kBlock) void k_rehash(const Rec* __restrict__ old,
   Rec* q = &T.recs[d];
   q->added = r.added; q->taken = r.taken; q->elapsed = r.elapsed;
   q->name0 = r.name0; q->name1 = r.name1; q->created = r.created; q->name2 = r.name2;
-  // a table that grows in the middle of a speculative batch (its misses'
-  // inserts) keeps the undo state of the records the batch touched
-  if (rec_epoch(r.name0)) {
-    q->undo_added = old[s].undo_added;
-    q->undo_taken = old[s].undo_taken;
-    q->undo_elapsed = old[s].undo_elapsed;
-  }
   T.aux[d] = old_aux[s];
 }
 

@@ -337,14 +337,13 @@ class GPURepo:
         return stop.value
 
     def receive_soa(self, names, added, taken, elapsed, now: int, name_offs=None, n=None,
-                    status=None, device=False, classify=False, reply=None, queue=False):
+                    status=None, device=False, reply=None, queue=False):
         """Receive over decoded states.  With device=True every array is a torch
         CUDA tensor (names = uint8 blob, name_offs = int32/uint32 offsets;
         reply: an int64 [n, 4] tensor for the phip_state replies).
-        classify=True: PHIP_RECV_CLASSIFY (classification pass first, no
-        speculation; the same results).  queue=True (device only):
-        PHIP_RECV_ASYNC, the batch is finished by the next call or flush()."""
-        fl = (_lib.RECV_CLASSIFY if classify else 0) | (_lib.RECV_ASYNC if queue else 0)
+        queue=True (device only): PHIP_RECV_ASYNC, the batch is finished by
+        the handle's next call or flush()."""
+        fl = _lib.RECV_ASYNC if queue else 0
         if device:
             m = phip_msgs(n, 0, _ptr(names), _ptr(name_offs), _ptr(added), _ptr(taken), _ptr(elapsed))
             res = phip_results(_ptr(status), None, None, _ptr(reply))

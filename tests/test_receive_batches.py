@@ -1,10 +1,10 @@
-"""Speculative receive (phip_receive_soa on batches of >= 2^16 messages,
-DESIGN.md §3.3) against the oracle and against the classify-first path.
+"""Large Receive batches (>= 2^16 messages: the hot directory, the clean
+prefix through the fast path, the dirty suffix through the ordered path)
+against the oracle, called synchronously and queued (PHIP_RECV_ASYNC: each
+batch finished by the handle's next call or flush).
 
-The fast pass merges every clean message at once and keeps each record's
-pre-batch state (epoch + undo state); the buckets named by incasts or -0.0
-fields are set back and replayed in batch order (repo.go:54-92,
-bucket.go:240-263).  Bar: bit-exact statuses, incast replies and tables.
+Bar: bit-exact statuses, incast replies and tables (repo.go:54-92,
+bucket.go:240-263).
 """
 import numpy as np
 import pytest
@@ -44,9 +44,10 @@ def f64(x):
 
 
 def seeded(pa, rng, K, log2_slots=17, negative=0.0, **kw):
-    """K buckets b0..b{K-1} on the GPU (spec and classify handles) and in
-    the oracle; a fraction `negative` of them holds negative added/taken
-    (where a -0.0 replica's place in the batch decides the sign of zero)."""
+    """K buckets b0..b{K-1} on the GPU (two handles: host batches, and device
+    batches queued) and in the oracle; a fraction `negative` of them holds
+    negative added/taken (where a -0.0 replica's place in the batch decides
+    the sign of zero)."""
     names = _gen.key_names(np.arange(K))
     a, t, e = _gen.clean_states(rng, K)
     neg = rng.random(K) < negative
@@ -62,16 +63,44 @@ def seeded(pa, rng, K, log2_slots=17, negative=0.0, **kw):
     return gs, gc, o
 
 
+def device_batch(names, a, t, e):
+    import torch
+    dev = torch.device("cuda", 0)
+    n = len(names)
+    offs = np.zeros(n + 1, np.int64)
+    offs[1:] = np.cumsum([len(x) for x in names])
+    tb = torch.from_numpy(np.frombuffer(b"".join(names) + b"\0" * 8, np.uint8).copy()).to(dev)
+    to = torch.from_numpy(offs.astype(np.int32)).to(dev)
+    ta, tt, te = (torch.from_numpy(x.view(np.int64).copy()).to(dev) for x in (a, t, e))
+    status = torch.zeros(n, dtype=torch.uint8, device=dev)
+    reply = torch.zeros((n, 4), dtype=torch.int64, device=dev)
+    return dict(n=n, tb=tb, to=to, ta=ta, tt=tt, te=te, status=status, reply=reply)
+
+
+def queue_batch(g, b, now):
+    g.receive_soa(b["tb"], b["ta"], b["tt"], b["te"], now, name_offs=b["to"], n=b["n"],
+                  status=b["status"], device=True, reply=b["reply"], queue=True)
+
+
+def check(res_status, res_reply, st, ra, rt, re):
+    assert np.array_equal(res_status, st), np.nonzero(res_status != st)[0][:8]
+    rep = (st & 0x7F) == 2
+    assert np.array_equal(res_reply[0][rep], ra[rep])
+    assert np.array_equal(res_reply[1][rep], rt[rep])
+    assert np.array_equal(res_reply[2][rep], re[rep])
+
+
 def run_all(gs, gc, o, names, a, t, e, now):
+    """gs: the host-pointer call; gc: the device batch queued, then flushed."""
     out = gs.receive_soa(names, a, t, e, now)
-    ref = gc.receive_soa(names, a, t, e, now, classify=True)
+    b = device_batch(names, a, t, e)
+    queue_batch(gc, b, now)
+    gc.flush()
     st, ra, rt, re = o.receive_soa(names, a, t, e, now)
-    for res in (out, ref):
-        assert np.array_equal(res["status"], st), np.nonzero(res["status"] != st)[0][:8]
-        rep = (st & 0x7F) == 2
-        assert np.array_equal(res["reply"]["a"][rep], ra[rep])
-        assert np.array_equal(res["reply"]["t"][rep], rt[rep])
-        assert np.array_equal(res["reply"]["e"][rep], re[rep])
+    check(out["status"], (out["reply"]["a"], out["reply"]["t"], out["reply"]["e"]), st, ra, rt, re)
+    r = b["reply"].cpu().numpy()
+    check(b["status"].cpu().numpy(), (r[:, 0].view(np.uint64), r[:, 1].view(np.uint64), r[:, 2]),
+          st, ra, rt, re)
     return st
 
 
@@ -97,7 +126,7 @@ def sprinkle(rng, ids, a, t, e, K, *, incast_hot=0, incast_cold=0, incast_new=0,
 
 
 @pytest.mark.parametrize("kind", ["incast_hot", "incast_cold_new", "negzero", "dirty_mix"])
-def test_spec_dirty_batches_vs_oracle_and_classify(pa, kind):
+def test_large_dirty_batches_vs_oracle(pa, kind):
     rng = np.random.default_rng({"incast_hot": 21, "incast_cold_new": 22, "negzero": 23,
                                  "dirty_mix": 24}[kind])
     K = 20000
@@ -130,9 +159,9 @@ def test_spec_dirty_batches_vs_oracle_and_classify(pa, kind):
     same(dump(gs), o.dump())
 
 
-def test_spec_dirty_with_many_new_buckets(pa):
-    """Over 2^16 new names (the dedupe + second speculative pass) with
-    incasts and -0.0 fields on new and existing buckets."""
+def test_large_dirty_batch_with_many_new_buckets(pa):
+    """Over 2^16 new names (the dedupe and a second fast pass) with incasts
+    and -0.0 fields on new and existing buckets."""
     rng = np.random.default_rng(31)
     K = 5000
     gs, gc, o = seeded(pa, rng, K, log2_slots=16)
@@ -152,9 +181,8 @@ def test_spec_dirty_with_many_new_buckets(pa):
 
 
 @pytest.mark.parametrize("tag_bits", [9, 14])
-def test_spec_narrow_tags(pa, tag_bits):
-    """Names sharing a tag with a dirty name are replayed with it (tags
-    truncated to force it): still exact."""
+def test_large_dirty_batch_narrow_tags(pa, tag_bits):
+    """Tags truncated so that names share them (names are always compared)."""
     rng = np.random.default_rng(40 + tag_bits)
     K = 20000
     gs, gc, o = seeded(pa, rng, K, debug_tag_bits=tag_bits)
@@ -167,9 +195,8 @@ def test_spec_narrow_tags(pa, tag_bits):
     same(dump(gs), o.dump())
 
 
-def test_spec_table_grows_mid_batch(pa):
-    """The batch's new buckets rehash the table before the dirty buckets
-    are set back: their undo states move with the records."""
+def test_large_dirty_batch_table_grows(pa):
+    """The batch's new buckets rehash the table in the middle of the batch."""
     rng = np.random.default_rng(51)
     K = 3000
     gs, gc, o = seeded(pa, rng, K, log2_slots=12)
@@ -184,44 +211,36 @@ def test_spec_table_grows_mid_batch(pa):
     same(dump(gs), o.dump())
 
 
-def test_spec_epoch_cycle(pa):
-    """More speculative batches than epoch values: bucket X is merged by
-    batch 0, left alone while the epochs cycle, then named by a dirty batch
-    that runs at batch 0's epoch value again (after the sweep).  A record
-    whose stale epoch matched would skip its undo state and restore batch
-    0's."""
+def test_queued_batches_back_to_back_many(pa):
+    """Twelve queued device batches in a row, each finished by the next call:
+    clean ones, ones with new buckets, ones with incasts and -0.0 fields
+    (the queued front of the next batch is queued again after such a
+    batch's work); every batch's outputs checked after the flush."""
     rng = np.random.default_rng(61)
     K = 4000
     gs, gc, o = seeded(pa, rng, K, log2_slots=14)
     n = 1 << 16
-    X = K - 1
-    others = _gen.zipf_ids(rng, n, K - 1)
-    now = _gen.T0
-    for j in range(66):
-        ids = others.copy()
+    bs, refs = [], []
+    for j in range(12):
+        ids = _gen.zipf_ids(rng, n, K + (300 if j % 3 == 1 else 0))
         a, t, e = _gen.clean_states(rng, n)
-        if j in (0, 63):   # X merged early in the batch (its record grows)
-            ids[10:20] = X
-            a[10:20] = f64(2e6 + j)
-            t[10:20] = f64(1e6 + j)
-        if j == 63:        # ... then an incast on X: its reply is the state at that point
-            ids[30] = X
-            a[30], t[30], e[30] = 0, 0, 0
-            ids[40:50] = X
-            a[40:50] = f64(3e6)
+        if j % 4 == 2:
+            sprinkle(rng, ids, a, t, e, K, incast_hot=1, incast_cold=5, negzero=5)
         names = _gen.key_names(ids)
-        now += SEC
-        if j in (0, 1, 62, 63, 64, 65):
-            run_all(gs, gc, o, names, a, t, e, now)
-        else:
-            gs.receive_soa(names, a, t, e, now)
-            gc.receive_soa(names, a, t, e, now, classify=True)
-            o.receive_soa(names, a, t, e, now)
-    same(dump(gs), o.dump())
+        b = device_batch(names, a, t, e)
+        queue_batch(gc, b, _gen.T0 + j * SEC)
+        bs.append(b)
+        refs.append(o.receive_soa(names, a, t, e, _gen.T0 + j * SEC))
+    gc.flush()
+    for b, (st, ra, rt, re) in zip(bs, refs):
+        r = b["reply"].cpu().numpy()
+        check(b["status"].cpu().numpy(), (r[:, 0].view(np.uint64), r[:, 1].view(np.uint64), r[:, 2]),
+              st, ra, rt, re)
+    same(dump(gc), o.dump())
 
 
 @pytest.mark.parametrize("queue", [False, True])
-def test_spec_back_to_back_device_batches(pa, queue):
+def test_back_to_back_device_batches(pa, queue):
     """Three device-resident batches back to back through phip_receive_soa
     (no host copy): one with new buckets, one with incasts and -0.0 fields
     late in the batch, one clean; statuses and replies checked per batch.
@@ -272,7 +291,7 @@ def test_spec_back_to_back_device_batches(pa, queue):
     same(dump(gs), o.dump())
 
 
-def test_spec_queued_batch_finished_by_other_calls(pa):
+def test_queued_batch_finished_by_other_calls(pa):
     """A queued batch (PHIP_RECV_ASYNC) with incasts is finished by whatever
     call comes next on the handle: a lookup sees its merges and replays."""
     import torch
