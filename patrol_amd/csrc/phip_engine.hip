@@ -60,7 +60,7 @@ enum BufId {
   B_SLOT, B_IDX, B_SSLOT, B_SIDX, B_USLOT, B_SCNT, B_SSTART, B_LONG, B_HUGE, B_TEMP, B_DUMP,
   B_OPS, B_HOFF, B_HOP, B_HVAL, B_RPOS, B_RST, B_RUNN, B_SEGEX, B_WOFF, B_SUMS, B_WRUN,
   B_WING, B_SEGXF, B_FOLDDBG, B_SMALL, B_HUGE2, B_LONG2,
-  B_STATES, B_NAME1, B_HOT, B_ROUTE, B_EXPORT, B_MSHARD, B_MSCNT, B_DEDUP, B_DSET, B_TSTATS, B_SEGT, B_RHOT,
+  B_STATES, B_NAME1, B_HOT, B_ROUTE, B_EXPORT, B_MSHARD, B_MSCNT, B_FSCNT, B_DEDUP, B_DSET, B_TSTATS, B_SEGT, B_RHOT,
   B_COUNT_
 };
 
@@ -111,6 +111,8 @@ struct phip_handle {
   u64* arena_cursor = nullptr;
   u32* ctr = nullptr;        // device counters [16]
   u32* ctr_host = nullptr;   // pinned mirror
+  u32* ctr_map = nullptr;    // ctr_host as the device sees it (k_shard_scan stores there)
+  u32 fpar = 0;              // parity of the last fast batch (its shard counters in B_FSCNT)
   u64 n_buckets = 0;
   u64 tag_mask = ~0ull;
   u64 seed = 0;              // placement seed (Table::home, seeded_mix)
@@ -131,6 +133,7 @@ struct phip_handle {
     const uint64_t *a = nullptr, *t = nullptr;
     const int64_t* e = nullptr;
     u32 n = 0;
+    u32 par = 0;
     i64 now = 0;
     OutView ow{};
   } pend;
@@ -586,8 +589,7 @@ int sharded(phip_handle* h, BufId base_id, u32 units, u32 per_unit, Sharded* out
 // Pack a sharded list into `out`: the total lands in ctr[total_slot] and is
 // returned in *total (one counter read-back).
 int pack_sharded(phip_handle* h, const Sharded& sh, u32 total_slot, u32* out, u32* total) {
-  HIPCHK(h, hipMemsetAsync(h->ctr + 13, 0, sizeof(u32), h->stream));
-  k_shard_scan<<<1, kShards, 0, h->stream>>>(sh.cnt, h->ctr + total_slot, h->ctr + 13);
+  k_shard_scan<<<1, kShards, 0, h->stream>>>(sh.cnt, h->ctr, total_slot, nullptr, 0, nullptr);
   HIPCHK(h, hipGetLastError());
   int rc;
   if ((rc = read_ctr(h))) return rc;
@@ -606,56 +608,84 @@ int fork_hot(phip_handle* h, Src src, u32 n, const HotHdr** hot, const HotEntry*
 
 // A fast batch in three parts, so that a queued batch (PHIP_RECV_ASYNC) can
 // put the next batch's front in front of its own read-back:
-//   front    counter reset, hot directory (stream2), status fill, k_classify;
-//   back     k_receive_fast (after the directory), its miss shards' scan,
-//            the counters to the host (read_ctr, or queued: ev_ctr);
+//   front    counter reset, hot directory (stream2), k_classify (which also
+//            fills the status column);
+//   back     k_receive_fast (after the directory), then one k_shard_scan
+//            that packs the miss shards' offsets and stores the counters in
+//            the host's mapped mirror (queued: and resets them for the next
+//            batch), ev_ctr behind it;
 //   collect  the miss list packed from the host's counters, flags, stats.
+// The miss list's shard counters alternate between two sets by batch parity
+// (B_FSCNT): the next batch's front resets its own set while the batch
+// before still has to pack its list from the other.
 struct FastFront {
   const HotHdr* hot = nullptr;
   const HotEntry* dir = nullptr;
+  u32 par = 0;
 };
+
+inline u32* fast_counts(phip_handle* h, u32 par) {
+  return (u32*)h->buf[B_FSCNT].p + par * 2 * kShards;
+}
+
+int fast_shards(phip_handle* h, u32 n, u32 par, Sharded* out) {
+  int rc;
+  u32* c;
+  out->cap = shard_cap((n + 63) / 64, 64);
+  if ((rc = ensure(h, B_MSHARD, (size_t)kShards * out->cap, &out->base)) ||
+      (rc = ensure(h, B_FSCNT, 4 * kShards, &c)))
+    return rc;
+  out->cnt = fast_counts(h, par);
+  return PHIP_OK;
+}
 
 // Enqueue order matters at this size (2 ms per 100M messages): the counter
 // reset and the classification go first, so the GPU starts reading the batch
 // while the host still enqueues the hot-directory chain on stream2 (about
 // 0.1 ms of API calls that used to sit in front of k_classify).
-// (shards: zero the miss list's shard counters here too, in the same
-// launch; a queued batch's next front leaves them to fast_back, as the
-// batch before it still has to pack its list from them)
+// reset = false: the batch queued just before (nothing since) reset the
+// counters in its last launch.
 template <class In, class HotSrc>
 int fast_front(phip_handle* h, In in, HotSrc hsrc, u32 n, u8* status, FastFront* ff,
-               bool shards = true) {
+               bool reset = true) {
   int rc;
   *ff = FastFront{};
-  Sharded msh;
-  if (shards && (rc = sharded(h, B_MSHARD, (n + 63) / 64, 64, &msh, false))) return rc;
-  k_batch_reset<<<1, kShards, 0, h->stream>>>(h->ctr, shards ? msh.cnt : nullptr);
-  HIPCHK(h, hipGetLastError());
+  u32* c;
+  if ((rc = ensure(h, B_FSCNT, 4 * kShards, &c))) return rc;
+  ff->par = h->fpar ^= 1u;
+  if (reset) {
+    k_batch_reset<<<1, kShards, 0, h->stream>>>(h->ctr, fast_counts(h, ff->par));
+    HIPCHK(h, hipGetLastError());
+  }
   const bool with_hot = n >= kHotMinBatch;
   // A small batch classifies in a few µs, less than the directory chain
   // takes: that chain goes first then.
   const bool hot_first = n < (1u << 23);
   // Statuses: the fast kernel merges most of the batch and writes none; the
-  // column is filled with PHIP_ST_MERGED up front on the main stream, and
-  // every message the kernel leaves is written again after it
-  // (k_receive_list and k_mark_created for misses, the ordered path for the
-  // dirty suffix).  Byte stores from the kernel's lanes cost it 2%; the
-  // fill on stream2 beside the classification slowed the classification
-  // more than it cost here.
+  // column is filled with PHIP_ST_MERGED up front (by k_classify_soa2 as it
+  // streams the batch, else a fill on the main stream), and every message
+  // the kernel leaves is written again after it (k_receive_list and
+  // k_mark_created for misses, the ordered path for the dirty suffix).  Byte
+  // stores from the fast kernel's lanes cost it 2%; a fill on stream2 beside
+  // the classification slowed the classification more than it cost here
+  // (DESIGN.md §4).
   if (with_hot) HIPCHK(h, hipEventRecord(h->ev_fork, h->stream));
   if (with_hot && hot_first && (rc = fork_hot(h, hsrc, n, &ff->hot, &ff->dir))) return rc;
-  if (status) HIPCHK(h, hipMemsetAsync(status, PHIP_ST_MERGED, n, h->stream));
   {
-    Launch l(h, "k_classify");
     bool done = false;
     if constexpr (In::kSoa) {
       if ((((uintptr_t)in.ma | (uintptr_t)in.mt) & 15) == 0) {
+        Launch l(h, "k_classify");
         k_classify_soa2<<<grid_for((n + 1) / 2), kBlock, 0, h->stream>>>(in.ma, in.mt, in.me, n,
-                                                                          h->ctr);
+                                                                          h->ctr, status);
         done = true;
       }
     }
-    if (!done) k_classify<In><<<grid_for(n), kBlock, 0, h->stream>>>(in, n, h->ctr);
+    if (!done) {
+      if (status) HIPCHK(h, hipMemsetAsync(status, PHIP_ST_MERGED, n, h->stream));
+      Launch l(h, "k_classify");
+      k_classify<In><<<grid_for(n), kBlock, 0, h->stream>>>(in, n, h->ctr);
+    }
   }
   HIPCHK(h, hipGetLastError());
   if (with_hot && !hot_first && (rc = fork_hot(h, hsrc, n, &ff->hot, &ff->dir))) return rc;
@@ -669,9 +699,7 @@ int fast_back(phip_handle* h, In in, u32 n, const FastFront& ff, bool queued) {
   u32* miss;
   int rc;
   Sharded msh;
-  if ((rc = ensure(h, B_MISS, n, &miss)) ||
-      (rc = sharded(h, B_MSHARD, (n + 63) / 64, 64, &msh, queued)))
-    return rc;
+  if ((rc = ensure(h, B_MISS, n, &miss)) || (rc = fast_shards(h, n, ff.par, &msh))) return rc;
   if ((rc = join_hot(h, ff.hot))) return rc;
   {
     Launch l(h, "k_receive_fast");
@@ -679,23 +707,21 @@ int fast_back(phip_handle* h, In in, u32 n, const FastFront& ff, bool queued) {
                                                                       h->ctr, ff.hot, ff.dir);
   }
   HIPCHK(h, hipGetLastError());
-  HIPCHK(h, hipMemsetAsync(h->ctr + 13, 0, sizeof(u32), h->stream));
-  k_shard_scan<<<1, kShards, 0, h->stream>>>(msh.cnt, h->ctr + 2, h->ctr + 13);
+  k_shard_scan<<<1, kShards, 0, h->stream>>>(msh.cnt, h->ctr, 2, h->ctr_map, kCtrWords,
+                                             queued ? fast_counts(h, ff.par ^ 1u) : nullptr);
   HIPCHK(h, hipGetLastError());
-  if (!queued) return read_ctr(h);
-  HIPCHK(h, hipMemcpyAsync(h->ctr_host, h->ctr, kCtrWords * sizeof(u32), hipMemcpyDeviceToHost,
-                           h->stream));
   HIPCHK(h, hipEventRecord(h->ev_ctr, h->stream));
+  if (!queued) HIPCHK(h, hipEventSynchronize(h->ev_ctr));
   return PHIP_OK;
 }
 
-int fast_collect(phip_handle* h, u32 n, u32* first_dirty, u32* nmiss) {
+int fast_collect(phip_handle* h, u32 n, u32 par, u32* first_dirty, u32* nmiss) {
   int rc;
   if ((rc = check_flags(h))) return rc;
   *nmiss = h->ctr_host[2];
   if (*nmiss) {
     Sharded msh;
-    if ((rc = sharded(h, B_MSHARD, (n + 63) / 64, 64, &msh, false))) return rc;
+    if ((rc = fast_shards(h, n, par, &msh))) return rc;
     Launch l(h, "k_shard_compact");
     dim3 grid(grid_for(h->ctr_host[13]), kShards);
     k_shard_compact<<<grid, 256, 0, h->stream>>>(msh.base, msh.cap, msh.cnt,
@@ -722,7 +748,7 @@ int fast_apply(phip_handle* h, In in, HotSrc hsrc, u32 n, u8* status, u32* first
   FastFront ff;
   if ((rc = fast_front(h, in, hsrc, n, status, &ff)) || (rc = fast_back(h, in, n, ff, false)))
     return rc;
-  return fast_collect(h, n, first_dirty, nmiss);
+  return fast_collect(h, n, ff.par, first_dirty, nmiss);
 }
 
 template <class Src>
@@ -1319,7 +1345,7 @@ int finish_pending(phip_handle* h, bool* worked) {
   HIPCHK(h, hipEventSynchronize(h->ev_ctr));
   u32 fd = p.n, nmiss = 0;
   int rc;
-  if ((rc = fast_collect(h, p.n, &fd, &nmiss))) return rc;
+  if ((rc = fast_collect(h, p.n, p.par, &fd, &nmiss))) return rc;
   if (nmiss == 0 && fd >= p.n) return PHIP_OK;
   if (worked) *worked = true;
   return finish_receive(h, p.src, p.a, p.t, p.e, p.n, fd, nmiss, p.now, p.ow);
@@ -1727,7 +1753,10 @@ int phip_open(const phip_config* cfg, phip_handle** out) {
   if ((e = hipMalloc(&h->arena, h->arena_cap + 64)) != hipSuccess) return fail(e);
   if ((e = hipMalloc(&h->arena_cursor, 64)) != hipSuccess) return fail(e);
   if ((e = hipMalloc(&h->ctr, kCtrWords * sizeof(u32))) != hipSuccess) return fail(e);
-  if ((e = hipHostMalloc(&h->ctr_host, kCtrWords * sizeof(u32), 0)) != hipSuccess) return fail(e);
+  if ((e = hipHostMalloc(&h->ctr_host, kCtrWords * sizeof(u32),
+                         hipHostMallocMapped | hipHostMallocCoherent)) != hipSuccess ||
+      (e = hipHostGetDevicePointer((void**)&h->ctr_map, h->ctr_host, 0)) != hipSuccess)
+    return fail(e);
   if ((e = hipMemsetAsync(h->recs, 0, h->cap * sizeof(Rec), h->stream)) != hipSuccess) return fail(e);
   if ((e = hipMemsetAsync(h->aux, 0, h->cap * sizeof(u32), h->stream)) != hipSuccess) return fail(e);
   if ((e = hipMemsetAsync(h->arena_cursor, 0, 64, h->stream)) != hipSuccess) return fail(e);
@@ -2088,6 +2117,7 @@ int phip_receive_soa(phip_handle* h, const phip_msgs* m, int64_t now, const phip
     h->pend.t = m->taken;
     h->pend.e = m->elapsed;
     h->pend.n = n;
+    h->pend.par = ff.par;
     h->pend.now = now;
     h->pend.ow = ow;
     return PHIP_OK;

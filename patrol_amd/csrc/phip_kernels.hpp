@@ -209,12 +209,22 @@ __global__ __launch_bounds__(kShards) void k_batch_reset(u32* ctr, u32* shard_cn
   if (shard_cnt) shard_cnt[t] = 0;
 }
 
-// One workgroup of kShards lanes: exclusive offsets of the shards (into
-// cnt[kShards + s]), the total into *total and the largest shard into *maxc.
-__global__ __launch_bounds__(kShards) void k_shard_scan(u32* cnt, u32* total, u32* maxc) {
+// One workgroup of kShards lanes over a sharded list's counters: exclusive
+// offsets of the shards (into cnt[kShards + s]), the total into ctr[tot] and
+// the largest shard into ctr[13].  With `host` (the handle's pinned counter
+// mirror, mapped into the device's address space), the first `words` counter
+// words are then stored there, which ends a fast batch without a copy; with
+// `next`, the batch counters and the next batch's shard counters are reset as
+// k_batch_reset does, so a queued batch's successor needs no reset launch.
+__global__ __launch_bounds__(kShards) void k_shard_scan(u32* cnt, u32* ctr, u32 tot, u32* host,
+                                                        u32 words, u32* next) {
   __shared__ u32 v[kShards];
+  __shared__ u32 wmax[kShards / 64];
   const u32 t = threadIdx.x, c = cnt[t];
   v[t] = c;
+  u32 m = c;
+  for (u32 d = 32; d; d >>= 1) m = max(m, (u32)__shfl_xor((int)m, d));
+  if ((t & 63) == 0) wmax[t >> 6] = m;
   __syncthreads();
   for (u32 off = 1; off < kShards; off <<= 1) {
     const u32 x = t >= off ? v[t - off] : 0u;
@@ -223,8 +233,22 @@ __global__ __launch_bounds__(kShards) void k_shard_scan(u32* cnt, u32* total, u3
     __syncthreads();
   }
   cnt[kShards + t] = v[t] - c;
-  if (t == kShards - 1) *total = v[t];
-  if (c) atomicMax(maxc, c);
+  const u32 total = v[kShards - 1];
+  u32 mx = 0;
+  for (u32 w = 0; w < kShards / 64; ++w) mx = max(mx, wmax[w]);
+  if (t == 0) {
+    ctr[tot] = total;
+    ctr[13] = mx;
+  }
+  if (host && t < words) {
+    const u32 w = t == tot ? total : t == 13 ? mx : ctr[t];
+    __hip_atomic_store(&host[t], w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  if (next) {
+    __syncthreads();
+    if (t < 16) ctr[t] = (t == 5 || t == 12) ? ~0u : 0u;
+    next[t] = 0;
+  }
 }
 
 // grid (ceil(max shard count / 256), kShards): shard s's entries, in order,
@@ -768,13 +792,23 @@ __global__ __launch_bounds__(kBlock) void k_classify(In in, u32 n, u32* ctr) {
 // messages per lane, one 16-byte load per column (the pass is a pure stream
 // of 16 bytes per message; elapsed is read only when both floats are zero).
 // Lane l holds messages 2l, 2l+1 of its wave's 128, so the lowest dirty lane
-// still holds the lowest dirty index.
+// still holds the lowest dirty index.  With `status`, the pass also fills the
+// status column with PHIP_ST_MERGED (2 bytes per lane), which the fast kernel
+// relies on: it writes no status for the messages it merges.
 typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
 __global__ __launch_bounds__(kBlock) void k_classify_soa2(const uint64_t* __restrict__ ma,
                                                           const uint64_t* __restrict__ mt,
                                                           const int64_t* __restrict__ me, u32 n,
-                                                          u32* ctr) {
+                                                          u32* ctr, u8* status) {
   const u32 i0 = 2 * (blockIdx.x * kBlock + threadIdx.x);
+  if (status) {   // every status starts as merged (the fast pass writes none)
+    if (i0 + 1 < n && ((uintptr_t)status & 1) == 0)
+      *reinterpret_cast<u16*>(status + i0) = (u16)(PHIP_ST_MERGED | (PHIP_ST_MERGED << 8));
+    else {
+      if (i0 < n) status[i0] = PHIP_ST_MERGED;
+      if (i0 + 1 < n) status[i0 + 1] = PHIP_ST_MERGED;
+    }
+  }
   bool d = false;
   u32 at = i0;
   if (i0 + 1 < n) {
