@@ -59,7 +59,7 @@ __global__ __launch_bounds__(256) void k_lookback(u64* desc, u32* ticket, u32 nt
     }
     const u64 ready = __ballot(f != 0);
     const u32 upto = pstar < kTiles ? pstar : kTiles - 1;
-    const u64 need = upto == 63 ? ~0ull : ((1ull << ((upto + 1) * W)) - 1);
+    const u64 need = (upto + 1) * W >= 64 ? ~0ull : ((1ull << ((upto + 1) * W)) - 1);
     if ((ready & need) != need) {   // a predecessor not published yet
       if (++nspin > (1ull << 22)) { sum = kVal; break; }   // bounded: a wrong result, never a hang
       continue;
