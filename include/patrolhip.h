@@ -57,6 +57,11 @@ extern "C" {
 /* bucket.go:36-44 */
 #define PHIP_BUCKET_FIXED_SIZE 25
 #define PHIP_BUCKET_PACKET_SIZE 256
+/* Names are 0..PHIP_MAX_NAME_LEN bytes (bucket.go:44-48).  Host batches are
+ * checked (PHIP_ERR_NAME_TOO_LARGE); a batch passed by device pointers is
+ * not read on the host, so its producer guarantees the bound.  (A datagram
+ * carries its name length in one byte: phip_receive_datagrams takes names
+ * of up to 255 bytes, as UnmarshalBinary does, bucket.go:72-91.) */
 #define PHIP_MAX_NAME_LEN 231
 
 typedef struct phip_handle phip_handle;
