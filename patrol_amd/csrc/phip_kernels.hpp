@@ -2,8 +2,9 @@
 //
 // Table: recs[2^L] 64-byte slot records (tag, state and name in one HBM
 // burst) + aux[2^L] u32 scratch used only by inserting/seeding batches.
-// Home slot = top L bits of tag * 2^64/phi (Fibonacci hashing), linear
-// probing; a lookup touches one 64-byte record per probe step.
+// Home slot = top L bits of seeded_mix(tag, seed) (a per-handle seed, as Go
+// seeds its map hash), linear probing; a lookup touches one 64-byte record
+// per probe step.
 #pragma once
 #include <type_traits>
 
