@@ -115,7 +115,9 @@ enum {
                                  call queues the batch and returns; the batch is finished
                                  (misses created, a dirty suffix through the ordered path,
                                  outputs final) by the handle's next call or phip_flush,
-                                 which also returns its error.  Inputs and outputs must stay
+                                 which also returns its error (phip_len and phip_capacity
+                                 finish it too, and leave its error to the handle's next
+                                 call that returns a status).  Inputs and outputs must stay
                                  untouched until then.  A receive call queues its batch's
                                  classification and hot directory behind the batch before
                                  it, so the host's read-back of that batch overlaps them. */

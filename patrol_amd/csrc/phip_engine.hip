@@ -138,6 +138,7 @@ struct phip_handle {
     OutView ow{};
   } pend;
   hipEvent_t ev_ctr = nullptr;   // a queued batch's counters reached ctr_host
+  int deferred_rc = 0;   // a queued batch's error met by a call that returns no status
 };
 
 namespace {
@@ -257,6 +258,11 @@ int after_error(phip_handle* h, int rc);
 // (finish_queued: a batch PHIP_RECV_ASYNC queued is finished first, and its
 // error is this call's)
 int begin_call(phip_handle* h, bool finish_queued = true) {
+  if (h->deferred_rc) {   // (phip_len / phip_capacity finished a queued batch that failed)
+    const int rc = h->deferred_rc;
+    h->deferred_rc = 0;
+    return rc;
+  }
   h->err.clear();
   if (h->timing && !h->timing_accumulate) {
     h->timings.clear();
@@ -1821,16 +1827,18 @@ int phip_flush(phip_handle* h) {
 }
 
 // (a queued PHIP_RECV_ASYNC batch is finished first: its new buckets count)
+// (their own result carries no status: a queued batch's error is kept for the
+// handle's next call that returns one)
 uint64_t phip_len(phip_handle* h) {
   if (!h) return 0;
   std::lock_guard<std::mutex> g(h->mu);
-  (void)begin_call(h);
+  if (!h->deferred_rc) h->deferred_rc = begin_call(h);
   return h->n_buckets;
 }
 uint64_t phip_capacity(phip_handle* h) {
   if (!h) return 0;
   std::lock_guard<std::mutex> g(h->mu);
-  (void)begin_call(h);
+  if (!h->deferred_rc) h->deferred_rc = begin_call(h);
   return h->cap;
 }
 

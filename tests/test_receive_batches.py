@@ -319,3 +319,50 @@ def test_queued_batch_finished_by_other_calls(pa):
     assert (got.added, got.taken, got.elapsed) == want[:3]
     assert np.array_equal(status.cpu().numpy(), st)
     same(dump(gs), o.dump())
+
+
+@pytest.mark.parametrize("first_call", ["flush", "len"])
+def test_queued_batch_error_reported_by_next_call(pa, first_call):
+    """A queued batch that cannot be finished (PHIP_CFG_NO_GROW: its new
+    buckets would pass the load limit) returns its error from the handle's
+    next call, or, when that call is phip_len (which has no status), from
+    the call after it.  As for a synchronous batch, the fast path has merged
+    the messages naming existing buckets and no new bucket is created; the
+    handle keeps working."""
+    rng = np.random.default_rng(91)
+    K = 300
+    names0 = _gen.key_names(np.arange(K))
+    a0, t0, e0 = _gen.clean_states(rng, K)
+    created = _gen.T0 - rng.integers(0, SEC, K)
+    g = pa.GPURepo(log2_slots=10, max_load_pct=50, grow=False)   # 512 buckets allowed
+    g.seed(names0, a0, t0, e0, created)
+    o = O.Repo()
+    o.seed(names0, a0, t0, e0, created)
+    n = 1 << 16
+    ids = rng.integers(0, K, n)
+    ids[rng.choice(n, 400, replace=False)] = K + np.arange(400)   # 400 new names: over the limit
+    names = _gen.key_names(ids)
+    a, t, e = _gen.clean_states(rng, n)
+    queue_batch(g, device_batch(names, a, t, e), _gen.T0)
+    if first_call == "len":
+        assert len(g) == K   # finishes the batch; its error waits for the next call
+    with pytest.raises(pa.PatrolHipError) as ei:
+        g.flush()
+    assert ei.value.code == -3
+    g.flush()   # reported once
+    keep = np.nonzero(ids < K)[0]
+    o.receive_soa([names[i] for i in keep], a[keep], t[keep], e[keep], _gen.T0)
+    same(dump(g), o.dump())
+    # the handle still works: a queued batch that fits, then its flush
+    ids2 = rng.integers(0, K + 100, n)
+    names2 = _gen.key_names(ids2)
+    a2, t2, e2 = _gen.clean_states(rng, n)
+    b = device_batch(names2, a2, t2, e2)
+    queue_batch(g, b, _gen.T0 + SEC)
+    g.flush()
+    st, ra, rt, re = o.receive_soa(names2, a2, t2, e2, _gen.T0 + SEC)
+    r = b["reply"].cpu().numpy()
+    check(b["status"].cpu().numpy(), (r[:, 0].view(np.uint64), r[:, 1].view(np.uint64), r[:, 2]),
+          st, ra, rt, re)
+    assert len(g) == K + 100
+    same(dump(g), o.dump())
