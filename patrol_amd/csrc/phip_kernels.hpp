@@ -475,8 +475,8 @@ __device__ inline u64 enc_replica_nz(u64 b) {
 }
 
 // ------------------------------------------------- hot-bucket directory --
-// Zipf-skewed batches put most messages on a few buckets (C2: the top 384 of
-// 10M buckets carry 59% of the messages).  Before the fast kernel runs, a
+// Zipf-skewed batches put most messages on a few buckets (C2: the 732
+// hottest of 10M buckets carry 63% of the messages).  Before the fast kernel runs, a
 // strided sample of the batch is resolved and counted; the (at most kHotMax)
 // buckets sampled most often form the batch's hot directory.  Every fast
 // workgroup keeps the directory in LDS and folds the messages of those
@@ -486,11 +486,16 @@ __device__ inline u64 enc_replica_nz(u64 b) {
 // the table read.
 // (PHIP_HOT_MAX / PHIP_HOT_LDS / PHIP_FAST_BLOCK / PHIP_FAST_PER_CU override
 // the defaults for tuning builds, tools/build_variants.sh.)
+// 736 entries in a 4096-slot lookup (18% load) with two 1024-lane
+// workgroups a CU fill its 160 KB of LDS; against 384 in 1024 slots with
+// four 512-lane workgroups: k_receive_fast 1.78-1.79 vs 1.85 ms on C2
+// (DESIGN.md §4 round 5).  The lookup's load matters as much as the size:
+// 640 entries in 1024 slots ran 2.06 ms.
 #ifndef PHIP_HOT_MAX
-#define PHIP_HOT_MAX 384
+#define PHIP_HOT_MAX 736
 #endif
 #ifndef PHIP_HOT_LDS
-#define PHIP_HOT_LDS 1024
+#define PHIP_HOT_LDS 4096
 #endif
 constexpr u32 kHotMax = PHIP_HOT_MAX;     // directory entries
 constexpr u32 kHotLds = PHIP_HOT_LDS;     // LDS lookup slots (power of 2, >= 1.5 * kHotMax)
@@ -646,9 +651,9 @@ __global__ void k_hot_build(const u32* __restrict__ ckeys, const u32* __restrict
 
 // ----------------------------------------------------- fast receive --------
 // Statuses: the caller's status column is filled with PHIP_ST_MERGED
-// before the kernel (fast_apply, beside the classification); every message
-// the kernel does not merge is written again later (misses by the miss path,
-// the dirty suffix by the ordered path).
+// before the kernel (by k_classify_soa2, or a fill beside k_classify); every
+// message the kernel does not merge is written again later (misses by the
+// miss path, the dirty suffix by the ordered path).
 // Persistent workgroups; every wave walks its own 64-message chunks
 // (grid-stride over waves, no workgroup barrier inside the loop, so a wave
 // waiting on a table read never holds up another).  Per message:
@@ -661,10 +666,10 @@ __global__ void k_hot_build(const u32* __restrict__ ckeys, const u32* __restrict
 // redundant atomic, never a lost update.  Misses are appended to `miss`; the
 // insert pipeline then creates their buckets and k_receive_list merges them.
 #ifndef PHIP_FAST_BLOCK
-#define PHIP_FAST_BLOCK 512
+#define PHIP_FAST_BLOCK 1024
 #endif
 #ifndef PHIP_FAST_PER_CU
-#define PHIP_FAST_PER_CU 4
+#define PHIP_FAST_PER_CU 2
 #endif
 constexpr u32 kFastBlock = PHIP_FAST_BLOCK;
 constexpr u32 kFastPerCU = PHIP_FAST_PER_CU;   // resident workgroups per CU (LDS-bound)
