@@ -114,6 +114,7 @@ class GPURepo:
         if getattr(self, "h", None) and getattr(self, "owned", True):
             self.L.phip_close(self.h)
         self.h = None
+        self._queued = None
 
     def __del__(self):
         try:
@@ -134,7 +135,9 @@ class GPURepo:
         return rc
 
     def flush(self):
-        self._check(self.L.phip_flush(self.h))
+        rc = self.L.phip_flush(self.h)
+        self._queued = None   # the queued batch is finished (or failed)
+        self._check(rc)
 
     def set_stream(self, stream=None):
         """Run the handle's work on `stream` (a torch.cuda.Stream, a raw
@@ -342,13 +345,18 @@ class GPURepo:
         CUDA tensor (names = uint8 blob, name_offs = int32/uint32 offsets;
         reply: an int64 [n, 4] tensor for the phip_state replies).
         queue=True (device only): PHIP_RECV_ASYNC, the batch is finished by
-        the handle's next call or flush()."""
+        the handle's next call or flush(); the binding holds the batch's
+        tensors until the next receive or flush(), so that the caching
+        allocator cannot hand their memory to another tensor meanwhile."""
         fl = _lib.RECV_ASYNC if queue else 0
         if device:
             m = phip_msgs(n, 0, _ptr(names), _ptr(name_offs), _ptr(added), _ptr(taken), _ptr(elapsed))
             res = phip_results(_ptr(status), None, None, _ptr(reply))
-            self._check(self.L.phip_receive_soa(self.h, C.byref(m), int(now), C.byref(res),
-                                                DEVICE_PTRS | fl))
+            rc = self.L.phip_receive_soa(self.h, C.byref(m), int(now), C.byref(res),
+                                         DEVICE_PTRS | fl)
+            self._queued = ((names, name_offs, added, taken, elapsed, status, reply)
+                            if queue and rc == 0 else None)
+            self._check(rc)
             return None
         n = len(names)
         blob, offs = names_blob(names)

@@ -321,13 +321,14 @@ def test_queued_batch_finished_by_other_calls(pa):
     same(dump(gs), o.dump())
 
 
-@pytest.mark.parametrize("first_call", ["flush", "len"])
+@pytest.mark.parametrize("first_call", ["flush", "len", "receive"])
 def test_queued_batch_error_reported_by_next_call(pa, first_call):
     """A queued batch that cannot be finished (PHIP_CFG_NO_GROW: its new
     buckets would pass the load limit) returns its error from the handle's
     next call, or, when that call is phip_len (which has no status), from
-    the call after it.  As for a synchronous batch, the fast path has merged
-    the messages naming existing buckets and no new bucket is created; the
+    the call after it; a queued receive that meets it returns it and queues
+    nothing.  As for a synchronous batch, the fast path has merged the
+    messages naming existing buckets and no new bucket is created; the
     handle keeps working."""
     rng = np.random.default_rng(91)
     K = 300
@@ -343,21 +344,27 @@ def test_queued_batch_error_reported_by_next_call(pa, first_call):
     ids[rng.choice(n, 400, replace=False)] = K + np.arange(400)   # 400 new names: over the limit
     names = _gen.key_names(ids)
     a, t, e = _gen.clean_states(rng, n)
-    queue_batch(g, device_batch(names, a, t, e), _gen.T0)
-    if first_call == "len":
-        assert len(g) == K   # finishes the batch; its error waits for the next call
-    with pytest.raises(pa.PatrolHipError) as ei:
-        g.flush()
-    assert ei.value.code == -3
-    g.flush()   # reported once
-    keep = np.nonzero(ids < K)[0]
-    o.receive_soa([names[i] for i in keep], a[keep], t[keep], e[keep], _gen.T0)
-    same(dump(g), o.dump())
-    # the handle still works: a queued batch that fits, then its flush
+    b1 = device_batch(names, a, t, e)   # held: a queued batch's inputs stay put until it is finished
+    queue_batch(g, b1, _gen.T0)
     ids2 = rng.integers(0, K + 100, n)
     names2 = _gen.key_names(ids2)
     a2, t2, e2 = _gen.clean_states(rng, n)
     b = device_batch(names2, a2, t2, e2)
+    if first_call == "len":
+        assert len(g) == K   # finishes the batch; its error waits for the next call
+    with pytest.raises(pa.PatrolHipError) as ei:
+        if first_call == "receive":
+            queue_batch(g, b, _gen.T0 + SEC)   # not queued: the error is the batch before's
+        else:
+            g.flush()
+    assert ei.value.code == -3
+    g.flush()   # reported once
+    del b1
+    keep = np.nonzero(ids < K)[0]
+    o.receive_soa([names[i] for i in keep], a[keep], t[keep], e[keep], _gen.T0)
+    same(dump(g), o.dump())
+    # the handle still works: a queued batch that fits, then its flush
+    b["status"].zero_()
     queue_batch(g, b, _gen.T0 + SEC)
     g.flush()
     st, ra, rt, re = o.receive_soa(names2, a2, t2, e2, _gen.T0 + SEC)
