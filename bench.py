@@ -93,6 +93,12 @@ def parse():
     p.add_argument("--sync-receive", action="store_true",
                    help="A/B only: c2 calls phip_receive_soa synchronously instead of queueing "
                         "each batch (PHIP_RECV_ASYNC) and flushing at the end of the timed steps")
+    p.add_argument("--split", default=None, choices=["off", "small"],
+                   help="A/B only: the ordered path's hot split off (PHIP_CFG_NO_SPLIT) or from "
+                        "2^16 ops for every sampled name (PHIP_CFG_SPLIT_SMALL)")
+    p.add_argument("--check-names", action="store_true",
+                   help="c2: pass the names blob's length (phip_msgs.names_len) so the device "
+                        "checks every name offset (the binding's default); the headline passes 0")
     p.add_argument("--no-status", action="store_true",
                    help="A/B only: the C2 step does not write the per-message status column")
     p.add_argument("--name-len", type=int, default=0,
@@ -100,6 +106,8 @@ def parse():
     p.add_argument("--no-routed", action="store_true",
                    help="c2: skip the owner_routed (strong-scaling) object")
     p.add_argument("--no-c3", action="store_true", help="c2: skip the c3 object")
+    p.add_argument("--no-variants", action="store_true",
+                   help="c2: skip the c2_variants object (uniform keys, 32-byte names)")
     p.add_argument("--no-c4", action="store_true", help="c2: skip the c4 object")
     p.add_argument("--no-ae", action="store_true", help="c2: skip the anti_entropy object")
     p.add_argument("--c4-keys", type=int, default=125_000_000,
@@ -479,7 +487,7 @@ def run_c3_leg(args, torch, dist, dev, local, rank, world):
     ca.c3_clock = "below"
     gen = torch.Generator(device=dev).manual_seed(args.seed + 303 + 7919 * rank)
     base = rank * K
-    repo = patrol_amd.GPURepo(device=local, log2_slots=L, arena_bytes=1 << 20)
+    repo = patrol_amd.GPURepo(device=local, log2_slots=L, arena_bytes=1 << 20, split=args.split)
     repo.use_torch_stream()
     keys = torch.arange(base, base + K, dtype=torch.int64, device=dev)
     kb, ko = names_for_ids(torch, keys)
@@ -661,6 +669,51 @@ def group_diag(group, world, stages, names):
     return out
 
 
+XGMI_GBPS = 7 * 153.0   # MI355X: 7 xGMI links x ~153 GB/s per GPU (one direction)
+
+
+def c4_stage_roofline(diag, n, name_bytes, sent, merged, world):
+    """Rank 0's stages of one routed C4 step against their bounds (busy ms
+    from HIP events on each stage's own stream, phip_group_stage_ms; the
+    stages overlap, so each rate is the stage's own):
+      pack      reads each message (offset 4 + name + 24 B of state) and
+                writes it owner-major (length 4 + name + 24): 2 x (28 +
+                name) B per message (SURVEY §8d's ~7 GB per 100M), HBM-bound;
+      exchange  the segments sent after the combine, (4 + name + 24) B each:
+                at N > 1 the (N-1)/N that leave go over xGMI (7 links x 153
+                GB/s per GPU); at N = 1 the RCCL send/recv to itself is a
+                device copy (read + write in HBM);
+      merge     88 B per merged message, HBM-bound."""
+    sb = (diag or {}).get("stage_busy_ms")
+    if not sb or sent is None:
+        return {}
+    msg = 28.0 + name_bytes
+    pack_b = 2.0 * msg * n
+    xfer_b = msg * sent * ((world - 1) / world if world > 1 else 1.0)
+    merge_b = BYTES_PER_MERGE * merged
+    out = {"algorithmic_bytes_per_step": {"pack": pack_b, "exchange": xfer_b, "merge": merge_b},
+           "stage_roofline": {}}
+    for nm, b in (("pack", pack_b), ("merge", merge_b)):
+        ms = sb.get(nm)
+        if ms:
+            gbs = b / (ms / 1e3) / 1e9
+            out["stage_roofline"][nm] = {"bound": "hbm", "achieved_GBps": gbs,
+                                         "peak_GBps": HBM_PEAK_GBS, "frac": gbs / HBM_PEAK_GBS}
+    ms = sb.get("exchange")
+    if ms:
+        gbs = xfer_b / (ms / 1e3) / 1e9
+        if world > 1:
+            out["stage_roofline"]["exchange"] = {"bound": "xgmi", "achieved_GBps": gbs,
+                                                 "peak_GBps": XGMI_GBPS, "frac": gbs / XGMI_GBPS}
+        else:   # a copy through RCCL: the bytes are read and written in HBM
+            out["stage_roofline"]["exchange"] = {
+                "bound": "hbm (N = 1: RCCL send/recv to itself, a device copy)",
+                "achieved_GBps": gbs, "peak_GBps": HBM_PEAK_GBS,
+                "frac": 2 * gbs / HBM_PEAK_GBS}
+    out["sent_after_combine_per_step_rank0"] = sent
+    return out
+
+
 LEG_LIMIT_S = 300   # each extra leg's watchdog (main())
 LEG_TIMEOUT_EXIT = 3   # exit status when a watchdog fired
 LEG_FAILED_EXIT = 4    # exit status when a leg raised or its in-run parity check failed
@@ -789,6 +842,110 @@ def _timed_steps(dist, torch, dev, args, warmup, steps, step):
     return float(_coll(dist, args, torch, el, "max").item())
 
 
+def run_c2_variants_leg(args, torch, dist, dev, local, rank, world):
+    """The `c2_variants` object: SURVEY §8d C2's other input shapes, each run
+    exactly as the headline (a 10M-bucket table in 2^25 slots, 100M-message
+    batches resident in HBM, queued phip_receive_soa with statuses, every
+    step a first application), a few steps each:
+      uniform   keys uniform over the 10M buckets (SURVEY §8d C1/C4's
+                "uniform variant"): no hot bucket, every message reads a
+                random record line;
+      names32   32-byte names "b" + "x"... + decimal id (arena names, up to
+                231 B per bucket.go:36-44; the headline's are 2-8 B).
+    `verified` per variant: 2^14 sampled bucket ids (plus the 256 hottest
+    Zipf ranks) read back through phip_export_datagrams equal an
+    independent max-reduce of every applied message naming them (torch
+    scatter_reduce amax; clean-domain states on a zero-state table:
+    Bucket.Merge, bucket.go:240-263, is the field-wise max)."""
+    import patrol_amd
+    K, n, L = args.keys, args.messages, args.log2_slots
+    warm, steps = 1, max(1, min(args.steps, 3))
+    out = {}
+    for name, zipf, width in (("uniform", 0.0, 0), ("names32", args.zipf, 32)):
+        gen = torch.Generator(device=dev).manual_seed(args.seed + 404 + 7919 * rank + width)
+        base = rank * K
+        arena = max(1 << 20, K * (width + 8)) if width > 22 else 1 << 20
+        repo = patrol_amd.GPURepo(device=local, log2_slots=L, arena_bytes=arena)
+        repo.use_torch_stream()
+        keys = torch.arange(base, base + K, dtype=torch.int64, device=dev)
+        kb, ko = names_for_ids(torch, keys, width)
+        st = torch.zeros((K, 4), dtype=torch.int64, device=dev)
+        st[:, 3] = T0
+        torch.cuda.synchronize()
+        repo.seed_device(kb, ko, st, K)
+        del kb, ko, st, keys
+        ids = zipf_ids(torch, gen, n, K, zipf, dev)
+        blob, offs = names_for_ids(torch, ids + base, width)
+        batches = [replica_states(torch, gen, n, j, dev) for j in range(warm + steps)]
+        status = [torch.empty(n, dtype=torch.uint8, device=dev) for _ in range(2)]
+        torch.cuda.synchronize()
+
+        def step(j):
+            a, t, e = batches[j]
+            repo.receive_soa(blob, a, t, e, T0 + j, name_offs=offs, n=n, status=status[j % 2],
+                             device=True, queue=True, names_len=0)   # (as the headline)
+        for j in range(warm):
+            step(j)
+        repo.flush()
+        torch.cuda.synchronize()
+        dist.barrier()
+        repo.set_timing(True, accumulate=True)
+        t0 = time.perf_counter()
+        for j in range(warm, warm + steps):
+            step(j)
+        repo.flush()
+        torch.cuda.synchronize()
+        dist.barrier()
+        el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+        el = float(_coll(dist, args, torch, el, "max").item())
+        kms = {}
+        for nm, ms in repo.timings():
+            kms[nm] = kms.get(nm, 0.0) + ms / steps
+        repo.set_timing(False)
+        # ---- sampled parity (outside the timed region)
+        vg = torch.Generator(device=dev).manual_seed(args.seed + 556)
+        hot = (torch.arange(256, dtype=torch.int64, device=dev) * zipf_mult(K)) % K
+        samp = torch.unique(torch.cat([torch.randint(0, K, (1 << 14,), device=dev, generator=vg),
+                                       hot]))
+        S = samp.numel()
+        pos = torch.searchsorted(samp, ids).clamp_(max=S - 1)
+        hit = samp[pos] == ids
+        pos = pos[hit]
+        want = torch.zeros((3, S), dtype=torch.int64, device=dev)
+        for a, t, e in batches:
+            for f, x in enumerate((a, t, e)):
+                want[f].scatter_reduce_(0, pos, x[hit], reduce="amax", include_self=True)
+        sb, so = names_for_ids(torch, samp + base, width)
+        ga, gt, ge, found = repo.export_states_device(sb, so, S)
+        bad = int(((ga != want[0]) | (gt != want[1]) | (ge != want[2])).sum())
+        ok = bool(found.all()) and bad == 0
+        okt = _coll(dist, args, torch, torch.tensor([int(ok)], dtype=torch.int64, device=dev), "sum")
+        st4 = repo.last_stats()
+        repo.close()
+        del batches, blob, offs, ids, status
+        torch.cuda.empty_cache()
+        step_s = el / steps
+        fast = kms.get(DOMINANT)
+        ach = BYTES_PER_MERGE * n / (fast / 1e3) / 1e9 if fast else None
+        out[name] = {
+            "value": world * n * steps / el, "unit": "merges/s", "ms_per_step": step_s * 1e3,
+            "steps": steps, "warmup": warm,
+            "workload": (f"C2 variant: {n} replica messages -> {K}-bucket table (2^{L} slots), " +
+                         ("uniform keys" if zipf == 0 else f"Zipf({zipf})") +
+                         (f", {width}-byte names" if width else ", names b<id> (2-8 B)")),
+            "roofline": {"bound": "hbm", "kernel": DOMINANT, "kernel_ms_per_step": fast,
+                         "achieved": ach, "peak": HBM_PEAK_GBS,
+                         "frac": ach / HBM_PEAK_GBS if ach else None,
+                         "algorithmic_bytes_per_step": BYTES_PER_MERGE * n},
+            "kernels_ms": kms,
+            "hot_directory": {"entries": int(st4[0]), "folded": int(st4[1])} if st4 else None,
+            "verified": int(okt.item()) == world,
+            "verify": {"sampled_buckets": S, "mismatched": bad, "all_found": bool(found.all())},
+        }
+    out["verified"] = all(v["verified"] for v in out.values())
+    return out
+
+
 def zipf_mult(K):
     """zipf_ids' rank -> id multiplier (a unit mod K)."""
     mult = 2654435761 % K or 1
@@ -855,16 +1012,19 @@ def run_c4_leg(args, torch, dist, dev, local, rank, world):
     torch.cuda.synchronize()
     group = open_group(args, dist, repo, rank, world)
     merged = []
+    sent = []
     stages = []
     if group is not None:
         group.set_timing(True)
+    name_bytes = float((offs[-1] - offs[0]).item()) / n   # mean name length of the batch
 
     def step(j):
         a, t, e = batches[j]
         if group is not None:
-            _, got = group.receive([(blob, offs, a, t, e)], T0 + j, combine=True,
-                                   rccl_self=world == 1)
+            snt, got = group.receive([(blob, offs, a, t, e)], T0 + j, combine=True,
+                                     rccl_self=world == 1)
             k = got[0]
+            sent.append(snt[0])
             if j >= warm:   # (the call ends host-synchronised: reading its events adds no wait)
                 stages.append(group.stage_ms())
         else:
@@ -909,6 +1069,8 @@ def run_c4_leg(args, torch, dist, dev, local, rank, world):
     sm = _coll(dist, args, torch, tt.clone(), "sum")
     mx = _coll(dist, args, torch, tt.clone(), "max")
     diag = group_diag(group, world, stages, ("pack", "exchange", "merge"))
+    roof = c4_stage_roofline(diag, n, name_bytes, float(np.mean(sent[warm:])) if sent else None,
+                             float(np.mean(merged[warm:])), world)
     if group is not None:
         group.close()
     repo.close()
@@ -933,6 +1095,7 @@ def run_c4_leg(args, torch, dist, dev, local, rank, world):
         "rehearsal": rehearsal,
         "setup_s": t_setup,
         **diag,
+        **roof,
         "verified": verified,
         "verify": {"sampled_buckets": S, "found_exactly_once": found_once, "mismatched": bad,
                    "reference": "independent per-id max-reduce of every rank's messages over all "
@@ -1037,7 +1200,31 @@ def run_ae_leg(args, torch, dist, dev, local, rank, world):
     # local max reads R*24 + writes 24, the apply reads 24 + R*24 per bucket
     bpo = 24.0 if world == 1 else (2 * R + 2) * 24 / R
     step_s = el / steps
+    roof = {}
+    sb = diag.get("stage_busy_ms")
+    if sb:
+        # the local join's bytes per round (world 1: the fused k_ae_join reads
+        # every replica's 24 B once; N > 1: k_ae_local_max reads R x 24 and
+        # writes 24 per bucket, k_ae_apply reads 24 + R x 24) against its busy
+        # time, and the all-reduce's bus bandwidth (ring: 2 (N-1)/N of the
+        # [3, B] int64 join per GPU) against xGMI
+        join_ms = sb.get("local_join", 0.0) + (sb.get("apply", 0.0) if world > 1 else 0.0)
+        roof["stage_roofline"] = {}
+        if join_ms:
+            gbs = bpo * R * B / (join_ms / 1e3) / 1e9
+            roof["stage_roofline"]["local_join"] = {"bound": "hbm", "achieved_GBps": gbs,
+                                                    "peak_GBps": HBM_PEAK_GBS,
+                                                    "frac": gbs / HBM_PEAK_GBS,
+                                                    "bytes_per_round": bpo * R * B}
+        ar_ms = sb.get("allreduce", 0.0)
+        if world > 1 and ar_ms:
+            alg = 3 * 8 * B / (ar_ms / 1e3) / 1e9
+            bus = alg * 2 * (world - 1) / world
+            roof["stage_roofline"]["allreduce"] = {"bound": "xgmi", "algbw_GBps": alg,
+                                                   "busbw_GBps": bus, "peak_GBps": XGMI_GBPS,
+                                                   "frac": bus / XGMI_GBPS}
     return {
+        **roof,
         "metric": "anti-entropy replica-bucket joins/sec (C5: all-reduce(max) over xGMI)",
         "value": world * R * B * steps / el, "unit": "joins/s", "scaling": "weak",
         "n_gpus": world, "steps": steps, "warmup": warm, "ms_per_step": step_s * 1e3,
@@ -1159,7 +1346,8 @@ def main():
     # One stream for torch's input generation and the engine's kernels, so
     # device-pointer calls see torch's results without extra synchronisation.
     torch.cuda.set_stream(torch.cuda.Stream(dev))
-    repo = patrol_amd.GPURepo(device=local, log2_slots=args.log2_slots, arena_bytes=1 << 20)
+    repo = patrol_amd.GPURepo(device=local, log2_slots=args.log2_slots, arena_bytes=1 << 20,
+                              split=args.split)
     repo.use_torch_stream()
     keys = torch.arange(base, base + K, dtype=torch.int64, device=dev)
     kb, ko = names_for_ids(torch, keys, args.name_len if args.workload == "c2" else 0)
@@ -1190,8 +1378,11 @@ def main():
         ids = zipf_ids(torch, gen, n, K, args.zipf, dev)
         blob, offs = names_for_ids(torch, ids + base, args.name_len)
         batches = [replica_states(torch, gen, n, j, dev) for j in range(args.warmup + args.steps)]
-        # the per-message status column a Receive caller reads (merge vs incast)
-        c2_status = None if args.no_status else torch.empty(n, dtype=torch.uint8, device=dev)
+        # the per-message status column a Receive caller reads (merge vs incast);
+        # two, alternating: a queued batch's outputs stay untouched until the
+        # next call finishes it (PHIP_RECV_ASYNC), so batch j+1 writes the other
+        c2_status = [None, None] if args.no_status else \
+            [torch.empty(n, dtype=torch.uint8, device=dev) for _ in range(2)]
         if args.insert:
             # SURVEY C2's insert-on-miss variant: every step names a fresh
             # key range (same Zipf shape), so each step creates the buckets it
@@ -1253,10 +1444,15 @@ def main():
                 repo.receive_soa(fb, a, t, e, T0 + j, name_offs=fo, n=n, device=True)
                 n_new.append(len(repo) - before)
         else:
+            # names_len = 0: this caller produced the batch and holds it until
+            # the call that finishes it returns, so the device does not check
+            # its offsets (the binding's default checks them: ~0.1 ms per
+            # 100M messages, patrolhip.h phip_msgs.names_len)
             def step(j):
                 a, t, e = batches[j]
-                repo.receive_soa(blob, a, t, e, T0 + j, name_offs=offs, n=n, status=c2_status,
-                                 device=True, queue=not args.sync_receive)
+                repo.receive_soa(blob, a, t, e, T0 + j, name_offs=offs, n=n, status=c2_status[j % 2],
+                                 device=True, queue=not args.sync_receive,
+                                 names_len=0 if not args.check_names else None)
 
     extra = {}
     for j in range(args.warmup):
@@ -1442,6 +1638,8 @@ def main():
         if args.workload == "c2":
             del batches, blob, offs, ids
         legs = [("owner_routed", run_routed)]
+        if not args.no_variants:
+            legs.append(("c2_variants", run_c2_variants_leg))
         if not args.no_c3:
             legs.append(("c3", run_c3_leg))
         if not args.no_c4:

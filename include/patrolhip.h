@@ -128,6 +128,10 @@ enum {
                                    multi-launch path (by default they run as one launch) */
 #define PHIP_CFG_FIXED_SEED 0x4u /* place buckets with hash_seed as given (0: the unseeded
                                     placement) instead of a random per-handle seed */
+#define PHIP_CFG_SPLIT_SMALL 0x8u /* (testing) the ordered path's hot split from
+                                     2^16 ops and for every sampled name, not only from 2^22
+                                     ops for the hottest buckets */
+#define PHIP_CFG_NO_SPLIT 0x10u   /* (testing, A/B) no hot split: every op through the sort */
 
 typedef struct phip_config {
   int32_t device;        /* HIP device ordinal                                          */
@@ -176,10 +180,28 @@ typedef struct phip_state {
  * Decoded replica states (the fields UnmarshalBinary fills, bucket.go:78-87).
  * Name i is names[name_offs[i] .. name_offs[i+1]).  With PHIP_DEVICE_PTRS the
  * names blob must stay readable 8 bytes past name_offs[n].
+ *
+ * names_len (the field was `reserved` before; same layout): the names blob's
+ * length in bytes, or 0.  Host batches are checked on the host either way.
+ * A device batch with names_len != 0 is checked on the device: every entry
+ * must have name_offs[i] <= name_offs[i+1] <= names_len and at most
+ * PHIP_MAX_NAME_LEN bytes.  No kernel then reads the blob at a malformed
+ * entry's offsets, and the call returns PHIP_ERR_INVALID:
+ *   - phip_receive_soa: the batch stops at the first malformed message k, as
+ *     the Go loop stops at a short datagram (repo.go:70-74): messages before
+ *     k are received as usual, k gets PHIP_ST_SHORT and every later one
+ *     PHIP_ST_NOT_PROCESSED (a queued batch reports it from the call that
+ *     finishes it);
+ *   - phip_upsert_soa / phip_apply_mixed (phip_ops.names_len): nothing of the
+ *     batch is applied.
+ * With names_len == 0 a device batch's offsets are trusted: a wild offset is
+ * a read of device memory the kernels do not own.  A queued batch's input
+ * columns must stay untouched until it is finished (PHIP_RECV_ASYNC): a
+ * column reused early reads as corrupted offsets.
  */
 typedef struct phip_msgs {
   uint32_t n;
-  uint32_t reserved;
+  uint32_t names_len;
   const uint8_t* names;
   const uint32_t* name_offs; /* n+1 entries */
   const uint64_t* added;     /* float64 bits */
@@ -190,7 +212,7 @@ typedef struct phip_msgs {
 /* A mixed ordered stream (one entry per op, applied in index order). */
 typedef struct phip_ops {
   uint32_t n;
-  uint32_t reserved;
+  uint32_t names_len;        /* the names blob's length, or 0 (see phip_msgs)   */
   const uint8_t* kind;       /* PHIP_OP_*                                       */
   const uint8_t* names;
   const uint32_t* name_offs; /* n+1 entries                                     */

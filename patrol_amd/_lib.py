@@ -43,6 +43,8 @@ DEVICE_PTRS = 0x1
 CFG_NO_GROW = 0x1
 CFG_NO_SMALL = 0x2
 CFG_FIXED_SEED = 0x4
+CFG_SPLIT_SMALL = 0x8   # (testing) the ordered path's hot split from 2^16 ops, every sampled name
+CFG_NO_SPLIT = 0x10     # (testing, A/B) no hot split
 ROUTE_COMBINE = 0x2
 GROUP_RCCL_SELF = 0x4
 GROUP_SMALL_CHUNKS = 0x8
@@ -63,13 +65,14 @@ class phip_state(C.Structure):
 
 
 class phip_msgs(C.Structure):
-    _fields_ = [("n", C.c_uint32), ("reserved", C.c_uint32), ("names", C.c_void_p),
+    # names_len: the names blob's byte length, 0 = unchecked (patrolhip.h)
+    _fields_ = [("n", C.c_uint32), ("names_len", C.c_uint32), ("names", C.c_void_p),
                 ("name_offs", C.c_void_p), ("added", C.c_void_p), ("taken", C.c_void_p),
                 ("elapsed", C.c_void_p)]
 
 
 class phip_ops(C.Structure):
-    _fields_ = [("n", C.c_uint32), ("reserved", C.c_uint32), ("kind", C.c_void_p),
+    _fields_ = [("n", C.c_uint32), ("names_len", C.c_uint32), ("kind", C.c_void_p),
                 ("names", C.c_void_p), ("name_offs", C.c_void_p), ("now", C.c_void_p),
                 ("freq", C.c_void_p), ("per", C.c_void_p), ("count", C.c_void_p),
                 ("added", C.c_void_p), ("taken", C.c_void_p), ("elapsed", C.c_void_p)]

@@ -30,15 +30,29 @@ __device__ inline u64 load_be64(const u8* p) {
 }
 
 // ---------------------------------------------------------- name sources --
-// Decoded messages: names[offs[i] .. offs[i+1]).
+// Decoded messages: names[offs[i] .. offs[i+1]).  lim: the blob's byte
+// length as the caller gave it (phip_msgs / phip_ops names_len), 0 when the
+// caller did not (unchecked).  With lim, an entry that is not
+// offs[i] <= offs[i+1] <= lim with at most PHIP_MAX_NAME_LEN bytes reads as
+// the empty name at offset 0 (get() returns true): no kernel reads the blob
+// at a wild offset, and the passes that check (k_classify_soa2,
+// k_resolve_batch) report the entry, so the call returns PHIP_ERR_INVALID
+// (bucket.go:71-91: malformed input is an error, not a crash).
 struct NamesOffs {
   const u8* blob;
   const u32* offs;
+  u32 lim = 0;
+  __device__ inline bool bad(u32 a, u32 b) const {
+    return lim != 0 && (b < a || b - a > PHIP_MAX_NAME_LEN || b > lim);
+  }
   template <bool NT = false>
-  __device__ inline void get(u32 i, u64& off, u32& len) const {
+  __device__ inline bool get(u32 i, u64& off, u32& len) const {
     u32 a = ld<NT>(offs + i), b = ld<NT>(offs + i + 1);
+    const bool x = bad(a, b);
+    if (x) a = b = 0;
     off = a;
     len = b - a;
+    return x;
   }
 };
 // Raw datagrams after decode: name at (off[i], len[i]) inside the datagram blob.
@@ -47,9 +61,10 @@ struct NamesPairs {
   const uint64_t* off;
   const u8* len;
   template <bool NT = false>
-  __device__ inline void get(u32 i, u64& o, u32& l) const {
+  __device__ inline bool get(u32 i, u64& o, u32& l) const {
     o = ld<NT>(off + i);
     l = ld<NT>(len + i);
+    return false;
   }
 };
 
@@ -60,12 +75,13 @@ struct Datagrams {
   const u8* blob;
   const uint64_t* offs;
   template <bool NT = false>
-  __device__ inline void get(u32 i, u64& o, u32& l) const {
+  __device__ inline bool get(u32 i, u64& o, u32& l) const {
     const u64 a = ld<NT>(offs + i), b = ld<NT>(offs + i + 1);
     o = a + 25;
     const u64 room = b > o ? b - o : 0;
     const u32 want = b >= a + 25 ? blob[a + 24] : 0;
     l = want < room ? want : (u32)room;
+    return false;
   }
 };
 
@@ -320,11 +336,26 @@ __device__ inline Rec load_rec(const Rec* p) {
 
 // The first 48 bytes only (tag, state, name words 0-1); name2 and created
 // are left 0.  Enough to find and merge a name of <= kShortName bytes.
+#ifndef PHIP_REC48_X2
+#define PHIP_REC48_X2 0
+#endif
 __device__ inline Rec load_rec48(const Rec* p) {
-  const uint4* q = reinterpret_cast<const uint4*>(p);
   // (plain loads: the kernel lives on L2 / Infinity Cache retention of warm
-  // records; non-temporal record loads made it 65% slower)
+  // records; non-temporal record loads made it 65% slower, DESIGN.md §4:
+  // an nt load does not allocate, so the three loads of a record fetch its
+  // 128-byte line ~2 times, tools/ubench_req)
+#if PHIP_REC48_X2
+  // six 8-byte loads (tools/ubench_req: random 48-byte records 2.27 ms per
+  // 100M as dwordx2, 3.30 as dwordx4, the same one 128-byte request each)
+  const u64* w = reinterpret_cast<const u64*>(p);
+  const u64 w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3], w4 = w[4], w5 = w[5];
+  const uint4 a{(u32)w0, (u32)(w0 >> 32), (u32)w1, (u32)(w1 >> 32)};
+  const uint4 b{(u32)w2, (u32)(w2 >> 32), (u32)w3, (u32)(w3 >> 32)};
+  const uint4 c{(u32)w4, (u32)(w4 >> 32), (u32)w5, (u32)(w5 >> 32)};
+#else
+  const uint4* q = reinterpret_cast<const uint4*>(p);
   uint4 a = q[0], b = q[1], c = q[2];
+#endif
   Rec r;
   r.tag = ((u64)a.y << 32) | a.x;
   r.added = ((u64)a.w << 32) | a.z;
@@ -365,13 +396,15 @@ __device__ inline int probe(const Table& T, const Name& nm, const u8* src, u32* 
 // handles.  The fast path applies the clean prefix before it (merges commute),
 // the ordered path the rest.
 constexpr u32 kCtrDirty = 12;
+constexpr u32 kCtrBadName = 1;   // an ordered batch's malformed name entry (k_resolve_batch)
 
 // Min-reduce the index of a wave's first dirty lane (lanes hold increasing
 // indices, so the lowest set lane has the lowest index).
-__device__ inline void note_dirty(bool d, u32 i, u32* ctr) {
+__device__ inline void note_min(bool d, u32 i, u32* word) {
   const u64 m = __ballot(d);
-  if (m && __lane_id() == (u32)(__ffsll((long long)m) - 1)) atomicMin(&ctr[kCtrDirty], i);
+  if (m && __lane_id() == (u32)(__ffsll((long long)m) - 1)) atomicMin(word, i);
 }
+__device__ inline void note_dirty(bool d, u32 i, u32* ctr) { note_min(d, i, &ctr[kCtrDirty]); }
 
 __device__ inline bool replica_dirty(u64 ab, u64 tb, i64 e) {
   const bool inc = is_zero_bits(ab) && is_zero_bits(tb) && e == 0;
@@ -592,7 +625,7 @@ __global__ void k_hot_hist(const u32* __restrict__ ccnt, u32* __restrict__ hist)
 // One workgroup of 256: the lowest threshold t >= kHotMinCount with at most
 // maxn sampled slots counted t or more times (maxn: the directory's size).
 __global__ __launch_bounds__(256) void k_hot_select(const u32* __restrict__ hist, HotHdr* hdr,
-                                                    u32 maxn) {
+                                                    u32 maxn, u32 minc = kHotMinCount) {
   constexpr u32 kPer = kHotHist / 256;
   __shared__ u32 part[256];
   __shared__ u32 best;
@@ -613,7 +646,7 @@ __global__ __launch_bounds__(256) void k_hot_select(const u32* __restrict__ hist
   __syncthreads();
   if (t == 0) {
     hdr->n = 0;
-    hdr->thresh = best > kHotMinCount ? best : kHotMinCount;
+    hdr->thresh = best > minc ? best : minc;
   }
 }
 
@@ -713,8 +746,16 @@ struct SoaIn {   // decoded messages (phip_receive_soa / decoded datagrams)
     load_words3<false>(src.blob, off, len, w0, w1, w2);
   }
   // Classification (elapsed matters only when both floats are zero, so it is
-  // read only then: a third of the pass's bytes on a clean batch).
+  // read only then: a third of the pass's bytes on a clean batch).  A
+  // malformed name entry (NamesOffs::bad, checked names only) min-reduces its
+  // index into ctr[5], as a short datagram does: the batch stops there.
   __device__ inline bool dirty(u32 i, u32* ctr) const {
+    if constexpr (kOffs) {
+      if (src.lim && src.bad(src.offs[i], src.offs[i + 1])) {
+        atomicMin(&ctr[5], i);
+        return false;
+      }
+    }
     const u64 ab = __builtin_nontemporal_load(ma + i), tb = __builtin_nontemporal_load(mt + i);
     if (is_zero_bits(ab) && is_zero_bits(tb)) return me[i] == 0 || ab == kSign || tb == kSign;
     return ab == kSign || tb == kSign;
@@ -801,12 +842,27 @@ __global__ __launch_bounds__(kBlock) void k_classify(In in, u32 n, u32* ctr) {
 // still holds the lowest dirty index.  With `status`, the pass also fills the
 // status column with PHIP_ST_MERGED (2 bytes per lane), which the fast kernel
 // relies on: it writes no status for the messages it merges.
+// With names.lim (a caller-given blob length), the pass also checks the name
+// offsets (two more 4-byte loads per lane) and min-reduces the first
+// malformed entry into ctr[5]: the fast kernel stops there (its gate), and so
+// does the batch (PHIP_ERR_INVALID).  Unchecked batches read no offsets (the
+// check costs the C2 step ~0.1 ms per 100M messages: a 0.4 GB stream).
 typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
 __global__ __launch_bounds__(kBlock) void k_classify_soa2(const uint64_t* __restrict__ ma,
                                                           const uint64_t* __restrict__ mt,
                                                           const int64_t* __restrict__ me, u32 n,
-                                                          u32* ctr, u8* status) {
+                                                          u32* ctr, u8* status, NamesOffs names) {
   const u32 i0 = 2 * (blockIdx.x * kBlock + threadIdx.x);
+  if (names.lim) {   // (uniform)
+    bool b0 = false, b1 = false;
+    if (i0 < n) {
+      const u32 o0 = names.offs[i0], o1 = names.offs[i0 + 1];
+      const u32 o2 = i0 + 1 < n ? names.offs[i0 + 2] : o1;
+      b0 = names.bad(o0, o1);
+      b1 = i0 + 1 < n && names.bad(o1, o2);
+    }
+    note_min(b0 || b1, b0 ? i0 : i0 + 1, &ctr[5]);
+  }
   if (status) {   // every status starts as merged (the fast pass writes none)
     if (i0 + 1 < n && ((uintptr_t)status & 1) == 0)
       *reinterpret_cast<u16*>(status + i0) = (u16)(PHIP_ST_MERGED | (PHIP_ST_MERGED << 8));
@@ -1198,8 +1254,13 @@ __global__ __launch_bounds__(kBlock) void k_resolve_batch(Src src, u32 n, Table 
   const u32 i0 = blockIdx.x * (kBlock * kResPer) + threadIdx.x;
   u64 off[kResPer], w0[kResPer], w1[kResPer], w2[kResPer];
   u32 len[kResPer];
+  bool bad = false;
 #pragma unroll
-  for (u32 k = 0; k < kResPer; ++k) src.get(min(i0 + k * kBlock, n - 1), off[k], len[k]);
+  for (u32 k = 0; k < kResPer; ++k) bad |= src.get(min(i0 + k * kBlock, n - 1), off[k], len[k]);
+  // a malformed name entry (checked names only): the batch is refused before
+  // anything is created (check_flags)
+  const u64 bm = __ballot(bad);
+  if (bm && __lane_id() == (u32)(__ffsll((long long)bm) - 1)) atomicOr(&ctr[kCtrBadName], 1u);
 #pragma unroll
   for (u32 k = 0; k < kResPer; ++k) load_words3<false>(src.blob, off[k], len[k], w0[k], w1[k], w2[k]);
   Name nm[kResPer];
@@ -2102,11 +2163,15 @@ __device__ inline void huge_scan(const u32* __restrict__ huge_list, u32 nhuge,
 // (the rest keep their order): the largest segments' folds are the step's
 // longest sequential chains, so they get their own stream and start first
 // (one block; out must not alias huge_list).
+// (nd: the list's length on the device, capped by nhuge; the hot split's)
 __global__ __launch_bounds__(1024) void k_huge_order(const u32* __restrict__ huge_list, u32 nhuge,
                                                      const u32* __restrict__ seg_count, u32 nfirst,
-                                                     u32* __restrict__ out) {
+                                                     u32* __restrict__ out,
+                                                     const u32* __restrict__ nd = nullptr) {
   __shared__ u64 part[1024];
   __shared__ u32 sel[kHugeFirstMax];
+  if (nd) nhuge = min(*nd, nhuge);
+  nfirst = min(nfirst, nhuge);
   const u32 tid = threadIdx.x;
   for (u32 r = 0; r < nfirst; ++r) {
     u64 best = 0;   // (count, ~index): the largest count, then the lowest index
@@ -2169,17 +2234,22 @@ __device__ inline bool huge_window(const u64* __restrict__ woff, u32 nhuge, u32 
 // folding a hot bucket streams its input instead of chasing one random
 // record per op (a single CU cannot keep enough random misses in flight).
 // The same pass writes the window's summary (WinSum).
+// kStaged (the hot split, k_opart_scatter): the segments' ops are already
+// contiguous in hop / hval; only the summaries are written.
 constexpr u32 kGatherPer = kFoldWin / kBlock;
 
+template <bool kStaged>
 __global__ __launch_bounds__(kBlock) void k_gather_huge(
     const u32* __restrict__ huge_list, u32 nhuge, const u64* __restrict__ hoff,
     const u64* __restrict__ woff, const u32* __restrict__ seg_start,
     const u32* __restrict__ seg_count, const u32* __restrict__ sval,
     const OpRec* __restrict__ ops, OpRec* __restrict__ hop, u32* __restrict__ hval,
-    WinSum* __restrict__ sums, u32 h_begin) {
+    WinSum* __restrict__ sums, u32 h_begin, const u32* __restrict__ nd = nullptr) {
   __shared__ u64 red[6][kBlock / 64];
   __shared__ u32 s_first;
   __shared__ u64 s_par[3];
+  if (nd) nhuge = min(*nd, nhuge);   // (the list's length on the device, capped)
+  if (h_begin >= nhuge) return;
   // segments [h_begin, nhuge) of the list: their windows follow
   // woff[h_begin]; a grid of a few blocks per CU walks them
   const u32 b_end = (u32)woff[nhuge];
@@ -2187,17 +2257,27 @@ __global__ __launch_bounds__(kBlock) void k_gather_huge(
   u32 h, w;
   huge_window(woff, nhuge, b, h, w);
   const u32 g = huge_list[h];
-  const u32 st = seg_start[g], cnt = seg_count[g];
+  const u32 cnt = seg_count[g];
   const u64 dst = hoff[h];
   const u32 tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const u32 p0 = w * kFoldWin, p1 = min(cnt, p0 + kFoldWin);
   if (tid == 0) s_first = 0xFFFFFFFFu;
   u32 v[kGatherPer];
   OpRec r[kGatherPer];
+  if constexpr (kStaged) {
 #pragma unroll
-  for (u32 k = 0; k < kGatherPer; ++k) v[k] = sval[st + min(p0 + k * kBlock + tid, p1 - 1)];
+    for (u32 k = 0; k < kGatherPer; ++k) {
+      const u64 j = dst + min(p0 + k * kBlock + tid, p1 - 1);
+      v[k] = hval[j];
+      r[k] = load_oprec(hop + j);
+    }
+  } else {
+    const u32 st = seg_start[g];
 #pragma unroll
-  for (u32 k = 0; k < kGatherPer; ++k) r[k] = load_oprec(ops + (v[k] & kOpIdxMask));
+    for (u32 k = 0; k < kGatherPer; ++k) v[k] = sval[st + min(p0 + k * kBlock + tid, p1 - 1)];
+#pragma unroll
+    for (u32 k = 0; k < kGatherPer; ++k) r[k] = load_oprec(ops + (v[k] & kOpIdxMask));
+  }
   u64 ea = 0, et = 0, ee = 0, nmin = ~0ull, nmax = 0;
   u32 first_take = 0xFFFFFFFFu;
   bool merge = false, dirty = false;
@@ -2205,10 +2285,12 @@ __global__ __launch_bounds__(kBlock) void k_gather_huge(
   for (u32 k = 0; k < kGatherPer; ++k) {
     const u32 j = p0 + k * kBlock + tid;
     if (j >= p1) continue;
-    ulonglong2* q = reinterpret_cast<ulonglong2*>(hop + dst + j);
-    q[0] = ulonglong2{(u64)r[k].now, r[k].x};
-    q[1] = ulonglong2{r[k].y, r[k].z};
-    hval[dst + j] = v[k];
+    if constexpr (!kStaged) {
+      ulonglong2* q = reinterpret_cast<ulonglong2*>(hop + dst + j);
+      q[0] = ulonglong2{(u64)r[k].now, r[k].x};
+      q[1] = ulonglong2{r[k].y, r[k].z};
+      hval[dst + j] = v[k];
+    }
     const u32 kind = v[k] >> kOpIdxBits;
     if (kind == PHIP_OP_TAKE) {
       const u64 nb = (u64)r[k].now ^ kSign;
@@ -2713,8 +2795,10 @@ __global__ __launch_bounds__(kFoldThreads) void k_fold_block(
     u32* __restrict__ run_pos, RunState* __restrict__ run_st, u32* __restrict__ run_n,
     u8* __restrict__ seg_existed, u32* __restrict__ seg_exact_from,
     const u64* __restrict__ woff, const WinSum* __restrict__ sums, u32* __restrict__ win_run,
-    GMax* __restrict__ win_g, u64* __restrict__ dbg, u32 h_begin) {
+    GMax* __restrict__ win_g, u64* __restrict__ dbg, u32 h_begin,
+    const u32* __restrict__ nd = nullptr) {
   __shared__ FoldShared sh;
+  if (nd) nhuge = min(*nd, nhuge);   // (the list's length on the device, capped)
   const u32 hs = h_begin + blockIdx.x;   // segments [h_begin, nhuge) of the list
   if (hs >= nhuge) return;
   // A hot segment's fold is one sequential chain of dependent rounds beside
@@ -2871,8 +2955,10 @@ __global__ __launch_bounds__(kBlock) void k_huge_outputs(
     const u32* __restrict__ run_pos, const RunState* __restrict__ run_st,
     const u32* __restrict__ run_n, const u8* __restrict__ seg_existed,
     const u32* __restrict__ seg_exact_from, const u32* __restrict__ win_run,
-    const GMax* __restrict__ win_g, OutView ow, u32 h_begin) {
+    const GMax* __restrict__ win_g, OutView ow, u32 h_begin, const u32* __restrict__ nd = nullptr) {
   __shared__ GMax wtot[kBlock / 64];
+  if (nd) nhuge = min(*nd, nhuge);   // (the list's length on the device, capped)
+  if (h_begin >= nhuge) return;
   // segments [h_begin, nhuge) of the list: their windows follow
   // woff[h_begin]; a grid of a few blocks per CU walks them
   const u32 b_end = (u32)woff[nhuge];
@@ -3057,10 +3143,13 @@ __device__ inline void seg_flush(u32* lst, u32& cnt, u32* gcnt, u32* out, u32* b
   __syncthreads();
 }
 
+// huge_min: segments longer than this are listed huge, shorter ones over
+// kLongSeg long (kHugeSeg; the hot split passes ~0: its hot segments are
+// partitioned before the sort, and a rare long cold one is a wave fold).
 __global__ __launch_bounds__(256) void k_seg_finish(const u32* __restrict__ tile_base, u32 ntiles,
                                                     const u32* __restrict__ sstart, u32 n,
                                                     u32* __restrict__ scnt, u32* __restrict__ lng,
-                                                    u32* __restrict__ huge, u32* ctr) {
+                                                    u32* __restrict__ huge, u32* ctr, u32 huge_min) {
   __shared__ u32 llist[kSegListCap], hlist[kSegListCap];
   __shared__ u32 lcnt, hcnt, base_sh;
   const u32 nseg = tile_base[ntiles];
@@ -3076,7 +3165,7 @@ __global__ __launch_bounds__(256) void k_seg_finish(const u32* __restrict__ tile
       c = (j + 1 < nseg ? sstart[j + 1] : n) - sstart[j];
       scnt[j] = c;
     }
-    const bool lo = c > kLongSeg && c <= kHugeSeg, hu = c > kHugeSeg;
+    const bool lo = c > kLongSeg && c <= huge_min, hu = c > huge_min;
     if (lo) llist[atomicAdd(&lcnt, 1u)] = j;
     if (hu) hlist[atomicAdd(&hcnt, 1u)] = j;
     __syncthreads();
@@ -3981,6 +4070,359 @@ __global__ void k_get_one(const u8* name, u32 len, Table T, Rec* out, int* found
   int pr = probe(T, nm, name, &s, &r);
   *found = pr == kFound;
   if (pr == kFound) *out = load_rec(&T.recs[s]);   // probe's copy may be the 48-byte view
+}
+
+// ------------------------------------------------- ordered: the hot split --
+// A large ordered batch (C3) is Zipf-skewed: in C3 the ~110 hottest of 10M
+// buckets carry half of the 50M ops, each over kHugeSeg of them.  Sorting
+// those ops by (slot, seq) and then copying each hot segment out of the
+// stream-order op records (k_gather_huge: a random 32-B record per op, a
+// 128-B line fetched for each) moved ~7 GB per step.  Instead the hot
+// names are found by name before the sort, in a sample (k_route_sample, the
+// owner pack's directory), and a stable partition of the batch in stream
+// order writes every hot op's record once, straight into its bucket's
+// contiguous run (k_opart_count -> k_opart_scan -> k_opart_scatter), beside
+// the resolve.  The radix sort then orders only the cold ops (their records
+// stay at their op index, as k_pack_ops wrote them), and the hot buckets'
+// block folds start as soon as the partition and their window summaries
+// are done.  Per-bucket order: a stable partition keeps every hot bucket's
+// ops in stream (seq) order, and a name is hot or cold as a whole (exact
+// name match on the canonical words of names of <= kShortName bytes;
+// longer names are always cold), so no bucket has ops on both sides.
+// (bucket.go:186-263 per op, repo.go:189-211 for create-on-miss, which the
+// resolve does for every op as before.)
+constexpr u32 kOpTile = 2048;                 // ops per partition tile (one workgroup)
+constexpr u32 kOpCold = kRouteHotMax;         // the code of an op that is not hot
+constexpr u32 kOpCodes = kRouteHotMax + 1;    // hot entries 0..kRouteHotMax-1, then cold
+constexpr u32 kOpBlock = kRouteBlock;         // (the scan kernels' workgroup)
+constexpr u32 kOpScanTiles = 64;              // tiles per block of the column scan
+
+struct OpartHdr {   // device totals of the partition (the host reads it back)
+  u32 nhot;         // directory entries used
+  u32 hot_total;    // ops in hot segments (= the cold list's offset)
+  u32 ncold;
+  u32 pad;
+};
+
+// Pass 1: every op's code (hot entry or kOpCold) and the per-(tile, code)
+// counts, tile-major rows of kOpCodes.  A workgroup takes a tile, every
+// thread kOpPer ops of it (k_pack_ops' shape: all their loads in flight
+// together; a wave walking a tile chunk by chunk kept one chunk in flight
+// and took 1.4 ms).  A chunk's counts: the wave splits its lanes by code
+// (code_groups: one ballot a distinct code, no memory access in the loop)
+// and each code's leader lane adds its count in LDS.
+constexpr u32 kOpThreads = 512;
+constexpr u32 kOpPer = kOpTile / kOpThreads;   // ops per thread (op i0 + k * kOpThreads)
+static_assert(kOpPer * kOpThreads == kOpTile, "partition tile");
+
+__device__ inline void code_groups(bool valid, u32 c, u32 lane, u32& lead, u32& rank, u32& cnt) {
+  const u64 lt = (1ull << lane) - 1;
+  lead = lane;
+  rank = 0;
+  cnt = 0;
+  u64 act = __ballot(valid);
+  while (act) {   // (wave-uniform)
+    const u32 l0 = (u32)__ffsll((long long)act) - 1;
+    const u32 c0 = (u32)__builtin_amdgcn_readlane((int)c, (int)l0);
+    const u64 m = __ballot(valid && c == c0);
+    if (valid && c == c0) {
+      lead = l0;
+      rank = (u32)__popcll(m & lt);
+    }
+    if (lane == l0) cnt = (u32)__popcll(m);
+    act &= ~m;
+  }
+}
+
+// route_lds_load for a workgroup of kOpThreads
+__device__ inline void opart_lds_load(RouteLds& L, const RouteHot* dir, u32 nh) {
+  for (u32 j = threadIdx.x; j < kRouteLds; j += kOpThreads) L.slot[j] = 0;
+  __syncthreads();
+  for (u32 j = threadIdx.x; j < nh; j += kOpThreads) {
+    const RouteHot d = dir[j];
+    L.h[j] = d.h; L.w0[j] = d.w0; L.w1[j] = d.w1; L.owner[j] = d.owner;
+    const u32 v = (u32)(d.h >> 48) << 16 | (j + 1);
+    u32 hs = route_home(d.h);
+    while (atomicCAS(&L.slot[hs], 0u, v) != 0) hs = (hs + 1) & (kRouteLds - 1);
+  }
+}
+
+template <class Src>
+__global__ __launch_bounds__(kOpThreads) void k_opart_count(Src src, u32 n, u32 ntile,
+                                                           const HotHdr* __restrict__ hot,
+                                                           const RouteHot* __restrict__ dir,
+                                                           u16* __restrict__ code,
+                                                           u32* __restrict__ cnt) {
+  __shared__ RouteLds L;
+  __shared__ u32 tcnt[kOpCodes];
+  const u32 nh = hot ? min(hot->n, kRouteHotMax) : 0u;
+  for (u32 j = threadIdx.x; j < kOpCodes; j += kOpThreads) tcnt[j] = 0;
+  opart_lds_load(L, dir, nh);
+  __syncthreads();
+  const u32 lane = threadIdx.x & 63;
+  const u32 tile = blockIdx.x;
+  const u64 t0 = (u64)tile * kOpTile, t1 = min((u64)n, t0 + kOpTile);
+  u64 off[kOpPer], w0[kOpPer], w1[kOpPer], w2[kOpPer];
+  u32 len[kOpPer];
+#pragma unroll
+  for (u32 k = 0; k < kOpPer; ++k)
+    src.template get<true>((u32)min(t0 + k * kOpThreads + threadIdx.x, t1 - 1), off[k], len[k]);
+#pragma unroll
+  for (u32 k = 0; k < kOpPer; ++k) {
+    w0[k] = w1[k] = w2[k] = 0;
+    if (nh && len[k] <= kShortName) load_words3<true>(src.blob, off[k], len[k], w0[k], w1[k], w2[k]);
+  }
+#pragma unroll
+  for (u32 k = 0; k < kOpPer; ++k) {
+    const u64 i = t0 + k * kOpThreads + threadIdx.x;
+    const bool valid = i < t1;
+    u32 c = kOpCold;
+    if (nh && len[k] <= kShortName) {
+      Name nm;
+      short_name(w0[k], w1[k], w2[k], off[k], len[k], nm);
+      const int e = route_hot_find(L, nm);
+      if (e >= 0) c = (u32)e;
+    }
+    if (valid) code[i] = (u16)c;
+    u32 lead, rank, m;
+    code_groups(valid, c, lane, lead, rank, m);
+    if (m) atomicAdd(&tcnt[c], m);   // (leaders; other waves may add to the same code)
+  }
+  __syncthreads();
+  for (u32 c = threadIdx.x; c < kOpCodes; c += kOpThreads) cnt[(u64)tile * kOpCodes + c] = tcnt[c];
+}
+
+// Pass 2 (three kernels): the exclusive prefix of the counts in code-major
+// order (all tiles of code 0, then code 1, ...), written back in place over
+// the tile-major rows: base(t, c) = sum_{c' < c} total(c') + sum_{t' < t}
+// cnt(t', c).  a) column sums per block of kOpScanTiles tiles; b) one block
+// scans them per code and the code totals; c) every block rewrites its rows.
+__global__ __launch_bounds__(kOpBlock) void k_opart_colsum(const u32* __restrict__ cnt, u32 ntile,
+                                                          u32* __restrict__ part) {
+  const u32 t0 = blockIdx.x * kOpScanTiles, t1 = min(ntile, t0 + kOpScanTiles);
+  for (u32 c = threadIdx.x; c < kOpCodes; c += kOpBlock) {
+    u32 s = 0;
+#pragma unroll 16
+    for (u32 t = t0; t < t1; ++t) s += cnt[(u64)t * kOpCodes + c];
+    part[(u64)blockIdx.x * kOpCodes + c] = s;
+  }
+}
+
+__global__ __launch_bounds__(1024) void k_opart_colscan(u32* __restrict__ part, u32 nblk,
+                                                       u32* __restrict__ ebase,
+                                                       u32* __restrict__ etotal,
+                                                       const HotHdr* __restrict__ hot,
+                                                       OpartHdr* __restrict__ out) {
+  __shared__ u32 tot[1024];
+  const u32 c = threadIdx.x;
+  u32 run = 0;
+  if (c < kOpCodes) {
+    // 16 blocks' values at a time: the loads of a group issue together (a
+    // store between two loads would make the second wait for it)
+    for (u32 b0 = 0; b0 < nblk; b0 += 16) {
+      u32 v[16];
+#pragma unroll
+      for (u32 k = 0; k < 16; ++k) v[k] = b0 + k < nblk ? part[(u64)(b0 + k) * kOpCodes + c] : 0u;
+#pragma unroll
+      for (u32 k = 0; k < 16; ++k) {
+        const u32 x = v[k];
+        v[k] = run;
+        run += x;
+      }
+#pragma unroll
+      for (u32 k = 0; k < 16; ++k)
+        if (b0 + k < nblk) part[(u64)(b0 + k) * kOpCodes + c] = v[k];
+    }
+  }
+  tot[c] = c < kOpCodes ? run : 0u;
+  __syncthreads();
+  for (u32 d = 1; d < 1024; d <<= 1) {   // inclusive scan of the code totals
+    const u32 v = c >= d ? tot[c - d] : 0u;
+    __syncthreads();
+    tot[c] += v;
+    __syncthreads();
+  }
+  if (c < kOpCodes) {
+    const u32 base = tot[c] - run;
+    ebase[c] = base;
+    etotal[c] = run;
+    if (c == kOpCold) {
+      out->nhot = hot ? min(hot->n, kRouteHotMax) : 0u;
+      out->hot_total = base;
+      out->ncold = run;
+      out->pad = 0;
+    }
+  }
+}
+
+// (the code bases are added here, with the block's column prefix)
+__global__ __launch_bounds__(kOpBlock) void k_opart_rowbase(u32* __restrict__ cnt, u32 ntile,
+                                                           const u32* __restrict__ part,
+                                                           const u32* __restrict__ ebase) {
+  const u32 t0 = blockIdx.x * kOpScanTiles, t1 = min(ntile, t0 + kOpScanTiles);
+  for (u32 c = threadIdx.x; c < kOpCodes; c += kOpBlock) {
+    u32 run = part[(u64)blockIdx.x * kOpCodes + c] + ebase[c];
+    for (u32 t0b = t0; t0b < t1; t0b += 16) {   // (loads of a group issue together)
+      u32 v[16];
+#pragma unroll
+      for (u32 k = 0; k < 16; ++k) v[k] = t0b + k < t1 ? cnt[(u64)(t0b + k) * kOpCodes + c] : 0u;
+#pragma unroll
+      for (u32 k = 0; k < 16; ++k) {
+        const u32 x = v[k];
+        v[k] = run;
+        run += x;
+      }
+#pragma unroll
+      for (u32 k = 0; k < 16; ++k)
+        if (t0b + k < t1) cnt[(u64)(t0b + k) * kOpCodes + c] = v[k];
+    }
+  }
+}
+
+// Pass 3: k_pack_ops' record of every op (the ABI columns read once,
+// coalesced; Rate.Interval divided once per wave when its Takes share a
+// rate), written where the folds read it: a hot op's record and sort value
+// at its place in its bucket's run (hop / hval), a cold op's record at its
+// op index (ops, for the sorted cold folds) and its sort value in the cold
+// list in stream order (coldv, the radix sort's input values).  Stable ranks
+// within the tile: op i0 + k * kOpThreads of wave w sits in chunk (k, w) of
+// the tile's order; each chunk's per-code counts (code_groups' leaders) go
+// to LDS, a prefix over the chunks in order gives every chunk its base per
+// code, and an op's place is its tile row's base + its chunk's base + its
+// rank within the chunk.  All loads of a thread's ops issue before the first
+// store.
+constexpr u32 kOpWv = kOpThreads / 64;
+__global__ __launch_bounds__(kOpThreads) void k_opart_scatter(OpView ov, u32 n, u32 ntile,
+                                                             const u16* __restrict__ code,
+                                                             const u32* __restrict__ base,
+                                                             const OpartHdr* __restrict__ hdr,
+                                                             OpRec* __restrict__ hop,
+                                                             u32* __restrict__ hval,
+                                                             OpRec* __restrict__ ops,
+                                                             u32* __restrict__ coldv) {
+  // chunk counts, then chunk bases relative to the tile's row (<= kOpTile)
+  __shared__ u16 cb[kOpPer][kOpWv][kOpCodes];
+  __shared__ u32 rb[kOpCodes];   // the tile's row of bases (k_opart_rowbase)
+  const u32 wave = threadIdx.x / 64, lane = threadIdx.x & 63;
+  const u32 tile = blockIdx.x;
+  const u64 t0 = (u64)tile * kOpTile, t1 = min((u64)n, t0 + kOpTile);
+  for (u32 j = threadIdx.x; j < kOpPer * kOpWv * kOpCodes; j += kOpThreads) (&cb[0][0][0])[j] = 0;
+  u32 c[kOpPer], kd[kOpPer];
+  i64 nw[kOpPer], f[kOpPer], p[kOpPer];
+  u64 cc[kOpPer], x[kOpPer], y[kOpPer], z[kOpPer];
+#pragma unroll
+  for (u32 k = 0; k < kOpPer; ++k) {
+    const u32 i = (u32)min(t0 + k * kOpThreads + threadIdx.x, t1 - 1);
+    c[k] = code[i];
+    kd[k] = ov.kind ? (u32)ld<true>(ov.kind + i) : ov.kind0;
+    nw[k] = ov.now ? ld<true>(ov.now + i) : ov.now0;
+    f[k] = ov.freq ? ld<true>(ov.freq + i) : 0;
+    p[k] = ov.per ? ld<true>(ov.per + i) : 0;
+    cc[k] = ov.count ? ld<true>(ov.count + i) : 0;
+    x[k] = ov.a ? ld<true>(ov.a + i) : 0;
+    y[k] = ov.t ? ld<true>(ov.t + i) : 0;
+    z[k] = ov.e ? (u64)ld<true>(ov.e + i) : 0;
+  }
+  __syncthreads();   // cb zeroed
+  u32 lead[kOpPer], rank[kOpPer];
+#pragma unroll
+  for (u32 k = 0; k < kOpPer; ++k) {
+    const bool valid = t0 + k * kOpThreads + threadIdx.x < t1;
+    u32 m;
+    code_groups(valid, c[k], lane, lead[k], rank[k], m);
+    if (m) cb[k][wave][c[k]] = (u16)m;   // (leaders: one per code and chunk)
+  }
+  __syncthreads();
+  for (u32 cd = threadIdx.x; cd < kOpCodes; cd += kOpThreads) {
+    rb[cd] = base[(u64)tile * kOpCodes + cd];
+    u32 run = 0;
+#pragma unroll
+    for (u32 k = 0; k < kOpPer; ++k)
+#pragma unroll
+      for (u32 w = 0; w < kOpWv; ++w) {
+        const u32 v = cb[k][w][cd];
+        cb[k][w][cd] = (u16)run;
+        run += v;
+      }
+  }
+  __syncthreads();
+  const u32 cold0 = hdr->hot_total;
+#pragma unroll
+  for (u32 k = 0; k < kOpPer; ++k) {
+    const u64 i64v = t0 + k * kOpThreads + threadIdx.x;
+    const bool valid = i64v < t1;
+    const bool take = valid && kd[k] == PHIP_OP_TAKE;
+    const u64 tm = __ballot(take);
+    if (tm) {   // as k_pack_ops: one division when the wave's Takes share a rate
+      const u32 l0 = (u32)__ffsll((long long)tm) - 1;
+      const i64 f0 = (i64)lane_u64((u64)f[k], l0), p0 = (i64)lane_u64((u64)p[k], l0);
+      i64 iv;
+      if (__ballot(take && (f[k] != f0 || p[k] != p0)) == 0) iv = rate_interval(f0, p0);
+      else iv = rate_interval(f[k], p[k]);
+      if (take) {
+        x[k] = (u64)iv;
+        y[k] = as_bits((double)f[k]);    // bucket.go:192
+        z[k] = as_bits((double)cc[k]);   // bucket.go:215
+      }
+    }
+    const u32 pos = rb[c[k]] + (u32)__shfl((int)cb[k][wave][c[k]], (int)lead[k]) + rank[k];
+    if (!valid) continue;
+    const u32 i = (u32)i64v;
+    const u32 sv = i | (kd[k] << kOpIdxBits);
+    const ulonglong2 q0{(u64)nw[k], x[k]}, q1{y[k], z[k]};
+    if (c[k] < kOpCold) {
+      ulonglong2* q = reinterpret_cast<ulonglong2*>(hop + pos);
+      q[0] = q0;
+      q[1] = q1;
+      hval[pos] = sv;
+    } else {
+      ulonglong2* q = reinterpret_cast<ulonglong2*>(ops + i);
+      q[0] = q0;
+      q[1] = q1;
+      coldv[pos - cold0] = sv;
+    }
+  }
+}
+
+// The radix sort's keys of the cold ops: their slots (k_resolve_batch's),
+// in the cold list's order.
+__global__ __launch_bounds__(kBlock) void k_cold_keys(const u32* __restrict__ coldv, u32 ncold,
+                                                     const u32* __restrict__ slot,
+                                                     u32* __restrict__ coldk) {
+  const u32 p = blockIdx.x * kBlock + threadIdx.x;
+  if (p < ncold) coldk[p] = slot[coldv[p] & kOpIdxMask];
+}
+
+// The hot segments as the block folds take them (one block): list position
+// h -> entry hl[h] (the nfirst largest first, k_huge_order's rule, done here
+// on the entry totals), its run's offset in hop (hoff) and its window offset
+// (woff, a scan of the window counts in list order).
+__global__ __launch_bounds__(1024) void k_hot_offsets(const u32* __restrict__ hl,
+                                                     const OpartHdr* __restrict__ hd,
+                                                     const u32* __restrict__ etotal,
+                                                     const u32* __restrict__ ebase,
+                                                     u64* __restrict__ hoff, u64* __restrict__ woff) {
+  __shared__ u64 part[1024];
+  const u32 nhot = hd->nhot;
+  for (u32 h = threadIdx.x; h < nhot; h += 1024) hoff[h] = ebase[hl[h]];
+  huge_scan<kFoldWin>(hl, nhot, etotal, woff, part);
+  if (threadIdx.x == 0 && nhot)
+    woff[nhot] = woff[nhot - 1] + (etotal[hl[nhot - 1]] + kFoldWin - 1) / kFoldWin;
+}
+
+// Each hot entry's slot: the resolve's slot of its first op (every op of the
+// entry names the same bucket).
+__global__ void k_hot_slots(const OpartHdr* __restrict__ hd, const u32* __restrict__ ebase,
+                            const u32* __restrict__ hval, const u32* __restrict__ slot,
+                            u32* __restrict__ eslot) {
+  const u32 e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e < hd->nhot) eslot[e] = slot[hval[ebase[e]] & kOpIdxMask];
+}
+
+// The identity list 0..nhot-1 (k_huge_order's input).
+__global__ void k_iota(u32* __restrict__ out, const OpartHdr* __restrict__ hd) {
+  const u32 e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e < hd->nhot) out[e] = e;
 }
 
 }  // namespace phip

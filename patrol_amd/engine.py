@@ -44,6 +44,16 @@ def _ptr(x):
     return x.ctypes.data
 
 
+def _names_len(names, names_len=None):
+    """phip_msgs / phip_ops names_len of a device names blob: the length the
+    device checks every name offset against (patrolhip.h), by default the
+    blob's own size; 0 (or a blob past 4 GiB) leaves the offsets unchecked."""
+    if names_len is not None:
+        return int(names_len)
+    nb = int(names.numel() * names.element_size()) if _is_torch(names) else int(names.nbytes)
+    return nb if 0 < nb < (1 << 32) else 0
+
+
 def _np(x, dtype):
     if x is None:
         return None
@@ -84,12 +94,16 @@ class GPURepo:
 
     def __init__(self, device: int = 0, log2_slots: int = 20, arena_bytes: int = 1 << 24,
                  max_load_pct: int = 90, debug_tag_bits: int = 0, grow: bool = True,
-                 small: bool = True, hash_seed: int | None = None):
+                 small: bool = True, hash_seed: int | None = None, split: str | None = None):
         """hash_seed: None = a random placement seed per handle (the default,
         as Go's map seeds its hash per process); an int pins it
-        (PHIP_CFG_FIXED_SEED; 0 = the unseeded placement)."""
+        (PHIP_CFG_FIXED_SEED; 0 = the unseeded placement).  split (testing):
+        None = the ordered path's hot split for batches of >= 2^22 ops,
+        "small" = from 2^16 ops for every sampled name (PHIP_CFG_SPLIT_SMALL),
+        "off" = never (PHIP_CFG_NO_SPLIT)."""
         self.L = _lib.load()
         flags = (0 if grow else _lib.CFG_NO_GROW) | (0 if small else _lib.CFG_NO_SMALL)
+        flags |= {None: 0, "small": _lib.CFG_SPLIT_SMALL, "off": _lib.CFG_NO_SPLIT}[split]
         if hash_seed is not None:
             flags |= _lib.CFG_FIXED_SEED
         cfg = phip_config(device, log2_slots, arena_bytes, max_load_pct, debug_tag_bits, flags, 0,
@@ -340,17 +354,21 @@ class GPURepo:
         return stop.value
 
     def receive_soa(self, names, added, taken, elapsed, now: int, name_offs=None, n=None,
-                    status=None, device=False, reply=None, queue=False):
+                    status=None, device=False, reply=None, queue=False, names_len=None):
         """Receive over decoded states.  With device=True every array is a torch
         CUDA tensor (names = uint8 blob, name_offs = int32/uint32 offsets;
         reply: an int64 [n, 4] tensor for the phip_state replies).
         queue=True (device only): PHIP_RECV_ASYNC, the batch is finished by
         the handle's next call or flush(); the binding holds the batch's
         tensors until the next receive or flush(), so that the caching
-        allocator cannot hand their memory to another tensor meanwhile."""
+        allocator cannot hand their memory to another tensor meanwhile.
+        names_len (device only): the blob length the device checks the name
+        offsets against (phip_msgs.names_len); default the blob's size, 0 =
+        unchecked."""
         fl = _lib.RECV_ASYNC if queue else 0
         if device:
-            m = phip_msgs(n, 0, _ptr(names), _ptr(name_offs), _ptr(added), _ptr(taken), _ptr(elapsed))
+            m = phip_msgs(n, _names_len(names, names_len), _ptr(names), _ptr(name_offs),
+                          _ptr(added), _ptr(taken), _ptr(elapsed))
             res = phip_results(_ptr(status), None, None, _ptr(reply))
             rc = self.L.phip_receive_soa(self.h, C.byref(m), int(now), C.byref(res),
                                          DEVICE_PTRS | fl)
@@ -396,9 +414,11 @@ class GPURepo:
 
     def apply_mixed_device(self, n, kind, names, name_offs, now, freq=None, per=None, count=None,
                            added=None, taken=None, elapsed=None, status=None, remaining=None,
-                           have=None):
-        """apply_mixed with every array a torch CUDA tensor (PHIP_DEVICE_PTRS)."""
-        ops = phip_ops(n, 0, _ptr(kind), _ptr(names), _ptr(name_offs), _ptr(now), _ptr(freq),
+                           have=None, names_len=None):
+        """apply_mixed with every array a torch CUDA tensor (PHIP_DEVICE_PTRS);
+        names_len as receive_soa's."""
+        ops = phip_ops(n, _names_len(names, names_len), _ptr(kind), _ptr(names), _ptr(name_offs),
+                       _ptr(now), _ptr(freq),
                        _ptr(per), _ptr(count), _ptr(added), _ptr(taken), _ptr(elapsed))
         res = phip_results(_ptr(status), _ptr(remaining), _ptr(have), None)
         self._check(self.L.phip_apply_mixed(self.h, C.byref(ops), C.byref(res), DEVICE_PTRS))
@@ -487,7 +507,7 @@ class GPUGroup:
         k = len(batches)
         msgs = (phip_msgs * k)()
         for i, (names, offs, a, t, e) in enumerate(batches):
-            msgs[i] = phip_msgs(offs.numel() - 1, 0, _ptr(names), _ptr(offs), _ptr(a), _ptr(t),
+            msgs[i] = phip_msgs(offs.numel() - 1, _names_len(names), _ptr(names), _ptr(offs), _ptr(a), _ptr(t),
                                 _ptr(e))
         sent, merged = (C.c_uint64 * k)(), (C.c_uint64 * k)()
         flags = DEVICE_PTRS | (_lib.ROUTE_COMBINE if combine else 0) | \

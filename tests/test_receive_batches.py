@@ -373,3 +373,121 @@ def test_queued_batch_error_reported_by_next_call(pa, first_call):
           st, ra, rt, re)
     assert len(g) == K + 100
     same(dump(g), o.dump())
+
+
+def test_queued_batch_outputs_final_when_next_call_returns(pa):
+    """A queued batch with a late dirty suffix (incasts, -0.0 in its last
+    messages: the ordered path's folds write those statuses and replies) is
+    finished by the next queued receive; its outputs are read right after
+    that call returns, on another stream, with no flush in between
+    (phip_engine.hip finish_pending: the leftover work is waited for)."""
+    import torch
+    rng = np.random.default_rng(95)
+    K = 20000
+    gs, gc, o = seeded(pa, rng, K, log2_slots=16)
+    n = 1 << 17
+    ids = _gen.zipf_ids(rng, n, K + 200)
+    a, t, e = _gen.clean_states(rng, n)
+    late = np.arange(n - 3000, n)
+    pos = rng.choice(late, 40, replace=False)
+    a[pos], t[pos], e[pos] = 0, 0, 0
+    pos = rng.choice(late, 40, replace=False)
+    t[pos] = NEG0
+    names = _gen.key_names(ids)
+    b1 = device_batch(names, a, t, e)
+    queue_batch(gc, b1, _gen.T0)
+    ids2 = _gen.zipf_ids(rng, n, K)
+    a2, t2, e2 = _gen.clean_states(rng, n)
+    names2 = _gen.key_names(ids2)
+    b2 = device_batch(names2, a2, t2, e2)
+    queue_batch(gc, b2, _gen.T0 + SEC)   # finishes b1 before it returns
+    with torch.cuda.stream(torch.cuda.Stream()):
+        s1 = b1["status"].cpu().numpy()
+        r1 = b1["reply"].cpu().numpy()
+    st, ra, rt, re = o.receive_soa(names, a, t, e, _gen.T0)
+    check(s1, (r1[:, 0].view(np.uint64), r1[:, 1].view(np.uint64), r1[:, 2]), st, ra, rt, re)
+    gc.flush()
+    st2, ra2, rt2, re2 = o.receive_soa(names2, a2, t2, e2, _gen.T0 + SEC)
+    r2 = b2["reply"].cpu().numpy()
+    check(b2["status"].cpu().numpy(), (r2[:, 0].view(np.uint64), r2[:, 1].view(np.uint64), r2[:, 2]),
+          st2, ra2, rt2, re2)
+    same(dump(gc), o.dump())
+
+
+@pytest.mark.parametrize("queue", [True, False])
+def test_corrupted_offset_column_is_an_error_not_a_fault(pa, queue):
+    """A device batch whose name offset column is corrupted (one entry far
+    past the blob: what a queued batch's freed and reused column reads as)
+    with names_len given (the binding's default: the blob's size): the
+    classification finds the first malformed entry, no kernel reads the blob
+    there, and the call (queued: the call that finishes it) returns
+    PHIP_ERR_INVALID.  The batch stops at that message as Go's loop stops at
+    a short datagram: the messages before it are received, it reads
+    PHIP_ST_SHORT and the rest PHIP_ST_NOT_PROCESSED; the handle keeps
+    working (bucket.go:71-91, repo.go:70-74)."""
+    rng = np.random.default_rng(97)
+    K = 8000
+    gs, gc, o = seeded(pa, rng, K, log2_slots=15)
+    g = gc if queue else gs
+    n = 1 << 17
+    ids = _gen.zipf_ids(rng, n, K + 100)
+    a, t, e = _gen.clean_states(rng, n)
+    sprinkle(rng, ids, a, t, e, K, incast_cold=5)
+    names = _gen.key_names(ids)
+    b = device_batch(names, a, t, e)
+    k = 70001
+    b["to"][k] = 0x7FFF0000   # message k-1 ends past the blob, message k starts there
+    stop = k - 1
+    with pytest.raises(pa.PatrolHipError) as ei:
+        if queue:
+            queue_batch(g, b, _gen.T0)
+            g.flush()
+        else:
+            g.receive_soa(b["tb"], b["ta"], b["tt"], b["te"], _gen.T0, name_offs=b["to"],
+                          n=n, status=b["status"], device=True, reply=b["reply"])
+    assert ei.value.code == -1
+    st, ra, rt, re = o.receive_soa(names[:stop], a[:stop], t[:stop], e[:stop], _gen.T0)
+    got = b["status"].cpu().numpy()
+    assert np.array_equal(got[:stop], st), np.nonzero(got[:stop] != st)[0][:8]
+    assert got[stop] == 4 and (got[stop + 1:] == 5).all()
+    same(dump(g), o.dump())
+    # the handle keeps working: the same batch with the column repaired
+    b2 = device_batch(names, a, t, e)
+    if queue:
+        queue_batch(g, b2, _gen.T0 + SEC)
+        g.flush()
+    else:
+        g.receive_soa(b2["tb"], b2["ta"], b2["tt"], b2["te"], _gen.T0 + SEC, name_offs=b2["to"],
+                      n=n, status=b2["status"], device=True, reply=b2["reply"])
+    o.receive_soa(names, a, t, e, _gen.T0 + SEC)
+    same(dump(g), o.dump())
+
+
+def test_corrupted_offsets_ordered_batch_refused_whole(pa):
+    """phip_apply_mixed with device pointers and names_len: a corrupted
+    offset column refuses the whole batch (PHIP_ERR_INVALID) before anything
+    is applied or created; the handle keeps working."""
+    import torch
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(99)
+    K = 5000
+    gs, gc, o = seeded(pa, rng, K, log2_slots=15)
+    before = dump(gs)
+    n = 1 << 16
+    ids = _gen.zipf_ids(rng, n, K + 50)
+    names = _gen.key_names(ids)
+    b = device_batch(names, *_gen.clean_states(rng, n))
+    kind = torch.ones(n, dtype=torch.uint8, device=dev)
+    kind[::2] = 0
+    now = torch.full((n,), _gen.T0, dtype=torch.int64, device=dev)
+    freq = torch.full((n,), 100, dtype=torch.int64, device=dev)
+    per = torch.full((n,), SEC, dtype=torch.int64, device=dev)
+    cnt = torch.ones(n, dtype=torch.int64, device=dev)
+    b["to"][n // 2] = 0x40000000
+    with pytest.raises(pa.PatrolHipError) as ei:
+        gs.apply_mixed_device(n, kind, b["tb"], b["to"], now, freq, per, cnt, b["ta"], b["tt"],
+                              b["te"], status=b["status"])
+    assert ei.value.code == -1
+    same(dump(gs), before)
+    g2 = gs.get(names[0])
+    assert g2 is not None

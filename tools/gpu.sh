@@ -16,6 +16,7 @@
 #   passes NAME REGEX [ARGS]  tools/pmc_passes.sh over kernels matching REGEX (PMC_PASSES: ';'-list)
 #   pmc NAME [ARGS]       tools/profile_workload.sh TAG/NAME ARGS        (counter passes)
 #   py NAME SCRIPT [ARGS] python3 -u SCRIPT ARGS                         NAME.log
+#   sh NAME SCRIPT [ARGS] bash SCRIPT ARGS                               NAME.log
 set -u
 TAG=$1; shift
 O=gpurun_out/$TAG
@@ -82,6 +83,10 @@ for spec in "$@"; do
       name=$1; shift
       run 900 "$O/$name.log" python3 -u "$@"
       tail -5 "$O/$name.log" ;;
+    sh)       # sh NAME SCRIPT [ARGS]: bash SCRIPT ARGS (its own steps time-limited)
+      name=$1; shift
+      run 900 "$O/$name.log" bash "$@"
+      tail -15 "$O/$name.log" ;;
     *) echo "unknown step $kind"; exit 2 ;;
   esac
 done
