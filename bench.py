@@ -93,9 +93,6 @@ def parse():
     p.add_argument("--sync-receive", action="store_true",
                    help="A/B only: c2 calls phip_receive_soa synchronously instead of queueing "
                         "each batch (PHIP_RECV_ASYNC) and flushing at the end of the timed steps")
-    p.add_argument("--split", default=None, choices=["off", "small"],
-                   help="A/B only: the ordered path's hot split off (PHIP_CFG_NO_SPLIT) or from "
-                        "2^16 ops for every sampled name (PHIP_CFG_SPLIT_SMALL)")
     p.add_argument("--check-names", action="store_true",
                    help="c2: pass the names blob's length (phip_msgs.names_len) so the device "
                         "checks every name offset (the binding's default); the headline passes 0")
@@ -487,7 +484,7 @@ def run_c3_leg(args, torch, dist, dev, local, rank, world):
     ca.c3_clock = "below"
     gen = torch.Generator(device=dev).manual_seed(args.seed + 303 + 7919 * rank)
     base = rank * K
-    repo = patrol_amd.GPURepo(device=local, log2_slots=L, arena_bytes=1 << 20, split=args.split)
+    repo = patrol_amd.GPURepo(device=local, log2_slots=L, arena_bytes=1 << 20)
     repo.use_torch_stream()
     keys = torch.arange(base, base + K, dtype=torch.int64, device=dev)
     kb, ko = names_for_ids(torch, keys)
@@ -851,7 +848,10 @@ def run_c2_variants_leg(args, torch, dist, dev, local, rank, world):
                 "uniform variant"): no hot bucket, every message reads a
                 random record line;
       names32   32-byte names "b" + "x"... + decimal id (arena names, up to
-                231 B per bucket.go:36-44; the headline's are 2-8 B).
+                231 B per bucket.go:36-44; the headline's are 2-8 B);
+      dirty     the headline batch with 64 incasts and 64 -0.0 fields at
+                random places (repo.go:86-90's incast, Go's asymmetric `<`
+                on zeros): the messages Receive must see in order.
     `verified` per variant: 2^14 sampled bucket ids (plus the 256 hottest
     Zipf ranks) read back through phip_export_datagrams equal an
     independent max-reduce of every applied message naming them (torch
@@ -861,7 +861,8 @@ def run_c2_variants_leg(args, torch, dist, dev, local, rank, world):
     K, n, L = args.keys, args.messages, args.log2_slots
     warm, steps = 1, max(1, min(args.steps, 3))
     out = {}
-    for name, zipf, width in (("uniform", 0.0, 0), ("names32", args.zipf, 32)):
+    for name, zipf, width in (("uniform", 0.0, 0), ("names32", args.zipf, 32),
+                              ("dirty", args.zipf, 0)):
         gen = torch.Generator(device=dev).manual_seed(args.seed + 404 + 7919 * rank + width)
         base = rank * K
         arena = max(1 << 20, K * (width + 8)) if width > 22 else 1 << 20
@@ -877,6 +878,15 @@ def run_c2_variants_leg(args, torch, dist, dev, local, rank, world):
         ids = zipf_ids(torch, gen, n, K, zipf, dev)
         blob, offs = names_for_ids(torch, ids + base, width)
         batches = [replica_states(torch, gen, n, j, dev) for j in range(warm + steps)]
+        if name == "dirty":
+            # Receive traffic as Patrol sees it: incasts (all-zero states, the
+            # GetBucket of a restarted peer, repo.go:86-90) and -0.0 fields
+            # among the merges, 64 of each at random places in every batch
+            for a, t, e in batches:
+                pos = torch.randint(0, n, (64,), device=dev, generator=gen)
+                a[pos], t[pos], e[pos] = 0, 0, 0
+                pos = torch.randint(0, n, (64,), device=dev, generator=gen)
+                t[pos] = -(1 << 63)   # -0.0
         status = [torch.empty(n, dtype=torch.uint8, device=dev) for _ in range(2)]
         torch.cuda.synchronize()
 
@@ -932,7 +942,9 @@ def run_c2_variants_leg(args, torch, dist, dev, local, rank, world):
             "steps": steps, "warmup": warm,
             "workload": (f"C2 variant: {n} replica messages -> {K}-bucket table (2^{L} slots), " +
                          ("uniform keys" if zipf == 0 else f"Zipf({zipf})") +
-                         (f", {width}-byte names" if width else ", names b<id> (2-8 B)")),
+                         (f", {width}-byte names" if width else ", names b<id> (2-8 B)") +
+                         (", 64 incasts and 64 -0.0 fields at random places per batch"
+                          if name == "dirty" else "")),
             "roofline": {"bound": "hbm", "kernel": DOMINANT, "kernel_ms_per_step": fast,
                          "achieved": ach, "peak": HBM_PEAK_GBS,
                          "frac": ach / HBM_PEAK_GBS if ach else None,
@@ -1346,8 +1358,7 @@ def main():
     # One stream for torch's input generation and the engine's kernels, so
     # device-pointer calls see torch's results without extra synchronisation.
     torch.cuda.set_stream(torch.cuda.Stream(dev))
-    repo = patrol_amd.GPURepo(device=local, log2_slots=args.log2_slots, arena_bytes=1 << 20,
-                              split=args.split)
+    repo = patrol_amd.GPURepo(device=local, log2_slots=args.log2_slots, arena_bytes=1 << 20)
     repo.use_torch_stream()
     keys = torch.arange(base, base + K, dtype=torch.int64, device=dev)
     kb, ko = names_for_ids(torch, keys, args.name_len if args.workload == "c2" else 0)

@@ -128,10 +128,6 @@ enum {
                                    multi-launch path (by default they run as one launch) */
 #define PHIP_CFG_FIXED_SEED 0x4u /* place buckets with hash_seed as given (0: the unseeded
                                     placement) instead of a random per-handle seed */
-#define PHIP_CFG_SPLIT_SMALL 0x8u /* (testing) the ordered path's hot split from
-                                     2^16 ops and for every sampled name, not only from 2^22
-                                     ops for the hottest buckets */
-#define PHIP_CFG_NO_SPLIT 0x10u   /* (testing, A/B) no hot split: every op through the sort */
 
 typedef struct phip_config {
   int32_t device;        /* HIP device ordinal                                          */

@@ -43,8 +43,6 @@ DEVICE_PTRS = 0x1
 CFG_NO_GROW = 0x1
 CFG_NO_SMALL = 0x2
 CFG_FIXED_SEED = 0x4
-CFG_SPLIT_SMALL = 0x8   # (testing) the ordered path's hot split from 2^16 ops, every sampled name
-CFG_NO_SPLIT = 0x10     # (testing, A/B) no hot split
 ROUTE_COMBINE = 0x2
 GROUP_RCCL_SELF = 0x4
 GROUP_SMALL_CHUNKS = 0x8

@@ -61,7 +61,6 @@ enum BufId {
   B_OPS, B_HOFF, B_HOP, B_HVAL, B_RPOS, B_RST, B_RUNN, B_SEGEX, B_WOFF, B_SUMS, B_WRUN,
   B_WING, B_SEGXF, B_FOLDDBG, B_SMALL, B_HUGE2, B_LONG2,
   B_STATES, B_NAME1, B_HOT, B_ROUTE, B_EXPORT, B_MSHARD, B_MSCNT, B_FSCNT, B_DEDUP, B_DSET, B_TSTATS, B_SEGT, B_RHOT,
-  B_OHOT, B_OCODE, B_OCELL, B_OPART, B_OMETA, B_COLDV, B_COLDK,
   B_COUNT_
 };
 
@@ -140,13 +139,6 @@ struct phip_handle {
   } pend;
   hipEvent_t ev_ctr = nullptr;   // a queued batch's counters reached ctr_host
   int deferred_rc = 0;   // a queued batch's error met by a call that returns no status
-  // the ordered path's hot split (phip_kernels.hpp "ordered: the hot split"):
-  // batches of at least split_min ops; a hot bucket is one sampled at least
-  // split_minc times; the partition's totals come back in opart_host
-  u32 split_min = 1u << 22;
-  bool split_small = false;   // PHIP_CFG_SPLIT_SMALL (tests)
-  OpartHdr* opart_host = nullptr;
-  hipEvent_t ev_scan = nullptr, ev_res = nullptr;
 };
 
 namespace {
@@ -987,198 +979,6 @@ int resolve_all(phip_handle* h, Src src, u32 n, const int64_t* now_arr, i64 now0
   return PHIP_OK;
 }
 
-// ---- the hot split (phip_kernels.hpp "ordered: the hot split") ---------
-#ifndef PHIP_SPLIT_SEG
-#define PHIP_SPLIT_SEG kHugeSeg   // ops a bucket is expected to carry to be partitioned hot
-#endif
-struct Split {
-  const HotHdr* hot = nullptr;
-  u16* code = nullptr;
-  u32 *cell = nullptr, *part = nullptr;
-  u32 *ebase = nullptr, *etotal = nullptr;
-  OpartHdr* hd = nullptr;   // device totals (copied to h->opart_host)
-  u32 *coldv = nullptr, *coldk = nullptr;
-  OpRec* hop = nullptr;
-  u32* hval = nullptr;
-  // the hot chain's scratch (sized for kRouteHotMax segments)
-  u32 *hl0 = nullptr, *hl = nullptr, *eslot = nullptr;
-  u64 *hoff = nullptr, *woff = nullptr;
-  WinSum* sums = nullptr;
-  u32 *wrun = nullptr, *rpos = nullptr, *runn = nullptr, *segxf = nullptr;
-  GMax* wing = nullptr;
-  RunState* rst = nullptr;
-  u8* segex = nullptr;
-  u32 ntile = 0;
-};
-
-// Queue the split's front on stream2, behind the handle stream's work: the
-// outputs' defaults (k_huge_outputs stores only results that differ), the hot
-// name directory of a strided sample, the partition's count and scans (their
-// totals copied to the host, ev_scan), the scatter of every op's record
-// (ev_pack: the main stream joins it before the cold ops' sort), and the hot
-// segments' list, offsets and window summaries.  Every buffer is sized here,
-// before anything of the batch is queued.
-template <class Src>
-int split_front(phip_handle* h, Src src, u32 n, const OpView& ov, const OutView& ow, OpRec* opr,
-                Split* sp) {
-  int rc;
-  hipStream_t st = h->stream2;
-  if (!h->opart_host) HIPCHK(h, hipHostMalloc(&h->opart_host, sizeof(OpartHdr)));
-  if (!h->ev_scan) HIPCHK(h, hipEventCreateWithFlags(&h->ev_scan, hipEventDisableTiming));
-  if (!h->ev_res) HIPCHK(h, hipEventCreateWithFlags(&h->ev_res, hipEventDisableTiming));
-  constexpr size_t kCnt = size_t(1) << kHotCntBits;
-  const size_t zero_bytes = 3 * kCnt * sizeof(u32) + kHotHist * sizeof(u32) + sizeof(HotHdr);
-  u8* hb;
-  sp->ntile = (u32)(((u64)n + kOpTile - 1) / kOpTile);
-  const u32 nblk = (sp->ntile + kOpScanTiles - 1) / kOpScanTiles;
-  const size_t nwin_max = (size_t)n / kFoldWin + kRouteHotMax + 1;
-  u8* meta;
-  if ((rc = ensure(h, B_OHOT, zero_bytes + kRouteHotMax * sizeof(RouteHot), &hb)) ||
-      (rc = ensure(h, B_OCODE, n, &sp->code)) ||
-      (rc = ensure(h, B_OCELL, (size_t)sp->ntile * kOpCodes, &sp->cell)) ||
-      (rc = ensure(h, B_OPART, (size_t)nblk * kOpCodes, &sp->part)) ||
-      (rc = ensure(h, B_OMETA, 4096 + 2 * kOpCodes * sizeof(u32) + 4 * kRouteHotMax * sizeof(u32) +
-                                   (2 * kRouteHotMax + 2) * sizeof(u64),
-                   &meta)) ||
-      (rc = ensure(h, B_COLDV, n, &sp->coldv)) || (rc = ensure(h, B_COLDK, n, &sp->coldk)) ||
-      (rc = ensure(h, B_HOP, n, &sp->hop)) || (rc = ensure(h, B_HVAL, n, &sp->hval)) ||
-      (rc = ensure(h, B_SUMS, nwin_max, &sp->sums)) || (rc = ensure(h, B_WRUN, nwin_max, &sp->wrun)) ||
-      (rc = ensure(h, B_WING, nwin_max, &sp->wing)) ||
-      (rc = ensure(h, B_RPOS, (size_t)n + kRouteHotMax, &sp->rpos)) ||
-      (rc = ensure(h, B_RST, (size_t)n + kRouteHotMax, &sp->rst)))
-    return rc;
-  u32* ckeys = (u32*)hb;
-  u32* ccnt = ckeys + kCnt;
-  u32* cidx = ccnt + kCnt;
-  u32* hist = cidx + kCnt;
-  HotHdr* hdr = (HotHdr*)(hist + kHotHist);
-  RouteHot* dir = (RouteHot*)(hdr + 1);
-  sp->hot = hdr;
-  sp->hd = (OpartHdr*)meta;
-  sp->ebase = (u32*)(meta + 256);
-  sp->etotal = sp->ebase + kOpCodes;
-  sp->hl0 = sp->etotal + kOpCodes;
-  sp->hl = sp->hl0 + kRouteHotMax;
-  sp->eslot = sp->hl + kRouteHotMax;
-  sp->runn = sp->eslot + kRouteHotMax;
-  sp->hoff = (u64*)(((uintptr_t)(sp->runn + kRouteHotMax) + 15) & ~(uintptr_t)15);
-  sp->woff = sp->hoff + kRouteHotMax;
-  // (the last small arrays reuse the per-segment buffers of the huge chain)
-  if ((rc = ensure(h, B_SEGEX, kRouteHotMax, &sp->segex)) ||
-      (rc = ensure(h, B_SEGXF, kRouteHotMax, &sp->segxf)))
-    return rc;
-
-  HIPCHK(h, hipEventRecord(h->ev_fork, h->stream));
-  HIPCHK(h, hipStreamWaitEvent(st, h->ev_fork, 0));
-  // the outputs' defaults first (the hot outputs store only the others; the
-  // main stream's folds write after its join on ev_pack)
-  if (ow.status) HIPCHK(h, hipMemsetAsync(ow.status, PHIP_ST_MERGED, n, st));
-  if (ow.remaining) HIPCHK(h, hipMemsetAsync(ow.remaining, 0, (size_t)n * 8, st));
-  if (ow.have) HIPCHK(h, hipMemsetAsync(ow.have, 0, (size_t)n * 8, st));
-  HIPCHK(h, hipMemsetAsync(hb, 0, zero_bytes, st));
-  const u32 stride = std::max<u32>(64, (n + kHotSampleMax - 1) / kHotSampleMax);
-  const u32 nsample = (n + stride - 1) / stride;
-  // a bucket is hot when the sample expects it to carry PHIP_SPLIT_SEG ops
-  const u32 minc = h->split_small
-                       ? kHotMinCount
-                       : std::max<u32>(kHotMinCount, (u32)((u64)PHIP_SPLIT_SEG * nsample / n));
-  {
-    Launch l(h, "k_split_dir", st);
-    k_route_sample<Src><<<grid_for(nsample, kHotSamplePerBlock), 256, 0, st>>>(src, n, stride,
-                                                                               nsample, ckeys, ccnt, cidx);
-    k_hot_hist<<<grid_for(kCnt), kBlock, 0, st>>>(ccnt, hist);
-    k_hot_select<<<1, 256, 0, st>>>(hist, hdr, kRouteHotMax, minc);
-    k_route_dir_build<Src><<<grid_for(kCnt), kBlock, 0, st>>>(ckeys, ccnt, cidx, hdr, src, 1u, dir);
-  }
-  HIPCHK(h, hipGetLastError());
-  const unsigned tgrid = sp->ntile;   // one workgroup a tile
-  {
-    Launch l(h, "k_opart_count", st);
-    k_opart_count<Src><<<tgrid, kOpThreads, 0, st>>>(src, n, sp->ntile, hdr, dir, sp->code, sp->cell);
-  }
-  HIPCHK(h, hipGetLastError());
-  {
-    Launch l(h, "k_opart_scan", st);
-    k_opart_colsum<<<nblk, kOpBlock, 0, st>>>(sp->cell, sp->ntile, sp->part);
-    k_opart_colscan<<<1, 1024, 0, st>>>(sp->part, nblk, sp->ebase, sp->etotal, hdr, sp->hd);
-    k_opart_rowbase<<<nblk, kOpBlock, 0, st>>>(sp->cell, sp->ntile, sp->part, sp->ebase);
-  }
-  HIPCHK(h, hipGetLastError());
-  HIPCHK(h, hipMemcpyAsync(h->opart_host, sp->hd, sizeof(OpartHdr), hipMemcpyDeviceToHost, st));
-  HIPCHK(h, hipEventRecord(h->ev_scan, st));
-  {
-    Launch l(h, "k_opart_scatter", st);
-    k_opart_scatter<<<tgrid, kOpThreads, 0, st>>>(ov, n, sp->ntile, sp->code, sp->cell, sp->hd,
-                                                 sp->hop, sp->hval, opr, sp->coldv);
-  }
-  HIPCHK(h, hipGetLastError());
-  HIPCHK(h, hipEventRecord(h->ev_pack, st));
-  return PHIP_OK;
-}
-
-// The hot segments' folds, queued once the host has the partition's totals
-// (nhot entries) and the resolve has queued the slots (ev_res): on stream2
-// the list (largest kFirst first, k_huge_order's rule), offsets and window
-// summaries, every entry's slot, then gather-free chains: the kFirst largest
-// segments' block folds and outputs on stream2, the rest on stream3.
-int split_chain(phip_handle* h, const Split& sp, u32 nhot, const u32* slot, const OutView& ow) {
-  hipStream_t st = h->stream2;
-  const u32 kFirst = std::min<u32>(PHIP_HUGE_FIRST, kHugeFirstMax);
-  const bool two = kFirst > 0 && nhot > kFirst;
-  const u32 hsplit = two ? kFirst : nhot;
-  k_iota<<<grid_for(kRouteHotMax), kBlock, 0, st>>>(sp.hl0, sp.hd);
-  const u32* hl = sp.hl0;
-  if (two) {
-    k_huge_order<<<1, 1024, 0, st>>>(sp.hl0, nhot, sp.etotal, kFirst, sp.hl);
-    hl = sp.hl;
-  }
-  k_hot_offsets<<<1, 1024, 0, st>>>(hl, sp.hd, sp.etotal, sp.ebase, sp.hoff, sp.woff);
-  HIPCHK(h, hipGetLastError());
-  const unsigned hgrid = (unsigned)std::max<u64>(1, (u64)h->ncu * 8);
-  {
-    Launch l(h, "k_win_sums", st);
-    k_gather_huge<true><<<hgrid, kBlock, 0, st>>>(hl, nhot, sp.hoff, sp.woff, nullptr, sp.etotal,
-                                                  nullptr, nullptr, sp.hop, sp.hval, sp.sums, 0);
-  }
-  HIPCHK(h, hipGetLastError());
-  HIPCHK(h, hipStreamWaitEvent(st, h->ev_res, 0));
-  k_hot_slots<<<grid_for(kRouteHotMax), kBlock, 0, st>>>(sp.hd, sp.ebase, sp.hval, slot, sp.eslot);
-  HIPCHK(h, hipGetLastError());
-  if (two) {
-    HIPCHK(h, hipEventRecord(h->ev_fork3, st));
-    HIPCHK(h, hipStreamWaitEvent(h->stream3, h->ev_fork3, 0));
-  }
-  auto chain = [&](u32 h0, u32 h1, hipStream_t cs, const char* nf, const char* no) -> int {
-    {
-      Launch l(h, nf, cs);
-      k_fold_block<<<h1 - h0, kFoldThreads, 0, cs>>>(hl, h1, sp.eslot, sp.hoff, sp.etotal, sp.hval,
-                                                     sp.hop, h->recs, sp.rpos, sp.rst, sp.runn,
-                                                     sp.segex, sp.segxf, sp.woff, sp.sums, sp.wrun,
-                                                     sp.wing, nullptr, h0);
-    }
-    HIPCHK(h, hipGetLastError());
-    {
-      Launch l(h, no, cs);
-#define PHIP_HOT_OUT(M)                                                                          \
-  k_huge_outputs<M><<<hgrid, kBlock, 0, cs>>>(hl, h1, sp.hoff, sp.woff, sp.etotal, sp.hval,      \
-                                              sp.hop, sp.rpos, sp.rst, sp.runn, sp.segex,        \
-                                              sp.segxf, sp.wrun, sp.wing, ow, h0)
-      PHIP_OUT_DISPATCH(out_mask(ow), PHIP_HOT_OUT);
-#undef PHIP_HOT_OUT
-    }
-    HIPCHK(h, hipGetLastError());
-    return PHIP_OK;
-  };
-  int rc;
-  if ((rc = chain(0, hsplit, st, "k_fold_block", "k_huge_outputs"))) return rc;
-  if (two) {
-    if ((rc = chain(hsplit, nhot, h->stream3, "k_fold_block2", "k_huge_outputs2"))) return rc;
-    HIPCHK(h, hipEventRecord(h->ev_join3, h->stream3));
-    HIPCHK(h, hipStreamWaitEvent(st, h->ev_join3, 0));
-  }
-  return PHIP_OK;
-}
-
 // Apply a mixed op stream in seq order.  The NEW flag of created buckets is
 // consumed (cleared) by the fold itself.
 template <class Src>
@@ -1221,56 +1021,22 @@ int ordered(phip_handle* h, Src src, u32 n, const OpView& ov, const OutView& ow)
     HIPCHK(h, hipEventRecord(h->ev_pack, h->stream2));
     return PHIP_OK;
   };
-  // The hot split (large batches): the hot buckets' ops partitioned into
-  // their runs on stream2 instead of packed in stream order, sorted and
-  // gathered (phip_kernels.hpp "ordered: the hot split").
-  const bool split = n >= h->split_min;
-  Split sp;
-  struct StreamJoin {   // stream2 joined on every return (the split's chain)
-    phip_handle* h;
-    bool armed = false;
-    ~StreamJoin() {
-      if (armed && hipEventRecord(h->ev_join, h->stream2) == hipSuccess)
-        (void)hipStreamWaitEvent(h->stream, h->ev_join, 0);
-    }
-  } split_join{h};
-  if (split) {
-    split_join.armed = true;
-    if ((rc = split_front(h, src, n, ov, ow, opr, &sp))) return rc;
-  } else if ((rc = fork_pack())) {
-    return rc;
-  }
+  if ((rc = fork_pack())) return rc;
   u32* slot;
   u32 n_claimed = 0;
   if ((rc = resolve_all(h, src, n, ov.now, ov.now0, &slot, &n_claimed,
-                        split ? SortVals{nullptr, 0, nullptr} : SortVals{ov.kind, ov.kind0, idx})))
+                        SortVals{ov.kind, ov.kind0, idx})))
     return rc;
   // Stable radix sort of (slot, seq) pairs: per-bucket arrival order kept.
-  // Split: the cold ops only, their slots gathered in the cold list's (stream)
-  // order; the hot chain continues on stream2 meanwhile.
-  const u32* skey = slot;
-  const u32* sval0 = idx;
-  u32 ns = n;
-  if (split) {
-    HIPCHK(h, hipEventRecord(h->ev_res, h->stream));
-    HIPCHK(h, hipEventSynchronize(h->ev_scan));   // (done beside the resolve)
-    const u32 nhot = h->opart_host->nhot;
-    ns = h->opart_host->ncold;
-    if (nhot && (rc = split_chain(h, sp, nhot, slot, ow))) return rc;
-    if ((rc = pack_join.join())) return rc;
-    if (ns) {
-      k_cold_keys<<<grid_for(ns), kBlock, 0, h->stream>>>(sp.coldv, ns, slot, sp.coldk);
-      HIPCHK(h, hipGetLastError());
-    }
-    skey = sp.coldk;
-    sval0 = sp.coldv;
-  }
+  // (A hot split, the hot buckets' ops partitioned by name before the sort
+  // and the sort ordering only the rest, was built and measured in round 6:
+  // slower)
   size_t tb = 0;
-  HIPCHK(h, rocprim::radix_sort_pairs<SlotSortConfig>(nullptr, tb, skey, sslot, sval0, sidx, ns, 0u,
-                                                       h->L, h->stream));
+  HIPCHK(h, rocprim::radix_sort_pairs<SlotSortConfig>(nullptr, tb, slot, sslot, idx, sidx, n, 0u, h->L,
+                                                       h->stream));
   // segmentation buffers and scan temp sized before the sort is enqueued (a
   // larger B_TEMP must not replace the one the sort is using)
-  const u32 ntiles = (u32)(((u64)ns + kSegTile - 1) / kSegTile);
+  const u32 ntiles = (u32)(((u64)n + kSegTile - 1) / kSegTile);
   u32 *segt = nullptr, *segb = nullptr;
   size_t tbs = 0;
   if ((rc = ensure(h, B_SEGT, 2 * ((size_t)ntiles + 1), &segt))) return rc;
@@ -1279,27 +1045,25 @@ int ordered(phip_handle* h, Src src, u32 n, const OpView& ov, const OutView& ow)
                                     rocprim::plus<u32>(), h->stream));
   u8* temp;
   if ((rc = ensure(h, B_TEMP, std::max(tb, tbs), &temp))) return rc;
+  {
+    Launch l(h, "radix_sort_pairs");
+    HIPCHK(h, rocprim::radix_sort_pairs<SlotSortConfig>(temp, tb, slot, sslot, idx, sidx, n, 0u,
+                                                         h->L, h->stream));
+  }
   u32 nseg = 0;
-  if (ns) {
-    {
-      Launch l(h, "radix_sort_pairs");
-      HIPCHK(h, rocprim::radix_sort_pairs<SlotSortConfig>(temp, tb, skey, sslot, sval0, sidx, ns,
-                                                           0u, h->L, h->stream));
-    }
+  {
     Launch l(h, "segments");
-    k_seg_count<<<ntiles, 256, 0, h->stream>>>(sslot, ns, segt, h->ctr);
+    k_seg_count<<<ntiles, 256, 0, h->stream>>>(sslot, n, segt, h->ctr);
     HIPCHK(h, rocprim::exclusive_scan(temp, tbs, segt, segb, 0u, (size_t)ntiles + 1,
                                       rocprim::plus<u32>(), h->stream));
-    k_seg_write<<<ntiles, 256, 0, h->stream>>>(sslot, ns, segb, uslot, sstart);
-    // (split: the hot buckets are partitioned already; a long cold segment
-    // the sample missed is a wave fold)
+    k_seg_write<<<ntiles, 256, 0, h->stream>>>(sslot, n, segb, uslot, sstart);
     k_seg_finish<<<std::max(1u, std::min<u32>(ntiles, (u32)h->ncu * 4)), 256, 0, h->stream>>>(
-        segb, ntiles, sstart, ns, scnt, lng, huge, h->ctr, split ? 0xFFFFFFFFu : kHugeSeg);
+        segb, ntiles, sstart, n, scnt, lng, huge, h->ctr);
     HIPCHK(h, hipGetLastError());
     if ((rc = read_ctr(h))) return rc;
     nseg = h->ctr_host[kCtrSegs];
   }
-  u32 nlong = ns ? h->ctr_host[6] : 0, nhuge = ns ? h->ctr_host[9] : 0;
+  u32 nlong = h->ctr_host[6], nhuge = h->ctr_host[9];
   if ((rc = pack_join.join())) return rc;
   // Different segments touch different slots, so the folds may overlap: the
   // hot-bucket workgroups run on stream2 beside the wave and thread folds.
@@ -1366,7 +1130,7 @@ int ordered(phip_handle* h, Src src, u32 n, const OpView& ov, const OutView& ow)
                      const char* nf, const char* no) -> int {
       {
         Launch l(h, ng, st);
-        k_gather_huge<false><<<hgrid, kBlock, 0, st>>>(hl, h1, hoff, woff, sstart, scnt, sidx, opr, hop,
+        k_gather_huge<<<hgrid, kBlock, 0, st>>>(hl, h1, hoff, woff, sstart, scnt, sidx, opr, hop,
                                                  hval, sums, h0);
       }
       HIPCHK(h, hipGetLastError());
@@ -2004,11 +1768,6 @@ int phip_open(const phip_config* cfg, phip_handle** out) {
   h->max_load = load_limit(h->cap, h->load_pct);
   h->grow = !(cfg->flags & PHIP_CFG_NO_GROW);
   h->small = !(cfg->flags & PHIP_CFG_NO_SMALL);
-  if (cfg->flags & PHIP_CFG_NO_SPLIT) h->split_min = 0xFFFFFFFFu;
-  if (cfg->flags & PHIP_CFG_SPLIT_SMALL) {
-    h->split_min = kHotMinBatch;
-    h->split_small = true;
-  }
   h->arena_cap = cfg->arena_bytes ? cfg->arena_bytes : (1ull << 20);
   if (cfg->debug_tag_bits && cfg->debug_tag_bits < 64) h->tag_mask = (1ull << cfg->debug_tag_bits) - 1;
   if (cfg->flags & PHIP_CFG_FIXED_SEED) {
@@ -2084,9 +1843,6 @@ void phip_close(phip_handle* h) {
   if (h->ctr) (void)hipFree(h->ctr);
   if (h->ctr_host) (void)hipHostFree(h->ctr_host);
   if (h->small_pin) (void)hipHostFree(h->small_pin);
-  if (h->opart_host) (void)hipHostFree(h->opart_host);
-  if (h->ev_scan) (void)hipEventDestroy(h->ev_scan);
-  if (h->ev_res) (void)hipEventDestroy(h->ev_res);
   if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
   if (h->ev_join) (void)hipEventDestroy(h->ev_join);
   if (h->ev_fork3) (void)hipEventDestroy(h->ev_fork3);

@@ -337,7 +337,7 @@ __device__ inline Rec load_rec(const Rec* p) {
 // The first 48 bytes only (tag, state, name words 0-1); name2 and created
 // are left 0.  Enough to find and merge a name of <= kShortName bytes.
 #ifndef PHIP_REC48_X2
-#define PHIP_REC48_X2 0
+#define PHIP_REC48_X2 1   // (k_receive_fast 1.765 / 1.762 against 1.770 / 1.773 ms, one box)
 #endif
 __device__ inline Rec load_rec48(const Rec* p) {
   // (plain loads: the kernel lives on L2 / Infinity Cache retention of warm
@@ -625,7 +625,7 @@ __global__ void k_hot_hist(const u32* __restrict__ ccnt, u32* __restrict__ hist)
 // One workgroup of 256: the lowest threshold t >= kHotMinCount with at most
 // maxn sampled slots counted t or more times (maxn: the directory's size).
 __global__ __launch_bounds__(256) void k_hot_select(const u32* __restrict__ hist, HotHdr* hdr,
-                                                    u32 maxn, u32 minc = kHotMinCount) {
+                                                    u32 maxn) {
   constexpr u32 kPer = kHotHist / 256;
   __shared__ u32 part[256];
   __shared__ u32 best;
@@ -646,7 +646,7 @@ __global__ __launch_bounds__(256) void k_hot_select(const u32* __restrict__ hist
   __syncthreads();
   if (t == 0) {
     hdr->n = 0;
-    hdr->thresh = best > minc ? best : minc;
+    hdr->thresh = best > kHotMinCount ? best : kHotMinCount;
   }
 }
 
@@ -2163,15 +2163,11 @@ __device__ inline void huge_scan(const u32* __restrict__ huge_list, u32 nhuge,
 // (the rest keep their order): the largest segments' folds are the step's
 // longest sequential chains, so they get their own stream and start first
 // (one block; out must not alias huge_list).
-// (nd: the list's length on the device, capped by nhuge; the hot split's)
 __global__ __launch_bounds__(1024) void k_huge_order(const u32* __restrict__ huge_list, u32 nhuge,
                                                      const u32* __restrict__ seg_count, u32 nfirst,
-                                                     u32* __restrict__ out,
-                                                     const u32* __restrict__ nd = nullptr) {
+                                                     u32* __restrict__ out) {
   __shared__ u64 part[1024];
   __shared__ u32 sel[kHugeFirstMax];
-  if (nd) nhuge = min(*nd, nhuge);
-  nfirst = min(nfirst, nhuge);
   const u32 tid = threadIdx.x;
   for (u32 r = 0; r < nfirst; ++r) {
     u64 best = 0;   // (count, ~index): the largest count, then the lowest index
@@ -2234,22 +2230,17 @@ __device__ inline bool huge_window(const u64* __restrict__ woff, u32 nhuge, u32 
 // folding a hot bucket streams its input instead of chasing one random
 // record per op (a single CU cannot keep enough random misses in flight).
 // The same pass writes the window's summary (WinSum).
-// kStaged (the hot split, k_opart_scatter): the segments' ops are already
-// contiguous in hop / hval; only the summaries are written.
 constexpr u32 kGatherPer = kFoldWin / kBlock;
 
-template <bool kStaged>
 __global__ __launch_bounds__(kBlock) void k_gather_huge(
     const u32* __restrict__ huge_list, u32 nhuge, const u64* __restrict__ hoff,
     const u64* __restrict__ woff, const u32* __restrict__ seg_start,
     const u32* __restrict__ seg_count, const u32* __restrict__ sval,
     const OpRec* __restrict__ ops, OpRec* __restrict__ hop, u32* __restrict__ hval,
-    WinSum* __restrict__ sums, u32 h_begin, const u32* __restrict__ nd = nullptr) {
+    WinSum* __restrict__ sums, u32 h_begin) {
   __shared__ u64 red[6][kBlock / 64];
   __shared__ u32 s_first;
   __shared__ u64 s_par[3];
-  if (nd) nhuge = min(*nd, nhuge);   // (the list's length on the device, capped)
-  if (h_begin >= nhuge) return;
   // segments [h_begin, nhuge) of the list: their windows follow
   // woff[h_begin]; a grid of a few blocks per CU walks them
   const u32 b_end = (u32)woff[nhuge];
@@ -2257,27 +2248,17 @@ __global__ __launch_bounds__(kBlock) void k_gather_huge(
   u32 h, w;
   huge_window(woff, nhuge, b, h, w);
   const u32 g = huge_list[h];
-  const u32 cnt = seg_count[g];
+  const u32 st = seg_start[g], cnt = seg_count[g];
   const u64 dst = hoff[h];
   const u32 tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const u32 p0 = w * kFoldWin, p1 = min(cnt, p0 + kFoldWin);
   if (tid == 0) s_first = 0xFFFFFFFFu;
   u32 v[kGatherPer];
   OpRec r[kGatherPer];
-  if constexpr (kStaged) {
 #pragma unroll
-    for (u32 k = 0; k < kGatherPer; ++k) {
-      const u64 j = dst + min(p0 + k * kBlock + tid, p1 - 1);
-      v[k] = hval[j];
-      r[k] = load_oprec(hop + j);
-    }
-  } else {
-    const u32 st = seg_start[g];
+  for (u32 k = 0; k < kGatherPer; ++k) v[k] = sval[st + min(p0 + k * kBlock + tid, p1 - 1)];
 #pragma unroll
-    for (u32 k = 0; k < kGatherPer; ++k) v[k] = sval[st + min(p0 + k * kBlock + tid, p1 - 1)];
-#pragma unroll
-    for (u32 k = 0; k < kGatherPer; ++k) r[k] = load_oprec(ops + (v[k] & kOpIdxMask));
-  }
+  for (u32 k = 0; k < kGatherPer; ++k) r[k] = load_oprec(ops + (v[k] & kOpIdxMask));
   u64 ea = 0, et = 0, ee = 0, nmin = ~0ull, nmax = 0;
   u32 first_take = 0xFFFFFFFFu;
   bool merge = false, dirty = false;
@@ -2285,12 +2266,10 @@ __global__ __launch_bounds__(kBlock) void k_gather_huge(
   for (u32 k = 0; k < kGatherPer; ++k) {
     const u32 j = p0 + k * kBlock + tid;
     if (j >= p1) continue;
-    if constexpr (!kStaged) {
-      ulonglong2* q = reinterpret_cast<ulonglong2*>(hop + dst + j);
-      q[0] = ulonglong2{(u64)r[k].now, r[k].x};
-      q[1] = ulonglong2{r[k].y, r[k].z};
-      hval[dst + j] = v[k];
-    }
+    ulonglong2* q = reinterpret_cast<ulonglong2*>(hop + dst + j);
+    q[0] = ulonglong2{(u64)r[k].now, r[k].x};
+    q[1] = ulonglong2{r[k].y, r[k].z};
+    hval[dst + j] = v[k];
     const u32 kind = v[k] >> kOpIdxBits;
     if (kind == PHIP_OP_TAKE) {
       const u64 nb = (u64)r[k].now ^ kSign;
@@ -2795,10 +2774,8 @@ __global__ __launch_bounds__(kFoldThreads) void k_fold_block(
     u32* __restrict__ run_pos, RunState* __restrict__ run_st, u32* __restrict__ run_n,
     u8* __restrict__ seg_existed, u32* __restrict__ seg_exact_from,
     const u64* __restrict__ woff, const WinSum* __restrict__ sums, u32* __restrict__ win_run,
-    GMax* __restrict__ win_g, u64* __restrict__ dbg, u32 h_begin,
-    const u32* __restrict__ nd = nullptr) {
+    GMax* __restrict__ win_g, u64* __restrict__ dbg, u32 h_begin) {
   __shared__ FoldShared sh;
-  if (nd) nhuge = min(*nd, nhuge);   // (the list's length on the device, capped)
   const u32 hs = h_begin + blockIdx.x;   // segments [h_begin, nhuge) of the list
   if (hs >= nhuge) return;
   // A hot segment's fold is one sequential chain of dependent rounds beside
@@ -2955,10 +2932,8 @@ __global__ __launch_bounds__(kBlock) void k_huge_outputs(
     const u32* __restrict__ run_pos, const RunState* __restrict__ run_st,
     const u32* __restrict__ run_n, const u8* __restrict__ seg_existed,
     const u32* __restrict__ seg_exact_from, const u32* __restrict__ win_run,
-    const GMax* __restrict__ win_g, OutView ow, u32 h_begin, const u32* __restrict__ nd = nullptr) {
+    const GMax* __restrict__ win_g, OutView ow, u32 h_begin) {
   __shared__ GMax wtot[kBlock / 64];
-  if (nd) nhuge = min(*nd, nhuge);   // (the list's length on the device, capped)
-  if (h_begin >= nhuge) return;
   // segments [h_begin, nhuge) of the list: their windows follow
   // woff[h_begin]; a grid of a few blocks per CU walks them
   const u32 b_end = (u32)woff[nhuge];
@@ -3143,13 +3118,10 @@ __device__ inline void seg_flush(u32* lst, u32& cnt, u32* gcnt, u32* out, u32* b
   __syncthreads();
 }
 
-// huge_min: segments longer than this are listed huge, shorter ones over
-// kLongSeg long (kHugeSeg; the hot split passes ~0: its hot segments are
-// partitioned before the sort, and a rare long cold one is a wave fold).
 __global__ __launch_bounds__(256) void k_seg_finish(const u32* __restrict__ tile_base, u32 ntiles,
                                                     const u32* __restrict__ sstart, u32 n,
                                                     u32* __restrict__ scnt, u32* __restrict__ lng,
-                                                    u32* __restrict__ huge, u32* ctr, u32 huge_min) {
+                                                    u32* __restrict__ huge, u32* ctr) {
   __shared__ u32 llist[kSegListCap], hlist[kSegListCap];
   __shared__ u32 lcnt, hcnt, base_sh;
   const u32 nseg = tile_base[ntiles];
@@ -3165,7 +3137,7 @@ __global__ __launch_bounds__(256) void k_seg_finish(const u32* __restrict__ tile
       c = (j + 1 < nseg ? sstart[j + 1] : n) - sstart[j];
       scnt[j] = c;
     }
-    const bool lo = c > kLongSeg && c <= huge_min, hu = c > huge_min;
+    const bool lo = c > kLongSeg && c <= kHugeSeg, hu = c > kHugeSeg;
     if (lo) llist[atomicAdd(&lcnt, 1u)] = j;
     if (hu) hlist[atomicAdd(&hcnt, 1u)] = j;
     __syncthreads();
@@ -4070,359 +4042,6 @@ __global__ void k_get_one(const u8* name, u32 len, Table T, Rec* out, int* found
   int pr = probe(T, nm, name, &s, &r);
   *found = pr == kFound;
   if (pr == kFound) *out = load_rec(&T.recs[s]);   // probe's copy may be the 48-byte view
-}
-
-// ------------------------------------------------- ordered: the hot split --
-// A large ordered batch (C3) is Zipf-skewed: in C3 the ~110 hottest of 10M
-// buckets carry half of the 50M ops, each over kHugeSeg of them.  Sorting
-// those ops by (slot, seq) and then copying each hot segment out of the
-// stream-order op records (k_gather_huge: a random 32-B record per op, a
-// 128-B line fetched for each) moved ~7 GB per step.  Instead the hot
-// names are found by name before the sort, in a sample (k_route_sample, the
-// owner pack's directory), and a stable partition of the batch in stream
-// order writes every hot op's record once, straight into its bucket's
-// contiguous run (k_opart_count -> k_opart_scan -> k_opart_scatter), beside
-// the resolve.  The radix sort then orders only the cold ops (their records
-// stay at their op index, as k_pack_ops wrote them), and the hot buckets'
-// block folds start as soon as the partition and their window summaries
-// are done.  Per-bucket order: a stable partition keeps every hot bucket's
-// ops in stream (seq) order, and a name is hot or cold as a whole (exact
-// name match on the canonical words of names of <= kShortName bytes;
-// longer names are always cold), so no bucket has ops on both sides.
-// (bucket.go:186-263 per op, repo.go:189-211 for create-on-miss, which the
-// resolve does for every op as before.)
-constexpr u32 kOpTile = 2048;                 // ops per partition tile (one workgroup)
-constexpr u32 kOpCold = kRouteHotMax;         // the code of an op that is not hot
-constexpr u32 kOpCodes = kRouteHotMax + 1;    // hot entries 0..kRouteHotMax-1, then cold
-constexpr u32 kOpBlock = kRouteBlock;         // (the scan kernels' workgroup)
-constexpr u32 kOpScanTiles = 64;              // tiles per block of the column scan
-
-struct OpartHdr {   // device totals of the partition (the host reads it back)
-  u32 nhot;         // directory entries used
-  u32 hot_total;    // ops in hot segments (= the cold list's offset)
-  u32 ncold;
-  u32 pad;
-};
-
-// Pass 1: every op's code (hot entry or kOpCold) and the per-(tile, code)
-// counts, tile-major rows of kOpCodes.  A workgroup takes a tile, every
-// thread kOpPer ops of it (k_pack_ops' shape: all their loads in flight
-// together; a wave walking a tile chunk by chunk kept one chunk in flight
-// and took 1.4 ms).  A chunk's counts: the wave splits its lanes by code
-// (code_groups: one ballot a distinct code, no memory access in the loop)
-// and each code's leader lane adds its count in LDS.
-constexpr u32 kOpThreads = 512;
-constexpr u32 kOpPer = kOpTile / kOpThreads;   // ops per thread (op i0 + k * kOpThreads)
-static_assert(kOpPer * kOpThreads == kOpTile, "partition tile");
-
-__device__ inline void code_groups(bool valid, u32 c, u32 lane, u32& lead, u32& rank, u32& cnt) {
-  const u64 lt = (1ull << lane) - 1;
-  lead = lane;
-  rank = 0;
-  cnt = 0;
-  u64 act = __ballot(valid);
-  while (act) {   // (wave-uniform)
-    const u32 l0 = (u32)__ffsll((long long)act) - 1;
-    const u32 c0 = (u32)__builtin_amdgcn_readlane((int)c, (int)l0);
-    const u64 m = __ballot(valid && c == c0);
-    if (valid && c == c0) {
-      lead = l0;
-      rank = (u32)__popcll(m & lt);
-    }
-    if (lane == l0) cnt = (u32)__popcll(m);
-    act &= ~m;
-  }
-}
-
-// route_lds_load for a workgroup of kOpThreads
-__device__ inline void opart_lds_load(RouteLds& L, const RouteHot* dir, u32 nh) {
-  for (u32 j = threadIdx.x; j < kRouteLds; j += kOpThreads) L.slot[j] = 0;
-  __syncthreads();
-  for (u32 j = threadIdx.x; j < nh; j += kOpThreads) {
-    const RouteHot d = dir[j];
-    L.h[j] = d.h; L.w0[j] = d.w0; L.w1[j] = d.w1; L.owner[j] = d.owner;
-    const u32 v = (u32)(d.h >> 48) << 16 | (j + 1);
-    u32 hs = route_home(d.h);
-    while (atomicCAS(&L.slot[hs], 0u, v) != 0) hs = (hs + 1) & (kRouteLds - 1);
-  }
-}
-
-template <class Src>
-__global__ __launch_bounds__(kOpThreads) void k_opart_count(Src src, u32 n, u32 ntile,
-                                                           const HotHdr* __restrict__ hot,
-                                                           const RouteHot* __restrict__ dir,
-                                                           u16* __restrict__ code,
-                                                           u32* __restrict__ cnt) {
-  __shared__ RouteLds L;
-  __shared__ u32 tcnt[kOpCodes];
-  const u32 nh = hot ? min(hot->n, kRouteHotMax) : 0u;
-  for (u32 j = threadIdx.x; j < kOpCodes; j += kOpThreads) tcnt[j] = 0;
-  opart_lds_load(L, dir, nh);
-  __syncthreads();
-  const u32 lane = threadIdx.x & 63;
-  const u32 tile = blockIdx.x;
-  const u64 t0 = (u64)tile * kOpTile, t1 = min((u64)n, t0 + kOpTile);
-  u64 off[kOpPer], w0[kOpPer], w1[kOpPer], w2[kOpPer];
-  u32 len[kOpPer];
-#pragma unroll
-  for (u32 k = 0; k < kOpPer; ++k)
-    src.template get<true>((u32)min(t0 + k * kOpThreads + threadIdx.x, t1 - 1), off[k], len[k]);
-#pragma unroll
-  for (u32 k = 0; k < kOpPer; ++k) {
-    w0[k] = w1[k] = w2[k] = 0;
-    if (nh && len[k] <= kShortName) load_words3<true>(src.blob, off[k], len[k], w0[k], w1[k], w2[k]);
-  }
-#pragma unroll
-  for (u32 k = 0; k < kOpPer; ++k) {
-    const u64 i = t0 + k * kOpThreads + threadIdx.x;
-    const bool valid = i < t1;
-    u32 c = kOpCold;
-    if (nh && len[k] <= kShortName) {
-      Name nm;
-      short_name(w0[k], w1[k], w2[k], off[k], len[k], nm);
-      const int e = route_hot_find(L, nm);
-      if (e >= 0) c = (u32)e;
-    }
-    if (valid) code[i] = (u16)c;
-    u32 lead, rank, m;
-    code_groups(valid, c, lane, lead, rank, m);
-    if (m) atomicAdd(&tcnt[c], m);   // (leaders; other waves may add to the same code)
-  }
-  __syncthreads();
-  for (u32 c = threadIdx.x; c < kOpCodes; c += kOpThreads) cnt[(u64)tile * kOpCodes + c] = tcnt[c];
-}
-
-// Pass 2 (three kernels): the exclusive prefix of the counts in code-major
-// order (all tiles of code 0, then code 1, ...), written back in place over
-// the tile-major rows: base(t, c) = sum_{c' < c} total(c') + sum_{t' < t}
-// cnt(t', c).  a) column sums per block of kOpScanTiles tiles; b) one block
-// scans them per code and the code totals; c) every block rewrites its rows.
-__global__ __launch_bounds__(kOpBlock) void k_opart_colsum(const u32* __restrict__ cnt, u32 ntile,
-                                                          u32* __restrict__ part) {
-  const u32 t0 = blockIdx.x * kOpScanTiles, t1 = min(ntile, t0 + kOpScanTiles);
-  for (u32 c = threadIdx.x; c < kOpCodes; c += kOpBlock) {
-    u32 s = 0;
-#pragma unroll 16
-    for (u32 t = t0; t < t1; ++t) s += cnt[(u64)t * kOpCodes + c];
-    part[(u64)blockIdx.x * kOpCodes + c] = s;
-  }
-}
-
-__global__ __launch_bounds__(1024) void k_opart_colscan(u32* __restrict__ part, u32 nblk,
-                                                       u32* __restrict__ ebase,
-                                                       u32* __restrict__ etotal,
-                                                       const HotHdr* __restrict__ hot,
-                                                       OpartHdr* __restrict__ out) {
-  __shared__ u32 tot[1024];
-  const u32 c = threadIdx.x;
-  u32 run = 0;
-  if (c < kOpCodes) {
-    // 16 blocks' values at a time: the loads of a group issue together (a
-    // store between two loads would make the second wait for it)
-    for (u32 b0 = 0; b0 < nblk; b0 += 16) {
-      u32 v[16];
-#pragma unroll
-      for (u32 k = 0; k < 16; ++k) v[k] = b0 + k < nblk ? part[(u64)(b0 + k) * kOpCodes + c] : 0u;
-#pragma unroll
-      for (u32 k = 0; k < 16; ++k) {
-        const u32 x = v[k];
-        v[k] = run;
-        run += x;
-      }
-#pragma unroll
-      for (u32 k = 0; k < 16; ++k)
-        if (b0 + k < nblk) part[(u64)(b0 + k) * kOpCodes + c] = v[k];
-    }
-  }
-  tot[c] = c < kOpCodes ? run : 0u;
-  __syncthreads();
-  for (u32 d = 1; d < 1024; d <<= 1) {   // inclusive scan of the code totals
-    const u32 v = c >= d ? tot[c - d] : 0u;
-    __syncthreads();
-    tot[c] += v;
-    __syncthreads();
-  }
-  if (c < kOpCodes) {
-    const u32 base = tot[c] - run;
-    ebase[c] = base;
-    etotal[c] = run;
-    if (c == kOpCold) {
-      out->nhot = hot ? min(hot->n, kRouteHotMax) : 0u;
-      out->hot_total = base;
-      out->ncold = run;
-      out->pad = 0;
-    }
-  }
-}
-
-// (the code bases are added here, with the block's column prefix)
-__global__ __launch_bounds__(kOpBlock) void k_opart_rowbase(u32* __restrict__ cnt, u32 ntile,
-                                                           const u32* __restrict__ part,
-                                                           const u32* __restrict__ ebase) {
-  const u32 t0 = blockIdx.x * kOpScanTiles, t1 = min(ntile, t0 + kOpScanTiles);
-  for (u32 c = threadIdx.x; c < kOpCodes; c += kOpBlock) {
-    u32 run = part[(u64)blockIdx.x * kOpCodes + c] + ebase[c];
-    for (u32 t0b = t0; t0b < t1; t0b += 16) {   // (loads of a group issue together)
-      u32 v[16];
-#pragma unroll
-      for (u32 k = 0; k < 16; ++k) v[k] = t0b + k < t1 ? cnt[(u64)(t0b + k) * kOpCodes + c] : 0u;
-#pragma unroll
-      for (u32 k = 0; k < 16; ++k) {
-        const u32 x = v[k];
-        v[k] = run;
-        run += x;
-      }
-#pragma unroll
-      for (u32 k = 0; k < 16; ++k)
-        if (t0b + k < t1) cnt[(u64)(t0b + k) * kOpCodes + c] = v[k];
-    }
-  }
-}
-
-// Pass 3: k_pack_ops' record of every op (the ABI columns read once,
-// coalesced; Rate.Interval divided once per wave when its Takes share a
-// rate), written where the folds read it: a hot op's record and sort value
-// at its place in its bucket's run (hop / hval), a cold op's record at its
-// op index (ops, for the sorted cold folds) and its sort value in the cold
-// list in stream order (coldv, the radix sort's input values).  Stable ranks
-// within the tile: op i0 + k * kOpThreads of wave w sits in chunk (k, w) of
-// the tile's order; each chunk's per-code counts (code_groups' leaders) go
-// to LDS, a prefix over the chunks in order gives every chunk its base per
-// code, and an op's place is its tile row's base + its chunk's base + its
-// rank within the chunk.  All loads of a thread's ops issue before the first
-// store.
-constexpr u32 kOpWv = kOpThreads / 64;
-__global__ __launch_bounds__(kOpThreads) void k_opart_scatter(OpView ov, u32 n, u32 ntile,
-                                                             const u16* __restrict__ code,
-                                                             const u32* __restrict__ base,
-                                                             const OpartHdr* __restrict__ hdr,
-                                                             OpRec* __restrict__ hop,
-                                                             u32* __restrict__ hval,
-                                                             OpRec* __restrict__ ops,
-                                                             u32* __restrict__ coldv) {
-  // chunk counts, then chunk bases relative to the tile's row (<= kOpTile)
-  __shared__ u16 cb[kOpPer][kOpWv][kOpCodes];
-  __shared__ u32 rb[kOpCodes];   // the tile's row of bases (k_opart_rowbase)
-  const u32 wave = threadIdx.x / 64, lane = threadIdx.x & 63;
-  const u32 tile = blockIdx.x;
-  const u64 t0 = (u64)tile * kOpTile, t1 = min((u64)n, t0 + kOpTile);
-  for (u32 j = threadIdx.x; j < kOpPer * kOpWv * kOpCodes; j += kOpThreads) (&cb[0][0][0])[j] = 0;
-  u32 c[kOpPer], kd[kOpPer];
-  i64 nw[kOpPer], f[kOpPer], p[kOpPer];
-  u64 cc[kOpPer], x[kOpPer], y[kOpPer], z[kOpPer];
-#pragma unroll
-  for (u32 k = 0; k < kOpPer; ++k) {
-    const u32 i = (u32)min(t0 + k * kOpThreads + threadIdx.x, t1 - 1);
-    c[k] = code[i];
-    kd[k] = ov.kind ? (u32)ld<true>(ov.kind + i) : ov.kind0;
-    nw[k] = ov.now ? ld<true>(ov.now + i) : ov.now0;
-    f[k] = ov.freq ? ld<true>(ov.freq + i) : 0;
-    p[k] = ov.per ? ld<true>(ov.per + i) : 0;
-    cc[k] = ov.count ? ld<true>(ov.count + i) : 0;
-    x[k] = ov.a ? ld<true>(ov.a + i) : 0;
-    y[k] = ov.t ? ld<true>(ov.t + i) : 0;
-    z[k] = ov.e ? (u64)ld<true>(ov.e + i) : 0;
-  }
-  __syncthreads();   // cb zeroed
-  u32 lead[kOpPer], rank[kOpPer];
-#pragma unroll
-  for (u32 k = 0; k < kOpPer; ++k) {
-    const bool valid = t0 + k * kOpThreads + threadIdx.x < t1;
-    u32 m;
-    code_groups(valid, c[k], lane, lead[k], rank[k], m);
-    if (m) cb[k][wave][c[k]] = (u16)m;   // (leaders: one per code and chunk)
-  }
-  __syncthreads();
-  for (u32 cd = threadIdx.x; cd < kOpCodes; cd += kOpThreads) {
-    rb[cd] = base[(u64)tile * kOpCodes + cd];
-    u32 run = 0;
-#pragma unroll
-    for (u32 k = 0; k < kOpPer; ++k)
-#pragma unroll
-      for (u32 w = 0; w < kOpWv; ++w) {
-        const u32 v = cb[k][w][cd];
-        cb[k][w][cd] = (u16)run;
-        run += v;
-      }
-  }
-  __syncthreads();
-  const u32 cold0 = hdr->hot_total;
-#pragma unroll
-  for (u32 k = 0; k < kOpPer; ++k) {
-    const u64 i64v = t0 + k * kOpThreads + threadIdx.x;
-    const bool valid = i64v < t1;
-    const bool take = valid && kd[k] == PHIP_OP_TAKE;
-    const u64 tm = __ballot(take);
-    if (tm) {   // as k_pack_ops: one division when the wave's Takes share a rate
-      const u32 l0 = (u32)__ffsll((long long)tm) - 1;
-      const i64 f0 = (i64)lane_u64((u64)f[k], l0), p0 = (i64)lane_u64((u64)p[k], l0);
-      i64 iv;
-      if (__ballot(take && (f[k] != f0 || p[k] != p0)) == 0) iv = rate_interval(f0, p0);
-      else iv = rate_interval(f[k], p[k]);
-      if (take) {
-        x[k] = (u64)iv;
-        y[k] = as_bits((double)f[k]);    // bucket.go:192
-        z[k] = as_bits((double)cc[k]);   // bucket.go:215
-      }
-    }
-    const u32 pos = rb[c[k]] + (u32)__shfl((int)cb[k][wave][c[k]], (int)lead[k]) + rank[k];
-    if (!valid) continue;
-    const u32 i = (u32)i64v;
-    const u32 sv = i | (kd[k] << kOpIdxBits);
-    const ulonglong2 q0{(u64)nw[k], x[k]}, q1{y[k], z[k]};
-    if (c[k] < kOpCold) {
-      ulonglong2* q = reinterpret_cast<ulonglong2*>(hop + pos);
-      q[0] = q0;
-      q[1] = q1;
-      hval[pos] = sv;
-    } else {
-      ulonglong2* q = reinterpret_cast<ulonglong2*>(ops + i);
-      q[0] = q0;
-      q[1] = q1;
-      coldv[pos - cold0] = sv;
-    }
-  }
-}
-
-// The radix sort's keys of the cold ops: their slots (k_resolve_batch's),
-// in the cold list's order.
-__global__ __launch_bounds__(kBlock) void k_cold_keys(const u32* __restrict__ coldv, u32 ncold,
-                                                     const u32* __restrict__ slot,
-                                                     u32* __restrict__ coldk) {
-  const u32 p = blockIdx.x * kBlock + threadIdx.x;
-  if (p < ncold) coldk[p] = slot[coldv[p] & kOpIdxMask];
-}
-
-// The hot segments as the block folds take them (one block): list position
-// h -> entry hl[h] (the nfirst largest first, k_huge_order's rule, done here
-// on the entry totals), its run's offset in hop (hoff) and its window offset
-// (woff, a scan of the window counts in list order).
-__global__ __launch_bounds__(1024) void k_hot_offsets(const u32* __restrict__ hl,
-                                                     const OpartHdr* __restrict__ hd,
-                                                     const u32* __restrict__ etotal,
-                                                     const u32* __restrict__ ebase,
-                                                     u64* __restrict__ hoff, u64* __restrict__ woff) {
-  __shared__ u64 part[1024];
-  const u32 nhot = hd->nhot;
-  for (u32 h = threadIdx.x; h < nhot; h += 1024) hoff[h] = ebase[hl[h]];
-  huge_scan<kFoldWin>(hl, nhot, etotal, woff, part);
-  if (threadIdx.x == 0 && nhot)
-    woff[nhot] = woff[nhot - 1] + (etotal[hl[nhot - 1]] + kFoldWin - 1) / kFoldWin;
-}
-
-// Each hot entry's slot: the resolve's slot of its first op (every op of the
-// entry names the same bucket).
-__global__ void k_hot_slots(const OpartHdr* __restrict__ hd, const u32* __restrict__ ebase,
-                            const u32* __restrict__ hval, const u32* __restrict__ slot,
-                            u32* __restrict__ eslot) {
-  const u32 e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e < hd->nhot) eslot[e] = slot[hval[ebase[e]] & kOpIdxMask];
-}
-
-// The identity list 0..nhot-1 (k_huge_order's input).
-__global__ void k_iota(u32* __restrict__ out, const OpartHdr* __restrict__ hd) {
-  const u32 e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e < hd->nhot) out[e] = e;
 }
 
 }  // namespace phip

@@ -1,15 +1,11 @@
-"""The ordered path's hot split (phip_kernels.hpp "ordered:
-the hot split") against the oracle: the hot buckets' ops partitioned by name
-into their runs before the sort (k_opart_count / _scan / _scatter), their
-block folds fed from those runs (k_win_sums, no gather), the cold ops sorted
-on their own.
-
-PHIP_CFG_SPLIT_SMALL runs the split from 2^16 ops and makes every sampled
-name hot (hundreds of runs, most short: every run length the block folds can
-meet); PHIP_CFG_NO_SPLIT is the same batch through the sort alone.  Both, the
-oracle and the default handle must agree bit for bit: statuses, remaining,
-have, reply states and the whole table (bucket.go:186-263, repo.go:54-92,
-repo.go:189-235).
+"""Large ordered batches against the oracle: C3's shape
+with refilling Takes on a seeded table, every op kind with dirty states and
+long names beside hot buckets, a Receive batch whose dirty suffix is most of
+it, and a 2^22-op device batch through phip_apply_mixed.  Bit for bit:
+statuses, remaining, have, reply states and the whole table
+(bucket.go:186-263, repo.go:54-92, repo.go:189-235).  (Written for round 6's
+hot split of the ordered path, which was measured slower and reverted; the
+batches stay as ordered-path parity cases.)
 """
 import numpy as np
 import pytest
@@ -34,16 +30,17 @@ def pa():
 
 
 def run_both(pa, args, log2_slots, reply=True, seed=None, **kw):
-    """The batch through the split (small), without it and through the
-    oracle, from the same seeded buckets."""
+    """The batch through the GPU (large path and, where it applies, the
+    one-launch small path is bypassed by size) and through the oracle, from
+    the same seeded buckets."""
     o = O.Repo()
-    gs = [pa.GPURepo(log2_slots=log2_slots, split=sp, **kw) for sp in ("small", "off")]
+    gs = [pa.GPURepo(log2_slots=log2_slots, **kw)]
     if seed is not None:
         for r in gs + [o]:
             r.seed(*seed)
     ref = o.apply_mixed(*args)
     take = np.asarray(args[0]) == 0
-    for g, sp in zip(gs, ("small", "off")):
+    for g, sp in zip(gs, ("default",)):
         out = g.apply_mixed(*args)
         assert np.array_equal(out["status"], ref["status"]), (sp, np.nonzero(out["status"] != ref["status"])[0][:8])
         assert np.array_equal(out["remaining"], ref["remaining"]), sp
@@ -57,7 +54,7 @@ def run_both(pa, args, log2_slots, reply=True, seed=None, **kw):
 
 
 @pytest.mark.parametrize("seed", [1, 2])
-def test_split_zipf_mixed_stream(pa, seed):
+def test_ordered_zipf_mixed_stream(pa, seed):
     """C3's shape at 2^18 ops: Take(100:1s) + clean merges, Zipf over 20k
     buckets, replica clocks below the local clock (Takes refill, succeed and
     deny), some buckets created by the batch."""
@@ -80,7 +77,7 @@ def test_split_zipf_mixed_stream(pa, seed):
              seed=(names0, z, z, np.zeros(K, np.int64), np.full(K, _gen.T0 - SEC, np.int64)))
 
 
-def test_split_adversarial_all_kinds(pa):
+def test_ordered_adversarial_all_kinds(pa):
     """Every op kind (Take with odd rates, Receive of dirty states: incasts,
     -0.0, NaN, negatives; Upsert), three buckets hot enough for the block
     folds, long (arena) names that are never hot, and many new buckets."""
@@ -96,7 +93,7 @@ def test_split_adversarial_all_kinds(pa):
     longs = [b"a-long-bucket-name-never-hot-%04d" % k for k in range(30)]
     for k in np.nonzero(rng.random(n) < 0.05)[0]:
         names[k] = longs[k % 30]
-    names[-1] = b"x" * 14   # a 14-byte short name (the longest the split takes)
+    names[-1] = b"x" * 14   # a 14-byte name (the longest short one)
     args[1] = names
     args[0] = rng.choice(np.array([0, 1, 2], np.uint8), n, p=[0.5, 0.4, 0.1])
     a, t, e = _gen.dirty_states(rng, n, 0.1)
@@ -104,10 +101,10 @@ def test_split_adversarial_all_kinds(pa):
     run_both(pa, args, 13)
 
 
-def test_split_receive_suffix(pa):
+def test_ordered_receive_suffix(pa):
     """A large Receive batch whose first dirty message is early: its suffix
-    (most of the batch) takes the ordered path, and there the split (incast
-    replies on hot and cold buckets, -0.0 fields)."""
+    (most of the batch) takes the ordered path (incast replies on hot and
+    cold buckets, -0.0 fields)."""
     from tests.test_receive_batches import sprinkle
     rng = np.random.default_rng(33)
     K = 20000
@@ -124,8 +121,8 @@ def test_split_receive_suffix(pa):
     o.seed(names0, a0, t0, e0, created)
     st, ra, rt, re = o.receive_soa(names, a, t, e, _gen.T0 + SEC)
     want = o.dump()
-    for sp in ("small", "off"):
-        g = pa.GPURepo(log2_slots=16, split=sp)
+    for sp in ("default",):
+        g = pa.GPURepo(log2_slots=16)
         g.seed(names0, a0, t0, e0, created)
         out = g.receive_soa(names, a, t, e, _gen.T0 + SEC)
         assert np.array_equal(out["status"], st), sp
@@ -135,10 +132,9 @@ def test_split_receive_suffix(pa):
         assert_same_dump(gpu_dump(g), want)
 
 
-def test_split_device_batch_and_default_threshold(pa):
-    """A 2^22-op device batch (the default split threshold) through
-    phip_apply_mixed with device pointers, against the oracle; the same batch
-    without the split gives the same results."""
+def test_ordered_device_batch_4m(pa):
+    """A 2^22-op device batch through
+    phip_apply_mixed with device pointers, against the oracle."""
     import torch
     dev = torch.device("cuda", 0)
     rng = np.random.default_rng(4)
@@ -161,8 +157,8 @@ def test_split_device_batch_and_default_threshold(pa):
     ref = o.apply_mixed(kind, names, now, np.full(n, 100, np.int64), np.full(n, SEC, np.int64),
                         np.ones(n, np.uint64), a, t, e)
     want = o.dump()
-    for sp in (None, "off"):
-        g = pa.GPURepo(log2_slots=18, split=sp)
+    for sp in (None,):
+        g = pa.GPURepo(log2_slots=18)
         st = torch.zeros(n, dtype=torch.uint8, device=dev)
         rm = torch.zeros(n, dtype=torch.int64, device=dev)
         hv = torch.zeros(n, dtype=torch.int64, device=dev)
