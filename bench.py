@@ -945,12 +945,18 @@ def run_c2_variants_leg(args, torch, dist, dev, local, rank, world):
                          (f", {width}-byte names" if width else ", names b<id> (2-8 B)") +
                          (", 64 incasts and 64 -0.0 fields at random places per batch"
                           if name == "dirty" else "")),
+            # (kernel: k_receive_fast's share; step: the whole step's, which is
+            # the figure for the dirty variant, whose deferred messages go
+            # through the ordered path's kernels)
             "roofline": {"bound": "hbm", "kernel": DOMINANT, "kernel_ms_per_step": fast,
                          "achieved": ach, "peak": HBM_PEAK_GBS,
                          "frac": ach / HBM_PEAK_GBS if ach else None,
+                         "step_achieved": BYTES_PER_MERGE * n / step_s / 1e9,
+                         "step_frac": BYTES_PER_MERGE * n / step_s / 1e9 / HBM_PEAK_GBS,
                          "algorithmic_bytes_per_step": BYTES_PER_MERGE * n},
             "kernels_ms": kms,
             "hot_directory": {"entries": int(st4[0]), "folded": int(st4[1])} if st4 else None,
+            "ordered_messages": int(st4[4]) if st4 and len(st4) > 4 else None,
             "verified": int(okt.item()) == world,
             "verify": {"sampled_buckets": S, "mismatched": bad, "all_found": bool(found.all())},
         }

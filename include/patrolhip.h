@@ -592,7 +592,9 @@ void phip_set_timing(phip_handle* h, int on);
 /* Counters of the last fast-path Receive batch: out[0] hot-directory
  * entries, out[1] messages folded through the directory, out[2] messages
  * that missed the table (inserted); out[3] table growths (rehashes) since
- * phip_open.  Returns the number written (<= 4). */
+ * phip_open; out[4] messages of the batch that went through the ordered path
+ * (its dirty buckets' messages, or its suffix from the first dirty message:
+ * PHIP_RECV_* "Dirty buckets").  Returns the number written (<= 5). */
 int phip_last_stats(phip_handle* h, uint64_t* out, int max);
 /* Placement quality of the table (one scan of the slots): out[0] buckets,
  * out[1] slots, out[2] the longest probe distance of a bucket from its home

@@ -61,6 +61,7 @@ enum BufId {
   B_OPS, B_HOFF, B_HOP, B_HVAL, B_RPOS, B_RST, B_RUNN, B_SEGEX, B_WOFF, B_SUMS, B_WRUN,
   B_WING, B_SEGXF, B_FOLDDBG, B_SMALL, B_HUGE2, B_LONG2,
   B_STATES, B_NAME1, B_HOT, B_ROUTE, B_EXPORT, B_MSHARD, B_MSCNT, B_FSCNT, B_DEDUP, B_DSET, B_TSTATS, B_SEGT, B_RHOT,
+  B_DLIST, B_DTAB, B_DEFSH, B_DSCNT, B_DEFL, B_DEFS, B_SOFF, B_SLEN, B_SA, B_ST, B_SE, B_SSTAT, B_SREP,
   B_COUNT_
 };
 
@@ -79,7 +80,8 @@ struct Timing {
 struct phip_handle {
   int device = 0;
   int ncu = 256;             // compute units (persistent grid size)
-  uint64_t stats[3] = {0, 0, 0};   // last fast batch: hot entries, hot hits, misses
+  uint64_t stats[4] = {0, 0, 0, 0};   // last fast batch: hot entries, hot hits, misses,
+                                      // messages it sent through the ordered path
   hipStream_t stream = nullptr;      // the stream every call runs on (own_stream or the caller's)
   hipStream_t own_stream = nullptr;  // created by phip_open
   hipStream_t stream2 = nullptr;   // second stream: the hot-bucket fold overlaps the others
@@ -113,6 +115,7 @@ struct phip_handle {
   u32* ctr_host = nullptr;   // pinned mirror
   u32* ctr_map = nullptr;    // ctr_host as the device sees it (k_shard_scan stores there)
   u32 fpar = 0;              // parity of the last fast batch (its shard counters in B_FSCNT)
+  u32 dpar = 0, dcap = 0;    // the last fast pass's deferred list: its counter parity, shard cap
   u64 n_buckets = 0;
   u64 tag_mask = ~0ull;
   u64 seed = 0;              // placement seed (Table::home, seeded_mix)
@@ -643,6 +646,32 @@ inline u32* fast_counts(phip_handle* h, u32 par) {
   return (u32*)h->buf[B_FSCNT].p + par * 2 * kShards;
 }
 
+// The deferred list (dirty buckets' messages, phip_kernels.hpp "Dirty
+// buckets"): shard counters by batch parity (B_DSCNT) as the miss list's.
+inline u32* defer_counts(phip_handle* h, u32 par) {
+  return (u32*)h->buf[B_DSCNT].p + par * 2 * kShards;
+}
+int defer_shards(phip_handle* h, u32 n, u32 par, Sharded* out) {
+  int rc;
+  u32* c;
+  out->cap = shard_cap((n + 63) / 64, 64);
+  if ((rc = ensure(h, B_DEFSH, (size_t)kShards * out->cap, &out->base)) ||
+      (rc = ensure(h, B_DSCNT, 4 * kShards, &c)))
+    return rc;
+  out->cnt = defer_counts(h, par);
+  return PHIP_OK;
+}
+int dirty_set(phip_handle* h, DirtySet* d, u32** dlist) {
+  int rc;
+  u64* b;
+  if ((rc = ensure(h, B_DTAB, 3 * (size_t)kDirtySlots, &b)) ||
+      (rc = ensure(h, B_DLIST, kDirtyCap, dlist)))
+    return rc;
+  d->key = b;
+  d->w = b + kDirtySlots;
+  return PHIP_OK;
+}
+
 int fast_shards(phip_handle* h, u32 n, u32 par, Sharded* out) {
   int rc;
   u32* c;
@@ -665,11 +694,16 @@ int fast_front(phip_handle* h, In in, HotSrc hsrc, u32 n, u8* status, FastFront*
                bool reset = true) {
   int rc;
   *ff = FastFront{};
-  u32* c;
-  if ((rc = ensure(h, B_FSCNT, 4 * kShards, &c))) return rc;
+  u32 *c, *dlist = nullptr;
+  DirtySet dset;
+  if ((rc = ensure(h, B_FSCNT, 4 * kShards, &c)) || (rc = ensure(h, B_DSCNT, 4 * kShards, &c)))
+    return rc;
+  if constexpr (In::kSoa)   // (decoded batches: their dirty messages listed)
+    if ((rc = dirty_set(h, &dset, &dlist))) return rc;
   ff->par = h->fpar ^= 1u;
   if (reset) {
-    k_batch_reset<<<1, kShards, 0, h->stream>>>(h->ctr, fast_counts(h, ff->par));
+    k_batch_reset<<<1, kShards, 0, h->stream>>>(h->ctr, fast_counts(h, ff->par),
+                                                defer_counts(h, ff->par));
     HIPCHK(h, hipGetLastError());
   }
   const bool with_hot = n >= kHotMinBatch;
@@ -696,14 +730,15 @@ int fast_front(phip_handle* h, In in, HotSrc hsrc, u32 n, u8* status, FastFront*
         NamesOffs chk{};
         if constexpr (In::kOffs) chk = in.src;
         k_classify_soa2<<<grid_for((n + 1) / 2), kBlock, 0, h->stream>>>(in.ma, in.mt, in.me, n,
-                                                                          h->ctr, status, chk);
+                                                                          h->ctr, status, chk,
+                                                                          dlist);
         done = true;
       }
     }
     if (!done) {
       if (status) HIPCHK(h, hipMemsetAsync(status, PHIP_ST_MERGED, n, h->stream));
       Launch l(h, "k_classify");
-      k_classify<In><<<grid_for(n), kBlock, 0, h->stream>>>(in, n, h->ctr);
+      k_classify<In><<<grid_for(n), kBlock, 0, h->stream>>>(in, n, h->ctr, dlist);
     }
   }
   HIPCHK(h, hipGetLastError());
@@ -717,24 +752,47 @@ template <class In>
 int fast_back(phip_handle* h, In in, u32 n, const FastFront& ff, bool queued) {
   u32* miss;
   int rc;
-  Sharded msh;
+  Sharded msh, dsh;
+  DirtySet dset{};
+  u32* dlist = nullptr;
   if ((rc = ensure(h, B_MISS, n, &miss)) || (rc = fast_shards(h, n, ff.par, &msh))) return rc;
+  if constexpr (In::kSoa) {
+    // the dirty set behind the classification (a batch without a dirty
+    // message returns at once), the deferred list beside the miss list
+    if ((rc = dirty_set(h, &dset, &dlist)) || (rc = defer_shards(h, n, ff.par, &dsh))) return rc;
+    h->dpar = ff.par;
+    h->dcap = dsh.cap;
+    k_dirty_build<In><<<1, 1024, 0, h->stream>>>(in, n, h->ctr, dlist, dset);
+    HIPCHK(h, hipGetLastError());
+  }
   if ((rc = join_hot(h, ff.hot))) return rc;
   {
     Launch l(h, "k_receive_fast");
     k_receive_fast<In><<<fast_grid(h, n), kFastBlock, 0, h->stream>>>(in, 0, n, table(h), msh,
-                                                                      h->ctr, ff.hot, ff.dir);
+                                                                      h->ctr, ff.hot, ff.dir,
+                                                                      dset, dsh);
   }
   HIPCHK(h, hipGetLastError());
-  k_shard_scan<<<1, kShards, 0, h->stream>>>(msh.cnt, h->ctr, 2, h->ctr_map, kCtrWords,
-                                             queued ? fast_counts(h, ff.par ^ 1u) : nullptr);
+  k_shard_scan<<<1, kShards, 0, h->stream>>>(
+      msh.cnt, h->ctr, 2, h->ctr_map, kCtrWords, queued ? fast_counts(h, ff.par ^ 1u) : nullptr,
+      In::kSoa ? dsh.cnt : nullptr, kCtrNDefer,
+      In::kSoa && queued ? defer_counts(h, ff.par ^ 1u) : nullptr);
   HIPCHK(h, hipGetLastError());
   HIPCHK(h, hipEventRecord(h->ev_ctr, h->stream));
   if (!queued) HIPCHK(h, hipEventSynchronize(h->ev_ctr));
   return PHIP_OK;
 }
 
-int fast_collect(phip_handle* h, u32 n, u32 par, u32* first_dirty, u32* nmiss) {
+// Whether the last fast pass over a decoded batch of n messages deferred its
+// dirty buckets (kernel gate: k_receive_fast) -- read from the mirrored counters.
+inline bool has_deferred(const phip_handle* h, u32 n) {
+  const u32 nd = h->ctr_host[kCtrNDirty];
+  return n != 0 && nd != 0 && nd <= kDirtyCap;
+}
+
+// *first_dirty: n when the batch's dirty buckets were deferred (decoded
+// batches, soa), else its first dirty message (the prefix rule).
+int fast_collect(phip_handle* h, u32 n, u32 par, u32* first_dirty, u32* nmiss, bool soa) {
   int rc;
   if ((rc = check_flags(h))) return rc;
   *nmiss = h->ctr_host[2];
@@ -747,7 +805,10 @@ int fast_collect(phip_handle* h, u32 n, u32 par, u32* first_dirty, u32* nmiss) {
                                                  (u32*)h->buf[B_MISS].p);
     HIPCHK(h, hipGetLastError());
   }
-  *first_dirty = std::min<u32>(h->ctr_host[kCtrDirty], n);
+  const u32 nd = h->ctr_host[kCtrNDirty];
+  const bool iso = soa && nd != 0 && nd <= kDirtyCap;
+  *first_dirty = iso ? n : std::min<u32>(h->ctr_host[kCtrDirty], n);
+  h->stats[3] = 0;   // (finish_receive: the messages it sends through the ordered path)
   h->stats[0] = h->ctr_host[11];
   h->stats[1] = h->ctr_host[10];
   h->stats[2] = *nmiss;
@@ -767,7 +828,7 @@ int fast_apply(phip_handle* h, In in, HotSrc hsrc, u32 n, u8* status, u32* first
   FastFront ff;
   if ((rc = fast_front(h, in, hsrc, n, status, &ff)) || (rc = fast_back(h, in, n, ff, false)))
     return rc;
-  return fast_collect(h, n, ff.par, first_dirty, nmiss);
+  return fast_collect(h, n, ff.par, first_dirty, nmiss, In::kSoa);
 }
 
 template <class Src>
@@ -1327,16 +1388,83 @@ inline OutView shifted(OutView o, u32 k) {
   return o;
 }
 
+// The deferred messages of the last fast pass (its dirty buckets' messages,
+// k_receive_fast): packed, put back in arrival order, gathered into an
+// ordered sub-batch (names in place in the batch's blob), run through the
+// ordered path, and its statuses and replies scattered back.  The dirty
+// buckets are disjoint from every bucket the fast path and its misses
+// touched, and Receive is per bucket (repo.go:77-106), so running them after
+// the rest of the batch gives each of them the Go loop's state sequence.
+int run_deferred(phip_handle* h, NamesOffs src, const uint64_t* a, const uint64_t* t,
+                 const int64_t* e, u32 n, i64 now, const OutView& ow) {
+  const u32 nd = h->ctr_host[kCtrNDefer];   // (the last fast pass's, mirrored or read back)
+  h->stats[3] = nd;
+  if (nd == 0) return PHIP_OK;
+  if (nd > n) return set_err(h, PHIP_ERR_HIP, "deferred list of %u > batch %u", nd, n);
+  int rc;
+  u32 *list, *sorted;
+  uint64_t *off2, *a2, *t2;
+  int64_t* e2;
+  u8 *len2, *st2 = nullptr;
+  phip_state* rep2 = nullptr;
+  if ((rc = ensure(h, B_DEFL, nd, &list)) || (rc = ensure(h, B_DEFS, nd, &sorted)) ||
+      (rc = ensure(h, B_SOFF, nd, &off2)) || (rc = ensure(h, B_SLEN, nd, &len2)) ||
+      (rc = ensure(h, B_SA, nd, &a2)) || (rc = ensure(h, B_ST, nd, &t2)) ||
+      (rc = ensure(h, B_SE, nd, &e2)) ||
+      (ow.status && (rc = ensure(h, B_SSTAT, nd, &st2))) ||
+      (ow.reply && (rc = ensure(h, B_SREP, nd, &rep2))))
+    return rc;
+  {
+    Launch l(h, "k_shard_compact");
+    Sharded dsh;
+    dsh.base = (u32*)h->buf[B_DEFSH].p;
+    dsh.cnt = defer_counts(h, h->dpar);
+    dsh.cap = h->dcap;
+    k_shard_compact<<<dim3(grid_for(dsh.cap), kShards), 256, 0, h->stream>>>(dsh.base, dsh.cap,
+                                                                              dsh.cnt, list);
+    HIPCHK(h, hipGetLastError());
+  }
+  u32 bits = 1;
+  while (bits < 32 && (1ull << bits) < n) ++bits;
+  size_t tb = 0;
+  HIPCHK(h, rocprim::radix_sort_keys(nullptr, tb, list, sorted, nd, 0u, bits, h->stream));
+  u8* temp;
+  if ((rc = ensure(h, B_TEMP, tb, &temp))) return rc;
+  HIPCHK(h, rocprim::radix_sort_keys(temp, tb, list, sorted, nd, 0u, bits, h->stream));
+  k_defer_gather<<<grid_for(nd), kBlock, 0, h->stream>>>(src, a, t, e, sorted, nd, off2, len2, a2,
+                                                         t2, e2);
+  HIPCHK(h, hipGetLastError());
+  if (rep2) HIPCHK(h, hipMemsetAsync(rep2, 0, (size_t)nd * sizeof(phip_state), h->stream));
+  OpView ov{};
+  ov.kind = nullptr; ov.kind0 = PHIP_OP_RECEIVE;
+  ov.now = nullptr; ov.now0 = now;
+  ov.a = a2; ov.t = t2; ov.e = e2;
+  if ((rc = ordered(h, NamesPairs{src.blob, off2, len2}, nd, ov,
+                    OutView{st2, nullptr, nullptr, rep2})))
+    return rc;
+  k_defer_scatter<<<grid_for(nd), kBlock, 0, h->stream>>>(sorted, nd, st2, rep2, ow);
+  HIPCHK(h, hipGetLastError());
+  return PHIP_OK;
+}
+inline int run_deferred(phip_handle*, NamesPairs, const uint64_t*, const uint64_t*,
+                        const int64_t*, u32, i64, const OutView&) {
+  return PHIP_OK;   // (datagram batches keep the prefix rule: nothing deferred)
+}
+
 // After the fast path: the clean prefix's new buckets (finish_misses), then
 // the ordered path over messages [first_dirty, stop), which starts from the
-// state the prefix left (the Go loop's state at that message).
+// state the prefix left (the Go loop's state at that message) -- or, when the
+// fast pass deferred the dirty buckets (first_dirty == n), over their
+// messages (run_deferred).
 template <class Src>
 int finish_receive(phip_handle* h, Src src, const uint64_t* a, const uint64_t* t,
                    const int64_t* e, u32 stop, u32 first_dirty, u32 nmiss, i64 now,
-                   const OutView& ow) {
+                   const OutView& ow, u32 n, bool deferred) {
   int rc;
   if ((rc = finish_misses(h, src, a, t, e, nmiss, std::min(stop, first_dirty), now, ow.status)))
     return rc;
+  if (deferred) return run_deferred(h, src, a, t, e, n, now, ow);
+  h->stats[3] = first_dirty < stop ? stop - first_dirty : 0;
   if (first_dirty >= stop) return PHIP_OK;
   const u32 k = first_dirty;
   OpView ov{};
@@ -1373,7 +1501,8 @@ int receive_decoded(phip_handle* h, Src src, const uint64_t* a, const uint64_t* 
   u32 fd = n, nmiss = 0;
   if ((rc = fast_apply(h, SoaIn<Src>{src, a, t, e}, src, n, ow.status, &fd, &nmiss))) return rc;
   const u32 stop = std::min<u32>(h->ctr_host[5], n);   // (a checked batch's malformed entry)
-  if ((rc = finish_receive(h, src, a, t, e, stop, fd, nmiss, now, ow))) return rc;
+  if ((rc = finish_receive(h, src, a, t, e, stop, fd, nmiss, now, ow, n, has_deferred(h, n))))
+    return rc;
   return stopped_at_bad_name(h, ow, n, stop);
 }
 
@@ -1388,11 +1517,13 @@ int finish_pending(phip_handle* h, bool* worked) {
   HIPCHK(h, hipEventSynchronize(h->ev_ctr));
   u32 fd = p.n, nmiss = 0;
   int rc;
-  if ((rc = fast_collect(h, p.n, p.par, &fd, &nmiss))) return rc;
+  if ((rc = fast_collect(h, p.n, p.par, &fd, &nmiss, true))) return rc;
   const u32 stop = std::min<u32>(h->ctr_host[5], p.n);   // (a checked batch's malformed entry)
-  if (nmiss == 0 && fd >= stop) return stopped_at_bad_name(h, p.ow, p.n, stop);
+  const bool deferred = has_deferred(h, p.n);
+  if (nmiss == 0 && fd >= stop && !deferred) return stopped_at_bad_name(h, p.ow, p.n, stop);
   if (worked) *worked = true;
-  if ((rc = finish_receive(h, p.src, p.a, p.t, p.e, stop, fd, nmiss, p.now, p.ow)) ||
+  if ((rc = finish_receive(h, p.src, p.a, p.t, p.e, stop, fd, nmiss, p.now, p.ow, p.n,
+                           deferred)) ||
       (rc = stopped_at_bad_name(h, p.ow, p.n, stop)))
     return rc;
   // The leftover work (the miss merges, the ordered path's folds, which also
@@ -2239,7 +2370,8 @@ int receive_datagrams_dev(phip_handle* h, const u8* d_bytes, const uint64_t* d_o
                                                           h->ctr);
       HIPCHK(h, hipGetLastError());
     }
-    if ((rc = finish_receive(h, NamesPairs{d_bytes, no, nl}, a, t, e, stop, fd, nmiss, now, ow)))
+    if ((rc = finish_receive(h, NamesPairs{d_bytes, no, nl}, a, t, e, stop, fd, nmiss, now, ow, n,
+                             false)))
       return after_error(h, rc);
   }
   if ((rc = copy_outputs(h, res, n, dev, ow))) return rc;
@@ -2703,9 +2835,9 @@ int phip_last_stats(phip_handle* h, uint64_t* out, int max) {
   // a queued PHIP_RECV_ASYNC batch is finished first, so the stats are its
   // own (its error, if any, is kept for the next call that returns one)
   if (h->pend.active && !h->deferred_rc) h->deferred_rc = begin_call(h);
-  const uint64_t v[4] = {h->stats[0], h->stats[1], h->stats[2], h->grows};
+  const uint64_t v[5] = {h->stats[0], h->stats[1], h->stats[2], h->grows, h->stats[3]};
   int k = 0;
-  for (; k < max && k < 4; ++k) out[k] = v[k];
+  for (; k < max && k < 5; ++k) out[k] = v[k];
   return k;
 }
 

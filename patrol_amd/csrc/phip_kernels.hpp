@@ -220,10 +220,12 @@ struct Sharded {
 // A batch's counters in one launch: ctr[16] zero except ctr[5] (first
 // malformed datagram) and ctr[kCtrDirty] (first dirty message), which start
 // at "none"; and, when given, a sharded list's kShards counters.
-__global__ __launch_bounds__(kShards) void k_batch_reset(u32* ctr, u32* shard_cnt) {
+__global__ __launch_bounds__(kShards) void k_batch_reset(u32* ctr, u32* shard_cnt,
+                                                         u32* shard_cnt2 = nullptr) {
   const u32 t = threadIdx.x;
   if (t < 16) ctr[t] = (t == 5 || t == 12) ? ~0u : 0u;
   if (shard_cnt) shard_cnt[t] = 0;
+  if (shard_cnt2) shard_cnt2[t] = 0;
 }
 
 // One workgroup of kShards lanes over a sharded list's counters: exclusive
@@ -233,11 +235,33 @@ __global__ __launch_bounds__(kShards) void k_batch_reset(u32* ctr, u32* shard_cn
 // words are then stored there, which ends a fast batch without a copy; with
 // `next`, the batch counters and the next batch's shard counters are reset as
 // k_batch_reset does, so a queued batch's successor needs no reset launch.
+// (cnt2 / tot2 / next2: a second sharded list scanned the same way, its
+// total into ctr[tot2]; the largest shard is the first list's only)
 __global__ __launch_bounds__(kShards) void k_shard_scan(u32* cnt, u32* ctr, u32 tot, u32* host,
-                                                        u32 words, u32* next) {
+                                                        u32 words, u32* next, u32* cnt2 = nullptr,
+                                                        u32 tot2 = 0, u32* next2 = nullptr) {
   __shared__ u32 v[kShards];
   __shared__ u32 wmax[kShards / 64];
-  const u32 t = threadIdx.x, c = cnt[t];
+  __shared__ u32 total2;
+  const u32 t = threadIdx.x;
+  if (cnt2) {
+    const u32 c2 = cnt2[t];
+    v[t] = c2;
+    __syncthreads();
+    for (u32 off = 1; off < kShards; off <<= 1) {
+      const u32 x = t >= off ? v[t - off] : 0u;
+      __syncthreads();
+      v[t] += x;
+      __syncthreads();
+    }
+    cnt2[kShards + t] = v[t] - c2;
+    if (t == kShards - 1) {
+      total2 = v[t];
+      ctr[tot2] = v[t];
+    }
+    __syncthreads();
+  }
+  const u32 c = cnt[t];
   v[t] = c;
   u32 m = c;
   for (u32 d = 32; d; d >>= 1) m = max(m, (u32)__shfl_xor((int)m, d));
@@ -258,13 +282,14 @@ __global__ __launch_bounds__(kShards) void k_shard_scan(u32* cnt, u32* ctr, u32 
     ctr[13] = mx;
   }
   if (host && t < words) {
-    const u32 w = t == tot ? total : t == 13 ? mx : ctr[t];
+    const u32 w = t == tot ? total : t == 13 ? mx : (cnt2 && t == tot2) ? total2 : ctr[t];
     __hip_atomic_store(&host[t], w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   if (next) {
     __syncthreads();
     if (t < 16) ctr[t] = (t == 5 || t == 12) ? ~0u : 0u;
     next[t] = 0;
+    if (next2) next2[t] = 0;
   }
 }
 
@@ -405,6 +430,42 @@ __device__ inline void note_min(bool d, u32 i, u32* word) {
   if (m && __lane_id() == (u32)(__ffsll((long long)m) - 1)) atomicMin(word, i);
 }
 __device__ inline void note_dirty(bool d, u32 i, u32* ctr) { note_min(d, i, &ctr[kCtrDirty]); }
+
+// Dirty buckets (round 6).  Go's Receive loop is per bucket in effect: a
+// message's result depends only on the messages before it that name the same
+// bucket (repo.go:54-92, bucket.go:240-263).  So instead of sending every
+// message from the first dirty one on through the ordered path (a batch with
+// one early incast was 5x slower than a clean one), the classification lists
+// every dirty message (incast, -0.0 field: the ones whose place matters), and
+// only the messages of buckets named by a dirty message are set aside: the
+// fast kernel merges every other message and defers those (in their order) to
+// the ordered path.  Buckets without a dirty message commute with everything,
+// so this is exact.  Up to kDirtyCap dirty messages with names of at most
+// kShortName bytes (the names the set compares exactly); otherwise the batch
+// keeps the prefix rule.
+constexpr u32 kCtrNDirty = 0;        // dirty messages listed (> kDirtyCap: the prefix rule)
+constexpr u32 kCtrNDefer = 18;       // deferred messages (k_shard_scan's second list)
+constexpr u32 kDirtyCap = 4096;
+constexpr u32 kDirtySlots = 2 * kDirtyCap;
+__device__ inline void note_dirty_list(bool d, u32 i, u32* ctr, u32* dlist) {
+  const u32 pos = wave_append(&ctr[kCtrNDirty], d);
+  if (d && pos < kDirtyCap) dlist[pos] = i;
+}
+// The dirty names: open addressing over kDirtySlots keys (FNV-1a, 0 stored as
+// 1; 0 = empty) with the canonical words beside them (exact for short names).
+struct DirtySet {
+  u64* key;
+  u64* w;   // [2 * kDirtySlots]: w0, w1 of slot s at 2s, 2s + 1
+};
+__device__ inline u32 dirty_home(u64 h) { return (u32)(h ^ (h >> 31)) & (kDirtySlots - 1); }
+__device__ inline bool dirty_find(const DirtySet& D, const Name& nm) {
+  const u64 k = nm.h ? nm.h : 1;
+  for (u32 s = dirty_home(k);; s = (s + 1) & (kDirtySlots - 1)) {
+    const u64 x = D.key[s];
+    if (x == 0) return false;
+    if (x == k && D.w[2 * s] == nm.w0 && D.w[2 * s + 1] == nm.w1) return true;
+  }
+}
 
 __device__ inline bool replica_dirty(u64 ab, u64 tb, i64 e) {
   const bool inc = is_zero_bits(ab) && is_zero_bits(tb) && e == 0;
@@ -830,9 +891,50 @@ struct WireIn {
 // ctr[kCtrDirty], the first malformed datagram into ctr[5].  One atomic per
 // wave that finds one, none on a clean batch.
 template <class In>
-__global__ __launch_bounds__(kBlock) void k_classify(In in, u32 n, u32* ctr) {
+__global__ __launch_bounds__(kBlock) void k_classify(In in, u32 n, u32* ctr, u32* dlist) {
   const u32 i = blockIdx.x * kBlock + threadIdx.x;
-  note_dirty(i < n && in.dirty(i, ctr), i, ctr);
+  const bool d = i < n && in.dirty(i, ctr);
+  note_dirty(d, i, ctr);
+  if (dlist && __ballot(d)) note_dirty_list(d, i, ctr, dlist);
+}
+
+// The dirty set of a classified batch (one workgroup, behind the
+// classification): every listed dirty message's name.  A batch with more
+// than kDirtyCap dirty messages, or one whose name is longer than
+// kShortName, is marked (ctr[kCtrNDirty] = ~0): it keeps the prefix rule.
+template <class In>
+__global__ __launch_bounds__(1024) void k_dirty_build(In in, u32 n, u32* ctr, const u32* dlist,
+                                                      DirtySet D) {
+  const u32 nd = ctr[kCtrNDirty];
+  if (nd == 0 || nd > kDirtyCap) return;
+  for (u32 s = threadIdx.x; s < kDirtySlots; s += 1024) D.key[s] = 0;
+  __syncthreads();
+  bool longname = false;
+  const u32 stop = min(n, ctr[5]);   // (a checked batch's first malformed entry: not read)
+  for (u32 j = threadIdx.x; j < nd; j += 1024) {
+    const u32 i = dlist[j];
+    if (i >= stop) continue;          // (stopped before it: its bucket needs no deferral)
+    u64 off, w0, w1, w2, ra, rt;
+    u32 len;
+    i64 re;
+    const typename In::Pre p = in.pre(i);
+    in.load(i, p, off, len, w0, w1, w2, ra, rt, re);
+    if (len > kShortName) {
+      longname = true;
+      continue;
+    }
+    Name nm;
+    short_name(w0, w1, w2, off, len, nm);
+    const u64 k = nm.h ? nm.h : 1;
+    for (u32 s = dirty_home(k);; s = (s + 1) & (kDirtySlots - 1)) {
+      if (atomicCAS(&D.key[s], 0ull, k) == 0ull) {
+        D.w[2 * s] = nm.w0;
+        D.w[2 * s + 1] = nm.w1;
+        break;
+      }
+    }
+  }
+  if (longname) ctr[kCtrNDirty] = ~0u;
 }
 
 // The same for decoded messages with 16-byte aligned replica columns: two
@@ -851,7 +953,8 @@ typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
 __global__ __launch_bounds__(kBlock) void k_classify_soa2(const uint64_t* __restrict__ ma,
                                                           const uint64_t* __restrict__ mt,
                                                           const int64_t* __restrict__ me, u32 n,
-                                                          u32* ctr, u8* status, NamesOffs names) {
+                                                          u32* ctr, u8* status, NamesOffs names,
+                                                          u32* dlist) {
   const u32 i0 = 2 * (blockIdx.x * kBlock + threadIdx.x);
   if (names.lim) {   // (uniform)
     bool b0 = false, b1 = false;
@@ -871,7 +974,7 @@ __global__ __launch_bounds__(kBlock) void k_classify_soa2(const uint64_t* __rest
       if (i0 + 1 < n) status[i0 + 1] = PHIP_ST_MERGED;
     }
   }
-  bool d = false;
+  bool d = false, e0 = false, e1 = false;
   u32 at = i0;
   if (i0 + 1 < n) {
     const u64x2 a = __builtin_nontemporal_load(reinterpret_cast<const u64x2*>(ma + i0));
@@ -882,11 +985,18 @@ __global__ __launch_bounds__(kBlock) void k_classify_soa2(const uint64_t* __rest
     const bool d1 = (z1 && me[i0 + 1] == 0) || a.y == kSign || t.y == kSign;
     d = d0 || d1;
     at = d0 ? i0 : i0 + 1;
+    e0 = d0;
+    e1 = d1;
   } else if (i0 < n) {
     const u64 a = ma[i0], t = mt[i0];
     d = (is_zero_bits(a) && is_zero_bits(t) && me[i0] == 0) || a == kSign || t == kSign;
+    e0 = d;
   }
   note_dirty(d, at, ctr);
+  if (dlist && __ballot(d)) {   // (rare: the dirty messages, listed)
+    note_dirty_list(e0, i0, ctr, dlist);
+    note_dirty_list(e1, i0 + 1, ctr, dlist);
+  }
 }
 
 // load_name_long for kInlineName < len <= kHotTailName, also returning the
@@ -922,7 +1032,8 @@ __device__ inline bool tail_match(const u64 (&htail)[kHotTailWords][kHotMax], u3
 template <class In>
 __global__ __launch_bounds__(kFastBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_receive_fast(
     In in, u32 lo, u32 n, Table T, Sharded miss, u32* ctr,
-    const HotHdr* __restrict__ hot, const HotEntry* __restrict__ hot_dir) {
+    const HotHdr* __restrict__ hot, const HotEntry* __restrict__ hot_dir, DirtySet dset,
+    Sharded defer) {
   __shared__ u32 hslot[kHotLds];        // directory index + 1 (0 = empty)
   __shared__ u64 htag[kHotMax], hw0[kHotMax], hw1[kHotMax], hw2[kHotMax];
   __shared__ u32 hrec[kHotMax], haoff[kHotMax];
@@ -934,7 +1045,11 @@ __global__ __launch_bounds__(kFastBlock) __attribute__((amdgpu_waves_per_eu(8, 8
   // prefix is applied, the messages before the first dirty one
   // (ctr[kCtrDirty]) and before the first malformed datagram (ctr[5]); none:
   // ~0.
-  n = min(n, min(ctr[5], ctr[kCtrDirty]));
+  // (dirty buckets, decoded batches: with a dirty set, the whole batch up to
+  // the first malformed message, the dirty buckets' messages deferred)
+  const u32 ndr = In::kSoa && defer.base ? ctr[kCtrNDirty] : 0u;
+  const bool iso = ndr != 0 && ndr <= kDirtyCap;
+  n = min(n, iso ? ctr[5] : min(ctr[5], ctr[kCtrDirty]));
   if (n <= lo) return;
   const u32 nh = hot ? min(hot->n, kHotMax) : 0u;
   for (u32 j = threadIdx.x; j < kHotLds; j += kFastBlock) hslot[j] = 0;
@@ -1014,7 +1129,8 @@ __global__ __launch_bounds__(kFastBlock) __attribute__((amdgpu_waves_per_eu(8, 8
     const u64 ea = enc_replica_nz(ra), et = enc_replica_nz(rt), ee = (u64)re ^ kSign;
 
     bool missed = false;
-    if (valid) {
+    const bool deferred = iso && valid && dirty_find(dset, nm);
+    if (valid && !deferred) {
       int hidx = -1;
       if (nh) {
         for (u32 hs = hot_home(tag);; hs = (hs + 1) & (kHotLds - 1)) {
@@ -1062,6 +1178,7 @@ __global__ __launch_bounds__(kFastBlock) __attribute__((amdgpu_waves_per_eu(8, 8
       }
     }
     miss.append(chunk, missed, i);
+    if (iso) defer.append(chunk, deferred, i);
   }
   if (hits) atomicAdd(&hhits, hits);
   __syncthreads();
@@ -1495,6 +1612,27 @@ __global__ void k_decode(const u8* __restrict__ bytes, const uint64_t* __restric
   }
 }
 
+// The deferred messages as an ordered sub-batch: message list[j] of a
+// decoded batch as entry j (its name in place in the batch's blob, NamesPairs;
+// its replica fields copied).
+__global__ void k_defer_gather(NamesOffs src, const uint64_t* __restrict__ a,
+                               const uint64_t* __restrict__ t, const int64_t* __restrict__ e,
+                               const u32* __restrict__ list, u32 nd, uint64_t* __restrict__ off2,
+                               u8* __restrict__ len2, uint64_t* __restrict__ a2,
+                               uint64_t* __restrict__ t2, int64_t* __restrict__ e2) {
+  const u32 j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= nd) return;
+  const u32 i = list[j];
+  u64 off;
+  u32 len;
+  src.get(i, off, len);
+  off2[j] = off;
+  len2[j] = (u8)len;
+  a2[j] = a[i];
+  t2[j] = t[i];
+  e2[j] = e[i];
+}
+
 // ------------------------------------------------------------ ordered ----
 // A view of a mixed op stream as the ABI hands it over; null arrays mean
 // "uniform value" (kind0 / now0).
@@ -1511,6 +1649,16 @@ struct OutView {
   uint64_t* have;
   phip_state* reply;
 };
+
+// The deferred sub-batch's statuses and replies back to their messages.
+__global__ void k_defer_scatter(const u32* __restrict__ list, u32 nd, const u8* __restrict__ st2,
+                                const phip_state* __restrict__ rep2, OutView ow) {
+  const u32 j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= nd) return;
+  const u32 i = list[j];
+  if (ow.status) ow.status[i] = st2[j];
+  if (ow.reply) ow.reply[i] = rep2[j];
+}
 
 // Lane l's value when l is wave-uniform (a ballot's first set lane): a
 // v_readlane into a scalar register instead of an LDS permute.

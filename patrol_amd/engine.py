@@ -174,9 +174,10 @@ class GPURepo:
 
     def last_stats(self):
         """(hot-directory entries, messages folded through it, misses) of the
-        last fast-path Receive batch, and the table's growths since open."""
-        out = (C.c_uint64 * 4)()
-        k = self.L.phip_last_stats(self.h, out, 4)
+        last fast-path Receive batch, the table's growths since open, and the
+        batch's messages that went through the ordered path."""
+        out = (C.c_uint64 * 5)()
+        k = self.L.phip_last_stats(self.h, out, 5)
         return tuple(int(out[i]) for i in range(k))
 
     def table_stats(self):

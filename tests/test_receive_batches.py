@@ -491,3 +491,123 @@ def test_corrupted_offsets_ordered_batch_refused_whole(pa):
     same(dump(gs), before)
     g2 = gs.get(names[0])
     assert g2 is not None
+
+
+def dirty_mask(a, t, e):
+    """The messages whose place in the batch matters (k_classify): incasts
+    (both floats zero, elapsed 0) and -0.0 fields."""
+    return ((a == 0) & (t == 0) & (e == 0)) | (a == NEG0) | (t == NEG0)
+
+
+def deferred_count(names, dirty):
+    dn = {names[i] for i in np.nonzero(dirty)[0]}
+    return sum(1 for x in names if x in dn)
+
+
+@pytest.mark.parametrize("seed", [61, 62])
+def test_dirty_buckets_deferred_alone(pa, seed):
+    """Dirty-bucket isolation: a batch with a few incasts (hot, cold and new
+    buckets) and -0.0 fields, the first of them near its start, sends only
+    the messages of the buckets those name through the ordered path (in
+    their order); every other message is merged by the fast path.  Called
+    synchronously and queued; bit-exact against the oracle, and the ordered
+    path's share is exactly the dirty buckets' messages (last_stats()[4])."""
+    rng = np.random.default_rng(seed)
+    K = 20000
+    gs, gc, o = seeded(pa, rng, K, negative=0.3)
+    n = 1 << 18
+    ids = _gen.zipf_ids(rng, n, K + 2000)
+    a, t, e = _gen.clean_states(rng, n)
+    sprinkle(rng, ids, a, t, e, K, incast_hot=1 if seed == 61 else 0, incast_cold=30,
+             incast_new=10, negzero=20)
+    ids[7] = 12345
+    a[7], t[7], e[7] = 0, 0, 0                     # an incast at message 7
+    names = _gen.key_names(ids)
+    dirty = dirty_mask(a, t, e)
+    assert 0 < dirty.sum() <= 4096 and np.argmax(dirty) <= 7
+    want = deferred_count(names, dirty)
+    assert want < n // 2
+    run_all(gs, gc, o, names, a, t, e, _gen.T0 + 2 * SEC)
+    assert gs.last_stats()[4] == want
+    assert gc.last_stats()[4] == want
+    same(dump(gs), o.dump())
+    same(dump(gc), o.dump())
+
+
+def test_dirty_buckets_over_cap_keep_prefix_rule(pa):
+    """More than 4096 dirty messages: the batch keeps the prefix rule (the
+    ordered path from the first dirty message on)."""
+    rng = np.random.default_rng(63)
+    K = 20000
+    gs, gc, o = seeded(pa, rng, K)
+    n = 1 << 17
+    ids = _gen.zipf_ids(rng, n, K + 500)
+    a, t, e = _gen.clean_states(rng, n)
+    sprinkle(rng, ids, a, t, e, K, incast_cold=4500, negzero=200)
+    names = _gen.key_names(ids)
+    dirty = dirty_mask(a, t, e)
+    assert dirty.sum() > 4096
+    run_all(gs, gc, o, names, a, t, e, _gen.T0 + SEC)
+    assert gs.last_stats()[4] == n - int(np.argmax(dirty))
+    same(dump(gs), o.dump())
+    same(dump(gc), o.dump())
+
+
+def test_dirty_long_name_keeps_prefix_rule(pa):
+    """A dirty message whose name is longer than 14 bytes (the dirty set
+    compares short names only): the batch keeps the prefix rule."""
+    rng = np.random.default_rng(64)
+    K = 20000
+    gs, gc, o = seeded(pa, rng, K)
+    n = 1 << 17
+    ids = _gen.zipf_ids(rng, n, K + 500)
+    a, t, e = _gen.clean_states(rng, n)
+    sprinkle(rng, ids, a, t, e, K, incast_cold=20)
+    names = _gen.key_names(ids)
+    for p in rng.choice(n, 50, replace=False):
+        names[p] = b"a-much-longer-bucket-name-%d" % (p % 7)   # (some of them dirty)
+    p = int(rng.integers(n // 4, n // 2))
+    names[p] = b"a-much-longer-bucket-name-3"
+    a[p], t[p], e[p] = 0, 0, 0
+    dirty = dirty_mask(a, t, e)
+    run_all(gs, gc, o, names, a, t, e, _gen.T0 + SEC)
+    assert gs.last_stats()[4] == n - int(np.argmax(dirty))
+    same(dump(gs), o.dump())
+    same(dump(gc), o.dump())
+
+
+def test_dirty_bucket_isolation_over_a_clean_batch_and_repeat(pa):
+    """A clean batch after a deferred one (the deferred list's counters start
+    again from zero), then the dirty batch again on the queued handle twice
+    in a row (parity counter sets)."""
+    import torch
+    rng = np.random.default_rng(65)
+    K = 10000
+    gs, gc, o = seeded(pa, rng, K)
+    n = 1 << 17
+    now = _gen.T0
+    for r in range(4):
+        ids = _gen.zipf_ids(rng, n, K + 300)
+        a, t, e = _gen.clean_states(rng, n)
+        if r != 1:
+            sprinkle(rng, ids, a, t, e, K, incast_cold=15, incast_new=5, negzero=5)
+        names = _gen.key_names(ids)
+        want = deferred_count(names, dirty_mask(a, t, e))
+        now += SEC
+        bs = []
+        for _ in range(2):   # two queued copies back to back (the second sees the first's state)
+            b = device_batch(names, a, t, e)
+            queue_batch(gc, b, now)
+            bs.append(b)
+        gc.flush()
+        gs.receive_soa(names, a, t, e, now)
+        gs.receive_soa(names, a, t, e, now)
+        assert gs.last_stats()[4] == want
+        o.receive_soa(names, a, t, e, now)
+        st, ra, rt, re = o.receive_soa(names, a, t, e, now)
+        r_ = bs[1]["reply"].cpu().numpy()
+        check(bs[1]["status"].cpu().numpy(),
+              (r_[:, 0].view(np.uint64), r_[:, 1].view(np.uint64), r_[:, 2]), st, ra, rt, re)
+        torch.cuda.synchronize()
+        same(dump(gs), o.dump())
+        same(dump(gc), o.dump())
