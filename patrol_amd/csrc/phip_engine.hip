@@ -61,7 +61,7 @@ enum BufId {
   B_OPS, B_HOFF, B_HOP, B_HVAL, B_RPOS, B_RST, B_RUNN, B_SEGEX, B_WOFF, B_SUMS, B_WRUN,
   B_WING, B_SEGXF, B_FOLDDBG, B_SMALL, B_HUGE2, B_LONG2,
   B_STATES, B_NAME1, B_HOT, B_ROUTE, B_EXPORT, B_MSHARD, B_MSCNT, B_FSCNT, B_DEDUP, B_DSET, B_TSTATS, B_SEGT, B_RHOT,
-  B_DLIST, B_DTAB, B_DEFSH, B_DSCNT, B_DEFL, B_DEFS, B_SOFF, B_SLEN, B_SA, B_ST, B_SE, B_SSTAT, B_SREP,
+  B_DLIST, B_DTAB, B_DMARK, B_SMAP, B_SOFF, B_SLEN, B_SA, B_ST, B_SE, B_SSTAT, B_SREP,
   B_COUNT_
 };
 
@@ -80,6 +80,7 @@ struct Timing {
 struct phip_handle {
   int device = 0;
   int ncu = 256;             // compute units (persistent grid size)
+  u32 ndef = 0;   // the last fast pass's ordered sub-batch (dirty buckets), entries
   uint64_t stats[4] = {0, 0, 0, 0};   // last fast batch: hot entries, hot hits, misses,
                                       // messages it sent through the ordered path
   hipStream_t stream = nullptr;      // the stream every call runs on (own_stream or the caller's)
@@ -115,7 +116,6 @@ struct phip_handle {
   u32* ctr_host = nullptr;   // pinned mirror
   u32* ctr_map = nullptr;    // ctr_host as the device sees it (k_shard_scan stores there)
   u32 fpar = 0;              // parity of the last fast batch (its shard counters in B_FSCNT)
-  u32 dpar = 0, dcap = 0;    // the last fast pass's deferred list: its counter parity, shard cap
   u64 n_buckets = 0;
   u64 tag_mask = ~0ull;
   u64 seed = 0;              // placement seed (Table::home, seeded_mix)
@@ -640,35 +640,37 @@ struct FastFront {
   const HotHdr* hot = nullptr;
   const HotEntry* dir = nullptr;
   u32 par = 0;
+  u8* mark = nullptr;   // decoded batches: the status column, or a cleared one (k_dirty_pass)
 };
 
 inline u32* fast_counts(phip_handle* h, u32 par) {
   return (u32*)h->buf[B_FSCNT].p + par * 2 * kShards;
 }
 
-// The deferred list (dirty buckets' messages, phip_kernels.hpp "Dirty
-// buckets"): shard counters by batch parity (B_DSCNT) as the miss list's.
-inline u32* defer_counts(phip_handle* h, u32 par) {
-  return (u32*)h->buf[B_DSCNT].p + par * 2 * kShards;
-}
-int defer_shards(phip_handle* h, u32 n, u32 par, Sharded* out) {
-  int rc;
-  u32* c;
-  out->cap = shard_cap((n + 63) / 64, 64);
-  if ((rc = ensure(h, B_DEFSH, (size_t)kShards * out->cap, &out->base)) ||
-      (rc = ensure(h, B_DSCNT, 4 * kShards, &c)))
-    return rc;
-  out->cnt = defer_counts(h, par);
-  return PHIP_OK;
-}
+// The dirty-bucket set and list (phip_kernels.hpp "Dirty buckets").
 int dirty_set(phip_handle* h, DirtySet* d, u32** dlist) {
   int rc;
   u64* b;
-  if ((rc = ensure(h, B_DTAB, 3 * (size_t)kDirtySlots, &b)) ||
-      (rc = ensure(h, B_DLIST, kDirtyCap, dlist)))
+  if ((rc = ensure(h, B_DTAB, DirtySet::kWords, &b)) || (rc = ensure(h, B_DLIST, kDirtyCap, dlist)))
     return rc;
-  d->key = b;
-  d->w = b + kDirtySlots;
+  *d = DirtySet::at(b);
+  return PHIP_OK;
+}
+// The ordered sub-batch dirty_finish builds (at most 3 entries per dirty
+// message).
+struct SubBatch {
+  uint64_t *off, *a, *t;
+  int64_t* e;
+  u8* len;
+  u32* map;
+};
+int sub_batch(phip_handle* h, SubBatch* b) {
+  constexpr size_t m = 3 * (size_t)kDirtyCap;
+  int rc;
+  if ((rc = ensure(h, B_SOFF, m, &b->off)) || (rc = ensure(h, B_SLEN, m, &b->len)) ||
+      (rc = ensure(h, B_SA, m, &b->a)) || (rc = ensure(h, B_ST, m, &b->t)) ||
+      (rc = ensure(h, B_SE, m, &b->e)) || (rc = ensure(h, B_SMAP, m, &b->map)))
+    return rc;
   return PHIP_OK;
 }
 
@@ -696,14 +698,18 @@ int fast_front(phip_handle* h, In in, HotSrc hsrc, u32 n, u8* status, FastFront*
   *ff = FastFront{};
   u32 *c, *dlist = nullptr;
   DirtySet dset;
-  if ((rc = ensure(h, B_FSCNT, 4 * kShards, &c)) || (rc = ensure(h, B_DSCNT, 4 * kShards, &c)))
-    return rc;
-  if constexpr (In::kSoa)   // (decoded batches: their dirty messages listed)
+  if ((rc = ensure(h, B_FSCNT, 4 * kShards, &c))) return rc;
+  if constexpr (In::kSoa) {   // (decoded batches: their dirty messages listed)
     if ((rc = dirty_set(h, &dset, &dlist))) return rc;
+    ff->mark = status;
+    if (!status) {   // (marks need a column: a cleared one)
+      if ((rc = ensure(h, B_DMARK, n, &ff->mark))) return rc;
+      HIPCHK(h, hipMemsetAsync(ff->mark, 0, n, h->stream));
+    }
+  }
   ff->par = h->fpar ^= 1u;
   if (reset) {
-    k_batch_reset<<<1, kShards, 0, h->stream>>>(h->ctr, fast_counts(h, ff->par),
-                                                defer_counts(h, ff->par));
+    k_batch_reset<<<1, kShards, 0, h->stream>>>(h->ctr, fast_counts(h, ff->par));
     HIPCHK(h, hipGetLastError());
   }
   const bool with_hot = n >= kHotMinBatch;
@@ -752,17 +758,17 @@ template <class In>
 int fast_back(phip_handle* h, In in, u32 n, const FastFront& ff, bool queued) {
   u32* miss;
   int rc;
-  Sharded msh, dsh;
+  Sharded msh;
   DirtySet dset{};
+  SubBatch sb{};
   u32* dlist = nullptr;
   if ((rc = ensure(h, B_MISS, n, &miss)) || (rc = fast_shards(h, n, ff.par, &msh))) return rc;
   if constexpr (In::kSoa) {
     // the dirty set behind the classification (a batch without a dirty
-    // message returns at once), the deferred list beside the miss list
-    if ((rc = dirty_set(h, &dset, &dlist)) || (rc = defer_shards(h, n, ff.par, &dsh))) return rc;
-    h->dpar = ff.par;
-    h->dcap = dsh.cap;
-    k_dirty_build<In><<<1, 1024, 0, h->stream>>>(in, n, h->ctr, dlist, dset);
+    // message returns at once: one launch of ~3 us)
+    if ((rc = dirty_set(h, &dset, &dlist)) || (rc = sub_batch(h, &sb))) return rc;
+    Launch l(h, "k_dirty_build");
+    k_dirty_build<In><<<1, 1024, 0, h->stream>>>(in, n, h->ctr, dlist, dset, table(h));
     HIPCHK(h, hipGetLastError());
   }
   if ((rc = join_hot(h, ff.hot))) return rc;
@@ -770,24 +776,31 @@ int fast_back(phip_handle* h, In in, u32 n, const FastFront& ff, bool queued) {
     Launch l(h, "k_receive_fast");
     k_receive_fast<In><<<fast_grid(h, n), kFastBlock, 0, h->stream>>>(in, 0, n, table(h), msh,
                                                                       h->ctr, ff.hot, ff.dir,
-                                                                      dset, dsh);
+                                                                      dset.key, ff.mark);
   }
   HIPCHK(h, hipGetLastError());
-  k_shard_scan<<<1, kShards, 0, h->stream>>>(
-      msh.cnt, h->ctr, 2, h->ctr_map, kCtrWords, queued ? fast_counts(h, ff.par ^ 1u) : nullptr,
-      In::kSoa ? dsh.cnt : nullptr, kCtrNDefer,
-      In::kSoa && queued ? defer_counts(h, ff.par ^ 1u) : nullptr);
+  if constexpr (In::kSoa) {
+    // the messages the fast kernel marked (an isolated batch's only: others
+    // return at once), then the dirty buckets' records unmarked and their
+    // ordered sub-batch built in the launch that ends the batch
+    {
+      Launch l(h, "k_dirty_pass");
+      const unsigned g = (unsigned)std::max<u64>(
+          1, std::min<u64>(((u64)n + 1023) / 1024, (u64)h->ncu * 2));
+      k_dirty_pass<In><<<g, 1024, 0, h->stream>>>(in, n, h->ctr, ff.mark, dset.key, table(h), msh);
+      HIPCHK(h, hipGetLastError());
+    }
+    k_batch_end<In><<<1, kShards, 0, h->stream>>>(
+        in, h->ctr, dset.key, table(h), SubOut{sb.off, sb.len, sb.a, sb.t, sb.e, sb.map}, msh.cnt,
+        h->ctr_map, kCtrWords, queued ? fast_counts(h, ff.par ^ 1u) : nullptr);
+  } else {
+    k_shard_scan<<<1, kShards, 0, h->stream>>>(msh.cnt, h->ctr, 2, h->ctr_map, kCtrWords,
+                                               queued ? fast_counts(h, ff.par ^ 1u) : nullptr);
+  }
   HIPCHK(h, hipGetLastError());
   HIPCHK(h, hipEventRecord(h->ev_ctr, h->stream));
   if (!queued) HIPCHK(h, hipEventSynchronize(h->ev_ctr));
   return PHIP_OK;
-}
-
-// Whether the last fast pass over a decoded batch of n messages deferred its
-// dirty buckets (kernel gate: k_receive_fast) -- read from the mirrored counters.
-inline bool has_deferred(const phip_handle* h, u32 n) {
-  const u32 nd = h->ctr_host[kCtrNDirty];
-  return n != 0 && nd != 0 && nd <= kDirtyCap;
 }
 
 // *first_dirty: n when the batch's dirty buckets were deferred (decoded
@@ -808,6 +821,7 @@ int fast_collect(phip_handle* h, u32 n, u32 par, u32* first_dirty, u32* nmiss, b
   const u32 nd = h->ctr_host[kCtrNDirty];
   const bool iso = soa && nd != 0 && nd <= kDirtyCap;
   *first_dirty = iso ? n : std::min<u32>(h->ctr_host[kCtrDirty], n);
+  h->ndef = iso ? h->ctr_host[kCtrNDefer] : 0;   // (the ordered sub-batch, run_deferred)
   h->stats[3] = 0;   // (finish_receive: the messages it sends through the ordered path)
   h->stats[0] = h->ctr_host[11];
   h->stats[1] = h->ctr_host[10];
@@ -1388,67 +1402,39 @@ inline OutView shifted(OutView o, u32 k) {
   return o;
 }
 
-// The deferred messages of the last fast pass (its dirty buckets' messages,
-// k_receive_fast): packed, put back in arrival order, gathered into an
-// ordered sub-batch (names in place in the batch's blob), run through the
-// ordered path, and its statuses and replies scattered back.  The dirty
-// buckets are disjoint from every bucket the fast path and its misses
-// touched, and Receive is per bucket (repo.go:77-106), so running them after
-// the rest of the batch gives each of them the Go loop's state sequence.
-int run_deferred(phip_handle* h, NamesOffs src, const uint64_t* a, const uint64_t* t,
-                 const int64_t* e, u32 n, i64 now, const OutView& ow) {
-  const u32 nd = h->ctr_host[kCtrNDefer];   // (the last fast pass's, mirrored or read back)
+// The last fast pass's ordered sub-batch (its dirty buckets' dirty messages
+// and the merges of their cells, dirty_finish) through the ordered path,
+// its statuses and replies scattered back.  The dirty buckets' other
+// messages were merged by the fast pass (before each bucket's first dirty
+// message) or folded into the cells (after it); no other bucket is touched,
+// and Receive is per bucket (repo.go:77-106), so applying the sub-batch
+// after the rest of the batch gives each dirty bucket the Go loop's states.
+template <class Src>
+int run_deferred(phip_handle* h, Src src, i64 now, const OutView& ow) {
+  const u32 nd = h->ndef;   // (the last fast pass's: a second pass rebuilt it)
   h->stats[3] = nd;
   if (nd == 0) return PHIP_OK;
-  if (nd > n) return set_err(h, PHIP_ERR_HIP, "deferred list of %u > batch %u", nd, n);
+  if (nd > 3 * kDirtyCap) return set_err(h, PHIP_ERR_HIP, "ordered sub-batch of %u entries", nd);
   int rc;
-  u32 *list, *sorted;
-  uint64_t *off2, *a2, *t2;
-  int64_t* e2;
-  u8 *len2, *st2 = nullptr;
+  SubBatch sb;
+  u8* st2 = nullptr;
   phip_state* rep2 = nullptr;
-  if ((rc = ensure(h, B_DEFL, nd, &list)) || (rc = ensure(h, B_DEFS, nd, &sorted)) ||
-      (rc = ensure(h, B_SOFF, nd, &off2)) || (rc = ensure(h, B_SLEN, nd, &len2)) ||
-      (rc = ensure(h, B_SA, nd, &a2)) || (rc = ensure(h, B_ST, nd, &t2)) ||
-      (rc = ensure(h, B_SE, nd, &e2)) ||
-      (ow.status && (rc = ensure(h, B_SSTAT, nd, &st2))) ||
+  if ((rc = sub_batch(h, &sb)) || (ow.status && (rc = ensure(h, B_SSTAT, nd, &st2))) ||
       (ow.reply && (rc = ensure(h, B_SREP, nd, &rep2))))
     return rc;
-  {
-    Launch l(h, "k_shard_compact");
-    Sharded dsh;
-    dsh.base = (u32*)h->buf[B_DEFSH].p;
-    dsh.cnt = defer_counts(h, h->dpar);
-    dsh.cap = h->dcap;
-    k_shard_compact<<<dim3(grid_for(dsh.cap), kShards), 256, 0, h->stream>>>(dsh.base, dsh.cap,
-                                                                              dsh.cnt, list);
-    HIPCHK(h, hipGetLastError());
-  }
-  u32 bits = 1;
-  while (bits < 32 && (1ull << bits) < n) ++bits;
-  size_t tb = 0;
-  HIPCHK(h, rocprim::radix_sort_keys(nullptr, tb, list, sorted, nd, 0u, bits, h->stream));
-  u8* temp;
-  if ((rc = ensure(h, B_TEMP, tb, &temp))) return rc;
-  HIPCHK(h, rocprim::radix_sort_keys(temp, tb, list, sorted, nd, 0u, bits, h->stream));
-  k_defer_gather<<<grid_for(nd), kBlock, 0, h->stream>>>(src, a, t, e, sorted, nd, off2, len2, a2,
-                                                         t2, e2);
-  HIPCHK(h, hipGetLastError());
   if (rep2) HIPCHK(h, hipMemsetAsync(rep2, 0, (size_t)nd * sizeof(phip_state), h->stream));
   OpView ov{};
   ov.kind = nullptr; ov.kind0 = PHIP_OP_RECEIVE;
   ov.now = nullptr; ov.now0 = now;
-  ov.a = a2; ov.t = t2; ov.e = e2;
-  if ((rc = ordered(h, NamesPairs{src.blob, off2, len2}, nd, ov,
+  ov.a = sb.a; ov.t = sb.t; ov.e = sb.e;
+  if ((rc = ordered(h, NamesPairs{src.blob, sb.off, sb.len}, nd, ov,
                     OutView{st2, nullptr, nullptr, rep2})))
     return rc;
-  k_defer_scatter<<<grid_for(nd), kBlock, 0, h->stream>>>(sorted, nd, st2, rep2, ow);
-  HIPCHK(h, hipGetLastError());
+  if (st2 || rep2) {
+    k_defer_scatter<<<grid_for(nd), kBlock, 0, h->stream>>>(sb.map, nd, st2, rep2, ow);
+    HIPCHK(h, hipGetLastError());
+  }
   return PHIP_OK;
-}
-inline int run_deferred(phip_handle*, NamesPairs, const uint64_t*, const uint64_t*,
-                        const int64_t*, u32, i64, const OutView&) {
-  return PHIP_OK;   // (datagram batches keep the prefix rule: nothing deferred)
 }
 
 // After the fast path: the clean prefix's new buckets (finish_misses), then
@@ -1463,7 +1449,7 @@ int finish_receive(phip_handle* h, Src src, const uint64_t* a, const uint64_t* t
   int rc;
   if ((rc = finish_misses(h, src, a, t, e, nmiss, std::min(stop, first_dirty), now, ow.status)))
     return rc;
-  if (deferred) return run_deferred(h, src, a, t, e, n, now, ow);
+  if (deferred) return run_deferred(h, src, now, ow);
   h->stats[3] = first_dirty < stop ? stop - first_dirty : 0;
   if (first_dirty >= stop) return PHIP_OK;
   const u32 k = first_dirty;
@@ -1501,7 +1487,7 @@ int receive_decoded(phip_handle* h, Src src, const uint64_t* a, const uint64_t* 
   u32 fd = n, nmiss = 0;
   if ((rc = fast_apply(h, SoaIn<Src>{src, a, t, e}, src, n, ow.status, &fd, &nmiss))) return rc;
   const u32 stop = std::min<u32>(h->ctr_host[5], n);   // (a checked batch's malformed entry)
-  if ((rc = finish_receive(h, src, a, t, e, stop, fd, nmiss, now, ow, n, has_deferred(h, n))))
+  if ((rc = finish_receive(h, src, a, t, e, stop, fd, nmiss, now, ow, n, h->ndef != 0)))
     return rc;
   return stopped_at_bad_name(h, ow, n, stop);
 }
@@ -1519,7 +1505,7 @@ int finish_pending(phip_handle* h, bool* worked) {
   int rc;
   if ((rc = fast_collect(h, p.n, p.par, &fd, &nmiss, true))) return rc;
   const u32 stop = std::min<u32>(h->ctr_host[5], p.n);   // (a checked batch's malformed entry)
-  const bool deferred = has_deferred(h, p.n);
+  const bool deferred = h->ndef != 0;
   if (nmiss == 0 && fd >= stop && !deferred) return stopped_at_bad_name(h, p.ow, p.n, stop);
   if (worked) *worked = true;
   if ((rc = finish_receive(h, p.src, p.a, p.t, p.e, stop, fd, nmiss, p.now, p.ow, p.n,

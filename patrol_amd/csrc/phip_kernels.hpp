@@ -220,12 +220,10 @@ struct Sharded {
 // A batch's counters in one launch: ctr[16] zero except ctr[5] (first
 // malformed datagram) and ctr[kCtrDirty] (first dirty message), which start
 // at "none"; and, when given, a sharded list's kShards counters.
-__global__ __launch_bounds__(kShards) void k_batch_reset(u32* ctr, u32* shard_cnt,
-                                                         u32* shard_cnt2 = nullptr) {
+__global__ __launch_bounds__(kShards) void k_batch_reset(u32* ctr, u32* shard_cnt) {
   const u32 t = threadIdx.x;
   if (t < 16) ctr[t] = (t == 5 || t == 12) ? ~0u : 0u;
   if (shard_cnt) shard_cnt[t] = 0;
-  if (shard_cnt2) shard_cnt2[t] = 0;
 }
 
 // One workgroup of kShards lanes over a sharded list's counters: exclusive
@@ -235,33 +233,15 @@ __global__ __launch_bounds__(kShards) void k_batch_reset(u32* ctr, u32* shard_cn
 // words are then stored there, which ends a fast batch without a copy; with
 // `next`, the batch counters and the next batch's shard counters are reset as
 // k_batch_reset does, so a queued batch's successor needs no reset launch.
-// (cnt2 / tot2 / next2: a second sharded list scanned the same way, its
-// total into ctr[tot2]; the largest shard is the first list's only)
+__device__ inline void shard_scan(u32* cnt, u32* ctr, u32 tot, u32* host, u32 words, u32* next);
 __global__ __launch_bounds__(kShards) void k_shard_scan(u32* cnt, u32* ctr, u32 tot, u32* host,
-                                                        u32 words, u32* next, u32* cnt2 = nullptr,
-                                                        u32 tot2 = 0, u32* next2 = nullptr) {
+                                                        u32 words, u32* next) {
+  shard_scan(cnt, ctr, tot, host, words, next);
+}
+__device__ inline void shard_scan(u32* cnt, u32* ctr, u32 tot, u32* host, u32 words, u32* next) {
   __shared__ u32 v[kShards];
   __shared__ u32 wmax[kShards / 64];
-  __shared__ u32 total2;
-  const u32 t = threadIdx.x;
-  if (cnt2) {
-    const u32 c2 = cnt2[t];
-    v[t] = c2;
-    __syncthreads();
-    for (u32 off = 1; off < kShards; off <<= 1) {
-      const u32 x = t >= off ? v[t - off] : 0u;
-      __syncthreads();
-      v[t] += x;
-      __syncthreads();
-    }
-    cnt2[kShards + t] = v[t] - c2;
-    if (t == kShards - 1) {
-      total2 = v[t];
-      ctr[tot2] = v[t];
-    }
-    __syncthreads();
-  }
-  const u32 c = cnt[t];
+  const u32 t = threadIdx.x, c = cnt[t];
   v[t] = c;
   u32 m = c;
   for (u32 d = 32; d; d >>= 1) m = max(m, (u32)__shfl_xor((int)m, d));
@@ -282,14 +262,13 @@ __global__ __launch_bounds__(kShards) void k_shard_scan(u32* cnt, u32* ctr, u32 
     ctr[13] = mx;
   }
   if (host && t < words) {
-    const u32 w = t == tot ? total : t == 13 ? mx : (cnt2 && t == tot2) ? total2 : ctr[t];
+    const u32 w = t == tot ? total : t == 13 ? mx : ctr[t];
     __hip_atomic_store(&host[t], w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   if (next) {
     __syncthreads();
     if (t < 16) ctr[t] = (t == 5 || t == 12) ? ~0u : 0u;
     next[t] = 0;
-    if (next2) next2[t] = 0;
   }
 }
 
@@ -433,38 +412,91 @@ __device__ inline void note_dirty(bool d, u32 i, u32* ctr) { note_min(d, i, &ctr
 
 // Dirty buckets (round 6).  Go's Receive loop is per bucket in effect: a
 // message's result depends only on the messages before it that name the same
-// bucket (repo.go:54-92, bucket.go:240-263).  So instead of sending every
-// message from the first dirty one on through the ordered path (a batch with
-// one early incast was 5x slower than a clean one), the classification lists
-// every dirty message (incast, -0.0 field: the ones whose place matters), and
-// only the messages of buckets named by a dirty message are set aside: the
-// fast kernel merges every other message and defers those (in their order) to
-// the ordered path.  Buckets without a dirty message commute with everything,
-// so this is exact.  Up to kDirtyCap dirty messages with names of at most
+// bucket (repo.go:54-92, bucket.go:240-263).  And between two dirty messages
+// (incast, -0.0 field: the ones whose place matters) of a bucket, its clean
+// messages commute: their effect is one merge of their field-wise maximum.
+// So a batch with a few dirty messages is not sent through the ordered path
+// from its first dirty message on (a batch with one early incast was 5x
+// slower than a clean one); instead the classification lists the dirty
+// messages, k_dirty_build makes a set of the buckets they name, sorted
+// per bucket, and the fast kernel
+//   - merges every message of a clean bucket, and every message of a dirty
+//     bucket before that bucket's first dirty message, as before;
+//   - folds each later clean message of a dirty bucket into a cell, the
+//     maximum of the clean messages between one of its dirty messages and
+//     the next (E-encoded, as the table's fields);
+// and dirty_finish turns the dirty messages and the non-empty cells into an
+// ordered sub-batch of at most 3 * kDirtyCap entries (a dirty message, then
+// the merge of its cell), which the ordered path applies after the rest of
+// the batch.  Exact: every bucket sees the Go loop's sequence of states at
+// its dirty messages.  Up to kDirtyCap dirty messages with names of at most
 // kShortName bytes (the names the set compares exactly); otherwise the batch
 // keeps the prefix rule.
 constexpr u32 kCtrNDirty = 0;        // dirty messages listed (> kDirtyCap: the prefix rule)
-constexpr u32 kCtrNDefer = 18;       // deferred messages (k_shard_scan's second list)
+constexpr u32 kCtrNDefer = 18;       // entries of the ordered sub-batch (dirty_finish)
+constexpr u32 kCtrNSorted = 19;      // dirty messages in the set (before the batch's stop)
 constexpr u32 kDirtyCap = 4096;
 constexpr u32 kDirtySlots = 2 * kDirtyCap;
+constexpr u64 kRecDirty = 4u;        // record flag: its bucket is in the batch's dirty set
 __device__ inline void note_dirty_list(bool d, u32 i, u32* ctr, u32* dlist) {
   const u32 pos = wave_append(&ctr[kCtrNDirty], d);
   if (d && pos < kDirtyCap) dlist[pos] = i;
 }
-// The dirty names: open addressing over kDirtySlots keys (FNV-1a, 0 stored as
-// 1; 0 = empty) with the canonical words beside them (exact for short names).
+// The dirty buckets: open addressing over kDirtySlots keys (FNV-1a, 0 stored
+// as 1; 0 = empty) with the canonical words beside them (exact for short
+// names); per bucket its first dirty message, its dirty messages' range in
+// `idx` (sorted by (set slot, message)) and its table slot.
 struct DirtySet {
-  u64* key;
-  u64* w;   // [2 * kDirtySlots]: w0, w1 of slot s at 2s, 2s + 1
+  u64* key;     // [kDirtySlots]
+  u64* w;       // [2 * kDirtySlots]: w0, w1 of slot s at 2s, 2s + 1
+  u32* ready;   // [kDirtySlots] w written
+  u32* first;   // [kDirtySlots]
+  u32* start;   // [kDirtySlots]
+  u32* cnt;     // [kDirtySlots]
+  u32* rslot;   // [kDirtySlots] table slot marked kRecDirty (~0: none)
+  u32* idx;     // [kDirtyCap] dirty messages by (set slot, message)
+  u32* dslot;   // [kDirtyCap] their set slots
+  u64* cell;    // [3 * 2 * kDirtyCap] cell j < kDirtyCap: maxima of the clean messages
+                //   after idx[j]; kDirtyCap + j: the bucket's messages before idx[j], its
+                //   first (its "pre" cell, j the bucket's start)
+  u32* premin;  // [kDirtyCap] the first message of the pre cell of start j
+  static constexpr size_t kWords = 3 * (size_t)kDirtySlots + 5 * (size_t)kDirtySlots / 2 +
+                                   (size_t)kDirtyCap + 6 * (size_t)kDirtyCap +
+                                   (size_t)kDirtyCap / 2;
+  __host__ __device__ static DirtySet at(u64* b) {
+    DirtySet d;
+    d.key = b;
+    d.w = b + kDirtySlots;
+    u32* u = reinterpret_cast<u32*>(b + 3 * (size_t)kDirtySlots);
+    d.ready = u;
+    d.first = u + kDirtySlots;
+    d.start = u + 2 * kDirtySlots;
+    d.cnt = u + 3 * kDirtySlots;
+    d.rslot = u + 4 * kDirtySlots;
+    d.idx = u + 5 * kDirtySlots;
+    d.dslot = d.idx + kDirtyCap;
+    d.cell = b + 3 * (size_t)kDirtySlots + 5 * (size_t)kDirtySlots / 2 + kDirtyCap;
+    d.premin = reinterpret_cast<u32*>(d.cell + 6 * (size_t)kDirtyCap);
+    return d;
+  }
 };
 __device__ inline u32 dirty_home(u64 h) { return (u32)(h ^ (h >> 31)) & (kDirtySlots - 1); }
-__device__ inline bool dirty_find(const DirtySet& D, const Name& nm) {
+// The set slot of a (short) name, or -1.
+__device__ inline int dirty_find(const DirtySet& D, const Name& nm) {
   const u64 k = nm.h ? nm.h : 1;
   for (u32 s = dirty_home(k);; s = (s + 1) & (kDirtySlots - 1)) {
     const u64 x = D.key[s];
-    if (x == 0) return false;
-    if (x == k && D.w[2 * s] == nm.w0 && D.w[2 * s + 1] == nm.w1) return true;
+    if (x == 0) return -1;
+    if (x == k && D.w[2 * s] == nm.w0 && D.w[2 * s + 1] == nm.w1) return (int)s;
   }
+}
+// A cell field back to its replica bits: 0 (no clean message, or only NaN /
+// -Inf, which never win Go's `<`) reads NaN, which never wins either.
+__device__ inline u64 dec_replica_max(u64 x) {
+  if (x == 0) return 0x7FF8000000000000ull;
+  if (x == kInfBits) return 0;                    // +-0 (a clean batch's are +0)
+  if (x > kInfBits) return x - kInfBits - 1;
+  return kSign | (kInfBits - x);
 }
 
 __device__ inline bool replica_dirty(u64 ab, u64 tb, i64 e) {
@@ -899,42 +931,135 @@ __global__ __launch_bounds__(kBlock) void k_classify(In in, u32 n, u32* ctr, u32
 }
 
 // The dirty set of a classified batch (one workgroup, behind the
-// classification): every listed dirty message's name.  A batch with more
-// than kDirtyCap dirty messages, or one whose name is longer than
-// kShortName, is marked (ctr[kCtrNDirty] = ~0): it keeps the prefix rule.
+// classification; a batch without a dirty message returns at once): every
+// listed dirty message's bucket, its dirty messages sorted, its record marked
+// kRecDirty (the fast kernel reads that flag with the record it loads anyway:
+// no set lookup for a clean bucket's message), its cells cleared.  A batch
+// with more than kDirtyCap dirty messages, or one with a name longer than
+// kShortName, is marked (ctr[kCtrNDirty] = ~0) before anything is marked: it
+// keeps the prefix rule.  Dirty messages at or past the batch's stop (a
+// checked batch's first malformed entry) are not read.
 template <class In>
 __global__ __launch_bounds__(1024) void k_dirty_build(In in, u32 n, u32* ctr, const u32* dlist,
-                                                      DirtySet D) {
+                                                      DirtySet D, Table T) {
+  __shared__ u64 sk[kDirtyCap];   // (set slot, message) keys
+  __shared__ u32 longname, nvalid;
   const u32 nd = ctr[kCtrNDirty];
   if (nd == 0 || nd > kDirtyCap) return;
-  for (u32 s = threadIdx.x; s < kDirtySlots; s += 1024) D.key[s] = 0;
+  const u32 tid = threadIdx.x;
+  for (u32 s = tid; s < kDirtySlots; s += 1024) {
+    D.key[s] = 0;
+    D.ready[s] = 0;
+    D.first[s] = ~0u;
+  }
+  if (tid == 0) { longname = 0; nvalid = 0; }
   __syncthreads();
-  bool longname = false;
-  const u32 stop = min(n, ctr[5]);   // (a checked batch's first malformed entry: not read)
-  for (u32 j = threadIdx.x; j < nd; j += 1024) {
+  const u32 stop = min(n, ctr[5]);
+  u32 valid = 0;
+  for (u32 j = tid; j < nd; j += 1024) {
     const u32 i = dlist[j];
-    if (i >= stop) continue;          // (stopped before it: its bucket needs no deferral)
+    sk[j] = ~0ull;
+    if (i >= stop) continue;
     u64 off, w0, w1, w2, ra, rt;
     u32 len;
     i64 re;
     const typename In::Pre p = in.pre(i);
     in.load(i, p, off, len, w0, w1, w2, ra, rt, re);
     if (len > kShortName) {
-      longname = true;
+      longname = 1;
       continue;
     }
     Name nm;
     short_name(w0, w1, w2, off, len, nm);
     const u64 k = nm.h ? nm.h : 1;
-    for (u32 s = dirty_home(k);; s = (s + 1) & (kDirtySlots - 1)) {
-      if (atomicCAS(&D.key[s], 0ull, k) == 0ull) {
+    // One slot per bucket: the lane that claims a key writes its words and
+    // then `ready`; a lane that finds the same key waits for `ready` by
+    // trying again (in the same loop, so lanes of one wave never wait on
+    // each other across a branch).
+    u32 s = dirty_home(k);
+    for (;;) {
+      const u64 old = atomicCAS(&D.key[s], 0ull, k);
+      if (old == 0ull) {
         D.w[2 * s] = nm.w0;
         D.w[2 * s + 1] = nm.w1;
+        __threadfence_block();
+        atomicExch(&D.ready[s], 1u);
         break;
+      }
+      if (old == k) {
+        if (__hip_atomic_load(&D.ready[s], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0)
+          continue;
+        if (D.w[2 * s] == nm.w0 && D.w[2 * s + 1] == nm.w1) break;
+      }
+      s = (s + 1) & (kDirtySlots - 1);
+    }
+    atomicMin(&D.first[s], i);
+    sk[j] = ((u64)s << 32) | i;
+    ++valid;
+  }
+  if (valid) atomicAdd(&nvalid, valid);
+  __syncthreads();
+  if (longname) {
+    if (tid == 0) ctr[kCtrNDirty] = ~0u;
+    return;
+  }
+  // bitonic sort of the keys (the unused ones, ~0, last)
+  u32 P = 1;
+  while (P < nd) P <<= 1;
+  for (u32 j = nd + tid; j < P; j += 1024) sk[j] = ~0ull;
+  __syncthreads();
+  for (u32 k = 2; k <= P; k <<= 1) {
+    for (u32 j = k >> 1; j > 0; j >>= 1) {
+      for (u32 t = tid; t < P; t += 1024) {
+        const u32 u = t ^ j;
+        if (u > t) {
+          const u64 x = sk[t], y = sk[u];
+          if ((x > y) == ((t & k) == 0)) { sk[t] = y; sk[u] = x; }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  const u32 nv = nvalid;
+  for (u32 j = tid; j < nv; j += 1024) {
+    const u32 s = (u32)(sk[j] >> 32);
+    D.idx[j] = (u32)sk[j];
+    D.dslot[j] = s;
+    D.cell[3 * j] = 0; D.cell[3 * j + 1] = 0; D.cell[3 * j + 2] = 0;
+    u64* pc = D.cell + 3 * ((size_t)kDirtyCap + j);
+    pc[0] = 0; pc[1] = 0; pc[2] = 0;
+    D.premin[j] = ~0u;
+    if (j == 0 || (u32)(sk[j - 1] >> 32) != s) D.start[s] = j;
+  }
+  __syncthreads();
+  for (u32 j = tid; j < nv; j += 1024) {
+    const u32 s = (u32)(sk[j] >> 32);
+    if (j + 1 == nv || (u32)(sk[j + 1] >> 32) != s) D.cnt[s] = j + 1 - D.start[s];
+    if (j == 0 || (u32)(sk[j - 1] >> 32) != s) {
+      // the bucket's record, if it has one: marked for the fast kernel
+      const u32 i = (u32)sk[j];
+      u64 off, w0, w1, w2, ra, rt;
+      u32 len;
+      i64 re;
+      const typename In::Pre p = in.pre(i);
+      in.load(i, p, off, len, w0, w1, w2, ra, rt, re);
+      Name nm;
+      short_name(w0, w1, w2, off, len, nm);
+      u32 slot;
+      Rec cur;
+      if (probe(T, nm, in.blob(), &slot, &cur) == kFound) {
+        D.rslot[s] = slot;
+        atomicOr(reinterpret_cast<unsigned long long*>(&T.recs[slot].name0),
+                 (unsigned long long)(kRecDirty << 8));
+      } else {
+        D.rslot[s] = ~0u;
       }
     }
   }
-  if (longname) ctr[kCtrNDirty] = ~0u;
+  if (tid == 0) {
+    ctr[kCtrNSorted] = nv;
+    if (nv == 0) ctr[kCtrNDirty] = 0;   // (every dirty message past the stop)
+  }
 }
 
 // The same for decoded messages with 16-byte aligned replica columns: two
@@ -1027,13 +1152,17 @@ __device__ inline bool tail_match(const u64 (&htail)[kHotTailWords][kHotMax], u3
   return eq;
 }
 
+// Mark byte of a message k_dirty_pass completes (in the status column,
+// whose statuses are < 0x40 or carry 0x80).
+constexpr u8 kMarkDirty = 0x40;
+
 // Messages [lo, n) of the batch (lo a multiple of 64: a segment of a batch
 // classified segment by segment, or 0).
 template <class In>
 __global__ __launch_bounds__(kFastBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_receive_fast(
     In in, u32 lo, u32 n, Table T, Sharded miss, u32* ctr,
-    const HotHdr* __restrict__ hot, const HotEntry* __restrict__ hot_dir, DirtySet dset,
-    Sharded defer) {
+    const HotHdr* __restrict__ hot, const HotEntry* __restrict__ hot_dir, const u64* dtab,
+    u8* __restrict__ mark) {
   __shared__ u32 hslot[kHotLds];        // directory index + 1 (0 = empty)
   __shared__ u64 htag[kHotMax], hw0[kHotMax], hw1[kHotMax], hw2[kHotMax];
   __shared__ u32 hrec[kHotMax], haoff[kHotMax];
@@ -1046,8 +1175,9 @@ __global__ __launch_bounds__(kFastBlock) __attribute__((amdgpu_waves_per_eu(8, 8
   // (ctr[kCtrDirty]) and before the first malformed datagram (ctr[5]); none:
   // ~0.
   // (dirty buckets, decoded batches: with a dirty set, the whole batch up to
-  // the first malformed message, the dirty buckets' messages deferred)
-  const u32 ndr = In::kSoa && defer.base ? ctr[kCtrNDirty] : 0u;
+  // the first malformed message; the messages that may name a dirty bucket
+  // are marked for k_dirty_pass)
+  const u32 ndr = In::kSoa && dtab ? ctr[kCtrNDirty] : 0u;
   const bool iso = ndr != 0 && ndr <= kDirtyCap;
   n = min(n, iso ? ctr[5] : min(ctr[5], ctr[kCtrDirty]));
   if (n <= lo) return;
@@ -1061,7 +1191,9 @@ __global__ __launch_bounds__(kFastBlock) __attribute__((amdgpu_waves_per_eu(8, 8
   for (u32 j = threadIdx.x; j < nh; j += kFastBlock) {
     const HotEntry d = hot_dir[j];
     htag[j] = d.tag; hw0[j] = d.w0; hw1[j] = d.w1; hw2[j] = d.w2;
-    hrec[j] = d.slot; haoff[j] = d.aoff;
+    // (bit 31: a dirty bucket's entry, its record marked by k_dirty_build)
+    hrec[j] = d.slot | (iso && (rec_flags(T.recs[d.slot]) & kRecDirty) ? 0x80000000u : 0u);
+    haoff[j] = d.aoff;
     for (u32 k = 0; k < kHotTailWords; ++k) htail[k][j] = d.tail[k];
     u32 hs = hot_home(d.tag);
     while (atomicCAS(&hslot[hs], 0u, j + 1) != 0) hs = (hs + 1) & (kHotLds - 1);
@@ -1129,8 +1261,7 @@ __global__ __launch_bounds__(kFastBlock) __attribute__((amdgpu_waves_per_eu(8, 8
     const u64 ea = enc_replica_nz(ra), et = enc_replica_nz(rt), ee = (u64)re ^ kSign;
 
     bool missed = false;
-    const bool deferred = iso && valid && dirty_find(dset, nm);
-    if (valid && !deferred) {
+    if (valid) {
       int hidx = -1;
       if (nh) {
         for (u32 hs = hot_home(tag);; hs = (hs + 1) & (kHotLds - 1)) {
@@ -1147,11 +1278,19 @@ __global__ __launch_bounds__(kFastBlock) __attribute__((amdgpu_waves_per_eu(8, 8
           }
         }
       }
+      // A message of a dirty bucket (iso only: its directory entry or record
+      // marked), or a short-named miss that may be one, is marked and left
+      // to k_dirty_pass (a byte store; doing that work here cost this kernel
+      // its registers: 11 spilled, 1.78 -> 2.54 ms on a clean C2 batch).
       if (hidx >= 0) {
-        ++hits;
-        if (ea > hmax[0][hidx]) atomicMax(&hmax[0][hidx], ea);
-        if (et > hmax[1][hidx]) atomicMax(&hmax[1][hidx], et);
-        if (ee > hmax[2][hidx]) atomicMax(&hmax[2][hidx], ee);
+        if (iso && (hrec[hidx] >> 31)) {
+          mark[i] = kMarkDirty;
+        } else {
+          ++hits;
+          if (ea > hmax[0][hidx]) atomicMax(&hmax[0][hidx], ea);
+          if (et > hmax[1][hidx]) atomicMax(&hmax[1][hidx], et);
+          if (ee > hmax[2][hidx]) atomicMax(&hmax[2][hidx], ee);
+        }
       } else {
         // round 3: the home slot
         u32 s = T.home(tag);
@@ -1167,10 +1306,16 @@ __global__ __launch_bounds__(kFastBlock) __attribute__((amdgpu_waves_per_eu(8, 8
           }
         }
         if (pr == kFound) {
-          Rec* r = &T.recs[s];
-          if (ea > cur.added) atomicMax(&r->added, ea);
-          if (et > cur.taken) atomicMax(&r->taken, et);
-          if (ee > ((u64)cur.elapsed ^ kSign)) atomicMax(&r->elapsed, (i64)(ee ^ kSign));
+          if (iso && (rec_flags(cur) & kRecDirty)) {
+            mark[i] = kMarkDirty;
+          } else {
+            Rec* r = &T.recs[s];
+            if (ea > cur.added) atomicMax(&r->added, ea);
+            if (et > cur.taken) atomicMax(&r->taken, et);
+            if (ee > ((u64)cur.elapsed ^ kSign)) atomicMax(&r->elapsed, (i64)(ee ^ kSign));
+          }
+        } else if (iso && shortname) {
+          mark[i] = kMarkDirty;
         } else {
           missed = true;
           if (pr == kFull) atomicOr(&ctr[8], 1u);
@@ -1178,7 +1323,6 @@ __global__ __launch_bounds__(kFastBlock) __attribute__((amdgpu_waves_per_eu(8, 8
       }
     }
     miss.append(chunk, missed, i);
-    if (iso) defer.append(chunk, deferred, i);
   }
   if (hits) atomicAdd(&hhits, hits);
   __syncthreads();
@@ -1191,13 +1335,111 @@ __global__ __launch_bounds__(kFastBlock) __attribute__((amdgpu_waves_per_eu(8, 8
   for (u32 j = threadIdx.x; j < nh; j += kFastBlock) {
     const u64 xa = hmax[0][j], xt = hmax[1][j], xe = hmax[2][j];
     if (!(xa | xt | xe)) continue;
-    Rec* r = &T.recs[hrec[j]];
+    Rec* r = &T.recs[hrec[j] & 0x7FFFFFFFu];
     const u64 ca = r->added, ct = r->taken, ce = (u64)r->elapsed ^ kSign;
     if (xa > ca) atomicMax(&r->added, xa);
     if (xt > ct) atomicMax(&r->taken, xt);
     if (xe > ce) atomicMax(&r->elapsed, (i64)(xe ^ kSign));
   }
 }
+
+// The marked messages of an isolated batch (after k_receive_fast, before the
+// launch that ends the batch; a grid-stride pass over the mark bytes, one
+// message a lane): each names a dirty bucket or is a short-named miss.
+//   - not in the dirty set: a miss (appended to the miss list, as the fast
+//     kernel would have);
+//   - dirty itself: left to the ordered sub-batch (dirty_finish);
+//   - before its bucket's first dirty message: folded into the bucket's pre
+//     cell (its first message kept: its merge may create the bucket);
+//   - after it: folded into the cell of the last dirty message of its bucket
+//     before it (the sorted dirty messages, at most 16 KB, searched in LDS).
+// Cells fold in an LDS cache first (a hot bucket's cells take millions of
+// messages: device atomics on one line serialise, 3.8 ms per C2 dirty
+// batch), flushed with one atomic per field per workgroup; a cell the cache
+// has no room for folds in device memory.
+// Every mark is put back to PHIP_ST_MERGED (the status every fast-path
+// message starts with; the miss path and the sub-batch write theirs after).
+constexpr u32 kCellCache = 2048;
+template <class In>
+__global__ __launch_bounds__(1024) void k_dirty_pass(In in, u32 n, u32* ctr, u8* mark,
+                                                     const u64* dtab, Table T, Sharded miss) {
+  __shared__ u32 sidx[kDirtyCap];
+  __shared__ u32 ckey[kCellCache], cmin[kCellCache];
+  __shared__ u64 cmax[3][kCellCache];
+  const u32 ndr = ctr[kCtrNDirty];
+  if (ndr == 0 || ndr > kDirtyCap) return;
+  n = min(n, ctr[5]);
+  const DirtySet D = DirtySet::at(const_cast<u64*>(dtab));
+  const u32 nv = ctr[kCtrNSorted];
+  for (u32 j = threadIdx.x; j < nv; j += 1024) sidx[j] = D.idx[j];
+  for (u32 j = threadIdx.x; j < kCellCache; j += 1024) {
+    ckey[j] = 0; cmin[j] = ~0u;
+    cmax[0][j] = 0; cmax[1][j] = 0; cmax[2][j] = 0;
+  }
+  __syncthreads();
+  const u32 stride = gridDim.x * 1024;
+  for (u32 i = blockIdx.x * 1024 + threadIdx.x; i < n; i += stride) {
+    if (mark[i] != kMarkDirty) continue;
+    u64 off, w0, w1, w2, ra, rt;
+    u32 len;
+    i64 re;
+    const typename In::Pre p = in.pre(i);
+    in.load(i, p, off, len, w0, w1, w2, ra, rt, re);
+    Name nm;
+    short_name(w0, w1, w2, off, len, nm);
+    mark[i] = PHIP_ST_MERGED;
+    const int s = dirty_find(D, nm);
+    if (s < 0) {   // a miss of a clean bucket
+      const u32 sh = (i / 64) & (kShards - 1);
+      miss.base[(size_t)sh * miss.cap + atomicAdd(&miss.cnt[sh], 1u)] = i;
+      continue;
+    }
+    if (replica_dirty(ra, rt, re)) continue;
+    u32 lo = D.start[s];
+    u32 cid;
+    if (i < D.first[s]) {
+      cid = kDirtyCap + lo;   // the pre cell
+    } else {
+      u32 hi = lo + D.cnt[s];
+      while (hi - lo > 1) {   // the last dirty message before i (sidx[lo] < i)
+        const u32 mid = (lo + hi) / 2;
+        if (sidx[mid] < i) lo = mid; else hi = mid;
+      }
+      cid = lo;
+    }
+    const u64 ea = enc_replica_nz(ra), et = enc_replica_nz(rt), ee = (u64)re ^ kSign;
+    u32 h = (cid * 2654435761u) >> (32 - 11);
+    int slot = -1;
+    for (u32 k = 0; k < 16; ++k, h = (h + 1) & (kCellCache - 1)) {
+      const u32 old = atomicCAS(&ckey[h], 0u, cid + 1);
+      if (old == 0u || old == cid + 1) { slot = (int)h; break; }
+    }
+    if (slot >= 0) {
+      if (ea > cmax[0][slot]) atomicMax(&cmax[0][slot], ea);
+      if (et > cmax[1][slot]) atomicMax(&cmax[1][slot], et);
+      if (ee > cmax[2][slot]) atomicMax(&cmax[2][slot], ee);
+      if (cid >= kDirtyCap && i < cmin[slot]) atomicMin(&cmin[slot], i);
+    } else {
+      u64* cl = D.cell + 3 * (size_t)cid;
+      atomicMax(reinterpret_cast<unsigned long long*>(&cl[0]), ea);
+      atomicMax(reinterpret_cast<unsigned long long*>(&cl[1]), et);
+      atomicMax(reinterpret_cast<unsigned long long*>(&cl[2]), ee);
+      if (cid >= kDirtyCap) atomicMin(&D.premin[cid - kDirtyCap], i);
+    }
+  }
+  __syncthreads();
+  for (u32 j = threadIdx.x; j < kCellCache; j += 1024) {
+    const u32 k = ckey[j];
+    if (!k) continue;
+    const u32 cid = k - 1;
+    u64* cl = D.cell + 3 * (size_t)cid;
+    atomicMax(reinterpret_cast<unsigned long long*>(&cl[0]), cmax[0][j]);
+    atomicMax(reinterpret_cast<unsigned long long*>(&cl[1]), cmax[1][j]);
+    atomicMax(reinterpret_cast<unsigned long long*>(&cl[2]), cmax[2][j]);
+    if (cid >= kDirtyCap) atomicMin(&D.premin[cid - kDirtyCap], cmin[j]);
+  }
+}
+
 
 // The messages of a list (the fast batch's misses, after the insert
 // pipeline created their buckets): GetBucket + Merge with creator tracking
@@ -1612,25 +1854,118 @@ __global__ void k_decode(const u8* __restrict__ bytes, const uint64_t* __restric
   }
 }
 
-// The deferred messages as an ordered sub-batch: message list[j] of a
-// decoded batch as entry j (its name in place in the batch's blob, NamesPairs;
-// its replica fields copied).
-__global__ void k_defer_gather(NamesOffs src, const uint64_t* __restrict__ a,
-                               const uint64_t* __restrict__ t, const int64_t* __restrict__ e,
-                               const u32* __restrict__ list, u32 nd, uint64_t* __restrict__ off2,
-                               u8* __restrict__ len2, uint64_t* __restrict__ a2,
-                               uint64_t* __restrict__ t2, int64_t* __restrict__ e2) {
-  const u32 j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= nd) return;
-  const u32 i = list[j];
-  u64 off;
-  u32 len;
-  src.get(i, off, len);
-  off2[j] = off;
-  len2[j] = (u8)len;
-  a2[j] = a[i];
-  t2[j] = t[i];
-  e2[j] = e[i];
+// After the fast kernel (one workgroup): the dirty buckets' records
+// unmarked, and the ordered sub-batch built -- per dirty bucket, in
+// (bucket, message) order: its pre cell as one merge (its messages before its
+// first dirty message), then each of its dirty messages followed by its
+// cell as one merge (a cell whose maxima read +0, +0, 0 would read as an
+// incast: it is split in two merges, (+0, +0, min) and (NaN, NaN, 0), the
+// same effect).  Entries name their bucket by its dirty message's name (in
+// place in the batch's blob); map2 holds the message an entry's status and
+// reply go back to: the message itself, a pre cell's first message (its
+// merge may create the bucket: PHIP_ST_CREATED), ~0 for a later cell's merge
+// (its messages keep PHIP_ST_MERGED: the bucket exists by then).
+// The entry count lands in ctr[kCtrNDefer].
+// (one workgroup of kShards lanes; k_batch_end runs it before the batch's
+// shard scan, in one launch)
+struct SubOut {
+  uint64_t* off;
+  u8* len;
+  uint64_t* a;
+  uint64_t* t;
+  int64_t* e;
+  u32* map;
+};
+template <class In>
+__device__ inline void dirty_finish(const In& in, u32* ctr, const DirtySet& D, const Table& T,
+                                    const SubOut& so) {
+  __shared__ u32 part[kShards];
+  uint64_t* __restrict__ off2 = so.off;
+  u8* __restrict__ len2 = so.len;
+  uint64_t* __restrict__ a2 = so.a;
+  uint64_t* __restrict__ t2 = so.t;
+  int64_t* __restrict__ e2 = so.e;
+  u32* __restrict__ map2 = so.map;
+  const u32 tid = threadIdx.x;
+  const u32 nd = ctr[kCtrNDirty];
+  if (nd == 0 || nd > kDirtyCap) {
+    if (tid == 0) ctr[kCtrNDefer] = 0;
+    return;
+  }
+  const u32 nv = ctr[kCtrNSorted];
+  // thread tid: set entries [j0, j1), up to three sub-batch entries each
+  const u32 per = (nv + kShards - 1) / kShards;
+  const u32 j0 = min(nv, tid * per), j1 = min(nv, j0 + per);
+  // entries of a cell's merge: 0 (empty), 1, or 2 (maxima +0, +0, 0 read
+  // as an incast: split in two merges of the same effect)
+  auto cell_n = [&](const u64* c) -> u32 {
+    if (!(c[0] | c[1] | c[2])) return 0u;
+    return c[0] == kInfBits && c[1] == kInfBits && c[2] == kSign ? 2u : 1u;
+  };
+  auto is_start = [&](u32 j) { return j == 0 || D.dslot[j - 1] != D.dslot[j]; };
+  u32 c = 0;
+  for (u32 j = j0; j < j1; ++j) {
+    c += 1 + cell_n(D.cell + 3 * j);
+    if (is_start(j)) {
+      c += cell_n(D.cell + 3 * ((size_t)kDirtyCap + j));
+      const u32 s = D.dslot[j];
+      if (D.rslot[s] != ~0u)
+        atomicAnd(reinterpret_cast<unsigned long long*>(&T.recs[D.rslot[s]].name0),
+                  ~(unsigned long long)(kRecDirty << 8));
+    }
+  }
+  part[tid] = c;
+  __syncthreads();
+  for (u32 off = 1; off < kShards; off <<= 1) {   // inclusive scan
+    const u32 v = tid >= off ? part[tid - off] : 0u;
+    __syncthreads();
+    part[tid] += v;
+    __syncthreads();
+  }
+  u32 o = part[tid] - c;
+  auto emit_cell = [&](const u64* cl, u64 off, u32 len, u32 to) {
+    const u32 k = cell_n(cl);
+    if (k == 0) return;
+    off2[o] = off; len2[o] = (u8)len; map2[o] = to;
+    if (k == 2) {
+      a2[o] = 0; t2[o] = 0; e2[o] = (int64_t)kSign;
+      ++o;
+      off2[o] = off; len2[o] = (u8)len; map2[o] = ~0u;
+      a2[o] = 0x7FF8000000000000ull; t2[o] = 0x7FF8000000000000ull; e2[o] = 0;
+    } else {
+      a2[o] = dec_replica_max(cl[0]); t2[o] = dec_replica_max(cl[1]);
+      e2[o] = (int64_t)(cl[2] ^ kSign);
+    }
+    ++o;
+  };
+  for (u32 j = j0; j < j1; ++j) {
+    const u32 i = D.idx[j];
+    u64 off;
+    u32 len;
+    in.src.get(i, off, len);
+    // the bucket's messages before its first dirty message: one merge, whose
+    // status (it may create the bucket) goes to the first of them
+    if (is_start(j)) emit_cell(D.cell + 3 * ((size_t)kDirtyCap + j), off, len, D.premin[j]);
+    off2[o] = off; len2[o] = (u8)len;
+    a2[o] = in.ma[i]; t2[o] = in.mt[i]; e2[o] = in.me[i];
+    map2[o] = i;
+    ++o;
+    emit_cell(D.cell + 3 * j, off, len, ~0u);
+  }
+  if (tid == kShards - 1) ctr[kCtrNDefer] = part[kShards - 1];
+}
+
+// The end of a decoded fast batch in one launch: dirty_finish (an isolated
+// batch's sub-batch; nothing otherwise), then the miss list's shard scan
+// (k_shard_scan: counters to the host mirror, the next batch's reset).
+template <class In>
+__global__ __launch_bounds__(kShards) void k_batch_end(In in, u32* ctr, const u64* dtab, Table T,
+                                                       SubOut so, u32* cnt, u32* host, u32 words,
+                                                       u32* next) {
+  dirty_finish(in, ctr, DirtySet::at(const_cast<u64*>(dtab)), T, so);
+  __threadfence_block();
+  __syncthreads();
+  shard_scan(cnt, ctr, 2, host, words, next);
 }
 
 // ------------------------------------------------------------ ordered ----
@@ -1650,12 +1985,14 @@ struct OutView {
   phip_state* reply;
 };
 
-// The deferred sub-batch's statuses and replies back to their messages.
-__global__ void k_defer_scatter(const u32* __restrict__ list, u32 nd, const u8* __restrict__ st2,
+// The ordered sub-batch's statuses and replies back to their messages
+// (dirty_finish's map2; ~0: a cell's merge, no output).
+__global__ void k_defer_scatter(const u32* __restrict__ map2, u32 nd, const u8* __restrict__ st2,
                                 const phip_state* __restrict__ rep2, OutView ow) {
   const u32 j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= nd) return;
-  const u32 i = list[j];
+  const u32 i = map2[j];
+  if (i == ~0u) return;
   if (ow.status) ow.status[i] = st2[j];
   if (ow.reply) ow.reply[i] = rep2[j];
 }
