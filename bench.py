@@ -847,11 +847,16 @@ def run_c2_variants_leg(args, torch, dist, dev, local, rank, world):
       uniform   keys uniform over the 10M buckets (SURVEY §8d C1/C4's
                 "uniform variant"): no hot bucket, every message reads a
                 random record line;
-      names32   32-byte names "b" + "x"... + decimal id (arena names, up to
-                231 B per bucket.go:36-44; the headline's are 2-8 B);
+      names15   15-byte names "b" + "x"... + decimal id (one byte past the
+                14 a record holds inline with its 2-byte header: the inline
+                form, bucket.go:36-44);
+      names32   32-byte names (arena names, up to 231 B per
+                bucket.go:36-44; the headline's are 2-8 B);
       dirty     the headline batch with 64 incasts and 64 -0.0 fields at
                 random places (repo.go:86-90's incast, Go's asymmetric `<`
-                on zeros): the messages Receive must see in order.
+                on zeros): the messages Receive must see in order (their
+                buckets through the ordered path's sub-batch, the rest
+                merged: phip_kernels.hpp "Dirty buckets").
     `verified` per variant: 2^14 sampled bucket ids (plus the 256 hottest
     Zipf ranks) read back through phip_export_datagrams equal an
     independent max-reduce of every applied message naming them (torch
@@ -861,8 +866,8 @@ def run_c2_variants_leg(args, torch, dist, dev, local, rank, world):
     K, n, L = args.keys, args.messages, args.log2_slots
     warm, steps = 1, max(1, min(args.steps, 3))
     out = {}
-    for name, zipf, width in (("uniform", 0.0, 0), ("names32", args.zipf, 32),
-                              ("dirty", args.zipf, 0)):
+    for name, zipf, width in (("uniform", 0.0, 0), ("names15", args.zipf, 15),
+                              ("names32", args.zipf, 32), ("dirty", args.zipf, 0)):
         gen = torch.Generator(device=dev).manual_seed(args.seed + 404 + 7919 * rank + width)
         base = rank * K
         arena = max(1 << 20, K * (width + 8)) if width > 22 else 1 << 20

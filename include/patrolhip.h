@@ -113,7 +113,7 @@ enum {
                                         batches run many pack / exchange rounds */
 #define PHIP_RECV_ASYNC 0x20u /* phip_receive_soa with PHIP_DEVICE_PTRS, >= 2^16 messages: the
                                  call queues the batch and returns; the batch is finished
-                                 (misses created, a dirty suffix through the ordered path,
+                                 (misses created, its dirty buckets through the ordered path,
                                  outputs final) by the handle's next call or phip_flush,
                                  which also returns its error (phip_len and phip_capacity
                                  finish it too, and leave its error to the handle's next
@@ -302,7 +302,16 @@ int phip_dump(phip_handle* h, uint8_t* names, uint64_t names_cap, uint64_t* name
 int phip_receive_datagrams(phip_handle* h, const uint8_t* bytes, const uint64_t* offs, uint32_t n,
                            int64_t now, const phip_results* res, uint32_t* stop_index,
                            uint32_t flags);
-/* The same loop over pre-decoded states. */
+/* The same loop over pre-decoded states.
+ * Order: a message's result depends only on the earlier messages naming its
+ * bucket (repo.go:77-106), and only incasts (a zero state) and -0.0 fields
+ * make that order visible.  A batch with at most 4096 such "dirty" messages,
+ * each named in at most 14 bytes, has its other buckets merged in one
+ * order-free pass and only its dirty buckets' sequences (each dirty message,
+ * and one merge of the clean messages between two of them) applied in order
+ * afterwards (phip_kernels.hpp "Dirty buckets").  phip_receive_datagrams and
+ * larger dirty sets apply everything from the first dirty message on in
+ * order.  The results are the Go loop's either way. */
 int phip_receive_soa(phip_handle* h, const phip_msgs* m, int64_t now, const phip_results* res,
                      uint32_t flags);
 /* LocalRepo.UpsertBucket for each state, in order. */
@@ -593,8 +602,8 @@ void phip_set_timing(phip_handle* h, int on);
  * entries, out[1] messages folded through the directory, out[2] messages
  * that missed the table (inserted); out[3] table growths (rehashes) since
  * phip_open; out[4] messages of the batch that went through the ordered path
- * (its dirty buckets' messages, or its suffix from the first dirty message:
- * PHIP_RECV_* "Dirty buckets").  Returns the number written (<= 5). */
+ * (the dirty buckets' sub-batch, or the suffix from the first dirty
+ * message: phip_receive_soa).  Returns the number written (<= 5). */
 int phip_last_stats(phip_handle* h, uint64_t* out, int max);
 /* Placement quality of the table (one scan of the slots): out[0] buckets,
  * out[1] slots, out[2] the longest probe distance of a bucket from its home

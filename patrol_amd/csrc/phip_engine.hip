@@ -112,10 +112,11 @@ struct phip_handle {
   u8* arena = nullptr;
   u64 arena_cap = 0;
   u64* arena_cursor = nullptr;
-  u32* ctr = nullptr;        // device counters [16]
+  u32* ctr = nullptr;        // device counters: kCtrWords general, then two fast-pass sets (fctr)
   u32* ctr_host = nullptr;   // pinned mirror
   u32* ctr_map = nullptr;    // ctr_host as the device sees it (k_shard_scan stores there)
   u32 fpar = 0;              // parity of the last fast batch (its shard counters in B_FSCNT)
+  u64 nfast = 0;             // fast passes begun (a queued front is redone after a nested one)
   u64 n_buckets = 0;
   u64 tag_mask = ~0ull;
   u64 seed = 0;              // placement seed (Table::home, seeded_mix)
@@ -128,7 +129,7 @@ struct phip_handle {
   u8* small_pin = nullptr;   // pinned staging of small ordered batches (both ways)
   size_t small_pin_cap = 0;
   // PHIP_RECV_ASYNC: a decoded batch whose fast pass is queued; its counters
-  // are read, and its misses / dirty suffix finished, at the handle's next
+  // are read, and its misses / dirty buckets finished, at the handle's next
   // call (or phip_flush)
   struct Pending {
     bool active = false;
@@ -607,7 +608,8 @@ int sharded(phip_handle* h, BufId base_id, u32 units, u32 per_unit, Sharded* out
 // Pack a sharded list into `out`: the total lands in ctr[total_slot] and is
 // returned in *total (one counter read-back).
 int pack_sharded(phip_handle* h, const Sharded& sh, u32 total_slot, u32* out, u32* total) {
-  k_shard_scan<<<1, kShards, 0, h->stream>>>(sh.cnt, h->ctr, total_slot, nullptr, 0, nullptr);
+  k_shard_scan<<<1, kShards, 0, h->stream>>>(sh.cnt, h->ctr, total_slot, nullptr, 0, nullptr,
+                                             nullptr);
   HIPCHK(h, hipGetLastError());
   int rc;
   if ((rc = read_ctr(h))) return rc;
@@ -640,8 +642,16 @@ struct FastFront {
   const HotHdr* hot = nullptr;
   const HotEntry* dir = nullptr;
   u32 par = 0;
+  u32* c = nullptr;     // the pass's counter set (fctr)
   u8* mark = nullptr;   // decoded batches: the status column, or a cleared one (k_dirty_pass)
 };
+
+// A fast pass's device counters: one of two sets by batch parity, apart
+// from the general set every other path uses (ordered batches, inserts, the
+// miss path), so that a queued batch's front -- its classification's
+// counters -- survives the previous batch's leftover work, and is queued
+// again only when that work ran a nested fast pass or grew the table.
+inline u32* fctr(phip_handle* h, u32 par) { return h->ctr + kCtrWords * (1 + par); }
 
 inline u32* fast_counts(phip_handle* h, u32 par) {
   return (u32*)h->buf[B_FSCNT].p + par * 2 * kShards;
@@ -708,8 +718,10 @@ int fast_front(phip_handle* h, In in, HotSrc hsrc, u32 n, u8* status, FastFront*
     }
   }
   ff->par = h->fpar ^= 1u;
+  ff->c = fctr(h, ff->par);
+  ++h->nfast;
   if (reset) {
-    k_batch_reset<<<1, kShards, 0, h->stream>>>(h->ctr, fast_counts(h, ff->par));
+    k_batch_reset<<<1, kShards, 0, h->stream>>>(ff->c, fast_counts(h, ff->par));
     HIPCHK(h, hipGetLastError());
   }
   const bool with_hot = n >= kHotMinBatch;
@@ -720,7 +732,7 @@ int fast_front(phip_handle* h, In in, HotSrc hsrc, u32 n, u8* status, FastFront*
   // column is filled with PHIP_ST_MERGED up front (by k_classify_soa2 as it
   // streams the batch, else a fill on the main stream), and every message
   // the kernel leaves is written again after it (k_receive_list and
-  // k_mark_created for misses, the ordered path for the dirty suffix).  Byte
+  // k_mark_created for misses, the ordered path for dirty buckets).  Byte
   // stores from the fast kernel's lanes cost it 2%; a fill on stream2 beside
   // the classification slowed the classification more than it cost here
   // (DESIGN.md §4).
@@ -736,7 +748,7 @@ int fast_front(phip_handle* h, In in, HotSrc hsrc, u32 n, u8* status, FastFront*
         NamesOffs chk{};
         if constexpr (In::kOffs) chk = in.src;
         k_classify_soa2<<<grid_for((n + 1) / 2), kBlock, 0, h->stream>>>(in.ma, in.mt, in.me, n,
-                                                                          h->ctr, status, chk,
+                                                                          ff->c, status, chk,
                                                                           dlist);
         done = true;
       }
@@ -744,7 +756,7 @@ int fast_front(phip_handle* h, In in, HotSrc hsrc, u32 n, u8* status, FastFront*
     if (!done) {
       if (status) HIPCHK(h, hipMemsetAsync(status, PHIP_ST_MERGED, n, h->stream));
       Launch l(h, "k_classify");
-      k_classify<In><<<grid_for(n), kBlock, 0, h->stream>>>(in, n, h->ctr, dlist);
+      k_classify<In><<<grid_for(n), kBlock, 0, h->stream>>>(in, n, ff->c, dlist);
     }
   }
   HIPCHK(h, hipGetLastError());
@@ -768,14 +780,14 @@ int fast_back(phip_handle* h, In in, u32 n, const FastFront& ff, bool queued) {
     // message returns at once: one launch of ~3 us)
     if ((rc = dirty_set(h, &dset, &dlist)) || (rc = sub_batch(h, &sb))) return rc;
     Launch l(h, "k_dirty_build");
-    k_dirty_build<In><<<1, 1024, 0, h->stream>>>(in, n, h->ctr, dlist, dset, table(h));
+    k_dirty_build<In><<<1, 1024, 0, h->stream>>>(in, n, ff.c, dlist, dset, table(h));
     HIPCHK(h, hipGetLastError());
   }
   if ((rc = join_hot(h, ff.hot))) return rc;
   {
     Launch l(h, "k_receive_fast");
     k_receive_fast<In><<<fast_grid(h, n), kFastBlock, 0, h->stream>>>(in, 0, n, table(h), msh,
-                                                                      h->ctr, ff.hot, ff.dir,
+                                                                      ff.c, ff.hot, ff.dir,
                                                                       dset.key, ff.mark);
   }
   HIPCHK(h, hipGetLastError());
@@ -787,15 +799,17 @@ int fast_back(phip_handle* h, In in, u32 n, const FastFront& ff, bool queued) {
       Launch l(h, "k_dirty_pass");
       const unsigned g = (unsigned)std::max<u64>(
           1, std::min<u64>(((u64)n + 1023) / 1024, (u64)h->ncu * 2));
-      k_dirty_pass<In><<<g, 1024, 0, h->stream>>>(in, n, h->ctr, ff.mark, dset.key, table(h), msh);
+      k_dirty_pass<In><<<g, 1024, 0, h->stream>>>(in, n, ff.c, ff.mark, dset.key, table(h), msh);
       HIPCHK(h, hipGetLastError());
     }
     k_batch_end<In><<<1, kShards, 0, h->stream>>>(
-        in, h->ctr, dset.key, table(h), SubOut{sb.off, sb.len, sb.a, sb.t, sb.e, sb.map}, msh.cnt,
-        h->ctr_map, kCtrWords, queued ? fast_counts(h, ff.par ^ 1u) : nullptr);
+        in, ff.c, dset.key, table(h), SubOut{sb.off, sb.len, sb.a, sb.t, sb.e, sb.map}, msh.cnt,
+        h->ctr_map, kCtrWords, queued ? fast_counts(h, ff.par ^ 1u) : nullptr,
+        fctr(h, ff.par ^ 1u));
   } else {
-    k_shard_scan<<<1, kShards, 0, h->stream>>>(msh.cnt, h->ctr, 2, h->ctr_map, kCtrWords,
-                                               queued ? fast_counts(h, ff.par ^ 1u) : nullptr);
+    k_shard_scan<<<1, kShards, 0, h->stream>>>(msh.cnt, ff.c, 2, h->ctr_map, kCtrWords,
+                                               queued ? fast_counts(h, ff.par ^ 1u) : nullptr,
+                                               fctr(h, ff.par ^ 1u));
   }
   HIPCHK(h, hipGetLastError());
   HIPCHK(h, hipEventRecord(h->ev_ctr, h->stream));
@@ -1493,7 +1507,7 @@ int receive_decoded(phip_handle* h, Src src, const uint64_t* a, const uint64_t* 
 }
 
 // PHIP_RECV_ASYNC: the queued batch's counters, then what its fast pass left
-// (misses, the dirty suffix).  *worked: whether anything was left (its work
+// (misses, dirty buckets).  *worked: whether anything was left (its work
 // has used the counters and maybe moved the table).
 int finish_pending(phip_handle* h, bool* worked) {
   if (worked) *worked = false;
@@ -1922,7 +1936,7 @@ int phip_open(const phip_config* cfg, phip_handle** out) {
   if ((e = hipMalloc(&h->aux, h->cap * sizeof(u32))) != hipSuccess) return fail(e);
   if ((e = hipMalloc(&h->arena, h->arena_cap + 64)) != hipSuccess) return fail(e);
   if ((e = hipMalloc(&h->arena_cursor, 64)) != hipSuccess) return fail(e);
-  if ((e = hipMalloc(&h->ctr, kCtrWords * sizeof(u32))) != hipSuccess) return fail(e);
+  if ((e = hipMalloc(&h->ctr, 3 * kCtrWords * sizeof(u32))) != hipSuccess) return fail(e);
   if ((e = hipHostMalloc(&h->ctr_host, kCtrWords * sizeof(u32),
                          hipHostMallocMapped | hipHostMallocCoherent)) != hipSuccess ||
       (e = hipHostGetDevicePointer((void**)&h->ctr_map, h->ctr_host, 0)) != hipSuccess)
@@ -1930,7 +1944,7 @@ int phip_open(const phip_config* cfg, phip_handle** out) {
   if ((e = hipMemsetAsync(h->recs, 0, h->cap * sizeof(Rec), h->stream)) != hipSuccess) return fail(e);
   if ((e = hipMemsetAsync(h->aux, 0, h->cap * sizeof(u32), h->stream)) != hipSuccess) return fail(e);
   if ((e = hipMemsetAsync(h->arena_cursor, 0, 64, h->stream)) != hipSuccess) return fail(e);
-  if ((e = hipMemsetAsync(h->ctr, 0, kCtrWords * sizeof(u32), h->stream)) != hipSuccess)
+  if ((e = hipMemsetAsync(h->ctr, 0, 3 * kCtrWords * sizeof(u32), h->stream)) != hipSuccess)
     return fail(e);
   if ((e = hipStreamSynchronize(h->stream)) != hipSuccess) return fail(e);
   *out = h;
@@ -2268,8 +2282,9 @@ int phip_receive_soa(phip_handle* h, const phip_msgs* m, int64_t now, const phip
     // Queue this batch's front (reset, directory, status fill,
     // classification) behind the batch queued before, read that batch's
     // counters meanwhile and finish it, then queue this batch's fast pass
-    // and return.  A previous batch that left work (misses, a dirty suffix)
-    // used the counters and the directory buffers: the front is queued again.
+    // and return.  The front's counters are a fast-pass set of their own
+    // (fctr), so the previous batch's leftover work leaves it standing
+    // unless that work ran a fast pass itself or grew the table (below).
     if (int rc0 = begin_call(h, false)) return rc0;
     NamesOffs src{m->names, m->name_offs, m->names_len};
     SoaIn<NamesOffs> in{src, m->added, m->taken, m->elapsed};
@@ -2280,8 +2295,15 @@ int phip_receive_soa(phip_handle* h, const phip_msgs* m, int64_t now, const phip
     if ((rc = outputs(h, res, n, true, &ow))) return rc;
     const bool prev = h->pend.active;
     if ((rc = fast_front(h, in, src, n, ow.status, &ff, !prev))) return after_error(h, rc);
+    const u64 nfast = h->nfast, grows = h->grows;
     if (prev && (rc = finish_pending(h, &worked))) return after_error(h, rc);
-    if (worked && (rc = fast_front(h, in, src, n, ow.status, &ff))) return after_error(h, rc);
+    // The leftover work of the batch before (its misses, its dirty buckets)
+    // runs on the general counters and leaves this front standing, unless it
+    // ran a fast pass of its own (the directory and dirty list buffers) or
+    // grew the table (the directory's slots).
+    if (worked && (h->nfast != nfast || h->grows != grows) &&
+        (rc = fast_front(h, in, src, n, ow.status, &ff)))
+      return after_error(h, rc);
     if ((rc = fast_back(h, in, n, ff, true))) return after_error(h, rc);
     h->pend.active = true;
     h->pend.src = src;

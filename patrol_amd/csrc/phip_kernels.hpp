@@ -231,14 +231,17 @@ __global__ __launch_bounds__(kShards) void k_batch_reset(u32* ctr, u32* shard_cn
 // the largest shard into ctr[13].  With `host` (the handle's pinned counter
 // mirror, mapped into the device's address space), the first `words` counter
 // words are then stored there, which ends a fast batch without a copy; with
-// `next`, the batch counters and the next batch's shard counters are reset as
-// k_batch_reset does, so a queued batch's successor needs no reset launch.
-__device__ inline void shard_scan(u32* cnt, u32* ctr, u32 tot, u32* host, u32 words, u32* next);
+// `next`, the next batch's counters (next_ctr: the other fast set) and its
+// shard counters are reset as k_batch_reset does, so a queued batch's
+// successor needs no reset launch.
+__device__ inline void shard_scan(u32* cnt, u32* ctr, u32 tot, u32* host, u32 words, u32* next,
+                                  u32* next_ctr);
 __global__ __launch_bounds__(kShards) void k_shard_scan(u32* cnt, u32* ctr, u32 tot, u32* host,
-                                                        u32 words, u32* next) {
-  shard_scan(cnt, ctr, tot, host, words, next);
+                                                        u32 words, u32* next, u32* next_ctr) {
+  shard_scan(cnt, ctr, tot, host, words, next, next_ctr);
 }
-__device__ inline void shard_scan(u32* cnt, u32* ctr, u32 tot, u32* host, u32 words, u32* next) {
+__device__ inline void shard_scan(u32* cnt, u32* ctr, u32 tot, u32* host, u32 words, u32* next,
+                                  u32* next_ctr) {
   __shared__ u32 v[kShards];
   __shared__ u32 wmax[kShards / 64];
   const u32 t = threadIdx.x, c = cnt[t];
@@ -266,8 +269,7 @@ __device__ inline void shard_scan(u32* cnt, u32* ctr, u32 tot, u32* host, u32 wo
     __hip_atomic_store(&host[t], w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   if (next) {
-    __syncthreads();
-    if (t < 16) ctr[t] = (t == 5 || t == 12) ? ~0u : 0u;
+    if (t < 16) next_ctr[t] = (t == 5 || t == 12) ? ~0u : 0u;
     next[t] = 0;
   }
 }
@@ -779,7 +781,7 @@ __global__ void k_hot_build(const u32* __restrict__ ckeys, const u32* __restrict
 // Statuses: the caller's status column is filled with PHIP_ST_MERGED
 // before the kernel (by k_classify_soa2, or a fill beside k_classify); every
 // message the kernel does not merge is written again later (misses by the
-// miss path, the dirty suffix by the ordered path).
+// miss path, dirty buckets by the ordered path).
 // Persistent workgroups; every wave walks its own 64-message chunks
 // (grid-stride over waves, no workgroup barrier inside the loop, so a wave
 // waiting on a table read never holds up another).  Per message:
@@ -1961,11 +1963,11 @@ __device__ inline void dirty_finish(const In& in, u32* ctr, const DirtySet& D, c
 template <class In>
 __global__ __launch_bounds__(kShards) void k_batch_end(In in, u32* ctr, const u64* dtab, Table T,
                                                        SubOut so, u32* cnt, u32* host, u32 words,
-                                                       u32* next) {
+                                                       u32* next, u32* next_ctr) {
   dirty_finish(in, ctr, DirtySet::at(const_cast<u64*>(dtab)), T, so);
   __threadfence_block();
   __syncthreads();
-  shard_scan(cnt, ctr, 2, host, words, next);
+  shard_scan(cnt, ctr, 2, host, words, next, next_ctr);
 }
 
 // ------------------------------------------------------------ ordered ----
