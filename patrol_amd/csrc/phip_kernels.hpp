@@ -1361,13 +1361,15 @@ __global__ __launch_bounds__(kFastBlock) __attribute__((amdgpu_waves_per_eu(8, 8
 // has no room for folds in device memory.
 // Every mark is put back to PHIP_ST_MERGED (the status every fast-path
 // message starts with; the miss path and the sub-batch write theirs after).
-constexpr u32 kCellCache = 2048;
+constexpr u32 kCellCacheBits = 10;
+constexpr u32 kCellCache = 1u << kCellCacheBits;
 template <class In>
 __global__ __launch_bounds__(1024) void k_dirty_pass(In in, u32 n, u32* ctr, u8* mark,
                                                      const u64* dtab, Table T, Sharded miss) {
   __shared__ u32 sidx[kDirtyCap];
   __shared__ u32 ckey[kCellCache], cmin[kCellCache];
   __shared__ u64 cmax[3][kCellCache];
+  __shared__ u32 queue[16][128];   // per wave: marked messages waiting for a full wave
   const u32 ndr = ctr[kCtrNDirty];
   if (ndr == 0 || ndr > kDirtyCap) return;
   n = min(n, ctr[5]);
@@ -1379,9 +1381,7 @@ __global__ __launch_bounds__(1024) void k_dirty_pass(In in, u32 n, u32* ctr, u8*
     cmax[0][j] = 0; cmax[1][j] = 0; cmax[2][j] = 0;
   }
   __syncthreads();
-  const u32 stride = gridDim.x * 1024;
-  for (u32 i = blockIdx.x * 1024 + threadIdx.x; i < n; i += stride) {
-    if (mark[i] != kMarkDirty) continue;
+  auto process = [&](u32 i) {
     u64 off, w0, w1, w2, ra, rt;
     u32 len;
     i64 re;
@@ -1394,9 +1394,9 @@ __global__ __launch_bounds__(1024) void k_dirty_pass(In in, u32 n, u32* ctr, u8*
     if (s < 0) {   // a miss of a clean bucket
       const u32 sh = (i / 64) & (kShards - 1);
       miss.base[(size_t)sh * miss.cap + atomicAdd(&miss.cnt[sh], 1u)] = i;
-      continue;
+      return;
     }
-    if (replica_dirty(ra, rt, re)) continue;
+    if (replica_dirty(ra, rt, re)) return;
     u32 lo = D.start[s];
     u32 cid;
     if (i < D.first[s]) {
@@ -1410,7 +1410,7 @@ __global__ __launch_bounds__(1024) void k_dirty_pass(In in, u32 n, u32* ctr, u8*
       cid = lo;
     }
     const u64 ea = enc_replica_nz(ra), et = enc_replica_nz(rt), ee = (u64)re ^ kSign;
-    u32 h = (cid * 2654435761u) >> (32 - 11);
+    u32 h = (cid * 2654435761u) >> (32 - kCellCacheBits);
     int slot = -1;
     for (u32 k = 0; k < 16; ++k, h = (h + 1) & (kCellCache - 1)) {
       const u32 old = atomicCAS(&ckey[h], 0u, cid + 1);
@@ -1428,7 +1428,34 @@ __global__ __launch_bounds__(1024) void k_dirty_pass(In in, u32 n, u32* ctr, u8*
       atomicMax(reinterpret_cast<unsigned long long*>(&cl[2]), ee);
       if (cid >= kDirtyCap) atomicMin(&D.premin[cid - kDirtyCap], i);
     }
+  };
+  // Each wave walks 64-message chunks and queues its marked messages in LDS;
+  // a full queue is processed a message a lane (a dirty batch marks a third
+  // of its messages, scattered: processed in place, two lanes in three idle).
+  const u32 w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const u64 below = (1ull << lane) - 1;
+  u32* q = queue[w];
+  u32 qn = 0;
+  const u32 stride = gridDim.x * 1024;
+  for (u32 base = blockIdx.x * 1024 + w * 64; base < n; base += stride) {
+    const u32 i = base + lane;
+    const bool mk = i < n && mark[i] == kMarkDirty;
+    const u64 m = __ballot(mk);
+    if (mk) q[qn + __popcll(m & below)] = i;
+    qn += (u32)__popcll(m);
+    if (qn >= 64) {
+      __builtin_amdgcn_wave_barrier();
+      const u32 mine = q[lane];
+      const u32 rest = qn - 64;
+      const u32 tail = lane < rest ? q[64 + lane] : 0u;
+      __builtin_amdgcn_wave_barrier();
+      if (lane < rest) q[lane] = tail;
+      qn = rest;
+      process(mine);
+    }
   }
+  __builtin_amdgcn_wave_barrier();
+  if (lane < qn) process(q[lane]);
   __syncthreads();
   for (u32 j = threadIdx.x; j < kCellCache; j += 1024) {
     const u32 k = ckey[j];
