@@ -309,9 +309,9 @@ int phip_receive_datagrams(phip_handle* h, const uint8_t* bytes, const uint64_t*
  * each named in at most 14 bytes, has its other buckets merged in one
  * order-free pass and only its dirty buckets' sequences (each dirty message,
  * and one merge of the clean messages between two of them) applied in order
- * afterwards (phip_kernels.hpp "Dirty buckets").  phip_receive_datagrams and
- * larger dirty sets apply everything from the first dirty message on in
- * order.  The results are the Go loop's either way. */
+ * afterwards (phip_kernels.hpp "Dirty buckets"; phip_receive_datagrams
+ * alike).  Larger dirty sets apply everything from the first dirty message
+ * on in order.  The results are the Go loop's either way. */
 int phip_receive_soa(phip_handle* h, const phip_msgs* m, int64_t now, const phip_results* res,
                      uint32_t flags);
 /* LocalRepo.UpsertBucket for each state, in order. */

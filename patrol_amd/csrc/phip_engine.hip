@@ -709,7 +709,7 @@ int fast_front(phip_handle* h, In in, HotSrc hsrc, u32 n, u8* status, FastFront*
   u32 *c, *dlist = nullptr;
   DirtySet dset;
   if ((rc = ensure(h, B_FSCNT, 4 * kShards, &c))) return rc;
-  if constexpr (In::kSoa) {   // (decoded batches: their dirty messages listed)
+  {   // (the dirty messages listed by the classification)
     if ((rc = dirty_set(h, &dset, &dlist))) return rc;
     ff->mark = status;
     if (!status) {   // (marks need a column: a cleared one)
@@ -775,7 +775,7 @@ int fast_back(phip_handle* h, In in, u32 n, const FastFront& ff, bool queued) {
   SubBatch sb{};
   u32* dlist = nullptr;
   if ((rc = ensure(h, B_MISS, n, &miss)) || (rc = fast_shards(h, n, ff.par, &msh))) return rc;
-  if constexpr (In::kSoa) {
+  {
     // the dirty set behind the classification (a batch without a dirty
     // message returns at once: one launch of ~3 us)
     if ((rc = dirty_set(h, &dset, &dlist)) || (rc = sub_batch(h, &sb))) return rc;
@@ -791,7 +791,7 @@ int fast_back(phip_handle* h, In in, u32 n, const FastFront& ff, bool queued) {
                                                                       dset.key, ff.mark);
   }
   HIPCHK(h, hipGetLastError());
-  if constexpr (In::kSoa) {
+  {
     // the messages the fast kernel marked (an isolated batch's only: others
     // return at once), then the dirty buckets' records unmarked and their
     // ordered sub-batch built in the launch that ends the batch
@@ -806,10 +806,6 @@ int fast_back(phip_handle* h, In in, u32 n, const FastFront& ff, bool queued) {
         in, ff.c, dset.key, table(h), SubOut{sb.off, sb.len, sb.a, sb.t, sb.e, sb.map}, msh.cnt,
         h->ctr_map, kCtrWords, queued ? fast_counts(h, ff.par ^ 1u) : nullptr,
         fctr(h, ff.par ^ 1u));
-  } else {
-    k_shard_scan<<<1, kShards, 0, h->stream>>>(msh.cnt, ff.c, 2, h->ctr_map, kCtrWords,
-                                               queued ? fast_counts(h, ff.par ^ 1u) : nullptr,
-                                               fctr(h, ff.par ^ 1u));
   }
   HIPCHK(h, hipGetLastError());
   HIPCHK(h, hipEventRecord(h->ev_ctr, h->stream));
@@ -817,9 +813,10 @@ int fast_back(phip_handle* h, In in, u32 n, const FastFront& ff, bool queued) {
   return PHIP_OK;
 }
 
-// *first_dirty: n when the batch's dirty buckets were deferred (decoded
-// batches, soa), else its first dirty message (the prefix rule).
-int fast_collect(phip_handle* h, u32 n, u32 par, u32* first_dirty, u32* nmiss, bool soa) {
+// *first_dirty: n when the batch's dirty buckets were set apart (at most
+// kDirtyCap dirty messages, short names), else its first dirty message (the
+// prefix rule).
+int fast_collect(phip_handle* h, u32 n, u32 par, u32* first_dirty, u32* nmiss) {
   int rc;
   if ((rc = check_flags(h))) return rc;
   *nmiss = h->ctr_host[2];
@@ -833,7 +830,7 @@ int fast_collect(phip_handle* h, u32 n, u32 par, u32* first_dirty, u32* nmiss, b
     HIPCHK(h, hipGetLastError());
   }
   const u32 nd = h->ctr_host[kCtrNDirty];
-  const bool iso = soa && nd != 0 && nd <= kDirtyCap;
+  const bool iso = nd != 0 && nd <= kDirtyCap;
   *first_dirty = iso ? n : std::min<u32>(h->ctr_host[kCtrDirty], n);
   h->ndef = iso ? h->ctr_host[kCtrNDefer] : 0;   // (the ordered sub-batch, run_deferred)
   h->stats[3] = 0;   // (finish_receive: the messages it sends through the ordered path)
@@ -856,7 +853,7 @@ int fast_apply(phip_handle* h, In in, HotSrc hsrc, u32 n, u8* status, u32* first
   FastFront ff;
   if ((rc = fast_front(h, in, hsrc, n, status, &ff)) || (rc = fast_back(h, in, n, ff, false)))
     return rc;
-  return fast_collect(h, n, ff.par, first_dirty, nmiss, In::kSoa);
+  return fast_collect(h, n, ff.par, first_dirty, nmiss);
 }
 
 template <class Src>
@@ -1517,7 +1514,7 @@ int finish_pending(phip_handle* h, bool* worked) {
   HIPCHK(h, hipEventSynchronize(h->ev_ctr));
   u32 fd = p.n, nmiss = 0;
   int rc;
-  if ((rc = fast_collect(h, p.n, p.par, &fd, &nmiss, true))) return rc;
+  if ((rc = fast_collect(h, p.n, p.par, &fd, &nmiss))) return rc;
   const u32 stop = std::min<u32>(h->ctr_host[5], p.n);   // (a checked batch's malformed entry)
   const bool deferred = h->ndef != 0;
   if (nmiss == 0 && fd >= stop && !deferred) return stopped_at_bad_name(h, p.ow, p.n, stop);
@@ -2352,8 +2349,11 @@ int receive_datagrams_dev(phip_handle* h, const u8* d_bytes, const uint64_t* d_o
   // Fast path straight from the wire bytes: k_classify reads the headers
   // (and finds the first malformed datagram), k_receive_fast reads every
   // datagram in place; no decoded copy is written.
-  // Only a clean prefix with new buckets, or an incast / -0.0, has the
-  // datagrams decoded to the SoA form, for the paths that need it.
+  // Only a clean prefix with new buckets, or an incast / -0.0 past the dirty
+  // set's reach, has the datagrams decoded to the SoA form, for the paths
+  // that need it; a batch's dirty buckets (at most kDirtyCap dirty messages)
+  // go through the ordered path as a sub-batch dirty_finish
+  // reads from the wire.
   u32 fd = n, nmiss = 0;
   if ((rc = fast_apply(h, WireIn{d_bytes, d_offs}, Datagrams{d_bytes, d_offs}, n, ow.status, &fd,
                        &nmiss)))
@@ -2364,7 +2364,7 @@ int receive_datagrams_dev(phip_handle* h, const u8* d_bytes, const uint64_t* d_o
     HIPCHK(h, hipMemsetAsync(ow.status + stop, PHIP_ST_NOT_PROCESSED, n - stop, h->stream));
     HIPCHK(h, hipMemsetAsync(ow.status + stop, PHIP_ST_SHORT, 1, h->stream));
   }
-  if (fd < stop || nmiss) {
+  if (fd < stop || nmiss || h->ndef) {
     uint64_t *a, *t, *no;
     int64_t* e;
     u8* nl;
@@ -2372,14 +2372,14 @@ int receive_datagrams_dev(phip_handle* h, const u8* d_bytes, const uint64_t* d_o
         (rc = ensure(h, B_DE, n, &e)) || (rc = ensure(h, B_NOFF, n, &no)) ||
         (rc = ensure(h, B_NLEN, n, &nl)))
       return rc;
-    {
+    if (fd < stop || nmiss) {   // (a batch whose dirty buckets alone are left reads no decode)
       Launch l(h, "k_decode");
       k_decode<<<grid_for(stop), kBlock, 0, h->stream>>>(d_bytes, d_offs, stop, a, t, e, no, nl,
                                                           h->ctr);
       HIPCHK(h, hipGetLastError());
     }
     if ((rc = finish_receive(h, NamesPairs{d_bytes, no, nl}, a, t, e, stop, fd, nmiss, now, ow, n,
-                             false)))
+                             h->ndef != 0)))
       return after_error(h, rc);
   }
   if ((rc = copy_outputs(h, res, n, dev, ow))) return rc;

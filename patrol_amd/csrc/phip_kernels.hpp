@@ -1179,7 +1179,7 @@ __global__ __launch_bounds__(kFastBlock) __attribute__((amdgpu_waves_per_eu(8, 8
   // (dirty buckets, decoded batches: with a dirty set, the whole batch up to
   // the first malformed message; the messages that may name a dirty bucket
   // are marked for k_dirty_pass)
-  const u32 ndr = In::kSoa && dtab ? ctr[kCtrNDirty] : 0u;
+  const u32 ndr = dtab ? ctr[kCtrNDirty] : 0u;
   const bool iso = ndr != 0 && ndr <= kDirtyCap;
   n = min(n, iso ? ctr[5] : min(ctr[5], ctr[kCtrDirty]));
   if (n <= lo) return;
@@ -1969,14 +1969,16 @@ __device__ inline void dirty_finish(const In& in, u32* ctr, const DirtySet& D, c
   };
   for (u32 j = j0; j < j1; ++j) {
     const u32 i = D.idx[j];
-    u64 off;
+    u64 off, w0, w1, w2, ra, rt;
     u32 len;
-    in.src.get(i, off, len);
+    i64 re;
+    const typename In::Pre pr = in.pre(i);
+    in.load(i, pr, off, len, w0, w1, w2, ra, rt, re);   // (decoded or wire form)
     // the bucket's messages before its first dirty message: one merge, whose
     // status (it may create the bucket) goes to the first of them
     if (is_start(j)) emit_cell(D.cell + 3 * ((size_t)kDirtyCap + j), off, len, D.premin[j]);
     off2[o] = off; len2[o] = (u8)len;
-    a2[o] = in.ma[i]; t2[o] = in.mt[i]; e2[o] = in.me[i];
+    a2[o] = ra; t2[o] = rt; e2[o] = re;
     map2[o] = i;
     ++o;
     emit_cell(D.cell + 3 * j, off, len, ~0u);

@@ -631,3 +631,33 @@ def test_dirty_bucket_isolation_over_a_clean_batch_and_repeat(pa):
         torch.cuda.synchronize()
         same(dump(gs), o.dump())
         same(dump(gc), o.dump())
+
+
+@pytest.mark.parametrize("short_at", [None, 150000])
+def test_dirty_buckets_datagrams(pa, short_at):
+    """The same isolation for raw datagrams (phip_receive_datagrams, the
+    sub-batch read from the wire): a few incasts and -0.0 fields on hot,
+    cold and new buckets, bit-exact statuses, incast replies and tables
+    against the oracle's datagram loop; with a short datagram the batch
+    stops there (dirty messages past it are never applied)."""
+    import struct
+    rng = np.random.default_rng(71 if short_at is None else 72)
+    K = 20000
+    gs, gc, o = seeded(pa, rng, K, negative=0.3)
+    n = 1 << 18
+    ids = _gen.zipf_ids(rng, n, K + 2000)
+    a, t, e = _gen.clean_states(rng, n)
+    sprinkle(rng, ids, a, t, e, K, incast_hot=1, incast_cold=30, incast_new=10, negzero=20)
+    names = _gen.key_names(ids)
+    dgs = [struct.pack(">QQQ", int(a[i]), int(t[i]), int(e[i]) & (2**64 - 1)) +
+           bytes([len(names[i])]) + names[i] for i in range(n)]
+    if short_at is not None:
+        dgs[short_at] = dgs[short_at][:20]
+    now = _gen.T0 + SEC
+    out = gs.receive_datagrams(dgs, now)
+    st, ra, rt, re, stop = o.receive(dgs, now)
+    assert out["stop"] == stop == (n if short_at is None else short_at)
+    check(out["status"], (out["reply"]["a"], out["reply"]["t"], out["reply"]["e"]), st, ra, rt, re)
+    if short_at is None:
+        assert gs.last_stats()[4] == deferred_count(names, dirty_mask(a, t, e))
+    same(dump(gs), o.dump())
