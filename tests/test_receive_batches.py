@@ -661,3 +661,52 @@ def test_dirty_buckets_datagrams(pa, short_at):
     if short_at is None:
         assert gs.last_stats()[4] == deferred_count(names, dirty_mask(a, t, e))
     same(dump(gs), o.dump())
+
+
+@pytest.mark.parametrize("queue", [False, True])
+def test_dirty_bucket_cells_that_read_as_incasts(pa, queue):
+    """A cell's merge whose maxima read (+0, +0, 0) -- clean messages
+    (-5, +0, 0) and (+0, -3, 0) of a bucket whose state is negative -- would
+    read as an incast if it went through the ordered path as one message; it
+    is split into two merges of the same effect (dirty_finish).  Bucket b0:
+    incast, the two clean messages, incast (their cell after the first
+    incast); bucket b1: the two clean messages before its first incast (its
+    pre cell).  The final incasts see a zero state: PHIP_ST_INCAST_NOREPLY,
+    as the Go loop gives; the oracle agrees on every status and reply."""
+    rng = np.random.default_rng(81)
+    K = 5000
+    names0 = _gen.key_names(np.arange(K))
+    a0, t0, e0 = _gen.clean_states(rng, K)
+    neg = np.float64(-10.0).view(np.uint64)
+    a0[:2], t0[:2], e0[:2] = neg, neg, -5
+    created = np.full(K, _gen.T0 - SEC, np.int64)
+    g = pa.GPURepo(log2_slots=15)
+    g.seed(names0, a0, t0, e0, created)
+    o = O.Repo()
+    o.seed(names0, a0, t0, e0, created)
+    n = 1 << 16
+    ids = 2 + rng.integers(0, K - 2, n)
+    a, t, e = _gen.clean_states(rng, n)
+    m5, m3 = np.float64(-5.0).view(np.uint64), np.float64(-3.0).view(np.uint64)
+    seq = {  # position: (bucket, a, t, e)
+        1000: (0, 0, 0, 0), 1010: (0, m5, 0, 0), 1020: (0, 0, m3, 0), 1030: (0, 0, 0, 0),
+        2000: (1, m5, 0, 0), 2005: (1, 0, m3, 0), 2010: (1, 0, 0, 0),
+    }
+    for p, (b, x, y, z) in seq.items():
+        ids[p], a[p], t[p], e[p] = b, x, y, z
+    names = _gen.key_names(ids)
+    now = _gen.T0
+    if queue:
+        bt = device_batch(names, a, t, e)
+        queue_batch(g, bt, now)
+        g.flush()
+        r = bt["reply"].cpu().numpy()
+        got = (bt["status"].cpu().numpy(), (r[:, 0].view(np.uint64), r[:, 1].view(np.uint64), r[:, 2]))
+    else:
+        out = g.receive_soa(names, a, t, e, now)
+        got = (out["status"], (out["reply"]["a"], out["reply"]["t"], out["reply"]["e"]))
+    st, ra, rt, re = o.receive_soa(names, a, t, e, now)
+    check(got[0], got[1], st, ra, rt, re)
+    assert st[1030] == 3 and st[2010] == 3   # PHIP_ST_INCAST_NOREPLY: the state is zero
+    assert g.last_stats()[4] >= 6            # the split merges went through the sub-batch
+    same(dump(g), o.dump())
