@@ -128,6 +128,10 @@ enum {
                                    multi-launch path (by default they run as one launch) */
 #define PHIP_CFG_FIXED_SEED 0x4u /* place buckets with hash_seed as given (0: the unseeded
                                     placement) instead of a random per-handle seed */
+#define PHIP_CFG_ISOLATE 0x8u   /* set every Receive batch's dirty buckets apart (phip_receive_soa
+                                   "Order"); by default a handle does so from the first batch
+                                   after one that held an incast or -0.0 field until 256
+                                   clean batches in a row (a clean batch pays ~30 us for it) */
 
 typedef struct phip_config {
   int32_t device;        /* HIP device ordinal                                          */

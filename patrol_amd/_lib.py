@@ -43,6 +43,7 @@ DEVICE_PTRS = 0x1
 CFG_NO_GROW = 0x1
 CFG_NO_SMALL = 0x2
 CFG_FIXED_SEED = 0x4
+CFG_ISOLATE = 0x8
 ROUTE_COMBINE = 0x2
 GROUP_RCCL_SELF = 0x4
 GROUP_SMALL_CHUNKS = 0x8

@@ -81,6 +81,13 @@ struct phip_handle {
   int device = 0;
   int ncu = 256;             // compute units (persistent grid size)
   u32 ndef = 0;   // the last fast pass's ordered sub-batch (dirty buckets), entries
+  // Dirty-bucket isolation (phip_kernels.hpp "Dirty buckets"): always
+  // (PHIP_CFG_ISOLATE), or while iso_left > 0 -- kIsoKeep fast passes after
+  // the last one that met a dirty message.  coll_iso: whether the pass whose
+  // counters were collected last ran with it (its nested pass must too).
+  bool iso_always = false;
+  u32 iso_left = 0;
+  bool coll_iso = false;
   uint64_t stats[4] = {0, 0, 0, 0};   // last fast batch: hot entries, hot hits, misses,
                                       // messages it sent through the ordered path
   hipStream_t stream = nullptr;      // the stream every call runs on (own_stream or the caller's)
@@ -138,6 +145,7 @@ struct phip_handle {
     const int64_t* e = nullptr;
     u32 n = 0;
     u32 par = 0;
+    bool iso = false;
     i64 now = 0;
     OutView ow{};
   } pend;
@@ -642,6 +650,7 @@ struct FastFront {
   const HotHdr* hot = nullptr;
   const HotEntry* dir = nullptr;
   u32 par = 0;
+  bool iso = false;     // this pass sets its dirty buckets apart (the isolation kernels run)
   u32* c = nullptr;     // the pass's counter set (fctr)
   u8* mark = nullptr;   // decoded batches: the status column, or a cleared one (k_dirty_pass)
 };
@@ -701,16 +710,21 @@ int fast_shards(phip_handle* h, u32 n, u32 par, Sharded* out) {
 // 0.1 ms of API calls that used to sit in front of k_classify).
 // reset = false: the batch queued just before (nothing since) reset the
 // counters in its last launch.
+// iso: whether the pass sets its dirty buckets apart (-1: the handle's
+// policy, phip_handle::iso_left).
 template <class In, class HotSrc>
 int fast_front(phip_handle* h, In in, HotSrc hsrc, u32 n, u8* status, FastFront* ff,
-               bool reset = true) {
+               bool reset = true, int iso = -1) {
   int rc;
   *ff = FastFront{};
+  ff->iso = iso >= 0 ? iso != 0 : (h->iso_always || h->iso_left > 0);
   u32 *c, *dlist = nullptr;
   DirtySet dset;
   if ((rc = ensure(h, B_FSCNT, 4 * kShards, &c))) return rc;
-  {   // (the dirty messages listed by the classification)
-    if ((rc = dirty_set(h, &dset, &dlist))) return rc;
+  // (the classification lists the dirty messages either way: the policy
+  // learns of them, and an isolating pass builds its set from the list)
+  if ((rc = dirty_set(h, &dset, &dlist))) return rc;
+  if (ff->iso) {
     ff->mark = status;
     if (!status) {   // (marks need a column: a cleared one)
       if ((rc = ensure(h, B_DMARK, n, &ff->mark))) return rc;
@@ -775,7 +789,7 @@ int fast_back(phip_handle* h, In in, u32 n, const FastFront& ff, bool queued) {
   SubBatch sb{};
   u32* dlist = nullptr;
   if ((rc = ensure(h, B_MISS, n, &miss)) || (rc = fast_shards(h, n, ff.par, &msh))) return rc;
-  {
+  if (ff.iso) {
     // the dirty set behind the classification (a batch without a dirty
     // message returns at once: one launch of ~3 us)
     if ((rc = dirty_set(h, &dset, &dlist)) || (rc = sub_batch(h, &sb))) return rc;
@@ -786,12 +800,11 @@ int fast_back(phip_handle* h, In in, u32 n, const FastFront& ff, bool queued) {
   if ((rc = join_hot(h, ff.hot))) return rc;
   {
     Launch l(h, "k_receive_fast");
-    k_receive_fast<In><<<fast_grid(h, n), kFastBlock, 0, h->stream>>>(in, 0, n, table(h), msh,
-                                                                      ff.c, ff.hot, ff.dir,
-                                                                      dset.key, ff.mark);
+    k_receive_fast<In><<<fast_grid(h, n), kFastBlock, 0, h->stream>>>(
+        in, 0, n, table(h), msh, ff.c, ff.hot, ff.dir, ff.iso ? dset.key : nullptr, ff.mark);
   }
   HIPCHK(h, hipGetLastError());
-  {
+  if (ff.iso) {
     // the messages the fast kernel marked (an isolated batch's only: others
     // return at once), then the dirty buckets' records unmarked and their
     // ordered sub-batch built in the launch that ends the batch
@@ -806,6 +819,10 @@ int fast_back(phip_handle* h, In in, u32 n, const FastFront& ff, bool queued) {
         in, ff.c, dset.key, table(h), SubOut{sb.off, sb.len, sb.a, sb.t, sb.e, sb.map}, msh.cnt,
         h->ctr_map, kCtrWords, queued ? fast_counts(h, ff.par ^ 1u) : nullptr,
         fctr(h, ff.par ^ 1u));
+  } else {
+    k_shard_scan<<<1, kShards, 0, h->stream>>>(msh.cnt, ff.c, 2, h->ctr_map, kCtrWords,
+                                               queued ? fast_counts(h, ff.par ^ 1u) : nullptr,
+                                               fctr(h, ff.par ^ 1u));
   }
   HIPCHK(h, hipGetLastError());
   HIPCHK(h, hipEventRecord(h->ev_ctr, h->stream));
@@ -813,10 +830,12 @@ int fast_back(phip_handle* h, In in, u32 n, const FastFront& ff, bool queued) {
   return PHIP_OK;
 }
 
-// *first_dirty: n when the batch's dirty buckets were set apart (at most
-// kDirtyCap dirty messages, short names), else its first dirty message (the
-// prefix rule).
-int fast_collect(phip_handle* h, u32 n, u32 par, u32* first_dirty, u32* nmiss) {
+// *first_dirty: n when the batch's dirty buckets were set apart (iso ran and
+// at most kDirtyCap dirty messages, short names), else its first dirty
+// message (the prefix rule).  Updates the isolation policy: kIsoKeep passes
+// after one that met a dirty message.
+constexpr u32 kIsoKeep = 256;
+int fast_collect(phip_handle* h, u32 n, u32 par, u32* first_dirty, u32* nmiss, bool iso_ran) {
   int rc;
   if ((rc = check_flags(h))) return rc;
   *nmiss = h->ctr_host[2];
@@ -830,8 +849,11 @@ int fast_collect(phip_handle* h, u32 n, u32 par, u32* first_dirty, u32* nmiss) {
     HIPCHK(h, hipGetLastError());
   }
   const u32 nd = h->ctr_host[kCtrNDirty];
-  const bool iso = nd != 0 && nd <= kDirtyCap;
+  const bool iso = iso_ran && nd != 0 && nd <= kDirtyCap;
   *first_dirty = iso ? n : std::min<u32>(h->ctr_host[kCtrDirty], n);
+  if (h->ctr_host[kCtrDirty] < n) h->iso_left = kIsoKeep;
+  else if (h->iso_left) --h->iso_left;
+  h->coll_iso = iso_ran;
   h->ndef = iso ? h->ctr_host[kCtrNDefer] : 0;   // (the ordered sub-batch, run_deferred)
   h->stats[3] = 0;   // (finish_receive: the messages it sends through the ordered path)
   h->stats[0] = h->ctr_host[11];
@@ -848,12 +870,13 @@ int fast_collect(phip_handle* h, u32 n, u32 par, u32* first_dirty, u32* nmiss) {
 // misses (*nmiss of them) are listed in B_MISS.
 template <class In, class HotSrc>
 int fast_apply(phip_handle* h, In in, HotSrc hsrc, u32 n, u8* status, u32* first_dirty,
-               u32* nmiss) {
+               u32* nmiss, int iso = -1) {
   int rc;
   FastFront ff;
-  if ((rc = fast_front(h, in, hsrc, n, status, &ff)) || (rc = fast_back(h, in, n, ff, false)))
+  if ((rc = fast_front(h, in, hsrc, n, status, &ff, true, iso)) ||
+      (rc = fast_back(h, in, n, ff, false)))
     return rc;
-  return fast_collect(h, n, ff.par, first_dirty, nmiss);
+  return fast_collect(h, n, ff.par, first_dirty, nmiss, ff.iso);
 }
 
 template <class Src>
@@ -910,7 +933,10 @@ int finish_many_misses(phip_handle* h, Src src, const uint64_t* a, const uint64_
   }
   // 4. the fast pass again
   u32 fd = prefix;
-  if ((rc = fast_apply(h, SoaIn<Src>{src, a, t, e}, src, prefix, status, &fd, nmiss2))) return rc;
+  // (as the pass being finished did: its dirty buckets stay apart)
+  if ((rc = fast_apply(h, SoaIn<Src>{src, a, t, e}, src, prefix, status, &fd, nmiss2,
+                       h->coll_iso ? 1 : 0)))
+    return rc;
   // 5. PHIP_ST_CREATED after the second pass wrote its statuses
   if (status && n_claimed) {
     Launch l(h, "k_mark_created");
@@ -1514,7 +1540,7 @@ int finish_pending(phip_handle* h, bool* worked) {
   HIPCHK(h, hipEventSynchronize(h->ev_ctr));
   u32 fd = p.n, nmiss = 0;
   int rc;
-  if ((rc = fast_collect(h, p.n, p.par, &fd, &nmiss))) return rc;
+  if ((rc = fast_collect(h, p.n, p.par, &fd, &nmiss, p.iso))) return rc;
   const u32 stop = std::min<u32>(h->ctr_host[5], p.n);   // (a checked batch's malformed entry)
   const bool deferred = h->ndef != 0;
   if (nmiss == 0 && fd >= stop && !deferred) return stopped_at_bad_name(h, p.ow, p.n, stop);
@@ -1895,6 +1921,7 @@ int phip_open(const phip_config* cfg, phip_handle** out) {
   h->load_pct = cfg->max_load_pct ? std::min<u32>(cfg->max_load_pct, 95) : 90;
   h->max_load = load_limit(h->cap, h->load_pct);
   h->grow = !(cfg->flags & PHIP_CFG_NO_GROW);
+  h->iso_always = cfg->flags & PHIP_CFG_ISOLATE;
   h->small = !(cfg->flags & PHIP_CFG_NO_SMALL);
   h->arena_cap = cfg->arena_bytes ? cfg->arena_bytes : (1ull << 20);
   if (cfg->debug_tag_bits && cfg->debug_tag_bits < 64) h->tag_mask = (1ull << cfg->debug_tag_bits) - 1;
@@ -2309,6 +2336,7 @@ int phip_receive_soa(phip_handle* h, const phip_msgs* m, int64_t now, const phip
     h->pend.e = m->elapsed;
     h->pend.n = n;
     h->pend.par = ff.par;
+    h->pend.iso = ff.iso;
     h->pend.now = now;
     h->pend.ow = ow;
     return PHIP_OK;

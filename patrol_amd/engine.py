@@ -94,12 +94,16 @@ class GPURepo:
 
     def __init__(self, device: int = 0, log2_slots: int = 20, arena_bytes: int = 1 << 24,
                  max_load_pct: int = 90, debug_tag_bits: int = 0, grow: bool = True,
-                 small: bool = True, hash_seed: int | None = None):
+                 small: bool = True, hash_seed: int | None = None, isolate: bool = False):
         """hash_seed: None = a random placement seed per handle (the default,
         as Go's map seeds its hash per process); an int pins it
-        (PHIP_CFG_FIXED_SEED; 0 = the unseeded placement)."""
+        (PHIP_CFG_FIXED_SEED; 0 = the unseeded placement).  isolate: set every
+        Receive batch's dirty buckets apart (PHIP_CFG_ISOLATE; by default only
+        after a dirty batch)."""
         self.L = _lib.load()
         flags = (0 if grow else _lib.CFG_NO_GROW) | (0 if small else _lib.CFG_NO_SMALL)
+        if isolate:
+            flags |= _lib.CFG_ISOLATE
         if hash_seed is not None:
             flags |= _lib.CFG_FIXED_SEED
         cfg = phip_config(device, log2_slots, arena_bytes, max_load_pct, debug_tag_bits, flags, 0,

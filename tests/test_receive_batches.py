@@ -48,6 +48,8 @@ def seeded(pa, rng, K, log2_slots=17, negative=0.0, **kw):
     batches queued) and in the oracle; a fraction `negative` of them holds
     negative added/taken (where a -0.0 replica's place in the batch decides
     the sign of zero)."""
+    kw.setdefault("isolate", True)   # (every batch's dirty buckets apart: test_dirty_isolation_policy
+    #                                    covers the default, adaptive policy)
     names = _gen.key_names(np.arange(K))
     a, t, e = _gen.clean_states(rng, K)
     neg = rng.random(K) < negative
@@ -680,7 +682,7 @@ def test_dirty_bucket_cells_that_read_as_incasts(pa, queue):
     neg = np.float64(-10.0).view(np.uint64)
     a0[:2], t0[:2], e0[:2] = neg, neg, -5
     created = np.full(K, _gen.T0 - SEC, np.int64)
-    g = pa.GPURepo(log2_slots=15)
+    g = pa.GPURepo(log2_slots=15, isolate=True)
     g.seed(names0, a0, t0, e0, created)
     o = O.Repo()
     o.seed(names0, a0, t0, e0, created)
@@ -710,3 +712,38 @@ def test_dirty_bucket_cells_that_read_as_incasts(pa, queue):
     assert st[1030] == 3 and st[2010] == 3   # PHIP_ST_INCAST_NOREPLY: the state is zero
     assert g.last_stats()[4] >= 6            # the split merges went through the sub-batch
     same(dump(g), o.dump())
+
+
+def test_dirty_isolation_policy(pa):
+    """The default policy: a handle sets a batch's dirty buckets apart only
+    after a batch that held a dirty message (a clean batch would pay the
+    isolation kernels for nothing), until 256 clean batches in a row.  The
+    first dirty batch of a fresh handle takes the prefix rule, the next one
+    is isolated, and a handle that only ever saw clean batches never
+    launches the isolation kernels; bit-exact against the oracle throughout."""
+    rng = np.random.default_rng(91)
+    K = 20000
+    gs, _, o = seeded(pa, rng, K, isolate=False)
+    n = 1 << 17
+    now = _gen.T0
+    for r, want_iso in ((0, False), (1, True)):
+        ids = _gen.zipf_ids(rng, n, K + 500)
+        a, t, e = _gen.clean_states(rng, n)
+        sprinkle(rng, ids, a, t, e, K, incast_cold=20, negzero=10)
+        names = _gen.key_names(ids)
+        dirty = dirty_mask(a, t, e)
+        now += SEC
+        out = gs.receive_soa(names, a, t, e, now)
+        st, ra, rt, re = o.receive_soa(names, a, t, e, now)
+        check(out["status"], (out["reply"]["a"], out["reply"]["t"], out["reply"]["e"]), st, ra, rt, re)
+        want = deferred_count(names, dirty) if want_iso else n - int(np.argmax(dirty))
+        assert gs.last_stats()[4] == want, (r, gs.last_stats())
+        same(dump(gs), o.dump())
+    # clean batches on a fresh handle: no isolation kernel runs
+    g2 = pa.GPURepo(log2_slots=17)
+    g2.set_timing(True)
+    ids = _gen.zipf_ids(rng, n, K)
+    a, t, e = _gen.clean_states(rng, n)
+    g2.receive_soa(_gen.key_names(ids), a, t, e, now)
+    names_run = [nm for nm, _ in g2.timings()]
+    assert "k_receive_fast" in names_run and "k_dirty_build" not in names_run, names_run
