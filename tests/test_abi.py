@@ -136,3 +136,16 @@ def test_e_encoding_is_order_preserving_bijection():
         want = G.f2b(ob) if bb < ob else b        # bucket.go:250-252
         oc = 0 if (o & ~S) > INF else enc(o)      # NaN replica: never adopted
         assert max(enc(b), oc) == enc(want), (hex(b), hex(o))
+
+
+def test_flag_constants_match_header():
+    """Every PHIP_* flag the Python binding passes has the header's value
+    (a cgo binding reads them from the header itself)."""
+    src = open(os.path.join(ROOT, "include", "patrolhip.h")).read()
+    defs = {m.group(1): int(m.group(2), 16)
+            for m in re.finditer(r"#define PHIP_([A-Z_0-9]+)\s+(0x[0-9a-fA-F]+)u", src)}
+    for name, want in (("DEVICE_PTRS", "DEVICE_PTRS"), ("RECV_ASYNC", "RECV_ASYNC"),
+                       ("CFG_NO_GROW", "CFG_NO_GROW"), ("CFG_NO_SMALL", "CFG_NO_SMALL"),
+                       ("CFG_FIXED_SEED", "CFG_FIXED_SEED"), ("CFG_ISOLATE", "CFG_ISOLATE")):
+        assert name in defs, name
+        assert getattr(_lib, want) == defs[name], (name, getattr(_lib, want), defs[name])
